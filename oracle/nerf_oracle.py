@@ -1,0 +1,288 @@
+"""CPU restatement (torch fp32, CPU only) of the reference's volumetric-render hot path.
+
+TEST INFRASTRUCTURE ONLY -- see oracle/__init__.py.  Every function cites the reference
+file:line it restates (paths relative to DJNing/articulated-object-nerf).  Pinned against
+golden vectors generated from the reference itself (tests/golden/make_golden.py,
+tests/test_oracle_golden.py).
+
+Numerical notes that the HIP kernels reproduce (measured on torch 2.10 CPU):
+  * torch CPU ``cumsum``/``cumprod`` accumulate fp32 inputs in fp64 and round every prefix;
+  * ``torch.linspace`` on CPU mixes a symmetric scalar formula with a vectorised arange, so
+    the 1-D sample schedules (helper.py:116, :229) are built on the host with torch itself
+    and handed to the device as tables;
+  * ``x + 0.5*np.pi`` in pos_enc is an fp32 add of 1.5707964f (helper.py:139).
+"""
+import math
+
+import numpy as np
+import torch
+
+
+# ----------------------------------------------------------------------------- rays
+def create_spheric_poses(radius=4.0, n=40, phi=-30.0):
+    """reference datasets/sapien_multi.py:29-72 -> (n, 4, 4) float32 c2w."""
+
+    def trans_t(t):
+        return torch.tensor([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, t], [0, 0, 0, 1]],
+                            dtype=torch.float32)
+
+    def rot_phi(p):
+        c, s = np.cos(p), np.sin(p)
+        return torch.tensor([[1, 0, 0, 0], [0, c, -s, 0], [0, s, c, 0], [0, 0, 0, 1]],
+                            dtype=torch.float32)
+
+    def rot_theta(th):
+        c, s = np.cos(th), np.sin(th)
+        return torch.tensor([[c, 0, -s, 0], [0, 1, 0, 0], [s, 0, c, 0], [0, 0, 0, 1]],
+                            dtype=torch.float32)
+
+    flip = torch.tensor([[-1, 0, 0, 0], [0, 0, 1, 0], [0, 1, 0, 0], [0, 0, 0, 1]],
+                        dtype=torch.float32)
+    poses = []
+    for angle in np.linspace(-180, 180, n + 1)[:-1]:
+        c2w = trans_t(radius)
+        c2w = rot_phi(phi / 180.0 * np.pi) @ c2w
+        c2w = rot_theta(angle / 180.0 * np.pi) @ c2w
+        poses.append(flip @ c2w)
+    return torch.stack(poses, 0)
+
+
+def get_ray_directions(H, W, focal):
+    """reference datasets/ray_utils.py:71-90 (kornia create_meshgrid, no +0.5 centring)."""
+    x = torch.linspace(0, W - 1, W)
+    y = torch.linspace(0, H - 1, H)
+    i, j = torch.meshgrid(x, y, indexing="xy")  # i: column (H,W), j: row (H,W)
+    return torch.stack([(i - W / 2) / focal, -(j - H / 2) / focal, -torch.ones_like(i)], -1)
+
+
+def get_rays(directions, c2w, output_view_dirs=False, output_radii=False):
+    """reference datasets/ray_utils.py:118-159.
+
+    With ``output_view_dirs`` the reference normalises ``viewdirs`` in place and it aliases
+    ``rays_d`` (ray_utils.py:145-147), so both returned direction tensors are unit vectors.
+    """
+    rays_d = directions @ c2w[:, :3].T
+    rays_o = c2w[:, 3].expand(rays_d.shape)
+    radius = None
+    if output_radii:
+        rd = directions @ c2w[:, :3].T
+        dx = torch.sqrt(torch.sum((rd[:-1, :, :] - rd[1:, :, :]) ** 2, dim=-1))
+        dx = torch.cat([dx, dx[-2:-1, :]], dim=0)
+        radius = (dx[..., None] * 2 / torch.sqrt(torch.tensor(12, dtype=torch.int8))).reshape(-1)
+    rays_d = rays_d / torch.norm(rays_d, dim=-1, keepdim=True)
+    rays_o = rays_o.reshape(-1, 3)
+    rays_d = rays_d.reshape(-1, 3)
+    if output_view_dirs:
+        if output_radii:
+            return rays_o, rays_d, rays_d.clone(), radius
+        return rays_o, rays_d, rays_d.clone()
+    return rays_o, rays_d
+
+
+def focal_from_fovy(H, fovy_deg=35.0):
+    """SAPIEN camera (datagen/data_gen.py:60-67): fy = 0.5*H/tan(0.5*fovy)."""
+    return 0.5 * H / math.tan(0.5 * math.radians(fovy_deg))
+
+
+# ----------------------------------------------------------------------------- sampling
+def coarse_schedule(num_samples, near, far, lindisp=False):
+    """The 1-D schedule of reference helper.py:116-125 -> (t, lower, upper), each (S+1,)."""
+    t = torch.linspace(0.0, 1.0, num_samples + 1)
+    if lindisp:
+        t = 1.0 / (1.0 / near * (1.0 - t) + 1.0 / far * t)
+    else:
+        t = near * (1.0 - t) + far * t
+    mids = 0.5 * (t[..., 1:] + t[..., :-1])
+    upper = torch.cat([mids, t[..., -1:]], -1)
+    lower = torch.cat([t[..., :1], mids], -1)
+    return t, lower, upper
+
+
+def cast_rays(t_vals, origins, directions):
+    """reference helper.py:25-26."""
+    return origins[..., None, :] + t_vals[..., None] * directions[..., None, :]
+
+
+def sample_along_rays(rays_o, rays_d, num_samples, near, far, randomized, lindisp, u=None):
+    """reference helper.py:106-133; ``u`` (B, S+1) replaces torch.rand at helper.py:126."""
+    B = rays_o.shape[0]
+    t, lower, upper = coarse_schedule(num_samples, near, far, lindisp)
+    if randomized:
+        if u is None:
+            u = torch.rand((B, num_samples + 1))
+        t_vals = lower + (upper - lower) * u
+    else:
+        t_vals = torch.broadcast_to(t, (B, num_samples + 1))
+    return t_vals, cast_rays(t_vals, rays_o, rays_d)
+
+
+def pos_enc(x, min_deg, max_deg):
+    """reference helper.py:136-140: [x, sin(x*2^d) (d-major, xyz-minor), sin(x*2^d + pi/2)]."""
+    scales = torch.tensor([2 ** i for i in range(min_deg, max_deg)]).type_as(x)
+    xb = torch.reshape(x[..., None, :] * scales[:, None], list(x.shape[:-1]) + [-1])
+    return torch.cat([x, torch.sin(torch.cat([xb, xb + 0.5 * np.pi], dim=-1))], dim=-1)
+
+
+def fine_u(num_samples, batch_shape, randomized, u=None):
+    """The u of reference helper.py:226-230 (eval: linspace(0, 1-2^-32) whose last entry is 1.0)."""
+    if randomized:
+        return torch.rand(list(batch_shape) + [num_samples]) if u is None else u
+    u = torch.linspace(0.0, 1.0 - 2 ** -32, num_samples)
+    return torch.broadcast_to(u, list(batch_shape) + [num_samples])
+
+
+def sorted_piecewise_constant_pdf(bins, weights, num_samples, randomized, u=None):
+    """reference helper.py:203-243, restated with a per-ray searchsorted.
+
+    The reference's mask form (mask = u >= cdf; bin0 = max over masked bins, bin1 = min over
+    unmasked, first/last fallbacks) equals ``idx = searchsorted(cdf, u, right=True)``,
+    ``i0 = clamp(idx-1, 0, n-1)``, ``i1 = clamp(idx, max=n-1)`` -- pinned bit-exactly by the
+    golden vectors (including zero-weight plateaus and u == cdf ties).
+    """
+    eps = 1e-5
+    weight_sum = weights.sum(dim=-1, keepdim=True)
+    padding = torch.fmax(torch.zeros_like(weight_sum), eps - weight_sum)
+    weights = weights + padding / weights.shape[-1]
+    weight_sum = weight_sum + padding
+    pdf = weights / weight_sum
+    cdf = torch.fmin(torch.ones_like(pdf[..., :-1]), torch.cumsum(pdf[..., :-1], dim=-1))
+    zeros = torch.zeros(list(cdf.shape[:-1]) + [1])
+    ones = torch.ones(list(cdf.shape[:-1]) + [1])
+    cdf = torch.cat([zeros, cdf, ones], dim=-1)
+    u = fine_u(num_samples, cdf.shape[:-1], randomized, u).contiguous()
+    n = cdf.shape[-1]
+    idx = torch.searchsorted(cdf.contiguous(), u, right=True)
+    i0 = torch.clamp(idx - 1, 0, n - 1)
+    i1 = torch.clamp(idx, max=n - 1)
+    bin0, bin1 = torch.gather(bins, -1, i0), torch.gather(bins, -1, i1)
+    cdf0, cdf1 = torch.gather(cdf, -1, i0), torch.gather(cdf, -1, i1)
+    t = torch.clip(torch.nan_to_num((u - cdf0) / (cdf1 - cdf0), 0), 0, 1)
+    return bin0 + t * (bin1 - bin0)
+
+
+def sample_pdf(bins, weights, origins, directions, t_vals, num_samples, randomized, u=None):
+    """reference helper.py:246-252 (sorted merge of coarse t and the pdf samples)."""
+    t_samples = sorted_piecewise_constant_pdf(bins, weights, num_samples, randomized, u).detach()
+    t_vals = torch.sort(torch.cat([t_vals, t_samples], dim=-1), dim=-1).values
+    return t_vals, cast_rays(t_vals, origins, directions)
+
+
+# ----------------------------------------------------------------------------- MLP
+def mlp_forward(p, x, condition, netdepth=8, skip_layer=4, netdepth_condition=1):
+    """reference models/vanilla_nerf/model.py:95-120 with ``p`` = {layer.weight/bias: tensor}.
+
+    x: (B, S, C) encoded points; condition: (B, Cv) encoded view directions.
+    Returns raw_rgb (B, S, 3), raw_density (B, S, 1).
+    """
+    S, C = x.shape[1:]
+    x = x.reshape(-1, C)
+    inputs = x
+    for idx in range(netdepth):
+        x = torch.relu(x @ p[f"pts_linears.{idx}.weight"].T + p[f"pts_linears.{idx}.bias"])
+        if idx % skip_layer == 0 and idx > 0:
+            x = torch.cat([x, inputs], dim=-1)
+    raw_density = (x @ p["density_layer.weight"].T + p["density_layer.bias"]).reshape(-1, S, 1)
+    bottleneck = x @ p["bottleneck_layer.weight"].T + p["bottleneck_layer.bias"]
+    cond = torch.tile(condition[:, None, :], (1, S, 1)).reshape(-1, condition.shape[-1])
+    x = torch.cat([bottleneck, cond], dim=-1)
+    for idx in range(netdepth_condition):
+        x = torch.relu(x @ p[f"views_linear.{idx}.weight"].T + p[f"views_linear.{idx}.bias"])
+    raw_rgb = (x @ p["rgb_layer.weight"].T + p["rgb_layer.bias"]).reshape(-1, S, 3)
+    return raw_rgb, raw_density
+
+
+# ----------------------------------------------------------------------------- composite
+def volumetric_rendering(rgb, density, t_vals, dirs, white_bkgd):
+    """reference helper.py:157-195 -> (comp_rgb, acc, weights, depth)."""
+    eps = 1e-10
+    dists = torch.cat([t_vals[..., 1:] - t_vals[..., :-1],
+                       torch.ones(t_vals[..., :1].shape) * 1e10], dim=-1)
+    dists = dists * torch.norm(dirs[..., None, :], dim=-1)
+    alpha = 1.0 - torch.exp(-density[..., 0] * dists)
+    trans = torch.cat([torch.ones_like(alpha[..., :1]),
+                       torch.cumprod(1.0 - alpha[..., :-1] + eps, dim=-1)], dim=-1)
+    weights = alpha * trans
+    comp_rgb = (weights[..., None] * rgb).sum(dim=-2)
+    depth = (weights * t_vals).sum(dim=-1)
+    depth = torch.nan_to_num(depth, float("inf"))
+    depth = torch.clamp(depth, torch.min(depth), torch.max(depth))
+    acc = weights.sum(dim=-1)
+    if white_bkgd:
+        comp_rgb = comp_rgb + (1.0 - acc[..., None])
+    return comp_rgb, acc, weights, depth
+
+
+# ----------------------------------------------------------------------------- NeRF
+def split_state_dict(sd):
+    """{coarse_mlp.x: t, fine_mlp.x: t} -> (coarse params, fine params) as torch tensors."""
+    out = ({}, {})
+    for k, v in sd.items():
+        level, name = k.split(".", 1)
+        out[0 if level == "coarse_mlp" else 1][name] = torch.as_tensor(v)
+    return out
+
+
+def nerf_forward(params, rays, randomized, white_bkgd, near, far, num_coarse_samples=64,
+                 num_fine_samples=128, min_deg_point=0, max_deg_point=10, deg_view=4,
+                 lindisp=False, u_coarse=None, u_fine=None, return_intermediates=False):
+    """reference models/vanilla_nerf/model.py:147-199 (two-level coarse/fine loop).
+
+    params: (coarse, fine) dicts as from :func:`split_state_dict`.
+    Returns [(rgb, acc, depth)_coarse, (rgb, acc, depth)_fine] (+ per-level intermediates).
+    """
+    ret, inter = [], []
+    weights = t_vals = None
+    for level in range(2):
+        if level == 0:
+            t_vals, samples = sample_along_rays(rays["rays_o"], rays["rays_d"], num_coarse_samples,
+                                                near, far, randomized, lindisp, u_coarse)
+        else:
+            t_mids = 0.5 * (t_vals[..., 1:] + t_vals[..., :-1])
+            t_vals, samples = sample_pdf(t_mids, weights[..., 1:-1], rays["rays_o"],
+                                         rays["rays_d"], t_vals, num_fine_samples, randomized,
+                                         u_fine)
+        enc = pos_enc(samples, min_deg_point, max_deg_point)
+        venc = pos_enc(rays["viewdirs"], 0, deg_view)
+        raw_rgb, raw_sigma = mlp_forward(params[level], enc, venc)
+        rgb = torch.sigmoid(raw_rgb)
+        sigma = torch.relu(raw_sigma)
+        comp_rgb, acc, weights, depth = volumetric_rendering(rgb, sigma, t_vals, rays["rays_d"],
+                                                             white_bkgd)
+        ret.append((comp_rgb, acc, depth))
+        inter.append(dict(t_vals=t_vals, raw_rgb=raw_rgb, raw_sigma=raw_sigma, weights=weights))
+    return (ret, inter) if return_intermediates else ret
+
+
+def render_rays(params, batch, chunk, white_bkgd, near, far, **kw):
+    """reference models/vanilla_nerf/model.py:295-321 (chunk loop, fine outputs concatenated)."""
+    B = batch["rays_o"].shape[0]
+    out = {"comp_rgb": [], "acc": [], "depth": []}
+    for i in range(0, B, chunk):
+        sub = {k: v[i:i + chunk] for k, v in batch.items()}
+        fine = nerf_forward(params, sub, False, white_bkgd, near, far, **kw)[1]
+        out["comp_rgb"].append(fine[0])
+        out["acc"].append(fine[1])
+        out["depth"].append(fine[2])
+    return {k: torch.cat(v, 0) for k, v in out.items()}
+
+
+# ----------------------------------------------------------------------------- metrics
+def img2mse(x, y):
+    """reference helper.py:17-18."""
+    return torch.mean((x - y) ** 2)
+
+
+def mse2psnr(x):
+    """reference helper.py:21-22."""
+    return -10.0 * torch.log(x) / np.log(10)
+
+
+def psnr_each(preds, gts):
+    """reference models/interface.py:54-62 (clip both to [0,1])."""
+    return torch.stack([mse2psnr(torch.mean((torch.clip(p, 0, 1) - torch.clip(g, 0, 1)) ** 2))
+                        for p, g in zip(preds, gts)])
+
+
+def psnr_legacy(pred, gt):
+    """reference models/interface.py:72-74 (no clipping)."""
+    return -10 * torch.log10(torch.mean((pred - gt) ** 2))

@@ -1,0 +1,287 @@
+"""Generate the golden vectors for the hot path by running the REFERENCE itself.
+
+Runs only in the build container (needs /root/reference); its outputs (tests/golden/*.npz) are
+the committed fixtures that travel to the GPU box.  Inputs are synthetic (no datasets offline):
+SAPIEN-style spherical poses (datasets/sapien_multi.py:29-72), fovy-35 focal
+(datagen/data_gen.py:64), near=2/far=6 (datasets/sapien.py:72-73), and NeRF weights regenerated
+from numpy PCG64 by oracle/weights.py (their sha256 is stored with every fixture).
+
+    python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+
+import _refimport  # noqa: E402
+from oracle import weights as W  # noqa: E402
+
+helper, model, ray_utils, sapien_multi = _refimport.load()
+torch.set_num_threads(8)
+
+
+class RandQueue:
+    """Replace torch.rand with recorded uniforms (reference helper.py:126, :227)."""
+
+    def __init__(self, seed):
+        self.rng = np.random.Generator(np.random.PCG64(seed))
+        self.drawn = []
+        self._orig = torch.rand
+
+    def __call__(self, *size, **kw):
+        if len(size) == 1 and isinstance(size[0], (list, tuple, torch.Size)):
+            size = tuple(size[0])
+        u = torch.from_numpy(self.rng.random(size, dtype=np.float32))
+        self.drawn.append(u.numpy().copy())
+        return u
+
+    def __enter__(self):
+        torch.rand = self
+        return self
+
+    def __exit__(self, *a):
+        torch.rand = self._orig
+
+
+def make_nerf(seed=0, **kw):
+    net = model.NeRF(**kw)
+    sd = W.nerf_state_dict(seed)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    net.eval()
+    return net, W.digest(sd)
+
+
+def frame_rays(H, W_, pose_idx=5, radius=4.0):
+    focal = 0.5 * H / np.tan(0.5 * np.deg2rad(35.0))
+    c2w = sapien_multi.create_spheric_poses(radius)[pose_idx][:3, :4]
+    dirs = ray_utils.get_ray_directions(H, W_, focal)
+    rays_o, viewdirs, rays_d = ray_utils.get_rays(dirs, c2w, output_view_dirs=True)
+    return dict(rays_o=rays_o.contiguous(), rays_d=rays_d.contiguous(),
+                viewdirs=viewdirs.contiguous()), c2w, focal, dirs
+
+
+def capture_forward(net, rays, randomized, white_bkgd, near=2.0, far=6.0):
+    """Run reference NeRF.forward and record per-level intermediates via module hooks."""
+    rec = {"t": [], "raw_rgb": [], "raw_sigma": [], "weights": [], "bins": [], "wpdf": []}
+    orig_vr, orig_pdf = helper.volumetric_rendering, helper.sample_pdf
+
+    def vr(rgb, density, t_vals, dirs, white_bkgd, nocs=None):
+        out = orig_vr(rgb, density, t_vals, dirs, white_bkgd, nocs)
+        rec["t"].append(t_vals.detach().clone())
+        rec["weights"].append(out[2].detach().clone())
+        return out
+
+    def pdf(bins, weights, *a, **k):
+        rec["bins"].append(bins.detach().clone())
+        rec["wpdf"].append(weights.detach().clone())
+        return orig_pdf(bins, weights, *a, **k)
+
+    def hook(mod, inp, out):
+        rec["raw_rgb"].append(out[0].detach().clone())
+        rec["raw_sigma"].append(out[1].detach().clone())  # returns None: output untouched
+
+    hooks = [mlp.register_forward_hook(hook) for mlp in (net.coarse_mlp, net.fine_mlp)]
+    helper.volumetric_rendering, helper.sample_pdf = vr, pdf
+    try:
+        with torch.no_grad():
+            ret = net(rays, randomized, white_bkgd, near, far)
+    finally:
+        helper.volumetric_rendering, helper.sample_pdf = orig_vr, orig_pdf
+        for h in hooks:
+            h.remove()
+    return ret, rec
+
+
+def level_arrays(ret, rec):
+    out = {}
+    for lv, name in enumerate(("coarse", "fine")):
+        out[f"{name}_rgb"] = ret[lv][0].numpy()
+        out[f"{name}_acc"] = ret[lv][1].numpy()
+        out[f"{name}_depth"] = ret[lv][2].numpy()
+        out[f"{name}_t"] = rec["t"][lv].numpy()
+        out[f"{name}_raw_rgb"] = rec["raw_rgb"][lv].numpy()
+        out[f"{name}_raw_sigma"] = rec["raw_sigma"][lv].numpy()
+        out[f"{name}_weights"] = rec["weights"][lv].numpy()
+    return out
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print(f"{name}: {os.path.getsize(path) / 1e3:.1f} kB  keys={sorted(arrays)}")
+
+
+def case_rays():
+    """get_ray_directions / get_rays (ray_utils.py:71-159) on a 48x64 frame + radii."""
+    out = {}
+    for k, (H, W_, pose) in enumerate(((48, 64, 5), (30, 40, 17))):
+        rays, c2w, focal, dirs = frame_rays(H, W_, pose)
+        _, _, _, radii = ray_utils.get_rays(dirs, c2w, output_view_dirs=True, output_radii=True)
+        o2, d2 = ray_utils.get_rays(dirs, c2w)
+        out.update({f"c2w{k}": c2w.numpy(), f"hwf{k}": np.array([H, W_, focal]),
+                    f"dirs{k}": dirs.numpy(), f"rays_o{k}": rays["rays_o"].numpy(),
+                    f"rays_d{k}": rays["rays_d"].numpy(), f"viewdirs{k}": rays["viewdirs"].numpy(),
+                    f"radii{k}": radii.numpy(), f"plain_o{k}": o2.numpy(), f"plain_d{k}": d2.numpy()})
+    out["poses"] = sapien_multi.create_spheric_poses(4.0).numpy()
+    save("rays.npz", **out)
+
+
+def case_forward_eval():
+    """NeRF.forward, randomized=False, white background, 64c+128f (config C2 semantics)."""
+    net, dig = make_nerf(0)
+    rays, c2w, focal, _ = frame_rays(24, 32, 5)
+    sel = torch.arange(0, 24 * 32, 3)  # 256 rays spread over the frame
+    rays = {k: v[sel].contiguous() for k, v in rays.items()}
+    ret, rec = capture_forward(net, rays, False, True)
+    save("forward_eval.npz", digest=np.array(dig), **{k: v.numpy() for k, v in rays.items()},
+         bins=rec["bins"][0].numpy(), wpdf=rec["wpdf"][0].numpy(), **level_arrays(ret, rec))
+
+
+def case_forward_random():
+    """NeRF.forward, randomized=True with recorded uniforms, black background."""
+    net, dig = make_nerf(0)
+    rays, _, _, _ = frame_rays(16, 16, 11)
+    rays = {k: v[:128].contiguous() for k, v in rays.items()}
+    with RandQueue(1) as rq:
+        ret, rec = capture_forward(net, rays, True, False)
+    assert len(rq.drawn) == 2, len(rq.drawn)
+    save("forward_random.npz", digest=np.array(dig), **{k: v.numpy() for k, v in rays.items()},
+         u_coarse=rq.drawn[0], u_fine=rq.drawn[1], **level_arrays(ret, rec))
+
+
+def case_render_frame():
+    """LitNeRF.render_rays chunk loop (model.py:295-321): 20x24 frame, chunk 100 (ragged tail)
+    and config C1 (64x64, num_coarse_samples=32) fine outputs."""
+    out = {}
+    for tag, (H, W_, nc, chunk) in (("a", (20, 24, 64, 100)), ("c1", (64, 64, 32, 3840))):
+        net, dig = make_nerf(0, num_coarse_samples=nc)
+        rays, c2w, focal, _ = frame_rays(H, W_, 7)
+        res = {"comp_rgb": [], "acc": [], "depth": []}
+        with torch.no_grad():
+            for i in range(0, H * W_, chunk):
+                sub = {k: v[i:i + chunk] for k, v in rays.items()}
+                fine = net(sub, False, True, 2.0, 6.0)[1]
+                for j, k in enumerate(("comp_rgb", "acc", "depth")):
+                    res[k].append(fine[j])
+        out.update({f"{tag}_hw": np.array([H, W_, nc, chunk]), f"{tag}_c2w": c2w.numpy(),
+                    f"{tag}_focal": np.array(focal), f"{tag}_digest": np.array(dig)})
+        out.update({f"{tag}_{k}": torch.cat(v).numpy() for k, v in res.items()})
+    save("render_frame.npz", **out)
+
+
+def case_pdf_edges():
+    """sorted_piecewise_constant_pdf / sample_pdf edge cases (helper.py:203-252)."""
+    rng = np.random.Generator(np.random.PCG64(7))
+    B, nb = 12, 64
+    bins = np.sort(rng.uniform(2, 6, size=(B, nb)).astype(np.float32), -1)
+    w = rng.uniform(0, 1, size=(B, nb - 1)).astype(np.float32)
+    w[0] = 0.0                          # all-zero -> padding branch
+    w[1, 10:40] = 0.0                   # plateau inside
+    w[2] = 0.0; w[2, 5] = 1.0           # single spike -> cdf hits 1.0 early
+    w[3] = 1e-9                         # tiny total below eps
+    w[4, :] = 1.0                       # uniform -> u == cdf ties on the linspace grid
+    w[5, -5:] = 0.0                     # zero tail
+    w[6] = 0.0; w[6, -1] = 3.0          # mass only in the last bin
+    w[7, ::2] = 0.0                     # alternating zeros
+    out = {"bins": bins, "weights": w}
+    for tag, randomized in (("eval", False), ("rand", True)):
+        for ns in (128, 16):
+            with RandQueue(3) as rq:
+                s = helper.sorted_piecewise_constant_pdf(torch.from_numpy(bins), torch.from_numpy(w),
+                                                         ns, randomized)
+            out[f"{tag}{ns}_samples"] = s.numpy()
+            if randomized:
+                out[f"{tag}{ns}_u"] = rq.drawn[0]
+    # u forced exactly onto cdf knots (ties) via a custom u table, uniform weights
+    t_c = np.sort(rng.uniform(2, 6, size=(B, nb + 1)).astype(np.float32), -1)
+    o = rng.normal(size=(B, 3)).astype(np.float32)
+    d = rng.normal(size=(B, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    with RandQueue(4) as rq:
+        tv, xyz = helper.sample_pdf(torch.from_numpy(bins), torch.from_numpy(w), torch.from_numpy(o),
+                                    torch.from_numpy(d), torch.from_numpy(t_c), 128, True)
+    out.update(sp_tc=t_c, sp_o=o, sp_d=d, sp_u=rq.drawn[0], sp_t=tv.numpy(), sp_xyz=xyz.numpy())
+    tv, xyz = helper.sample_pdf(torch.from_numpy(bins), torch.from_numpy(w), torch.from_numpy(o),
+                                torch.from_numpy(d), torch.from_numpy(t_c), 128, False)
+    out.update(spe_t=tv.numpy(), spe_xyz=xyz.numpy())
+    save("pdf_edges.npz", **out)
+
+
+def case_composite_edges():
+    """volumetric_rendering (helper.py:157-195) on crafted densities."""
+    rng = np.random.Generator(np.random.PCG64(9))
+    B, S = 16, 65
+    t = np.sort(rng.uniform(2, 6, size=(B, S)).astype(np.float32), -1)
+    rgb = rng.uniform(0, 1, size=(B, S, 3)).astype(np.float32)
+    sig = rng.uniform(0, 2, size=(B, S, 1)).astype(np.float32)
+    sig[0] = 0.0                        # empty ray -> acc 0, background
+    sig[1, :, 0] = 1e4                  # opaque at the first sample
+    sig[2, :-1] = 0.0                   # only the last (1e10 interval) sample
+    sig[3, -1] = 0.0                    # last sample empty
+    sig[4] = 1e-12                      # tiny densities against 1e10 last interval
+    t[5, 10] = t[5, 11]                 # zero-length interval
+    d = rng.normal(size=(B, 3)).astype(np.float32)
+    d[:8] /= np.linalg.norm(d[:8], axis=-1, keepdims=True)  # half unit, half not
+    out = {"t": t, "rgb": rgb, "sigma": sig, "dirs": d}
+    for wb in (False, True):
+        r = helper.volumetric_rendering(torch.from_numpy(rgb), torch.from_numpy(sig),
+                                        torch.from_numpy(t), torch.from_numpy(d), wb)
+        for k, v in zip(("comp_rgb", "acc", "weights", "depth"), r):
+            out[f"wb{int(wb)}_{k}"] = v.numpy()
+    save("composite_edges.npz", **out)
+
+
+def case_pos_enc():
+    """pos_enc (helper.py:136-140) including |x|~10 (args up to 2^9*10)."""
+    rng = np.random.Generator(np.random.PCG64(11))
+    x = rng.uniform(-10, 10, size=(64, 3)).astype(np.float32)
+    x[0] = 0.0
+    x[1] = [1e-7, -3.1415927, 10.0]
+    v = rng.normal(size=(32, 3)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=-1, keepdims=True)
+    save("pos_enc.npz", x=x, enc_x=helper.pos_enc(torch.from_numpy(x), 0, 10).numpy(),
+         v=v, enc_v=helper.pos_enc(torch.from_numpy(v), 0, 4).numpy())
+
+
+def case_train_step():
+    """LitNeRF.training_step loss (model.py:256-282) + autograd grads, randomized with recorded
+    uniforms (config C5 semantics at 64 rays)."""
+    net, dig = make_nerf(0)
+    net.train()
+    rays, _, _, _ = frame_rays(16, 16, 3)
+    sel = torch.arange(0, 256, 4)
+    rays = {k: v[sel].contiguous() for k, v in rays.items()}
+    rng = np.random.Generator(np.random.PCG64(3))
+    target = torch.from_numpy(rng.uniform(0, 1, size=(64, 3)).astype(np.float32))
+    with RandQueue(2) as rq:
+        ret = net(rays, True, True, 2.0, 6.0)
+    loss0 = helper.img2mse(ret[0][0], target)
+    loss1 = helper.img2mse(ret[1][0], target)
+    loss = loss1 + loss0
+    loss.backward()
+    keep = ("bias", "density_layer.weight", "rgb_layer.weight", "fine_mlp.pts_linears.0.weight",
+            "fine_mlp.views_linear.0.weight")
+    grads = {f"grad::{k}": p.grad.numpy().copy() for k, p in net.named_parameters()
+             if any(k.endswith(s) for s in keep)}
+    save("train_step.npz", digest=np.array(dig), **{k: v.numpy() for k, v in rays.items()},
+         target=target.numpy(), u_coarse=rq.drawn[0], u_fine=rq.drawn[1],
+         loss=np.array(loss.item(), dtype=np.float32), loss0=np.array(loss0.item(), np.float32),
+         loss1=np.array(loss1.item(), np.float32),
+         psnr0=helper.mse2psnr(loss0).detach().numpy(), **grads)
+
+
+if __name__ == "__main__":
+    case_rays()
+    case_forward_eval()
+    case_forward_random()
+    case_render_frame()
+    case_pdf_edges()
+    case_composite_edges()
+    case_pos_enc()
+    case_train_step()
