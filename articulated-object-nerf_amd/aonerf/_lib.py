@@ -1,0 +1,97 @@
+"""ctypes binding of the C ABI in include/aonerf.h (libaonerf.so, built for gfx950).
+
+This is the reference-side binding a maintainer adds: plain pointers, sizes
+and the current torch stream go through; tensors stay owned by PyTorch.  There is NO CPU
+fallback: a missing library or a non-CUDA tensor raises.
+"""
+import ctypes
+import os
+
+import torch  # load torch's HIP runtime first: libaonerf.so binds to the same libamdhip64.so.7
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("AONERF_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libaonerf.so"))
+
+c_i64, c_int, c_float, c_size, vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+
+PREC = {"fp32": 0, "bf16x3": 1, "bf16": 2}
+ACT_NONE, ACT_VANILLA, ACT_ARTIC = 0, 1, 2
+
+
+class AonMlpParams(ctypes.Structure):
+    _fields_ = [("pts_w", vp * 8), ("pts_b", vp * 8), ("density_w", vp), ("density_b", vp),
+                ("bottleneck_w", vp), ("bottleneck_b", vp), ("views_w", vp), ("views_b", vp),
+                ("rgb_w", vp), ("rgb_b", vp)]
+
+
+_SIGNATURES = {
+    "aon_abi_version": (c_int, []),
+    "aon_last_error": (ctypes.c_char_p, []),
+    "aon_ray_directions": (c_int, [c_int, c_int, c_float, vp, vp]),
+    "aon_get_rays": (c_int, [vp, c_i64, vp, vp, vp, vp, c_int, c_int, vp, vp]),
+    "aon_frame_rays": (c_int, [c_int, c_int, c_float, vp, c_i64, c_i64, vp, vp, vp, vp]),
+    "aon_sample_along_rays": (c_int, [vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp]),
+    "aon_pos_enc": (c_int, [vp, c_i64, c_int, c_int, vp, vp]),
+    "aon_sample_pdf": (c_int, [vp, c_i64, vp, c_i64, c_i64, c_int, c_int, vp, c_i64, vp, c_int,
+                               vp, vp, vp, vp, vp]),
+    "aon_mlp_packed_bytes": (c_size, [c_int]),
+    "aon_mlp_pack": (c_int, [ctypes.POINTER(AonMlpParams), c_int, vp, vp]),
+    "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, vp, vp]),
+    "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, vp, vp]),
+    "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,
+                                  vp, vp, vp, vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libaonerf.so once; raise loudly if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"aonerf: HIP library not built: {LIB_PATH} "
+                              "(run `make -C articulated-object-nerf_amd/csrc` or __graft_entry__.build())")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        if handle.aon_abi_version() != 1:
+            raise ImportError("aonerf: ABI version mismatch")
+        _lib = handle
+    return _lib
+
+
+def call(name, *args):
+    """Invoke an aon_* entry point and turn a non-zero status into an exception."""
+    st = getattr(lib(), name)(*args)
+    if st != 0:
+        msg = lib().aon_last_error().decode(errors="replace")
+        if st < 0:
+            raise ValueError(f"{name}: {msg}")
+        raise RuntimeError(f"{name}: HIP error {st}: {msg}")
+
+
+def stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def require_gpu(*tensors):
+    """Every hot-path tensor must be a CUDA (HIP) fp32 tensor; the product path never runs on CPU."""
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise ValueError("aonerf runs on the MI355X only: got a CPU tensor "
+                             "(the CPU restatement lives in oracle/, test infrastructure only)")
+        if t.dtype != torch.float32:
+            raise ValueError(f"aonerf expects float32 tensors, got {t.dtype}")
+
+
+def contig(t):
+    return t if t.is_contiguous() else t.contiguous()

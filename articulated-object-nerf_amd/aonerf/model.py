@@ -1,0 +1,218 @@
+"""Drop-in for ``NeRFMLP`` / ``NeRF`` of the reference (models/vanilla_nerf/model.py:39-199).
+
+Identical constructor keywords, forward signatures, return tuples and parameter (state_dict)
+names, so a reference Lightning checkpoint (``model.coarse_mlp.pts_linears.0.weight`` ...)
+loads unchanged.  The forward pass runs on the fused HIP kernels:
+
+    level 0: aon_sample_along_rays (t only) -> aon_mlp_fwd (xyz + pos_enc + MLP fused)
+             -> aon_composite_fwd (sigmoid/relu + alpha compositing, weights kept)
+    level 1: aon_sample_pdf (mids, pdf/cdf, inverse CDF, sort/merge) -> aon_mlp_fwd
+             -> aon_composite_fwd
+
+Intermediates live in HBM (a 640x480 frame needs ~1.6 GB), so a whole frame is one launch
+per stage instead of the reference's 80 chunk iterations.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.init as init
+
+from . import _lib as L
+from . import helper
+
+_DEFAULT_GEOMETRY = dict(min_deg_point=0, max_deg_point=10, deg_view=4, netdepth=8, netwidth=256,
+                         netdepth_condition=1, netwidth_condition=128, skip_layer=4, input_ch=3,
+                         input_ch_view=3, num_rgb_channels=3, num_density_channels=1)
+
+
+class NeRFMLP(nn.Module):
+    """reference model.py:39-120 (same nn.Linear layout and init)."""
+
+    def __init__(self, min_deg_point, max_deg_point, deg_view, netdepth: int = 8,
+                 netwidth: int = 256, netdepth_condition: int = 1, netwidth_condition: int = 128,
+                 skip_layer: int = 4, input_ch: int = 3, input_ch_view: int = 3,
+                 num_rgb_channels: int = 3, num_density_channels: int = 1,
+                 precision: str = "fp32"):
+        super().__init__()
+        self.min_deg_point, self.max_deg_point, self.deg_view = min_deg_point, max_deg_point, deg_view
+        self.netdepth, self.netwidth, self.skip_layer = netdepth, netwidth, skip_layer
+        self.netdepth_condition, self.netwidth_condition = netdepth_condition, netwidth_condition
+        self.input_ch, self.input_ch_view = input_ch, input_ch_view
+        self.num_rgb_channels, self.num_density_channels = num_rgb_channels, num_density_channels
+        geometry = dict(min_deg_point=min_deg_point, max_deg_point=max_deg_point, deg_view=deg_view,
+                        netdepth=netdepth, netwidth=netwidth, netdepth_condition=netdepth_condition,
+                        netwidth_condition=netwidth_condition, skip_layer=skip_layer,
+                        input_ch=input_ch, input_ch_view=input_ch_view,
+                        num_rgb_channels=num_rgb_channels, num_density_channels=num_density_channels)
+        if geometry != _DEFAULT_GEOMETRY:
+            raise ValueError("aonerf's fused MLP kernel implements the reference's default NeRFMLP "
+                             f"geometry {_DEFAULT_GEOMETRY}; got {geometry}")
+        if precision not in L.PREC:
+            raise ValueError(f"precision must be one of {sorted(L.PREC)}")
+        self.precision = precision
+
+        pos_size = ((max_deg_point - min_deg_point) * 2 + 1) * input_ch
+        view_pos_size = (deg_view * 2 + 1) * input_ch_view
+        init_layer = nn.Linear(pos_size, netwidth)
+        init.xavier_uniform_(init_layer.weight)
+        pts = [init_layer]
+        for idx in range(netdepth - 1):
+            k = netwidth + pos_size if (idx % skip_layer == 0 and idx > 0) else netwidth
+            layer = nn.Linear(k, netwidth)
+            init.xavier_uniform_(layer.weight)
+            pts.append(layer)
+        self.pts_linears = nn.ModuleList(pts)
+        views = [nn.Linear(netwidth + view_pos_size, netwidth_condition)]  # default init (model.py:79)
+        for idx in range(netdepth_condition - 1):
+            layer = nn.Linear(netwidth_condition, netwidth_condition)
+            init.xavier_uniform_(layer.weight)
+            views.append(layer)
+        self.views_linear = nn.ModuleList(views)
+        self.bottleneck_layer = nn.Linear(netwidth, netwidth)
+        self.density_layer = nn.Linear(netwidth, num_density_channels)
+        self.rgb_layer = nn.Linear(netwidth_condition, num_rgb_channels)
+        for m in (self.bottleneck_layer, self.density_layer, self.rgb_layer):
+            init.xavier_uniform_(m.weight)
+        self._packed = None
+        self._packed_key = None
+
+    # -- weight packing (cached; repacked whenever a parameter is replaced or updated in place)
+    def _layers(self):
+        return list(self.pts_linears) + [self.density_layer, self.bottleneck_layer,
+                                         self.views_linear[0], self.rgb_layer]
+
+    def packed_weights(self):
+        params = [p for m in self._layers() for p in (m.weight, m.bias)]
+        L.require_gpu(*params)
+        key = (self.precision,) + tuple((p.data_ptr(), p._version) for p in params)
+        if key != self._packed_key:
+            params = [L.contig(p.detach()) for p in params]
+            prm = L.AonMlpParams()
+            for i in range(8):
+                prm.pts_w[i] = params[2 * i].data_ptr()
+                prm.pts_b[i] = params[2 * i + 1].data_ptr()
+            for name, idx in (("density", 8), ("bottleneck", 9), ("views", 10), ("rgb", 11)):
+                setattr(prm, f"{name}_w", params[2 * idx].data_ptr())
+                setattr(prm, f"{name}_b", params[2 * idx + 1].data_ptr())
+            prec = L.PREC[self.precision]
+            nbytes = L.lib().aon_mlp_packed_bytes(prec)
+            if nbytes == 0:
+                raise NotImplementedError(f"precision {self.precision!r} is not built yet")
+            buf = torch.empty(nbytes // 4, dtype=torch.float32, device=params[0].device)
+            L.call("aon_mlp_pack", L.ctypes.byref(prm), prec, L.ptr(buf), L.stream(buf.device))
+            self._packed, self._packed_key = buf, key
+        return self._packed
+
+    def forward_rays(self, rays_o, rays_d, viewdirs, t_vals):
+        """Fused cast_rays + pos_enc + forward: raw (B*S, 4) = [raw_rgb, raw_sigma]."""
+        L.require_gpu(rays_o, rays_d, viewdirs, t_vals)
+        B, S = t_vals.shape
+        raw = torch.empty((B * S, 4), device=t_vals.device)
+        L.call("aon_mlp_fwd", L.ptr(self.packed_weights()), L.PREC[self.precision],
+               L.ptr(L.contig(rays_o)), L.ptr(L.contig(rays_d)), L.ptr(L.contig(viewdirs)),
+               L.ptr(L.contig(t_vals)), B, S, L.ptr(raw), L.stream(t_vals.device))
+        return raw
+
+    def forward(self, x, condition):
+        """reference model.py:95-120: x (B, S, 63) encoded points, condition (B, 27)."""
+        L.require_gpu(x, condition)
+        B, S, C = x.shape
+        if C != 63 or tuple(condition.shape) != (B, 27):
+            raise ValueError("NeRFMLP.forward expects x (B, S, 63) and condition (B, 27)")
+        raw = torch.empty((B * S, 4), device=x.device)
+        L.call("aon_mlp_fwd_encoded", L.ptr(self.packed_weights()), L.PREC[self.precision],
+               L.ptr(L.contig(x)), L.ptr(L.contig(condition)), B, S, L.ptr(raw), L.stream(x.device))
+        raw = raw.view(B, S, 4)
+        return raw[..., :3], raw[..., 3:]
+
+
+def _events(timers):
+    """HIP events bracketing one launch on the current stream (the stream the C ABI uses)."""
+    if timers is None:
+        return None
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev[0].record()
+    return ev
+
+
+def _record(timers, ev, key, rows):
+    if ev is not None:
+        ev[1].record()
+        timers.setdefault(key, []).append((ev[0], ev[1], rows))
+
+
+class NeRF(nn.Module):
+    """reference model.py:123-199 (two-level coarse/fine render)."""
+
+    def __init__(self, num_levels: int = 2, min_deg_point: int = 0, max_deg_point: int = 10,
+                 deg_view: int = 4, num_coarse_samples: int = 64, num_fine_samples: int = 128,
+                 use_viewdirs: bool = True, noise_std: float = 0.0, lindisp: bool = False,
+                 precision: str = "fp32"):
+        super().__init__()
+        if num_levels != 2:
+            raise ValueError("the reference NeRF is two-level (coarse + fine)")
+        self.num_levels, self.min_deg_point, self.max_deg_point = num_levels, min_deg_point, max_deg_point
+        self.deg_view, self.num_coarse_samples, self.num_fine_samples = deg_view, num_coarse_samples, num_fine_samples
+        self.use_viewdirs, self.noise_std, self.lindisp = use_viewdirs, noise_std, lindisp
+        self.coarse_mlp = NeRFMLP(min_deg_point, max_deg_point, deg_view, precision=precision)
+        self.fine_mlp = NeRFMLP(min_deg_point, max_deg_point, deg_view, precision=precision)
+
+    def set_precision(self, precision):
+        for m in (self.coarse_mlp, self.fine_mlp):
+            if precision not in L.PREC:
+                raise ValueError(precision)
+            m.precision = precision
+        return self
+
+    @torch.no_grad()
+    def forward(self, rays, randomized, white_bkgd, near, far, *, u_coarse=None, u_fine=None,
+                return_weights=False, timers=None):
+        """reference model.py:147-199 -> [(comp_rgb, acc, depth)_coarse, (...)_fine].
+
+        ``u_coarse`` (B, Sc+1) / ``u_fine`` (B, Nf) inject the uniforms of randomized mode;
+        ``return_weights`` adds each level's weights (B, S) as a 4th element;
+        ``timers`` (dict) records hip events around each level's MLP launch.
+        """
+        o, d, v = rays["rays_o"], rays["rays_d"], rays["viewdirs"]
+        L.require_gpu(o, d, v)
+        o, d, v = L.contig(o), L.contig(d), L.contig(v)
+        B = o.shape[0]
+        dev = o.device
+        ret = []
+        t_vals = weights = None
+        for level in range(2):
+            if level == 0:
+                t_vals, _ = helper.sample_along_rays(o, d, self.num_coarse_samples, near, far,
+                                                     randomized, self.lindisp, u=u_coarse,
+                                                     want_coords=False)
+                mlp = self.coarse_mlp
+            else:
+                Sc = t_vals.shape[1]
+                if randomized:
+                    u = torch.rand((B, self.num_fine_samples), device=dev) if u_fine is None else L.contig(u_fine)
+                    u_stride = self.num_fine_samples
+                else:
+                    u, u_stride = helper.eval_u(self.num_fine_samples, dev), 0
+                t_new = torch.empty((B, Sc + self.num_fine_samples), device=dev)
+                # bins = mids of t (model.py:163), weights[..., 1:-1] as a strided view
+                L.call("aon_sample_pdf", None, 0, L.ptr(weights[:, 1:]), Sc, B, Sc - 1,
+                       self.num_fine_samples, L.ptr(u), u_stride, L.ptr(t_vals), Sc, None, None,
+                       L.ptr(t_new), None, L.stream(dev))
+                t_vals = t_new
+                mlp = self.fine_mlp
+            S = t_vals.shape[1]
+            ev = _events(timers)
+            raw = mlp.forward_rays(o, d, v, t_vals)
+            _record(timers, ev, f"mlp{level}", B * S)
+            if self.noise_std > 0 and randomized:
+                raw[:, 3] += torch.rand_like(raw[:, 3]) * self.noise_std
+            comp = torch.empty((B, 3), device=dev)
+            acc = torch.empty((B,), device=dev)
+            weights = torch.empty((B, S), device=dev)
+            depth = torch.empty((B,), device=dev)
+            ev = _events(timers)
+            L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
+                   B, S, int(bool(white_bkgd)), L.ACT_VANILLA, L.ptr(comp), L.ptr(acc),
+                   L.ptr(weights), L.ptr(depth), L.stream(dev))
+            _record(timers, ev, f"comp{level}", B * S)
+            ret.append((comp, acc, depth, weights) if return_weights else (comp, acc, depth))
+        return ret

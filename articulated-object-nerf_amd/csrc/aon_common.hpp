@@ -1,0 +1,77 @@
+// Shared helpers of the aonerf HIP library (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "aonerf.h"
+
+namespace aon {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// thread-local error message behind aon_last_error()
+void set_error(const std::string& msg);
+
+#define AON_REQUIRE(cond, msg)                                   \
+  do {                                                           \
+    if (!(cond)) {                                               \
+      ::aon::set_error(std::string(__func__) + ": " + (msg));    \
+      return -1;                                                 \
+    }                                                            \
+  } while (0)
+
+inline int launch_status(const char* fn) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(fn) + ": " + hipGetErrorString(e));
+    return static_cast<int>(e);
+  }
+  return 0;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline int grid_for(int64_t work, int per_block, int cap = 1 << 20) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<int>(g);
+}
+
+// torch.nan_to_num(x, nan=nan_val) with default posinf/neginf (float max / lowest)
+__device__ __forceinline__ float nan_to_num(float x, float nan_val) {
+  if (x != x) return nan_val;
+  if (x == __builtin_inff()) return 3.40282347e+38f;
+  if (x == -__builtin_inff()) return -3.40282347e+38f;
+  return x;
+}
+
+// fp32(0.5 * pi) as torch adds it to an fp32 tensor (reference helper.py:139)
+constexpr float kHalfPi = 1.57079637050628662109375f;
+
+// One pos_enc feature f of a 3-vector (reference helper.py:136-140):
+//   f < 3            -> x[f]
+//   3 <= f < 3+3L    -> sin(x[c] * 2^d),          (f-3) = 3d + c
+//   3+3L <= f < 3+6L -> sin(x[c] * 2^d + pi/2f),  (f-3-3L) = 3d + c
+//   otherwise        -> 0 (K padding)
+__device__ __forceinline__ float pos_enc_feature(float x0, float x1, float x2, int f, int min_deg,
+                                                 int L) {
+  if (f < 3) return f == 0 ? x0 : (f == 1 ? x1 : x2);
+  int q = f - 3;
+  bool cosine = false;
+  if (q >= 3 * L) {
+    q -= 3 * L;
+    cosine = true;
+  }
+  if (q >= 3 * L) return 0.f;
+  const int d = q / 3, c = q - 3 * d;
+  const float xc = c == 0 ? x0 : (c == 1 ? x1 : x2);
+  const float xb = xc * __builtin_ldexpf(1.0f, min_deg + d);  // exact power-of-two scaling
+  return sinf(cosine ? __fadd_rn(xb, kHalfPi) : xb);
+}
+
+}  // namespace aon

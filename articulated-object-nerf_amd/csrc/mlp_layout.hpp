@@ -1,0 +1,70 @@
+// Compile-time layout of the packed NeRFMLP weight stream (shared by pack and forward).
+//
+// The MLP runs "feature-major": a layer computes D[out][sample] = W[out][in] . H[in][sample]
+// with 16x16 MFMA tiles, samples on the MFMA column (lane & 15) and features on the rows.
+// The accumulator of one layer is then already the B operand of the next (no LDS round
+// trip): k-step (t, r) of the next layer takes register r of feature tile t, whose lane group
+// g = lane >> 4 holds input feature 16t + 4g + r.
+//
+// Weight stream = the A operands in consumption order.  One 1-KB "block" (t, u) holds, for lane
+// l, the float4 W[16u + (l & 15)][16t + 4(l >> 4) + 0..3] -> one conflict-free ds_read_b128 per
+// lane feeds 4 MFMAs.  Blocks are ordered layer by layer, t-major, u-minor, and padded to whole
+// LDS chunks.  Inputs with two concatenated segments (the skip layer cat[h, enc], the view
+// layer cat[bottleneck, enc_dir]; reference model.py:102-103, 113) are two K ranges of the same
+// layer; padded features (63 -> 64, 27 -> 32) carry zero weights.
+#pragma once
+
+namespace aon {
+namespace mlp {
+
+struct LayerDesc {
+  int ka, kb;        // 16-feature input tiles of segment A / B
+  int u;             // 16-row output tiles
+  int len_a, len_b;  // real columns of segment A / B in the torch weight ([out][len_a+len_b])
+  int out_real;      // real output rows
+  int blk0;          // first 1-KB block in the stream
+  int bias0;         // first float in the bias table (u*16 floats per layer)
+};
+
+enum { L0 = 0, L1, L2, L3, L4, L5, L6, L7, LDEN, LBOT, LVIEW, LRGB, kNumLayers };
+
+constexpr int kChunk = 16;  // 1-KB blocks per LDS pipeline stage
+
+constexpr LayerDesc kLayers[kNumLayers] = {
+    {4, 0, 16, 63, 0, 256, 0, 0},             // pts_linears.0   256 x 63
+    {16, 0, 16, 256, 0, 256, 64, 256},        // pts_linears.1
+    {16, 0, 16, 256, 0, 256, 320, 512},       // pts_linears.2
+    {16, 0, 16, 256, 0, 256, 576, 768},       // pts_linears.3
+    {16, 0, 16, 256, 0, 256, 832, 1024},      // pts_linears.4
+    {16, 4, 16, 256, 63, 256, 1088, 1280},    // pts_linears.5   256 x (256 + 63)
+    {16, 0, 16, 256, 0, 256, 1408, 1536},     // pts_linears.6
+    {16, 0, 16, 256, 0, 256, 1664, 1792},     // pts_linears.7
+    {16, 0, 1, 256, 0, 1, 1920, 2048},        // density_layer     1 x 256
+    {16, 0, 16, 256, 0, 256, 1936, 2064},     // bottleneck_layer 256 x 256
+    {16, 2, 8, 256, 27, 128, 2192, 2320},     // views_linear.0  128 x (256 + 27)
+    {8, 0, 1, 128, 0, 3, 2336, 2448},         // rgb_layer         3 x 128
+};
+
+constexpr int kBlocks = 2344;                                     // sum of (ka+kb)*u
+constexpr int kStreamBlocks = (kBlocks + kChunk - 1) / kChunk * kChunk;  // 2352
+constexpr int kNumChunks = kStreamBlocks / kChunk;                // 147
+constexpr int kBiasFloats = 2464;
+constexpr size_t kStreamBytesF32 = (size_t)kStreamBlocks * 1024;
+constexpr size_t kPackedBytesF32 = kStreamBytesF32 + kBiasFloats * 4;
+
+constexpr bool layout_ok() {
+  int blk = 0, bias = 0;
+  for (int i = 0; i < kNumLayers; ++i) {
+    const LayerDesc& d = kLayers[i];
+    if (d.blk0 != blk || d.bias0 != bias) return false;
+    if (d.blk0 % kChunk) return false;  // every layer starts on a chunk boundary
+    if (!(d.u == 1 || d.u % 4 == 0)) return false;
+    blk += (d.ka + d.kb) * d.u;
+    bias += d.u * 16;
+  }
+  return blk == kBlocks && bias == kBiasFloats;
+}
+static_assert(layout_ok(), "inconsistent MLP stream layout");
+
+}  // namespace mlp
+}  // namespace aon

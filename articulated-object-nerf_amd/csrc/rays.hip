@@ -1,0 +1,198 @@
+// Ray generation, stratified sampling and positional encoding (HBM-bound, one lane per
+// element, coalesced).  Rounding follows the reference's torch CPU ops: the (n,3)@(3,3)
+// product and the row norm are forward fma chains (measured bit-exact against torch 2.10).
+#include "aon_common.hpp"
+
+namespace aon {
+
+struct Mat34 {
+  float m[12];
+};
+
+// rays_d = dirs @ R^T (fma chain over k = 0, 1, 2), then / ||rays_d||
+__device__ __forceinline__ void rotate_normalize(float x, float y, float z, const Mat34& c,
+                                                 float& ox, float& oy, float& oz, float& rx,
+                                                 float& ry, float& rz, bool normalize) {
+  rx = fmaf(z, c.m[2], fmaf(y, c.m[1], __fmul_rn(x, c.m[0])));
+  ry = fmaf(z, c.m[6], fmaf(y, c.m[5], __fmul_rn(x, c.m[4])));
+  rz = fmaf(z, c.m[10], fmaf(y, c.m[9], __fmul_rn(x, c.m[8])));
+  if (normalize) {
+    const float n = sqrtf(fmaf(rz, rz, fmaf(ry, ry, __fmul_rn(rx, rx))));
+    rx = __fdiv_rn(rx, n);
+    ry = __fdiv_rn(ry, n);
+    rz = __fdiv_rn(rz, n);
+  }
+  ox = c.m[3];
+  oy = c.m[7];
+  oz = c.m[11];
+}
+
+// reference datasets/ray_utils.py:84-88 (kornia grid: i = column, j = row; no +0.5)
+__device__ __forceinline__ void pixel_dir(int64_t p, int H, int W, float focal, float& x,
+                                          float& y) {
+  const int row = static_cast<int>(p / W), col = static_cast<int>(p - static_cast<int64_t>(row) * W);
+  x = __fdiv_rn(__fsub_rn(static_cast<float>(col), 0.5f * static_cast<float>(W)), focal);
+  y = __fdiv_rn(-__fsub_rn(static_cast<float>(row), 0.5f * static_cast<float>(H)), focal);
+}
+
+__global__ void k_ray_directions(int H, int W, float focal, float* __restrict__ dirs) {
+  const int64_t n = static_cast<int64_t>(H) * W;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    float x, y;
+    pixel_dir(p, H, W, focal, x, y);
+    dirs[3 * p + 0] = x;
+    dirs[3 * p + 1] = y;
+    dirs[3 * p + 2] = -1.0f;
+  }
+}
+
+__global__ void k_get_rays(const float* __restrict__ dirs, int64_t n, Mat34 c2w,
+                           float* __restrict__ ro, float* __restrict__ rd,
+                           float* __restrict__ vd) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    float ox, oy, oz, rx, ry, rz;
+    rotate_normalize(dirs[3 * p], dirs[3 * p + 1], dirs[3 * p + 2], c2w, ox, oy, oz, rx, ry, rz,
+                     true);
+    ro[3 * p] = ox; ro[3 * p + 1] = oy; ro[3 * p + 2] = oz;
+    rd[3 * p] = rx; rd[3 * p + 1] = ry; rd[3 * p + 2] = rz;
+    if (vd) { vd[3 * p] = rx; vd[3 * p + 1] = ry; vd[3 * p + 2] = rz; }
+  }
+}
+
+// radii (ray_utils.py:138-143): || rd[y] - rd[y+1] || * 2 / sqrt(12) on UNnormalised
+// world directions; the last row repeats row H-2.
+__global__ void k_radii(const float* __restrict__ dirs, int H, int W, Mat34 c2w,
+                        float* __restrict__ radii) {
+  const int64_t n = static_cast<int64_t>(H) * W;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    int64_t row = p / W;
+    const int64_t col = p - row * W;
+    if (row == H - 1) row = H - 2;
+    const int64_t a = row * W + col, b = (row + 1) * W + col;
+    float o0, o1, o2, ax, ay, az, bx, by, bz;
+    rotate_normalize(dirs[3 * a], dirs[3 * a + 1], dirs[3 * a + 2], c2w, o0, o1, o2, ax, ay, az,
+                     false);
+    rotate_normalize(dirs[3 * b], dirs[3 * b + 1], dirs[3 * b + 2], c2w, o0, o1, o2, bx, by, bz,
+                     false);
+    const float dx = __fsub_rn(ax, bx), dy = __fsub_rn(ay, by), dz = __fsub_rn(az, bz);
+    // torch.sum over 3 squared terms (pairwise order of a 3-wide reduction: (x+y)+z)
+    const float s = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+    radii[p] = __fdiv_rn(__fmul_rn(sqrtf(s), 2.0f), 3.46410155f);
+  }
+}
+
+__global__ void k_frame_rays(int H, int W, float focal, Mat34 c2w, int64_t p0, int64_t n,
+                             float* __restrict__ ro, float* __restrict__ rd,
+                             float* __restrict__ vd) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    float x, y, ox, oy, oz, rx, ry, rz;
+    pixel_dir(p0 + p, H, W, focal, x, y);
+    rotate_normalize(x, y, -1.0f, c2w, ox, oy, oz, rx, ry, rz, true);
+    ro[3 * p] = ox; ro[3 * p + 1] = oy; ro[3 * p + 2] = oz;
+    rd[3 * p] = rx; rd[3 * p + 1] = ry; rd[3 * p + 2] = rz;
+    if (vd) { vd[3 * p] = rx; vd[3 * p + 1] = ry; vd[3 * p + 2] = rz; }
+  }
+}
+
+// helper.py:122-131: t = lower + (upper - lower) * u (randomized) or the schedule; xyz = o + t*d
+__global__ void k_sample_along_rays(const float* __restrict__ ro, const float* __restrict__ rd,
+                                    int64_t B, int S, const float* __restrict__ lower,
+                                    const float* __restrict__ upper, const float* __restrict__ u,
+                                    float* __restrict__ t_out, float* __restrict__ xyz) {
+  const int64_t n = B * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / S;
+    const int s = static_cast<int>(i - b * S);
+    float t = lower[s];
+    if (u) t = __fadd_rn(t, __fmul_rn(__fsub_rn(upper[s], lower[s]), u[i]));
+    t_out[i] = t;
+    if (xyz) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) xyz[3 * i + c] = __fadd_rn(ro[3 * b + c], __fmul_rn(t, rd[3 * b + c]));
+    }
+  }
+}
+
+__global__ void k_pos_enc(const float* __restrict__ x, int64_t n, int min_deg, int L,
+                          float* __restrict__ out) {
+  const int C = 3 + 6 * L;
+  const int64_t total = n * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / C;
+    const int f = static_cast<int>(i - r * C);
+    out[i] = pos_enc_feature(x[3 * r], x[3 * r + 1], x[3 * r + 2], f, min_deg, L);
+  }
+}
+
+static Mat34 load_c2w(const float* h) {
+  Mat34 m;
+  for (int i = 0; i < 12; ++i) m.m[i] = h[i];
+  return m;
+}
+
+}  // namespace aon
+
+using namespace aon;
+
+extern "C" int aon_ray_directions(int H, int W, float focal, float* dirs, aon_stream_t stream) {
+  AON_REQUIRE(H > 0 && W > 0 && dirs, "bad arguments");
+  hipLaunchKernelGGL(k_ray_directions, grid_for((int64_t)H * W, 256, 65536), 256, 0,
+                     (hipStream_t)stream, H, W, focal, dirs);
+  return launch_status(__func__);
+}
+
+extern "C" int aon_get_rays(const float* dirs, int64_t n, const float* c2w_host, float* rays_o,
+                            float* rays_d, float* viewdirs, int H, int W, float* radii,
+                            aon_stream_t stream) {
+  AON_REQUIRE(dirs && c2w_host && rays_o && rays_d && n >= 0, "null pointer or negative n");
+  if (n == 0) return 0;
+  const Mat34 c = load_c2w(c2w_host);
+  hipLaunchKernelGGL(k_get_rays, grid_for(n, 256, 65536), 256, 0, (hipStream_t)stream, dirs, n, c,
+                     rays_o, rays_d, viewdirs);
+  if (radii) {
+    AON_REQUIRE(H >= 2 && (int64_t)H * W == n, "radii need a full (H>=2, W) direction grid");
+    hipLaunchKernelGGL(k_radii, grid_for(n, 256, 65536), 256, 0, (hipStream_t)stream, dirs, H, W,
+                       c, radii);
+  }
+  return launch_status(__func__);
+}
+
+extern "C" int aon_frame_rays(int H, int W, float focal, const float* c2w_host, int64_t p0,
+                              int64_t n, float* rays_o, float* rays_d, float* viewdirs,
+                              aon_stream_t stream) {
+  AON_REQUIRE(H > 0 && W > 0 && c2w_host && rays_o && rays_d, "bad arguments");
+  AON_REQUIRE(p0 >= 0 && n >= 0 && p0 + n <= (int64_t)H * W, "pixel range outside the frame");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_frame_rays, grid_for(n, 256, 65536), 256, 0, (hipStream_t)stream, H, W,
+                     focal, load_c2w(c2w_host), p0, n, rays_o, rays_d, viewdirs);
+  return launch_status(__func__);
+}
+
+extern "C" int aon_sample_along_rays(const float* rays_o, const float* rays_d, int64_t B, int S,
+                                     const float* t_lower, const float* t_upper, const float* u,
+                                     float* t_out, float* xyz_out, aon_stream_t stream) {
+  AON_REQUIRE(B >= 0 && S > 0 && t_lower && t_out, "bad arguments");
+  AON_REQUIRE(!u || t_upper, "randomized sampling needs t_upper");
+  AON_REQUIRE(!xyz_out || (rays_o && rays_d), "xyz needs rays_o/rays_d");
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(k_sample_along_rays, grid_for(B * S, 256, 65536), 256, 0, (hipStream_t)stream,
+                     rays_o, rays_d, B, S, t_lower, t_upper, u, t_out, xyz_out);
+  return launch_status(__func__);
+}
+
+extern "C" int aon_pos_enc(const float* x, int64_t n, int min_deg, int max_deg, float* out,
+                           aon_stream_t stream) {
+  AON_REQUIRE(x && out && n >= 0 && max_deg >= min_deg && min_deg >= -126 && max_deg <= 127,
+              "bad arguments");
+  if (n == 0) return 0;
+  const int L = max_deg - min_deg;
+  hipLaunchKernelGGL(k_pos_enc, grid_for(n * (3 + 6 * L), 256, 65536), 256, 0, (hipStream_t)stream,
+                     x, n, min_deg, L, out);
+  return launch_status(__func__);
+}

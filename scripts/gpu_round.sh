@@ -1,0 +1,26 @@
+#!/usr/bin/env bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel trace + HBM counters.
+# Usage (from the repo root, on the box):  bash scripts/gpu_round.sh [tag] [bench args...]
+# Every GPU step has its own time limit; the script stops at the first crash/timeout.
+set -u
+TAG=${1:-r01}; shift || true
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>: run, log, stop the session on crash/timeout
+  local name=$1 lim=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q -s -p no:cacheprovider
+step bench 600 python bench.py "$@"
+tail -1 "$OUT/bench.log" > "$OUT/bench.json"
+[ "${SKIP_PROF:-0}" = 1 ] && exit 0
+step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@"
+step rocprof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@"
+step rocprof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@"
+echo done
