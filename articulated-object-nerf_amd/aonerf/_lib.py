@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("AONERF_LIB", os.path.join(os.path.dirname(_HERE), "li
 
 c_i64, c_int, c_float, c_size, vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 
-PREC = {"fp32": 0, "bf16x3": 1, "bf16": 2}
+PREC = {"fp32": 0, "f16x3": 1}
 ACT_NONE, ACT_VANILLA, ACT_ARTIC = 0, 1, 2
 
 

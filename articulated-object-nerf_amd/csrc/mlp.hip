@@ -13,6 +13,7 @@
 // reference's fp32 GEMM only by summation order.
 #include "aon_common.hpp"
 #include "mlp_layout.hpp"
+#include "mlp_pipe.hpp"
 
 namespace aon {
 namespace mlp {
@@ -21,31 +22,6 @@ constexpr int kWaves = 8;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kRowsPerWave = 16;
 constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
-constexpr int kStageRegs = kChunk * 64 / kThreads;  // f4 per thread per chunk
-static_assert(kStageRegs * kThreads == kChunk * 64, "chunk must split evenly over threads");
-
-struct Pipe {
-  f4* wbuf;  // [2][kChunk * 64] f4 in LDS
-  const f4* __restrict__ src;
-  f4 stage[kStageRegs];
-  int tid, lane;
-
-  __device__ __forceinline__ void load(int c) {
-#pragma unroll
-    for (int i = 0; i < kStageRegs; ++i) stage[i] = src[(size_t)c * kChunk * 64 + tid + i * kThreads];
-  }
-  // first use of chunk c: publish it to LDS, then prefetch chunk c + 1
-  __device__ __forceinline__ void begin(int c) {
-    f4* dst = wbuf + (c & 1) * kChunk * 64;
-#pragma unroll
-    for (int i = 0; i < kStageRegs; ++i) dst[tid + i * kThreads] = stage[i];
-    __syncthreads();
-    if (c + 1 < kNumChunks) load(c + 1);
-  }
-  __device__ __forceinline__ f4 block(int b) const {
-    return wbuf[((b / kChunk) & 1) * kChunk * 64 + (b % kChunk) * 64 + lane];
-  }
-};
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -53,7 +29,7 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
 
 // acc[u] (+)= W . [xa ; xb] over the layer's blocks, U output tiles (U % 4 == 0)
 template <int LAYER, int NA, int NB, int NACC>
-__device__ __forceinline__ void gemm(Pipe& p, const f4 (&xa)[NA], const f4 (&xb)[NB],
+__device__ __forceinline__ void gemm(Pipe<kThreads>& p, const f4 (&xa)[NA], const f4 (&xb)[NB],
                                      f4 (&acc)[NACC]) {
   constexpr LayerDesc d = kLayers[LAYER];
   constexpr int U = d.u;
@@ -79,7 +55,7 @@ __device__ __forceinline__ void gemm(Pipe& p, const f4 (&xa)[NA], const f4 (&xb)
 
 // single output tile (density / rgb heads): two interleaved accumulators over t
 template <int LAYER, int NA>
-__device__ __forceinline__ f4 gemm_u1(Pipe& p, const f4 (&xa)[NA], f4 init) {
+__device__ __forceinline__ f4 gemm_u1(Pipe<kThreads>& p, const f4 (&xa)[NA], f4 init) {
   constexpr LayerDesc d = kLayers[LAYER];
   static_assert(d.u == 1 && d.kb == 0 && d.ka <= NA && d.ka % 2 == 0, "head layer shape");
   f4 acc0 = init, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -130,7 +106,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd_f32(
   const int64_t rr = row < N ? row : N - 1;
   const int64_t ray = rr / S;
 
-  Pipe p;
+  Pipe<kThreads> p;
   p.wbuf = wbuf;
   p.src = wstream;
   p.tid = tid;
@@ -232,12 +208,6 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd_f32(
 }
 
 // ---- packing: torch [out][in] fp32 -> stream blocks (+ padded biases)
-struct PackArgs {
-  const float* w[kNumLayers];
-  const float* b[kNumLayers];
-  LayerDesc layers[kNumLayers];  // the constexpr table, passed by value for runtime indexing
-};
-
 __global__ void k_pack_f32(PackArgs a, float* __restrict__ out) {
   const int64_t total = (int64_t)kStreamBlocks * 256 + kBiasFloats;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
@@ -280,14 +250,23 @@ using namespace aon;
 using namespace aon::mlp;
 
 extern "C" size_t aon_mlp_packed_bytes(int precision) {
-  if (precision == AON_PREC_FP32) return kPackedBytesF32;
+  // both precisions use the same block grid: fp32 tiles, or hi+lo fp16 pairs of equal size
+  if (precision == AON_PREC_FP32 || precision == AON_PREC_F16X3) return kPackedBytesF32;
   return 0;
+}
+
+static int f16x3_ncol() {
+  static int ncol = [] {
+    const char* e = getenv("AON_F16X3_NCOL");  // tuning knob: samples per wave = 16 * ncol
+    return (e && atoi(e) == 2) ? 2 : 1;
+  }();
+  return ncol;
 }
 
 extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* packed,
                             aon_stream_t stream) {
   AON_REQUIRE(prm && packed, "null pointer");
-  AON_REQUIRE(precision == AON_PREC_FP32, "unsupported precision");
+  AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3, "unsupported precision");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
   PackArgs a;
   for (int i = 0; i < 8; ++i) {
@@ -300,8 +279,9 @@ extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* pack
   a.w[LRGB] = prm->rgb_w;        a.b[LRGB] = prm->rgb_b;
   for (int i = 0; i < kNumLayers; ++i) {
     AON_REQUIRE(a.w[i] && a.b[i], "null layer parameter");
-    a.layers[i] = kLayers[i];
+    a.layers[i] = precision == AON_PREC_FP32 ? kLayers[i] : kLayersH[i];
   }
+  if (precision == AON_PREC_F16X3) return pack_f16x3(a, packed, (hipStream_t)stream);
   const int64_t total = (int64_t)kStreamBlocks * 256 + kBiasFloats;
   hipLaunchKernelGGL(k_pack_f32, grid_for(total, 256, 4096), 256, 0, (hipStream_t)stream, a,
                      static_cast<float*>(packed));
@@ -312,12 +292,14 @@ static int mlp_launch(int mode, const void* packed, int precision, const float* 
                       const float* a1, const float* a2, const float* a3, int64_t B, int S,
                       float* raw, aon_stream_t stream) {
   AON_REQUIRE(packed && raw && a0 && a1, "null pointer");
-  AON_REQUIRE(precision == AON_PREC_FP32, "unsupported precision");
+  AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3, "unsupported precision");
   AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
   AON_REQUIRE(aligned16(packed) && aligned16(raw), "packed / raw must be 16-byte aligned");
   const int64_t N = B * S;
   if (N == 0) return 0;
   AON_REQUIRE((N + kRowsPerBlock - 1) / kRowsPerBlock < (1ll << 31), "too many rows");
+  if (precision == AON_PREC_F16X3)
+    return launch_f16x3(mode, f16x3_ncol(), packed, a0, a1, a2, a3, B, S, raw, (hipStream_t)stream);
   const int grid = static_cast<int>((N + kRowsPerBlock - 1) / kRowsPerBlock);
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + kStreamBytesF32);

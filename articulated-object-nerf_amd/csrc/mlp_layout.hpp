@@ -45,6 +45,29 @@ constexpr LayerDesc kLayers[kNumLayers] = {
     {8, 0, 1, 128, 0, 3, 2336, 2448},         // rgb_layer         3 x 128
 };
 
+// The fp16x3 kernel (mlp_f16x3.hip) walks the SAME block grid with 32-feature k-steps and
+// two 1-KB blocks (hi, lo) per (u, k-step): ka/kb count 32-feature k-steps, and segment B
+// (enc / enc_dir, computed in-register) uses the natural feature order.
+constexpr LayerDesc kLayersH[kNumLayers] = {
+    {0, 2, 16, 0, 63, 256, 0, 0},             // pts_linears.0: enc only (segment B)
+    {8, 0, 16, 256, 0, 256, 64, 256},
+    {8, 0, 16, 256, 0, 256, 320, 512},
+    {8, 0, 16, 256, 0, 256, 576, 768},
+    {8, 0, 16, 256, 0, 256, 832, 1024},
+    {8, 2, 16, 256, 63, 256, 1088, 1280},
+    {8, 0, 16, 256, 0, 256, 1408, 1536},
+    {8, 0, 16, 256, 0, 256, 1664, 1792},
+    {8, 0, 1, 256, 0, 1, 1920, 2048},
+    {8, 0, 16, 256, 0, 256, 1936, 2064},
+    {8, 1, 8, 256, 27, 128, 2192, 2320},
+    {4, 0, 1, 128, 0, 3, 2336, 2448},
+};
+
+// activations and biases of the fp16x3 path are carried at 2^-8 scale (overflow only past
+// |x| = 65504 * 256); the lo halves are carried at 2^11 scale
+constexpr float kActScale = 1.0f / 256.0f;
+constexpr float kLoScale = 2048.0f;
+
 constexpr int kBlocks = 2344;                                     // sum of (ka+kb)*u
 constexpr int kStreamBlocks = (kBlocks + kChunk - 1) / kChunk * kChunk;  // 2352
 constexpr int kNumChunks = kStreamBlocks / kChunk;                // 147
@@ -65,6 +88,30 @@ constexpr bool layout_ok() {
   return blk == kBlocks && bias == kBiasFloats;
 }
 static_assert(layout_ok(), "inconsistent MLP stream layout");
+
+constexpr bool layout_h_ok() {
+  for (int i = 0; i < kNumLayers; ++i) {
+    const LayerDesc& a = kLayers[i];
+    const LayerDesc& h = kLayersH[i];
+    if (a.blk0 != h.blk0 || a.bias0 != h.bias0 || a.u != h.u) return false;
+    if ((h.ka + h.kb) * h.u * 2 != (a.ka + a.kb) * a.u) return false;
+  }
+  return true;
+}
+static_assert(layout_h_ok(), "fp16x3 layout must share the block grid");
+
+// pack-kernel arguments: per-layer torch parameter pointers + the layout table by value
+struct PackArgs {
+  const float* w[kNumLayers];
+  const float* b[kNumLayers];
+  LayerDesc layers[kNumLayers];
+};
+
+// fp16x3 path (mlp_f16x3.hip)
+int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream);
+int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,
+                 const float* a2, const float* a3, int64_t B, int S, float* raw,
+                 hipStream_t stream);
 
 }  // namespace mlp
 }  // namespace aon

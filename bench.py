@@ -29,7 +29,7 @@ import torch.distributed as dist  # noqa: E402
 H, W = 480, 640
 NC, NF = 64, 128
 MAC_PER_SAMPLE = 593_408            # NeRFMLP multiply-accumulates per sample
-PEAK_TFLOPS = {"fp32": 157.3, "bf16x3": 2500.0, "bf16": 2500.0}   # dense MFMA peak of the issued dtype
+PEAK_TFLOPS = {"fp32": 157.3, "f16x3": 2500.0}   # dense MFMA peak of the issued dtype
 PEAK_HBM_GBS = 8000.0
 
 

@@ -27,9 +27,9 @@ typedef void* aon_stream_t; /* hipStream_t */
 #define AON_ABI_VERSION 1
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
-#define AON_PREC_FP32 0   /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32): parity mode */
-#define AON_PREC_BF16X3 1 /* 3-pass bf16 split (hi*hi + hi*lo + lo*hi) on bf16 MFMA */
-#define AON_PREC_BF16 2   /* plain bf16 MFMA, fp32 accumulate (training throughput mode) */
+#define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
+#define AON_PREC_F16X3 1 /* fp16 hi/lo split, 3 products (hi*hi + hi*lo + lo*hi) per weight on
+                            v_mfma_f32_16x16x32_f16, fp32 accumulate: ~22-bit operands */
 
 /* Output activation applied by the compositor (reference model.py:186-187,
  * model_autodecoder.py:321-323). */

@@ -40,14 +40,20 @@ def npy(t):
     return t.detach().float().cpu().numpy()
 
 
-@pytest.fixture(scope="module")
-def nerf():
+PRECISIONS = ["fp32", "f16x3"]
+
+
+def make_nerf(precision, **kw):
     from aonerf.model import NeRF
 
-    net = NeRF().cuda()
-    sd = W.nerf_state_dict(0)
-    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    net = NeRF(precision=precision, **kw).cuda()
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.nerf_state_dict(0).items()})
     return net
+
+
+@pytest.fixture(scope="module", params=PRECISIONS)
+def nerf(request):
+    return make_nerf(request.param)
 
 
 def rays_of(g):
@@ -227,17 +233,16 @@ def test_forward_randomized_end_to_end(golden, nerf):
     check_levels(ret, g)
 
 
-def test_render_frame_chunks(golden, nerf):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_render_frame_chunks(golden, precision):
     """render_rays chunk loop and config C1 (64x64, 32 coarse samples) from c2w alone."""
-    from aonerf.model import NeRF
     from aonerf.render import render_frame, render_rays
     from aonerf.ray_utils import frame_rays
 
     g = golden("render_frame.npz")
     for tag in ("a", "c1"):
         H, Wd, nc, chunk = (int(x) for x in g[f"{tag}_hw"])
-        net = NeRF(num_coarse_samples=nc).cuda()
-        net.load_state_dict({k: torch.from_numpy(v) for k, v in W.nerf_state_dict(0).items()})
+        net = make_nerf(precision, num_coarse_samples=nc)
         c2w = torch.from_numpy(g[f"{tag}_c2w"])
         rays = frame_rays(c2w, H, Wd, float(g[f"{tag}_focal"]))
         out = render_rays(net, rays, chunk, True, 2.0, 6.0)
@@ -248,16 +253,14 @@ def test_render_frame_chunks(golden, nerf):
         np.testing.assert_array_equal(npy(full[:, :3]), npy(out["comp_rgb"]))
 
 
-def test_psnr_delta(golden, nerf):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_psnr_delta(golden, precision):
     """PSNR of the GPU render vs the reference render, both against one synthetic target."""
     g = golden("render_frame.npz")
     from aonerf.render import render_frame
 
     H, Wd = (int(x) for x in g["c1_hw"][:2])
-    from aonerf.model import NeRF
-
-    net = NeRF(num_coarse_samples=32).cuda()
-    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.nerf_state_dict(0).items()})
+    net = make_nerf(precision, num_coarse_samples=32)
     out = render_frame(net, torch.from_numpy(g["c1_c2w"]), H, Wd, float(g["c1_focal"]))
     target = torch.from_numpy(np.random.Generator(np.random.PCG64(3)).uniform(0, 1, (H * Wd, 3)).astype(np.float32))
     p_gpu = O.psnr_each([out[:, :3].cpu()], [target]).item()
