@@ -5,12 +5,14 @@ Tolerances (north star: <= 1e-4 abs on RGB/depth/weights vs the reference on ide
 weights; PSNR within 0.05 dB):
   * stage-isolated (each kernel fed the reference's own inputs): 1e-6 for ray generation,
     pos_enc and compositing, 1e-5 for the MLP raw outputs (fp32 MFMA re-association only);
-  * end-to-end two-level render: 1e-4 abs on rgb/acc/depth/weights for >= 99% of rays (>= 98%
-    for depth), worst ray <= 5e-3, PSNR delta <= 0.05 dB.  The fine level moves by
-    delta-cdf / pdf: any fp32 re-association of the MLP GEMMs -- even
-    the reference itself with an fp64 GEMM -- lands up to ~1e-4 away on depth
-    (tests/test_oracle_envelope.py measures that envelope), so the last-percent outliers are a
-    property of the reference's arithmetic, not of the kernels.
+  * end-to-end two-level render: every ray within 1e-4 abs on rgb/acc/depth/weights, EXCEPT
+    where the reference itself moves by at least a quarter of the error under a pure
+    re-association of its fp32 GEMMs (per-ray envelope `env_*` recorded in the fixtures by
+    make_golden.py: max over an fp64 GEMM and a split-K GEMM), and >= 98% of rays within 1e-4
+    outright; PSNR delta <= 0.05 dB.  The fine level re-samples along the coarse CDF, so an ulp
+    in the coarse MLP moves fine samples by delta-cdf / pdf: the
+    reference's own envelope reaches 5.6e-3 on acc and 2.6e-2 on depth for a few rays of the
+    64x64 / 32-sample frame.
 """
 import numpy as np
 import pytest
@@ -22,14 +24,18 @@ from oracle import weights as W
 pytestmark = pytest.mark.gpu
 
 E2E_ATOL = 1e-4
-E2E_MIN_FRAC = {"rgb": 0.99, "acc": 0.99, "weights": 0.99, "depth": 0.98, "comp_rgb": 0.99}
-E2E_MAX = 5e-3
+E2E_MIN_FRAC = 0.98
+ENV_FACTOR = 4.0
 
 
-def assert_e2e(name, err, key):
-    frac = (err <= E2E_ATOL).mean() if err.ndim == 1 else (err <= E2E_ATOL).all(axis=-1).mean()
-    assert frac >= E2E_MIN_FRAC[key], f"{name}: only {frac * 100:.2f}% of rays within {E2E_ATOL}"
-    assert err.max() <= E2E_MAX, f"{name}: worst ray {err.max():.3e}"
+def assert_e2e(name, err, env):
+    """err, env: per-ray (or per-ray-sample) |gpu - ref| and the reference's own envelope."""
+    ok = (err <= E2E_ATOL) | (err <= ENV_FACTOR * env)
+    bad = np.argwhere(~ok)
+    assert ok.all(), (f"{name}: {len(bad)} entries outside max(1e-4, {ENV_FACTOR} x reference "
+                      f"envelope), e.g. {bad[:3].tolist()} err={err[~ok][:3]} env={env[~ok][:3]}")
+    frac = (err <= E2E_ATOL).mean()
+    assert frac >= E2E_MIN_FRAC, f"{name}: only {frac * 100:.2f}% within {E2E_ATOL}"
 
 
 def cuda(a):
@@ -217,7 +223,7 @@ def check_levels(ret, g):
             if name == "coarse":  # no resampling upstream: every ray within 1e-4
                 assert err.max() <= E2E_ATOL, f"coarse {k}: {err.max():.3e}"
             else:
-                assert_e2e(f"fine {k}", err, k)
+                assert_e2e(f"fine {k}", err, g[f"env_fine_{k}"])
 
 
 def test_forward_eval_end_to_end(golden, nerf):
@@ -248,7 +254,7 @@ def test_render_frame_chunks(golden, precision):
         out = render_rays(net, rays, chunk, True, 2.0, 6.0)
         for k in ("comp_rgb", "acc", "depth"):
             err = report(f"frame {tag} {k}", npy(out[k]), g[f"{tag}_{k}"], E2E_ATOL)
-            assert_e2e(f"frame {tag} {k}", err, k)
+            assert_e2e(f"frame {tag} {k}", err, g[f"{tag}_env_{k}"])
         full = render_frame(net, c2w, H, Wd, float(g[f"{tag}_focal"]))
         np.testing.assert_array_equal(npy(full[:, :3]), npy(out["comp_rgb"]))
 
@@ -293,9 +299,27 @@ def test_full_frame_properties(nerf):
     dirs = O.get_ray_directions(H, Wd, f)
     ro, rv, rd = O.get_rays(dirs, c2w[:3, :4], True)
     params = O.split_state_dict(W.nerf_state_dict(0))
-    ref = O.nerf_forward(params, {"rays_o": ro[sel], "rays_d": rd[sel], "viewdirs": rv[sel]}, False, True,
-                         2.0, 6.0)[1]
+    sub = {"rays_o": ro[sel], "rays_d": rd[sel], "viewdirs": rv[sel]}
+    ref = O.nerf_forward(params, sub, False, True, 2.0, 6.0)[1]
+    env = oracle_envelope(params, sub)
     for j, k in ((0, "rgb"), (2, "depth"), (1, "acc")):
         got = o[sel][:, {0: slice(0, 3), 2: 3, 1: 4}[j]]
         err = report(f"640x480 subset {k}", got, ref[j].numpy(), E2E_ATOL)
-        assert_e2e(f"640x480 subset {k}", err, k)
+        assert_e2e(f"640x480 subset {k}", err, env[j])
+
+
+def oracle_envelope(params, rays):
+    """Per-ray envelope of the oracle under the GEMM re-associations of make_golden.py."""
+    from test_oracle_envelope import VARIANTS, mlp_with
+
+    base = O.nerf_forward(params, rays, False, True, 2.0, 6.0)[1]
+    env = [np.zeros_like(x.numpy()) for x in base]
+    orig = O.mlp_forward
+    try:
+        for fn in VARIANTS.values():
+            O.mlp_forward = mlp_with(fn)
+            out = O.nerf_forward(params, rays, False, True, 2.0, 6.0)[1]
+            env = [np.maximum(e, np.abs(a.numpy() - b.numpy())) for e, a, b in zip(env, out, base)]
+    finally:
+        O.mlp_forward = orig
+    return env
