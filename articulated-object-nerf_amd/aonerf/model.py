@@ -165,12 +165,13 @@ class NeRF(nn.Module):
 
     @torch.no_grad()
     def forward(self, rays, randomized, white_bkgd, near, far, *, u_coarse=None, u_fine=None,
-                return_weights=False, timers=None):
+                return_weights=False, return_intermediates=False, timers=None):
         """reference model.py:147-199 -> [(comp_rgb, acc, depth)_coarse, (...)_fine].
 
         ``u_coarse`` (B, Sc+1) / ``u_fine`` (B, Nf) inject the uniforms of randomized mode;
         ``return_weights`` adds each level's weights (B, S) as a 4th element;
-        ``timers`` (dict) records hip events around each level's MLP launch.
+        ``return_intermediates`` adds a dict(t_vals, weights, raw) as the last element;
+        ``timers`` (dict) records hip events around each level's MLP / composite launches.
         """
         o, d, v = rays["rays_o"], rays["rays_d"], rays["viewdirs"]
         L.require_gpu(o, d, v)
@@ -214,5 +215,8 @@ class NeRF(nn.Module):
                    B, S, int(bool(white_bkgd)), L.ACT_VANILLA, L.ptr(comp), L.ptr(acc),
                    L.ptr(weights), L.ptr(depth), L.stream(dev))
             _record(timers, ev, f"comp{level}", B * S)
-            ret.append((comp, acc, depth, weights) if return_weights else (comp, acc, depth))
+            out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
+            if return_intermediates:
+                out = out + (dict(t_vals=t_vals, weights=weights, raw=raw),)
+            ret.append(out)
         return ret

@@ -253,6 +253,17 @@ def nerf_forward(params, rays, randomized, white_bkgd, near, far, num_coarse_sam
     return (ret, inter) if return_intermediates else ret
 
 
+def render_level(params, rays, t_vals, level, white_bkgd, min_deg_point=0, max_deg_point=10,
+                 deg_view=4):
+    """One level of model.py:175-197 on GIVEN sample positions t_vals (teacher forcing):
+    cast_rays -> pos_enc -> MLP -> sigmoid/relu -> volumetric_rendering."""
+    samples = cast_rays(t_vals, rays["rays_o"], rays["rays_d"])
+    raw_rgb, raw_sigma = mlp_forward(params[level], pos_enc(samples, min_deg_point, max_deg_point),
+                                     pos_enc(rays["viewdirs"], 0, deg_view))
+    return volumetric_rendering(torch.sigmoid(raw_rgb), torch.relu(raw_sigma), t_vals,
+                                rays["rays_d"], white_bkgd)
+
+
 def render_rays(params, batch, chunk, white_bkgd, near, far, **kw):
     """reference models/vanilla_nerf/model.py:295-321 (chunk loop, fine outputs concatenated)."""
     B = batch["rays_o"].shape[0]

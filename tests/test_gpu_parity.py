@@ -5,14 +5,18 @@ Tolerances (north star: <= 1e-4 abs on RGB/depth/weights vs the reference on ide
 weights; PSNR within 0.05 dB):
   * stage-isolated (each kernel fed the reference's own inputs): 1e-6 for ray generation,
     pos_enc and compositing, 1e-5 for the MLP raw outputs (fp32 MFMA re-association only);
-  * end-to-end two-level render: every ray within 1e-4 abs on rgb/acc/depth/weights, EXCEPT
-    where the reference itself moves by at least a quarter of the error under a pure
-    re-association of its fp32 GEMMs (per-ray envelope `env_*` recorded in the fixtures by
-    make_golden.py: max over an fp64 GEMM and a split-K GEMM), and >= 98% of rays within 1e-4
-    outright; PSNR delta <= 0.05 dB.  The fine level re-samples along the coarse CDF, so an ulp
-    in the coarse MLP moves fine samples by delta-cdf / pdf: the
-    reference's own envelope reaches 5.6e-3 on acc and 2.6e-2 on depth for a few rays of the
-    64x64 / 32-sample frame.
+  * end-to-end two-level render, decomposed so that every link is gated at 1e-4 on EVERY ray:
+      (1) coarse level vs the reference: rgb/acc/depth/weights within 1e-4;
+      (2) fine sample positions == the reference's sample_pdf applied to OUR coarse weights,
+          bit for bit (the oracle's pdf is pinned bit-exactly to the reference);
+      (3) fine level vs the reference evaluated on OUR fine sample positions: within 1e-4;
+    and against the reference's own end-to-end outputs: >= 98% of rays within 1e-4, PSNR
+    delta <= 0.05 dB.  The remaining rays are the reference's own discontinuity: where coarse
+    weights are exactly 0 (ReLU'd density) the CDF has plateaus, and a coarse-weight change of
+    ~1e-7 can move a u across a plateau edge, shifting a fine sample by a whole bin (observed:
+    one ray of 480 moves 0.0625 in t and 6e-4 in rgb from a 1.8e-7 coarse-weight difference).
+    Any fp32 implementation with a different summation order shows the same (the reference
+    with an fp64 or split-K GEMM moves 2.6e-2 on depth on a 64x64 frame: `env_*` arrays).
 """
 import numpy as np
 import pytest
@@ -28,14 +32,44 @@ E2E_MIN_FRAC = 0.98
 ENV_FACTOR = 4.0
 
 
-def assert_e2e(name, err, env):
-    """err, env: per-ray (or per-ray-sample) |gpu - ref| and the reference's own envelope."""
-    ok = (err <= E2E_ATOL) | (err <= ENV_FACTOR * env)
-    bad = np.argwhere(~ok)
-    assert ok.all(), (f"{name}: {len(bad)} entries outside max(1e-4, {ENV_FACTOR} x reference "
-                      f"envelope), e.g. {bad[:3].tolist()} err={err[~ok][:3]} env={env[~ok][:3]}")
+def assert_e2e(name, err, env=None):
+    """Direct comparison with the reference's end-to-end output: >= 98% of entries within 1e-4
+    (the rest: CDF-plateau flips, see the module docstring; `env` reported for context)."""
     frac = (err <= E2E_ATOL).mean()
+    if frac < 1 and env is not None:
+        bad = err > E2E_ATOL
+        print(f"  {name}: {bad.sum()} entries > 1e-4 (reference re-association envelope there: "
+              f"max {env[bad].max():.2e})")
     assert frac >= E2E_MIN_FRAC, f"{name}: only {frac * 100:.2f}% within {E2E_ATOL}"
+
+
+def check_chain(net, rays, params, randomized=False, white=True, u_coarse=None, u_fine=None,
+                coarse_ref=None):
+    """Links (1)-(3) of the module docstring on one batch; returns the GPU outputs."""
+    ret = net(rays, randomized, white, 2.0, 6.0, u_coarse=u_coarse, u_fine=u_fine,
+              return_weights=True, return_intermediates=True)
+    rc = {k: v.cpu() for k, v in rays.items()}
+    # (1) coarse level
+    if coarse_ref is None:
+        t_c = ret[0][4]["t_vals"].cpu()
+        coarse_ref = O.render_level(params, rc, t_c, 0, white)
+        coarse_ref = (coarse_ref[0], coarse_ref[1], coarse_ref[3], coarse_ref[2])
+    for j, k in enumerate(("rgb", "acc", "depth", "weights")):
+        err = report(f"chain coarse {k}", npy(ret[0][j]), np.asarray(coarse_ref[j]), E2E_ATOL)
+        assert err.max() <= E2E_ATOL, f"coarse {k}: {err.max():.3e}"
+    # (2) fine sample positions = reference sampling on our coarse weights
+    t_c, w_c = ret[0][4]["t_vals"].cpu(), ret[0][3].cpu()
+    t_f, _ = O.sample_pdf(0.5 * (t_c[..., 1:] + t_c[..., :-1]), w_c[..., 1:-1], rc["rays_o"],
+                          rc["rays_d"], t_c, net.num_fine_samples, randomized,
+                          u=None if u_fine is None else u_fine.cpu())
+    np.testing.assert_array_equal(npy(ret[1][4]["t_vals"]), t_f.numpy())
+    # (3) fine level vs the reference on those positions
+    fine = O.render_level(params, rc, t_f, 1, white)
+    for j, k in ((0, "rgb"), (1, "acc"), (3, "depth"), (2, "weights")):
+        jj = {"rgb": 0, "acc": 1, "depth": 2, "weights": 3}[k]
+        err = report(f"chain fine {k}", npy(ret[1][jj]), fine[j].numpy(), E2E_ATOL)
+        assert err.max() <= E2E_ATOL, f"fine {k}: {err.max():.3e}"
+    return ret
 
 
 def cuda(a):
@@ -226,16 +260,22 @@ def check_levels(ret, g):
                 assert_e2e(f"fine {k}", err, g[f"env_fine_{k}"])
 
 
+def golden_coarse(g):
+    return tuple(g[f"coarse_{k}"] for k in ("rgb", "acc", "depth", "weights"))
+
+
 def test_forward_eval_end_to_end(golden, nerf):
     g = golden("forward_eval.npz")
-    ret = nerf(rays_of(g), False, True, 2.0, 6.0, return_weights=True)
+    params = O.split_state_dict(W.nerf_state_dict(0))
+    ret = check_chain(nerf, rays_of(g), params, coarse_ref=golden_coarse(g))
     check_levels(ret, g)
 
 
 def test_forward_randomized_end_to_end(golden, nerf):
     g = golden("forward_random.npz")
-    ret = nerf(rays_of(g), True, False, 2.0, 6.0, u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]),
-               return_weights=True)
+    params = O.split_state_dict(W.nerf_state_dict(0))
+    ret = check_chain(nerf, rays_of(g), params, randomized=True, white=False,
+                      u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]), coarse_ref=golden_coarse(g))
     check_levels(ret, g)
 
 
@@ -246,11 +286,13 @@ def test_render_frame_chunks(golden, precision):
     from aonerf.ray_utils import frame_rays
 
     g = golden("render_frame.npz")
+    params = O.split_state_dict(W.nerf_state_dict(0))
     for tag in ("a", "c1"):
         H, Wd, nc, chunk = (int(x) for x in g[f"{tag}_hw"])
         net = make_nerf(precision, num_coarse_samples=nc)
         c2w = torch.from_numpy(g[f"{tag}_c2w"])
         rays = frame_rays(c2w, H, Wd, float(g[f"{tag}_focal"]))
+        check_chain(net, rays, params)
         out = render_rays(net, rays, chunk, True, 2.0, 6.0)
         for k in ("comp_rgb", "acc", "depth"):
             err = report(f"frame {tag} {k}", npy(out[k]), g[f"{tag}_{k}"], E2E_ATOL)
@@ -306,6 +348,13 @@ def test_full_frame_properties(nerf):
         got = o[sel][:, {0: slice(0, 3), 2: 3, 1: 4}[j]]
         err = report(f"640x480 subset {k}", got, ref[j].numpy(), E2E_ATOL)
         assert_e2e(f"640x480 subset {k}", err, env[j])
+    # every link gated at 1e-4 on the same subset, through the GPU's own rays
+    from aonerf.ray_utils import frame_rays
+
+    gr = frame_rays(c2w, H, Wd, f)
+    sel_t = torch.from_numpy(sel).cuda()
+    got_sub = check_chain(nerf, {k: v[sel_t].contiguous() for k, v in gr.items()}, params)
+    np.testing.assert_array_equal(npy(got_sub[1][0]), o[sel][:, :3])
 
 
 def oracle_envelope(params, rays):
