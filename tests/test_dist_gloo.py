@@ -1,0 +1,81 @@
+"""Multi-process (world_size 2, gloo on CPU) checks of the row-band sharding and the frame gather
+used by bench.py on N GPUs (aonerf/parallel.py).  The GPU render is replaced by a payload that
+encodes the pixel index, so the test checks exactly the partition + gather + re-assembly."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from aonerf.parallel import assemble, band, gather_frame
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def fake_payload(H, W, rank, world):
+    p0, n, n_max = band(H, W, rank, world)
+    out = torch.zeros((n_max, 5))
+    pix = torch.arange(p0, p0 + n, dtype=torch.float32)
+    out[:n, 0] = pix
+    out[:n, 1] = pix // W
+    out[:n, 2] = pix % W
+    out[:n, 3] = rank
+    out[:n, 4] = 1.0
+    return out
+
+
+def _worker(rank, world, port, H, W, q):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        frame = gather_frame(fake_payload(H, W, rank, world), H, W, dst=0)
+        if rank == 0:
+            q.put(frame)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("H,W", [(480, 640), (7, 5), (3, 4)])
+def test_band_partition_covers_frame(H, W):
+    for world in (1, 2, 3, 4, 8):
+        covered = []
+        for r in range(world):
+            p0, n, n_max = band(H, W, r, world)
+            assert 0 <= n <= n_max and p0 % W == 0
+            covered.extend(range(p0, p0 + n))
+        assert covered == list(range(H * W))
+
+
+def test_assemble_single_process():
+    H, W, world = 9, 4, 4
+    parts = [fake_payload(H, W, r, world) for r in range(world)]
+    frame = assemble(parts, H, W)
+    assert torch.equal(frame[:, 0], torch.arange(H * W, dtype=torch.float32))
+
+
+@pytest.mark.parametrize("H,W", [(48, 64), (7, 5)])
+def test_gather_frame_gloo_world2(H, W):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert frame.shape == (H * W, 5)
+    assert torch.equal(frame[:, 0], torch.arange(H * W, dtype=torch.float32))
+    assert torch.equal(frame[:, 1] * W + frame[:, 2], frame[:, 0])
+    assert torch.all(frame[:, 4] == 1.0)
+    # rank r rendered rows [r * ceil(H/2), ...)
+    rows = -(-H // world)
+    assert torch.equal(frame[:, 3], (frame[:, 1] // rows).float())
