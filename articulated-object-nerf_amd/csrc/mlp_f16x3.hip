@@ -45,8 +45,8 @@ struct Frag {
 };
 
 // one layer with U >= 2 output tiles: out = act(W . [a ; b] + bias) as next-layer fragments
-template <int LAYER, bool RELU, int THREADS, int NCOL, int NA, int NB, int NO>
-__device__ __forceinline__ void layer_h(Pipe<THREADS>& p, const Frag<NA, NCOL>& a,
+template <int LAYER, bool RELU, typename P, int NCOL, int NA, int NB, int NO>
+__device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
                                         const Frag<NB, NCOL>& b, Frag<NO, NCOL>& out,
                                         const float* bias_s, int g) {
   constexpr LayerDesc d = kLayersH[LAYER];
@@ -98,8 +98,8 @@ __device__ __forceinline__ void layer_h(Pipe<THREADS>& p, const Frag<NA, NCOL>& 
 }
 
 // single-tile head (density / rgb): returns the 16-row tile at activation scale
-template <int LAYER, int THREADS, int NCOL, int NA>
-__device__ __forceinline__ void head_h(Pipe<THREADS>& p, const Frag<NA, NCOL>& a, f4 (&res)[NCOL],
+template <int LAYER, typename P, int NCOL, int NA>
+__device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[NCOL],
                                        const float* bias_s, int g) {
   constexpr LayerDesc d = kLayersH[LAYER];
   static_assert(d.u == 1 && d.kb == 0 && d.ka <= NA, "head shape");
@@ -128,6 +128,8 @@ __device__ __forceinline__ void head_h(Pipe<THREADS>& p, const Frag<NA, NCOL>& a
     for (int r = 0; r < 4; ++r) res[c][r] = fmaf(xx[c][r], 1.0f / kLoScale, hh[c][r]);
 }
 
+constexpr int kRing = 4;  // LDS-DMA ring depth (chunks); 3 chunks of weights in flight
+
 template <int NCOL>
 struct GeomH {
   static constexpr int kWaves = NCOL == 1 ? 8 : 4;
@@ -143,19 +145,20 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
     int64_t B, int S, float* __restrict__ raw) {
   using G = GeomH<NCOL>;
-  __shared__ f4 wbuf[2 * kChunk * 64];
-  __shared__ __attribute__((aligned(16))) float bias_s[kBiasFloats];
+  // ONE __shared__ object: weight ring + bias table (see DmaPipe)
+  __shared__ f4 smem[kRing * kChunk * 64 + kBiasFloats / 4];
+  float* bias_s = reinterpret_cast<float*>(smem + kRing * kChunk * 64);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, j = lane & 15;
   const int64_t N = B * S;
 
-  Pipe<G::kThreads> p;
-  p.wbuf = wbuf;
+  DmaPipe<G::kThreads, kRing> p;
+  p.wbuf = smem;
   p.src = wstream;
   p.tid = tid;
   p.lane = lane;
-  p.load(0);
+  p.start();
   for (int i = tid; i < kBiasFloats; i += G::kThreads) bias_s[i] = bias_g[i];
 
   // layer-0 (enc) and view-layer (enc_dir) fragments: k-step k, lane group g, element e

@@ -40,3 +40,79 @@ struct Pipe {
 
 }  // namespace mlp
 }  // namespace aon
+
+namespace aon {
+namespace mlp {
+
+// s_waitcnt vmcnt(n) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | [15:14], expcnt[6:4], lgkmcnt[11:8]).
+// The builtin wants a literal: after unrolling n is a constant and the switch folds to one case.
+#define AON_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4))
+__device__ __forceinline__ void wait_vm_lgkm0(int n) {
+  switch (n) {
+    case 0: AON_WAIT_VM(0); break;
+    case 1: AON_WAIT_VM(1); break;
+    case 2: AON_WAIT_VM(2); break;
+    case 3: AON_WAIT_VM(3); break;
+    case 4: AON_WAIT_VM(4); break;
+    case 5: AON_WAIT_VM(5); break;
+    case 6: AON_WAIT_VM(6); break;
+    case 7: AON_WAIT_VM(7); break;
+    case 8: AON_WAIT_VM(8); break;
+    case 9: AON_WAIT_VM(9); break;
+    case 10: AON_WAIT_VM(10); break;
+    case 11: AON_WAIT_VM(11); break;
+    case 12: AON_WAIT_VM(12); break;
+    case 13: AON_WAIT_VM(13); break;
+    case 14: AON_WAIT_VM(14); break;
+    default: AON_WAIT_VM(15); break;
+  }
+}
+#undef AON_WAIT_VM
+
+// LDS-DMA ring: chunk c is copied HBM/L2 -> LDS buffer c % NBUF by global_load_lds (16 B per
+// lane, no VGPR staging), NBUF - 1 chunks ahead of its first use.  At the first use of chunk c
+// every wave waits until its own copies of chunk c have landed (counted vmcnt: the copies of the
+// chunks after c stay in flight), drains its LDS reads, and joins one workgroup barrier; then
+// the buffer of chunk c - 1 (fully read: every wave is past its last use) is refilled with
+// chunk c + NBUF - 1.  All LDS of the kernel lives in ONE __shared__ array (a second object can
+// make hipcc drain vmcnt before every ds_read, cdna_hip_programming.md section 5 item 4a).
+template <int THREADS, int NBUF>
+struct DmaPipe {
+  static constexpr int kCopies = kChunk * 64 / THREADS;  // 16-B copies per thread per chunk
+  static_assert(kCopies * THREADS == kChunk * 64, "chunk must split evenly over threads");
+  static_assert(NBUF >= 2, "ring needs two buffers");
+  f4* wbuf;  // [NBUF][kChunk * 64] f4
+  const f4* __restrict__ src;
+  int tid, lane;
+
+  __device__ __forceinline__ void issue(int c) {
+    f4* dst = wbuf + (c % NBUF) * kChunk * 64;
+#pragma unroll
+    for (int i = 0; i < kCopies; ++i) {
+      const int e = i * THREADS + tid;  // 16-B element of the chunk; LDS dst is lane-linear
+      __builtin_amdgcn_global_load_lds(
+          reinterpret_cast<const void*>(src + (size_t)c * kChunk * 64 + e),
+          reinterpret_cast<__attribute__((address_space(3))) void*>(
+              reinterpret_cast<uintptr_t>(dst + e - lane)),
+          16, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void start() {
+#pragma unroll
+    for (int c = 0; c < NBUF - 1 && c < kNumChunks; ++c) issue(c);
+  }
+  __device__ __forceinline__ void begin(int c) {
+    // copies issued after chunk c's: chunks c+1 .. min(c+NBUF-2, last)
+    const int ahead = (c + NBUF - 2 < kNumChunks - 1 ? c + NBUF - 2 : kNumChunks - 1) - c;
+    static_assert((NBUF - 2) * kCopies <= 15, "vmcnt budget");
+    wait_vm_lgkm0(ahead * kCopies);
+    __builtin_amdgcn_s_barrier();
+    if (c + NBUF - 1 < kNumChunks) issue(c + NBUF - 1);
+  }
+  __device__ __forceinline__ f4 block(int b) const {
+    return wbuf[((b / kChunk) % NBUF) * kChunk * 64 + (b % kChunk) * 64 + lane];
+  }
+};
+
+}  // namespace mlp
+}  // namespace aon
