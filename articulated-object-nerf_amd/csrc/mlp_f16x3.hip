@@ -39,6 +39,48 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
   }
 }
 
+// One-step-ahead fragment prefetch over the weight stream: blocks are consumed strictly in
+// stream order (2 per (u, k-step)), so the step after block b is always b + 2.  The hi/lo pair
+// of the NEXT step is read from LDS before the MFMAs of the current step are issued, hiding the
+// LDS latency behind 3*NCOL MFMAs (hipcc issues ds_read -> lgkmcnt(0) -> MFMA otherwise).
+#ifndef AON_SCHED_MASK
+#define AON_SCHED_MASK 0
+#endif
+
+#ifndef AON_PREFETCH
+#define AON_PREFETCH 2
+#endif
+
+template <typename P, int D = AON_PREFETCH>
+struct FragPipe {
+  P& p;
+  f4 nh[D], nl[D];  // fragments of the next D steps
+  __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
+  __device__ __forceinline__ void fetch_into(int blk, f4& h, f4& l) {
+    if (blk >= kBlocks) return;
+    if (blk % kChunk == 0) p.begin(blk / kChunk);
+    h = p.block(blk);
+    l = p.block(blk + 1);
+  }
+  __device__ __forceinline__ void start() {
+#pragma unroll
+    for (int i = 0; i < D; ++i) fetch_into(2 * i, nh[i], nl[i]);
+  }
+  // fragments of block pair `blk` (fetched D steps earlier); prefetches blk + 2D
+  __device__ __forceinline__ void take(int blk, h8& wh, h8& wl) {
+    wh = as_h8(nh[0]);
+    wl = as_h8(nl[0]);
+#pragma unroll
+    for (int i = 0; i + 1 < D; ++i) {
+      nh[i] = nh[i + 1];
+      nl[i] = nl[i + 1];
+    }
+    fetch_into(blk + 2 * D, nh[D - 1], nl[D - 1]);
+    // keep the prefetch reads above this step's MFMAs (hipcc otherwise sinks them to their use)
+    __builtin_amdgcn_sched_barrier(AON_SCHED_MASK);
+  }
+};
+
 template <int N, int NCOL>
 struct Frag {
   h8 hi[N][NCOL], lo[N][NCOL];
@@ -69,8 +111,8 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
 #pragma unroll
       for (int uu = 0; uu < 2; ++uu) {
         const int blk = d.blk0 + 2 * ((pr * K + k) * 2 + uu);
-        if (blk % kChunk == 0 && blk > 0) p.begin(blk / kChunk);
-        const h8 wh = as_h8(p.block(blk)), wl = as_h8(p.block(blk + 1));
+        h8 wh, wl;
+        p.take(blk, wh, wl);
 #pragma unroll
         for (int c = 0; c < NCOL; ++c) {
           const int ia = k < NA ? k : 0, ib = (k >= d.ka && k - d.ka < NB) ? k - d.ka : 0;
@@ -113,8 +155,8 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
 #pragma unroll
   for (int k = 0; k < d.ka; ++k) {
     const int blk = d.blk0 + 2 * k;
-    if (blk % kChunk == 0 && blk > 0) p.begin(blk / kChunk);
-    const h8 wh = as_h8(p.block(blk)), wl = as_h8(p.block(blk + 1));
+    h8 wh, wl;
+    p.take(blk, wh, wl);
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
       hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
@@ -145,9 +187,12 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
     int64_t B, int S, float* __restrict__ raw) {
   using G = GeomH<NCOL>;
-  // ONE __shared__ object: weight ring + bias table (see DmaPipe)
-  __shared__ f4 smem[kRing * kChunk * 64 + kBiasFloats / 4];
+  // ONE __shared__ object: weight ring | bias table | per-lane stash of the encodings
+  constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
+  __shared__ f4 smem[kRing * kChunk * 64 + kBiasFloats / 4 + kStash];
   float* bias_s = reinterpret_cast<float*>(smem + kRing * kChunk * 64);
+  f4* stash = smem + kRing * kChunk * 64 + kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 6 * NCOL +
+              (threadIdx.x & 63);  // lane-private slots: written and read by the same lane
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, j = lane & 15;
@@ -214,23 +259,49 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     split8(vv, venc.hi[0][c], venc.lo[0][c]);
   }
 
-  p.begin(0);  // also publishes bias_s
+  // park the encodings in LDS until the skip / view layers need them (frees 24 VGPRs for the
+  // fragment prefetch); only the owning lane ever touches its slots
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      stash[64 * (6 * c + 2 * k)] = __builtin_bit_cast(f4, enc.hi[k][c]);
+      stash[64 * (6 * c + 2 * k + 1)] = __builtin_bit_cast(f4, enc.lo[k][c]);
+    }
+    stash[64 * (6 * c + 4)] = __builtin_bit_cast(f4, venc.hi[0][c]);
+    stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
+  }
+
+  FragPipe<DmaPipe<G::kThreads, kRing>> fp(p);
+  fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
 
   Frag<8, NCOL> x, y;
   Frag<1, NCOL> none;
-  layer_h<L0, true>(p, none, enc, x, bias_s, g);
-  layer_h<L1, true>(p, x, none, y, bias_s, g);
-  layer_h<L2, true>(p, y, none, x, bias_s, g);
-  layer_h<L3, true>(p, x, none, y, bias_s, g);
-  layer_h<L4, true>(p, y, none, x, bias_s, g);
-  layer_h<L5, true>(p, x, enc, y, bias_s, g);  // skip: cat[h, enc] (model.py:102-103)
-  layer_h<L6, true>(p, y, none, x, bias_s, g);
-  layer_h<L7, true>(p, x, none, y, bias_s, g);
+  layer_h<L0, true>(fp, none, enc, x, bias_s, g);
+  layer_h<L1, true>(fp, x, none, y, bias_s, g);
+  layer_h<L2, true>(fp, y, none, x, bias_s, g);
+  layer_h<L3, true>(fp, x, none, y, bias_s, g);
+  layer_h<L4, true>(fp, y, none, x, bias_s, g);
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
+      enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
+    }
+  layer_h<L5, true>(fp, x, enc, y, bias_s, g);  // skip: cat[h, enc] (model.py:102-103)
+  layer_h<L6, true>(fp, y, none, x, bias_s, g);
+  layer_h<L7, true>(fp, x, none, y, bias_s, g);
   f4 dens[NCOL], rgb[NCOL];
-  head_h<LDEN>(p, y, dens, bias_s, g);             // model.py:105-107
-  layer_h<LBOT, false>(p, y, none, x, bias_s, g);  // bottleneck, no activation (model.py:109)
-  layer_h<LVIEW, true>(p, x, venc, y, bias_s, g);  // cat[bottleneck, enc_dir] + ReLU (:110-116)
-  head_h<LRGB>(p, y, rgb, bias_s, g);              // model.py:118
+  head_h<LDEN>(fp, y, dens, bias_s, g);             // model.py:105-107
+  layer_h<LBOT, false>(fp, y, none, x, bias_s, g);  // bottleneck, no activation (model.py:109)
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
+    venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
+  }
+  layer_h<LVIEW, true>(fp, x, venc, y, bias_s, g);  // cat[bottleneck, enc_dir] + ReLU (:110-116)
+  head_h<LRGB>(fp, y, rgb, bias_s, g);              // model.py:118
 
   if (g == 0) {
 #pragma unroll
