@@ -58,7 +58,7 @@ struct FragPipe {
   __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
   __device__ __forceinline__ void fetch_into(int blk, f4& h, f4& l) {
     if (blk >= kBlocks) return;
-    if (blk % kChunk == 0) p.begin(blk / kChunk);
+    if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
     h = p.block(blk);
     l = p.block(blk + 1);
   }
@@ -170,7 +170,14 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
     for (int r = 0; r < 4; ++r) res[c][r] = fmaf(xx[c][r], 1.0f / kLoScale, hh[c][r]);
 }
 
-constexpr int kRing = 4;  // LDS-DMA ring depth (chunks); 3 chunks of weights in flight
+#ifndef AON_RING
+#define AON_RING 3
+#endif
+#ifndef AON_CHUNK_H
+#define AON_CHUNK_H 32
+#endif
+constexpr int kRing = AON_RING;      // LDS-DMA ring depth (chunks in LDS)
+constexpr int kChunkH = AON_CHUNK_H;  // 1-KB blocks per chunk
 
 template <int NCOL>
 struct GeomH {
@@ -189,16 +196,16 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   using G = GeomH<NCOL>;
   // ONE __shared__ object: weight ring | bias table | per-lane stash of the encodings
   constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
-  __shared__ f4 smem[kRing * kChunk * 64 + kBiasFloats / 4 + kStash];
-  float* bias_s = reinterpret_cast<float*>(smem + kRing * kChunk * 64);
-  f4* stash = smem + kRing * kChunk * 64 + kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 6 * NCOL +
+  __shared__ f4 smem[kRing * kChunkH * 64 + kBiasFloats / 4 + kStash];
+  float* bias_s = reinterpret_cast<float*>(smem + kRing * kChunkH * 64);
+  f4* stash = smem + kRing * kChunkH * 64 + kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 6 * NCOL +
               (threadIdx.x & 63);  // lane-private slots: written and read by the same lane
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, j = lane & 15;
   const int64_t N = B * S;
 
-  DmaPipe<G::kThreads, kRing> p;
+  DmaPipe<G::kThreads, kRing, kChunkH> p;
   p.wbuf = smem;
   p.src = wstream;
   p.tid = tid;
@@ -272,7 +279,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
 
-  FragPipe<DmaPipe<G::kThreads, kRing>> fp(p);
+  FragPipe<DmaPipe<G::kThreads, kRing, kChunkH>> fp(p);
   fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
 
   Frag<8, NCOL> x, y;

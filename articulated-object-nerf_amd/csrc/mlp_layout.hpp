@@ -69,8 +69,8 @@ constexpr float kActScale = 1.0f / 256.0f;
 constexpr float kLoScale = 2048.0f;
 
 constexpr int kBlocks = 2344;                                     // sum of (ka+kb)*u
-constexpr int kStreamBlocks = (kBlocks + kChunk - 1) / kChunk * kChunk;  // 2352
-constexpr int kNumChunks = kStreamBlocks / kChunk;                // 147
+constexpr int kStreamBlocks = (kBlocks + 63) / 64 * 64;          // 2368: whole chunks of 16/32/64
+constexpr int kNumChunks = kStreamBlocks / kChunk;                // 148
 constexpr int kBiasFloats = 2464;
 constexpr size_t kStreamBytesF32 = (size_t)kStreamBlocks * 1024;
 constexpr size_t kPackedBytesF32 = kStreamBytesF32 + kBiasFloats * 4;

@@ -76,8 +76,11 @@ __device__ __forceinline__ void wait_vm_lgkm0(int n) {
 // the buffer of chunk c - 1 (fully read: every wave is past its last use) is refilled with
 // chunk c + NBUF - 1.  All LDS of the kernel lives in ONE __shared__ array (a second object can
 // make hipcc drain vmcnt before every ds_read, cdna_hip_programming.md section 5 item 4a).
-template <int THREADS, int NBUF>
+template <int THREADS, int NBUF, int CHUNK>
 struct DmaPipe {
+  static constexpr int kChunk = CHUNK;  // 1-KB blocks per chunk (shadows the fp32 pipe's)
+  static constexpr int kNumChunks = kStreamBlocks / CHUNK;
+  static_assert(kNumChunks * CHUNK == kStreamBlocks, "stream must be whole chunks");
   static constexpr int kCopies = kChunk * 64 / THREADS;  // 16-B copies per thread per chunk
   static_assert(kCopies * THREADS == kChunk * 64, "chunk must split evenly over threads");
   static_assert(NBUF >= 2, "ring needs two buffers");
