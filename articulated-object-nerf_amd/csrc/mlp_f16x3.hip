@@ -86,16 +86,38 @@ struct Frag {
   h8 hi[N][NCOL], lo[N][NCOL];
 };
 
-// one layer with U >= 2 output tiles: out = act(W . [a ; b] + bias) as next-layer fragments
+// epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
+// part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
+template <bool RELU, int NCOL, int NO>
+__device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
+                                         Frag<NO, NCOL>& out, int pr) {
+  const int uu = q >> 1, r0 = (q & 1) * 2;
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float v = fmaf(xx[uu][c][r0 + e], 1.0f / kLoScale, hh[uu][c][r0 + e]);
+      if (RELU) v = fmaxf(v, 0.0f);
+      const _Float16 h = static_cast<_Float16>(v);
+      out.hi[pr][c][2 * q + e] = h;
+      out.lo[pr][c][2 * q + e] = static_cast<_Float16>(__fmul_rn(__fsub_rn(v, static_cast<float>(h)), kLoScale));
+    }
+  }
+}
+
+// one layer with U >= 2 output tiles: out = act(W . [a ; b] + bias) as next-layer fragments.
+// Pair p's epilogue is spread over the first k-steps of pair p+1 (compute[cur] || finish[prev]).
 template <int LAYER, bool RELU, typename P, int NCOL, int NA, int NB, int NO>
 __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
                                         const Frag<NB, NCOL>& b, Frag<NO, NCOL>& out,
                                         const float* bias_s, int g) {
   constexpr LayerDesc d = kLayersH[LAYER];
   constexpr int K = d.ka + d.kb;
-  static_assert(d.u % 2 == 0 && d.u / 2 <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
+  constexpr int NP = d.u / 2;
+  static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
+  f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
 #pragma unroll
-  for (int pr = 0; pr < d.u / 2; ++pr) {
+  for (int pr = 0; pr < NP; ++pr) {
     f4 hh[2][NCOL], xx[2][NCOL];
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
@@ -123,20 +145,22 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
           xx[uu][c] = mfma16(wl, xh, xx[uu][c]);
         }
       }
+      if (pr > 0 && k < 4) epi_part<RELU>(k, phh, pxx, out, pr - 1);
+    }
+    if (pr > 0) {
+#pragma unroll
+      for (int q = K; q < 4; ++q) epi_part<RELU>(q, phh, pxx, out, pr - 1);
     }
 #pragma unroll
-    for (int c = 0; c < NCOL; ++c) {
-      float v[8];
+    for (int uu = 0; uu < 2; ++uu)
 #pragma unroll
-      for (int uu = 0; uu < 2; ++uu)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float y = fmaf(xx[uu][c][r], 1.0f / kLoScale, hh[uu][c][r]);
-          v[4 * uu + r] = RELU ? fmaxf(y, 0.0f) : y;
-        }
-      split8(v, out.hi[pr][c], out.lo[pr][c]);
-    }
+      for (int c = 0; c < NCOL; ++c) {
+        phh[uu][c] = hh[uu][c];
+        pxx[uu][c] = xx[uu][c];
+      }
   }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) epi_part<RELU>(q, phh, pxx, out, NP - 1);
 }
 
 // single-tile head (density / rgb): returns the 16-row tile at activation scale
