@@ -58,6 +58,12 @@ struct FragPipe {
   __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
   __device__ __forceinline__ void fetch_into(int blk, f4& h, f4& l) {
     if (blk >= kBlocks) return;
+#ifdef AON_ABLATE_LDS  // timing-only build: reuse the first fragments (no LDS reads, wrong results)
+    if (blk >= 2 * D) {
+      if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
+      return;
+    }
+#endif
     if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
     h = p.block(blk);
     l = p.block(blk + 1);
@@ -202,6 +208,18 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
 #endif
 constexpr int kRing = AON_RING;      // LDS-DMA ring depth (chunks in LDS)
 constexpr int kChunkH = AON_CHUNK_H;  // 1-KB blocks per chunk
+// Weight pipeline: the LDS-DMA ring, or (AON_PIPE_REG) the register-staged double buffer.
+// hipcc drains lgkmcnt to 0 before every LDS read while any global_load_lds is in flight, which
+// defeats the fragment prefetch; the register-staged pipe keeps precise lgkmcnt(N) waits.
+#ifdef AON_PIPE_REG
+template <int THREADS>
+using WeightPipe = Pipe<THREADS>;
+constexpr int kLdsWeights = 2 * kChunk * 64;  // f4
+#else
+template <int THREADS>
+using WeightPipe = DmaPipe<THREADS, kRing, kChunkH>;
+constexpr int kLdsWeights = kRing * kChunkH * 64;
+#endif
 
 template <int NCOL>
 struct GeomH {
@@ -220,16 +238,16 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   using G = GeomH<NCOL>;
   // ONE __shared__ object: weight ring | bias table | per-lane stash of the encodings
   constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
-  __shared__ f4 smem[kRing * kChunkH * 64 + kBiasFloats / 4 + kStash];
-  float* bias_s = reinterpret_cast<float*>(smem + kRing * kChunkH * 64);
-  f4* stash = smem + kRing * kChunkH * 64 + kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 6 * NCOL +
+  __shared__ f4 smem[kLdsWeights + kBiasFloats / 4 + kStash];
+  float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
+  f4* stash = smem + kLdsWeights + kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 6 * NCOL +
               (threadIdx.x & 63);  // lane-private slots: written and read by the same lane
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, j = lane & 15;
   const int64_t N = B * S;
 
-  DmaPipe<G::kThreads, kRing, kChunkH> p;
+  WeightPipe<G::kThreads> p;
   p.wbuf = smem;
   p.src = wstream;
   p.tid = tid;
@@ -303,7 +321,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
 
-  FragPipe<DmaPipe<G::kThreads, kRing, kChunkH>> fp(p);
+  FragPipe<WeightPipe<G::kThreads>> fp(p);
   fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
 
   Frag<8, NCOL> x, y;

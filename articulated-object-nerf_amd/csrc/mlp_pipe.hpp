@@ -14,6 +14,7 @@ namespace mlp {
 
 template <int THREADS>
 struct Pipe {
+  static constexpr int kChunk = mlp::kChunk;
   static constexpr int kStageRegs = kChunk * 64 / THREADS;  // f4 per thread per chunk
   static_assert(kStageRegs * THREADS == kChunk * 64, "chunk must split evenly over threads");
   f4* wbuf;  // [2][kChunk * 64] f4 in LDS
@@ -25,6 +26,7 @@ struct Pipe {
 #pragma unroll
     for (int i = 0; i < kStageRegs; ++i) stage[i] = src[(size_t)c * kChunk * 64 + tid + i * THREADS];
   }
+  __device__ __forceinline__ void start() { load(0); }
   // first use of chunk c: publish it to LDS, then prefetch chunk c + 1
   __device__ __forceinline__ void begin(int c) {
     f4* dst = wbuf + (c & 1) * kChunk * 64;
@@ -105,6 +107,9 @@ struct DmaPipe {
     for (int c = 0; c < NBUF - 1 && c < kNumChunks; ++c) issue(c);
   }
   __device__ __forceinline__ void begin(int c) {
+#ifdef AON_ABLATE_RING  // timing-only build: every chunk reads buffer 0 (wrong results)
+    if (c > 0) return;
+#endif
     // copies issued after chunk c's: chunks c+1 .. min(c+NBUF-2, last)
     const int ahead = (c + NBUF - 2 < kNumChunks - 1 ? c + NBUF - 2 : kNumChunks - 1) - c;
     static_assert((NBUF - 2) * kCopies <= 15, "vmcnt budget");
@@ -113,6 +118,9 @@ struct DmaPipe {
     if (c + NBUF - 1 < kNumChunks) issue(c + NBUF - 1);
   }
   __device__ __forceinline__ f4 block(int b) const {
+#ifdef AON_ABLATE_RING
+    return wbuf[(b % kChunk) * 64 + lane];
+#endif
     return wbuf[((b / kChunk) % NBUF) * kChunk * 64 + (b % kChunk) * 64 + lane];
   }
 };
