@@ -31,7 +31,7 @@ class NeRFMLP(nn.Module):
                  netwidth: int = 256, netdepth_condition: int = 1, netwidth_condition: int = 128,
                  skip_layer: int = 4, input_ch: int = 3, input_ch_view: int = 3,
                  num_rgb_channels: int = 3, num_density_channels: int = 1,
-                 precision: str = "fp32"):
+                 precision: str = "f16x3"):
         super().__init__()
         self.min_deg_point, self.max_deg_point, self.deg_view = min_deg_point, max_deg_point, deg_view
         self.netdepth, self.netwidth, self.skip_layer = netdepth, netwidth, skip_layer
@@ -146,7 +146,7 @@ class NeRF(nn.Module):
     def __init__(self, num_levels: int = 2, min_deg_point: int = 0, max_deg_point: int = 10,
                  deg_view: int = 4, num_coarse_samples: int = 64, num_fine_samples: int = 128,
                  use_viewdirs: bool = True, noise_std: float = 0.0, lindisp: bool = False,
-                 precision: str = "fp32"):
+                 precision: str = "f16x3"):
         super().__init__()
         if num_levels != 2:
             raise ValueError("the reference NeRF is two-level (coarse + fine)")
