@@ -36,8 +36,8 @@ _SIGNATURES = {
                                vp, vp, vp, vp, vp]),
     "aon_mlp_packed_bytes": (c_size, [c_int]),
     "aon_mlp_pack": (c_int, [ctypes.POINTER(AonMlpParams), c_int, vp, vp]),
-    "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, vp, vp]),
-    "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, vp, vp]),
+    "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
+    "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,
                                   vp, vp, vp, vp]),
 }
@@ -57,7 +57,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.aon_abi_version() != 1:
+        if handle.aon_abi_version() != 2:
             raise ImportError("aonerf: ABI version mismatch")
         _lib = handle
     return _lib

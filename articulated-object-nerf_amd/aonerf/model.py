@@ -4,8 +4,8 @@ Identical constructor keywords, forward signatures, return tuples and parameter 
 names, so a reference Lightning checkpoint (``model.coarse_mlp.pts_linears.0.weight`` ...)
 loads unchanged.  The forward pass runs on the fused HIP kernels:
 
-    level 0: aon_sample_along_rays (t only) -> aon_mlp_fwd (xyz + pos_enc + MLP fused)
-             -> aon_composite_fwd (sigmoid/relu + alpha compositing, weights kept)
+    level 0: aon_sample_along_rays (t only) -> aon_mlp_fwd (xyz + pos_enc + MLP + sigmoid/relu
+             fused) -> aon_composite_fwd (alpha compositing, weights kept)
     level 1: aon_sample_pdf (mids, pdf/cdf, inverse CDF, sort/merge) -> aon_mlp_fwd
              -> aon_composite_fwd
 
@@ -102,14 +102,15 @@ class NeRFMLP(nn.Module):
             self._packed, self._packed_key = buf, key
         return self._packed
 
-    def forward_rays(self, rays_o, rays_d, viewdirs, t_vals):
-        """Fused cast_rays + pos_enc + forward: raw (B*S, 4) = [raw_rgb, raw_sigma]."""
+    def forward_rays(self, rays_o, rays_d, viewdirs, t_vals, act=L.ACT_NONE):
+        """Fused cast_rays + pos_enc + forward: (B*S, 4) = [raw_rgb, raw_sigma]; with
+        ``act=L.ACT_VANILLA`` the rgb/sigma activations of model.py:186-187 are applied too."""
         L.require_gpu(rays_o, rays_d, viewdirs, t_vals)
         B, S = t_vals.shape
         raw = torch.empty((B * S, 4), device=t_vals.device)
         L.call("aon_mlp_fwd", L.ptr(self.packed_weights()), L.PREC[self.precision],
                L.ptr(L.contig(rays_o)), L.ptr(L.contig(rays_d)), L.ptr(L.contig(viewdirs)),
-               L.ptr(L.contig(t_vals)), B, S, L.ptr(raw), L.stream(t_vals.device))
+               L.ptr(L.contig(t_vals)), B, S, act, L.ptr(raw), L.stream(t_vals.device))
         return raw
 
     def forward(self, x, condition):
@@ -120,7 +121,8 @@ class NeRFMLP(nn.Module):
             raise ValueError("NeRFMLP.forward expects x (B, S, 63) and condition (B, 27)")
         raw = torch.empty((B * S, 4), device=x.device)
         L.call("aon_mlp_fwd_encoded", L.ptr(self.packed_weights()), L.PREC[self.precision],
-               L.ptr(L.contig(x)), L.ptr(L.contig(condition)), B, S, L.ptr(raw), L.stream(x.device))
+               L.ptr(L.contig(x)), L.ptr(L.contig(condition)), B, S, L.ACT_NONE, L.ptr(raw),
+               L.stream(x.device))
         raw = raw.view(B, S, 4)
         return raw[..., :3], raw[..., 3:]
 
@@ -170,7 +172,8 @@ class NeRF(nn.Module):
 
         ``u_coarse`` (B, Sc+1) / ``u_fine`` (B, Nf) inject the uniforms of randomized mode;
         ``return_weights`` adds each level's weights (B, S) as a 4th element;
-        ``return_intermediates`` adds a dict(t_vals, weights, raw) as the last element;
+        ``return_intermediates`` adds a dict(t_vals, weights, rgb_sigma) as the last element
+        (rgb_sigma (B*S, 4): the activated MLP outputs the compositor consumed);
         ``timers`` (dict) records hip events around each level's MLP / composite launches.
         """
         o, d, v = rays["rays_o"], rays["rays_d"], rays["viewdirs"]
@@ -201,10 +204,13 @@ class NeRF(nn.Module):
                 t_vals = t_new
                 mlp = self.fine_mlp
             S = t_vals.shape[1]
+            # the activations (model.py:186-187) run in the MLP epilogue, unless density noise
+            # must be added to the raw sigma first (model.py:183-184)
+            noisy = self.noise_std > 0 and randomized
             ev = _events(timers)
-            raw = mlp.forward_rays(o, d, v, t_vals)
+            raw = mlp.forward_rays(o, d, v, t_vals, act=L.ACT_NONE if noisy else L.ACT_VANILLA)
             _record(timers, ev, f"mlp{level}", B * S)
-            if self.noise_std > 0 and randomized:
+            if noisy:
                 raw[:, 3] += torch.rand_like(raw[:, 3]) * self.noise_std
             comp = torch.empty((B, 3), device=dev)
             acc = torch.empty((B,), device=dev)
@@ -212,11 +218,11 @@ class NeRF(nn.Module):
             depth = torch.empty((B,), device=dev)
             ev = _events(timers)
             L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
-                   B, S, int(bool(white_bkgd)), L.ACT_VANILLA, L.ptr(comp), L.ptr(acc),
-                   L.ptr(weights), L.ptr(depth), L.stream(dev))
+                   B, S, int(bool(white_bkgd)), L.ACT_VANILLA if noisy else L.ACT_NONE,
+                   L.ptr(comp), L.ptr(acc), L.ptr(weights), L.ptr(depth), L.stream(dev))
             _record(timers, ev, f"comp{level}", B * S)
             out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
             if return_intermediates:
-                out = out + (dict(t_vals=t_vals, weights=weights, raw=raw),)
+                out = out + (dict(t_vals=t_vals, weights=weights, rgb_sigma=raw),)
             ret.append(out)
         return ret

@@ -51,6 +51,22 @@ __device__ __forceinline__ float nan_to_num(float x, float nan_val) {
   return x;
 }
 
+// rgb_activation / sigma_activation (reference model.py:142-143, 186-187; articulated:
+// model_autodecoder.py:265, 323), shared by the MLP epilogue and the compositor
+__device__ __forceinline__ float act_rgb(float x, int act) {
+  if (act == AON_ACT_NONE) return x;
+  const float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-x)));
+  return act == AON_ACT_ARTIC ? __fsub_rn(__fmul_rn(s, 1.002f), 0.001f) : s;
+}
+
+__device__ __forceinline__ float act_sigma(float x, int act) {
+  if (act == AON_ACT_NONE) return x;
+  if (act == AON_ACT_VANILLA) return fmaxf(x, 0.0f);
+  // softplus(x - 1) with torch's threshold 20 (model_autodecoder.py:323)
+  const float z = __fsub_rn(x, 1.0f);
+  return z > 20.0f ? z : log1pf(expf(z));
+}
+
 // fp32(0.5 * pi) as torch adds it to an fp32 tensor (reference helper.py:139)
 constexpr float kHalfPi = 1.57079637050628662109375f;
 

@@ -1,12 +1,12 @@
 // Alpha compositing (reference models/vanilla_nerf/helper.py:157-195) -- HBM-bound.
 //
 // One 64-lane wave per ray; lane i owns samples i, i+64, ...: every load is a coalesced
-// wave-wide read of the ray's contiguous (S, 4) raw block / (S,) t row, the transmittance is a
-// wavefront prefix-product scan (6 __shfl_up steps per 64-sample block) carried across blocks.
-// The scan runs in fp64 and rounds each prefix to fp32, which is what torch CPU's cumprod does
-// (fp64 accumulator, measured), so T_i matches the reference bit-for-bit in practice.
-// The per-ray sums (acc = sum w, depth = sum w*t, rgb = sum w*c) are staged in LDS and reduced
-// in torch's CPU summation order (torch_sum.hpp), spread over lanes.
+// wave-wide read of the ray's contiguous (S, 4) raw block / (S,) t row, all issued before any
+// math.  The transmittance is an fp64 prefix product (DPP row shifts/broadcasts, 6 steps per
+// 64-sample block) carried across blocks and rounded per prefix to fp32, which is what torch
+// CPU's cumprod does (fp64 accumulator, measured), so T_i matches the reference bit-for-bit in
+// practice.  The per-ray sums (acc = sum w, depth = sum w*t, rgb = sum w*c) are staged in LDS
+// and evaluated in torch's CPU summation order by the whole wave (torch_sum.hpp).
 #include "aon_common.hpp"
 #include "torch_sum.hpp"
 
@@ -14,137 +14,183 @@ namespace aon {
 
 constexpr int kCompWaves = 4;
 constexpr int kCompMaxS = 512;
-
-struct CompLds {
-  float w[kCompMaxS], wt[kCompMaxS], wc[3 * kCompMaxS];
-};
+constexpr int kCompScratch = 256;  // wave_row_sums task partials (<= 236 at S = 512)
 
 __device__ __forceinline__ void wave_sync_c() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ float act_rgb(float x, int act) {
-  if (act == AON_ACT_NONE) return x;
-  const float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-x)));
-  return act == AON_ACT_ARTIC ? __fsub_rn(__fmul_rn(s, 1.002f), 0.001f) : s;
+// ---- DPP lane moves (gfx9 controls).  Lanes whose source is outside the pattern keep `old`.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_f64(double src, double old) {
+  const long long s = __builtin_bit_cast(long long, src), o = __builtin_bit_cast(long long, old);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)s, CTRL, ROW_MASK, 0xF, false);
+  const int hi =
+      __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(s >> 32), CTRL, ROW_MASK, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
-__device__ __forceinline__ float act_sigma(float x, int act) {
-  if (act == AON_ACT_NONE) return x;
-  if (act == AON_ACT_VANILLA) return fmaxf(x, 0.0f);
-  // softplus(x - 1) with torch's threshold 20 (model_autodecoder.py:323)
-  const float z = __fsub_rn(x, 1.0f);
-  return z > 20.0f ? z : log1pf(expf(z));
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long s = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)s, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(s >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
+// inclusive prefix product over the 64 lanes: row_shr 1/2/4/8 inside 16-lane rows, then
+// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- VALU lane moves, no LDS
+__device__ __forceinline__ double wave_incl_prod(double x) {
+  x *= dpp_f64<0x111>(x, 1.0);
+  x *= dpp_f64<0x112>(x, 1.0);
+  x *= dpp_f64<0x114>(x, 1.0);
+  x *= dpp_f64<0x118>(x, 1.0);
+  x *= dpp_f64<0x142, 0xA>(x, 1.0);
+  x *= dpp_f64<0x143, 0xC>(x, 1.0);
+  return x;
+}
+
+// One 64-lane wave per ray, NB = ceil(S/64) blocks of 64 samples (lane i owns samples i + 64b).
+// All of a ray's loads are issued up front (NB x {16-B raw, 4-B t} per lane), the
+// transmittance is an fp64 DPP prefix product per block (torch CPU's cumprod accumulates in
+// fp64) carried across blocks, and the per-ray sums are evaluated in torch's CPU order by the
+// whole wave (wave_row_sums) from planar LDS arrays w, w*t, w*r, w*g, w*b.
+// RAW4: rgb and sigma interleaved as one (.., 4) fp32 row, 16-B aligned -> one dwordx4 load.
+template <int NB, bool RAW4>
 __global__ __launch_bounds__(64 * kCompWaves) void k_composite_fwd(
     const float* __restrict__ rgb, int64_t rgb_stride, const float* __restrict__ sig,
     int64_t sig_stride, const float* __restrict__ tv, const float* __restrict__ dirs, int64_t B,
     int S, int white, int act, float* __restrict__ out_rgb, float* __restrict__ out_acc,
     float* __restrict__ out_w, float* __restrict__ out_depth) {
-  __shared__ CompLds lds_all[kCompWaves];
-  CompLds& Ls = lds_all[threadIdx.x >> 6];
+  constexpr int SM = 64 * NB;
+  __shared__ float lds_all[kCompWaves][5 * SM + kCompScratch + 32];
+  float* P = lds_all[threadIdx.x >> 6];  // P[q * SM + i]: q = 0 w, 1 w*t, 2..4 w*rgb
+  float* scratch = P + 5 * SM;
+  float* sums = scratch + kCompScratch;
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * kCompWaves;
+  const bool inner8 = S >= 8;
   for (int64_t ray = (int64_t)blockIdx.x * kCompWaves + (threadIdx.x >> 6); ray < B;
        ray += nwaves) {
+    const int64_t row0 = ray * S;
+    const float* t = tv + row0;
+    float tt[NB];
+    f4 raw[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int i = 64 * b + lane;
+      tt[b] = 0.f;
+      raw[b] = f4{0.f, 0.f, 0.f, 0.f};
+      if (i < S) {
+        tt[b] = t[i];
+        if (RAW4) {
+          raw[b] = *reinterpret_cast<const f4*>(rgb + (row0 + i) * 4);
+        } else {
+          const float* c = rgb + (row0 + i) * rgb_stride;
+          raw[b] = f4{c[0], c[1], c[2], sig[(row0 + i) * sig_stride]};
+        }
+      }
+    }
     const float dx = dirs[3 * ray], dy = dirs[3 * ray + 1], dz = dirs[3 * ray + 2];
     const float dnorm = sqrtf(fmaf(dz, dz, fmaf(dy, dy, __fmul_rn(dx, dx))));
-    const float* t = tv + ray * S;
-    const int64_t row0 = ray * S;
     double carry = 1.0;  // prod_{j < block start} (1 - alpha_j + 1e-10)
-    for (int base = 0; base < S; base += 64) {
-      const int i = base + lane;
-      const bool valid = i < S;
-      float w = 0.f;
-      double f = 1.0;
-      float ti = 0.f, cr = 0.f, cg = 0.f, cb = 0.f;
-      if (valid) {
-        ti = t[i];
-        const float dist = (i + 1 < S) ? __fsub_rn(t[i + 1], ti) : 1e10f;
-        const float sgm = act_sigma(sig[(row0 + i) * sig_stride], act);
-        const float alpha = __fsub_rn(1.0f, expf(__fmul_rn(-sgm, __fmul_rn(dist, dnorm))));
-        if (i + 1 < S) f = (double)__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f);
-        w = alpha;  // times T_i below
-        const float* c = rgb + (row0 + i) * rgb_stride;
-        cr = act_rgb(c[0], act);
-        cg = act_rgb(c[1], act);
-        cb = act_rgb(c[2], act);
-      }
-      // inclusive prefix product over the block, then exclusive via one more shift
-      double incl = f;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double v = __shfl_up(incl, o);
-        if (lane >= o) incl *= v;
-      }
-      double excl = __shfl_up(incl, 1);
-      if (lane == 0) excl = 1.0;
-      const float T = (float)(carry * excl);
-      carry *= __shfl(incl, 63);
+    for (int b = 0; b < NB; ++b) {
+      const int i = 64 * b + lane;
+      const bool valid = i < S;
+      // t[i + 1]: lane i + 1 of this block, or lane 0 of the next (wave_shl:1)
+      const float tnext0 = b + 1 < NB ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                                      __builtin_bit_cast(int, tt[b + 1]), 0))
+                                      : 0.f;
+      const float tn = __builtin_bit_cast(
+          float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, tnext0),
+                                             __builtin_bit_cast(int, tt[b]), 0x130, 0xF, 0xF, false));
+      const float ti = tt[b];
+      float alpha = 0.f;
+      double f = 1.0;
       if (valid) {
-        w = __fmul_rn(w, T);
+        const float dist = (i + 1 < S) ? __fsub_rn(tn, ti) : 1e10f;
+        const float sgm = act_sigma(raw[b].w, act);
+        alpha = __fsub_rn(1.0f, expf(__fmul_rn(-sgm, __fmul_rn(dist, dnorm))));
+        if (i + 1 < S) f = (double)__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f);
+      }
+      const double incl = wave_incl_prod(f);
+      const double excl = dpp_f64<0x138>(incl, 1.0);  // wave_shr:1, lane 0 -> 1
+      const float T = (float)(carry * excl);
+      if (b + 1 < NB) carry *= readlane_f64(incl, 63);
+      if (valid) {
+        const float w = __fmul_rn(alpha, T);
         if (out_w) out_w[row0 + i] = w;
-        Ls.w[i] = w;
-        Ls.wt[i] = __fmul_rn(w, ti);
-        Ls.wc[3 * i] = __fmul_rn(w, cr);
-        Ls.wc[3 * i + 1] = __fmul_rn(w, cg);
-        Ls.wc[3 * i + 2] = __fmul_rn(w, cb);
+        P[i] = w;
+        P[SM + i] = __fmul_rn(w, ti);
+        P[2 * SM + i] = __fmul_rn(w, act_rgb(raw[b].x, act));
+        P[3 * SM + i] = __fmul_rn(w, act_rgb(raw[b].y, act));
+        P[4 * SM + i] = __fmul_rn(w, act_rgb(raw[b].z, act));
       }
     }
     wave_sync_c();
-    // torch-order reductions, one partial per lane (torch_sum.hpp)
-    const float* lw = Ls.w;
-    const float* lwt = Ls.wt;
-    const float* lwc = Ls.wc;
-    float v = 0.f;
-    const bool vec = S >= 8;
-    if (lane < 8) {
-      v = vec ? inner_sum_lane([&](int e) { return lw[e]; }, S, lane)
-              : (lane == 0 ? row_sum_ilp4([&](int e) { return lw[e]; }, S) : 0.f);
-    } else if (lane < 16) {
-      v = vec ? inner_sum_lane([&](int e) { return lwt[e]; }, S, lane - 8)
-              : (lane == 8 ? row_sum_ilp4([&](int e) { return lwt[e]; }, S) : 0.f);
-    } else if (lane < 19) {
-      const int ch = lane - 16;
-      v = row_sum_ilp4([&](int e) { return lwc[3 * e + ch]; }, S);
-    } else if (lane == 19) {
-      v = vec ? inner_sum_tail([&](int e) { return lw[e]; }, S) : 0.f;
-    } else if (lane == 20) {
-      v = vec ? inner_sum_tail([&](int e) { return lwt[e]; }, S) : 0.f;
-    }
-    float sa, sd;
-    if (vec) {
-      sa = __shfl(v, 19);
-      sd = __shfl(v, 20);
+    // torch-order sums (torch_sum.hpp): specs 0..2 = rgb over S terms (stride-3 outer sum);
+    // S >= 8: specs 3..18 = the 8 vector lanes of the inner sums of w (3..10) and w*t (11..18)
+    // over S/8 terms each; S < 8: specs 3, 4 = scalar sums of w, w*t.
+    wave_row_sums(
+        [&](int sp, const float*& base, int& str) {
+          if (sp < 3) {
+            base = P + (2 + sp) * SM;
+            str = 1;
+          } else if (inner8) {
+            base = P + ((sp - 3) >> 3) * SM + ((sp - 3) & 7);
+            str = 8;
+          } else {
+            base = P + (sp - 3) * SM;
+            str = 1;
+          }
+        },
+        3, S, inner8 ? 16 : 2, inner8 ? S / 8 : S, scratch, sums, lane, wave_sync_c);
+    if (lane < 2) {
+      // acc (lane 0) / depth (lane 1): tail x[8m..S) from 0, then + vector lanes 0..7
+      float s;
+      if (inner8) {
+        s = 0.f;
+        for (int e = (S / 8) * 8; e < S; ++e) s = __fadd_rn(s, P[lane * SM + e]);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        sa = __fadd_rn(sa, __shfl(v, c));
-        sd = __fadd_rn(sd, __shfl(v, 8 + c));
+        for (int c = 0; c < 8; ++c) s = __fadd_rn(s, sums[3 + 8 * lane + c]);
+      } else {
+        s = sums[3 + lane];
       }
-    } else {
-      sa = __shfl(v, 0);
-      sd = __shfl(v, 8);
+      if (lane == 0) {
+        float sr = sums[0], sg = sums[1], sb = sums[2];
+        if (white) {
+          const float bg = __fsub_rn(1.0f, s);
+          sr = __fadd_rn(sr, bg);
+          sg = __fadd_rn(sg, bg);
+          sb = __fadd_rn(sb, bg);
+        }
+        out_rgb[3 * ray] = sr;
+        out_rgb[3 * ray + 1] = sg;
+        out_rgb[3 * ray + 2] = sb;
+        out_acc[ray] = s;
+      } else {
+        // nan_to_num(depth, nan=inf) then clamp(depth, min, max) over the chunk, which is the
+        // identity on the resulting values (helper.py:182-183)
+        out_depth[ray] = nan_to_num(s, __builtin_inff());
+      }
     }
-    float sr = __shfl(v, 16), sg = __shfl(v, 17), sb = __shfl(v, 18);
     wave_sync_c();  // LDS reuse by this wave's next ray
-    if (lane == 0) {
-      if (white) {
-        const float bg = __fsub_rn(1.0f, sa);
-        sr = __fadd_rn(sr, bg);
-        sg = __fadd_rn(sg, bg);
-        sb = __fadd_rn(sb, bg);
-      }
-      out_rgb[3 * ray] = sr;
-      out_rgb[3 * ray + 1] = sg;
-      out_rgb[3 * ray + 2] = sb;
-      out_acc[ray] = sa;
-      // nan_to_num(depth, nan=inf) then clamp(depth, min, max) over the chunk, which is the
-      // identity on the resulting values (helper.py:182-183)
-      out_depth[ray] = nan_to_num(sd, __builtin_inff());
-    }
   }
+}
+
+template <int NB>
+static void launch_composite(bool raw4, int grid, hipStream_t st, const float* rgb,
+                             int64_t rgb_stride, const float* sig, int64_t sig_stride,
+                             const float* t, const float* dirs, int64_t B, int S, int white,
+                             int act, float* comp, float* acc, float* w, float* depth) {
+  if (raw4)
+    hipLaunchKernelGGL((k_composite_fwd<NB, true>), grid, 64 * kCompWaves, 0, st, rgb, rgb_stride,
+                       sig, sig_stride, t, dirs, B, S, white, act, comp, acc, w, depth);
+  else
+    hipLaunchKernelGGL((k_composite_fwd<NB, false>), grid, 64 * kCompWaves, 0, st, rgb,
+                       rgb_stride, sig, sig_stride, t, dirs, B, S, white, act, comp, acc, w,
+                       depth);
 }
 
 }  // namespace aon
@@ -160,8 +206,24 @@ extern "C" int aon_composite_fwd(const float* rgb, int64_t rgb_stride, const flo
               "bad shape (1 <= S <= 512)");
   AON_REQUIRE(act >= AON_ACT_NONE && act <= AON_ACT_ARTIC, "bad activation");
   if (B == 0) return 0;
-  hipLaunchKernelGGL(k_composite_fwd, grid_for(B, kCompWaves, 1 << 16), 64 * kCompWaves, 0,
-                     (hipStream_t)stream, rgb, rgb_stride, sigma, sigma_stride, t, dirs, B, S,
-                     white_bkgd, act, comp_rgb, acc, weights, depth);
+  const bool raw4 = rgb_stride == 4 && sigma_stride == 4 && sigma == rgb + 3 && aligned16(rgb);
+  const int grid = grid_for(B, kCompWaves, 1 << 16);
+  hipStream_t st = (hipStream_t)stream;
+  switch ((S + 63) / 64) {
+#define AON_COMP_CASE(nb)                                                                       \
+  case nb:                                                                                      \
+    launch_composite<nb>(raw4, grid, st, rgb, rgb_stride, sigma, sigma_stride, t, dirs, B, S,   \
+                         white_bkgd, act, comp_rgb, acc, weights, depth);                       \
+    break;
+    AON_COMP_CASE(1)
+    AON_COMP_CASE(2)
+    AON_COMP_CASE(3)
+    AON_COMP_CASE(4)
+    AON_COMP_CASE(5)
+    AON_COMP_CASE(6)
+    AON_COMP_CASE(7)
+    AON_COMP_CASE(8)
+#undef AON_COMP_CASE
+  }
   return launch_status(__func__);
 }

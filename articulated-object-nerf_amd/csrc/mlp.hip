@@ -95,7 +95,7 @@ template <int MODE>
 __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd_f32(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
-    int64_t B, int S, float* __restrict__ raw) {
+    int64_t B, int S, int act, float* __restrict__ raw) {
   __shared__ f4 wbuf[2 * kChunk * 64];
   __shared__ __attribute__((aligned(16))) float bias_s[kBiasFloats];
 
@@ -202,7 +202,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd_f32(
   const f4 rgb = gemm_u1<LRGB>(p, h, *reinterpret_cast<const f4*>(bias_s + kLayers[LRGB].bias0 + 4 * g));
 
   if (g == 0 && row < N) {
-    const f4 o = {rgb[0], rgb[1], rgb[2], dens[0]};
+    const f4 o = {act_rgb(rgb[0], act), act_rgb(rgb[1], act), act_rgb(rgb[2], act),
+                  act_sigma(dens[0], act)};
     *reinterpret_cast<f4*>(raw + 4 * row) = o;
   }
 }
@@ -290,37 +291,39 @@ extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* pack
 
 static int mlp_launch(int mode, const void* packed, int precision, const float* a0,
                       const float* a1, const float* a2, const float* a3, int64_t B, int S,
-                      float* raw, aon_stream_t stream) {
+                      int act, float* raw, aon_stream_t stream) {
   AON_REQUIRE(packed && raw && a0 && a1, "null pointer");
   AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3, "unsupported precision");
   AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
+  AON_REQUIRE(act >= AON_ACT_NONE && act <= AON_ACT_ARTIC, "bad activation");
   AON_REQUIRE(aligned16(packed) && aligned16(raw), "packed / raw must be 16-byte aligned");
   const int64_t N = B * S;
   if (N == 0) return 0;
   AON_REQUIRE((N + kRowsPerBlock - 1) / kRowsPerBlock < (1ll << 31), "too many rows");
   if (precision == AON_PREC_F16X3)
-    return launch_f16x3(mode, f16x3_ncol(), packed, a0, a1, a2, a3, B, S, raw, (hipStream_t)stream);
+    return launch_f16x3(mode, f16x3_ncol(), packed, a0, a1, a2, a3, B, S, act, raw,
+                        (hipStream_t)stream);
   const int grid = static_cast<int>((N + kRowsPerBlock - 1) / kRowsPerBlock);
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + kStreamBytesF32);
   if (mode == 0)
     hipLaunchKernelGGL(k_mlp_fwd_f32<0>, grid, kThreads, 0, (hipStream_t)stream, ws, bias, a0, a1,
-                       a2, a3, B, S, raw);
+                       a2, a3, B, S, act, raw);
   else
     hipLaunchKernelGGL(k_mlp_fwd_f32<1>, grid, kThreads, 0, (hipStream_t)stream, ws, bias, a0, a1,
-                       a2, a3, B, S, raw);
+                       a2, a3, B, S, act, raw);
   return launch_status("aon_mlp_fwd");
 }
 
 extern "C" int aon_mlp_fwd(const void* packed, int precision, const float* rays_o,
                            const float* rays_d, const float* viewdirs, const float* t, int64_t B,
-                           int S, float* raw, aon_stream_t stream) {
+                           int S, int act, float* raw, aon_stream_t stream) {
   AON_REQUIRE(viewdirs && t, "null pointer");
-  return mlp_launch(0, packed, precision, rays_o, rays_d, viewdirs, t, B, S, raw, stream);
+  return mlp_launch(0, packed, precision, rays_o, rays_d, viewdirs, t, B, S, act, raw, stream);
 }
 
 extern "C" int aon_mlp_fwd_encoded(const void* packed, int precision, const float* x,
-                                   const float* condition, int64_t B, int S, float* raw,
-                                   aon_stream_t stream) {
-  return mlp_launch(1, packed, precision, x, condition, nullptr, nullptr, B, S, raw, stream);
+                                   const float* condition, int64_t B, int S, int act,
+                                   float* raw, aon_stream_t stream) {
+  return mlp_launch(1, packed, precision, x, condition, nullptr, nullptr, B, S, act, raw, stream);
 }

@@ -234,7 +234,7 @@ template <int MODE, int NCOL>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_fwd_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
-    int64_t B, int S, float* __restrict__ raw) {
+    int64_t B, int S, int act, float* __restrict__ raw) {
   using G = GeomH<NCOL>;
   // ONE __shared__ object: weight ring | bias table | per-lane stash of the encodings
   constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
@@ -357,7 +357,8 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     for (int c = 0; c < NCOL; ++c) {
       if (rows[c] < N) {
         const float s = 1.0f / kActScale;
-        const f4 o = {rgb[c][0] * s, rgb[c][1] * s, rgb[c][2] * s, dens[c][0] * s};
+        const f4 o = {act_rgb(rgb[c][0] * s, act), act_rgb(rgb[c][1] * s, act),
+                      act_rgb(rgb[c][2] * s, act), act_sigma(dens[c][0] * s, act)};
         *reinterpret_cast<f4*>(raw + 4 * rows[c]) = o;
       }
     }
@@ -423,7 +424,7 @@ int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream) {
 }
 
 int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,
-                 const float* a2, const float* a3, int64_t B, int S, float* raw,
+                 const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
                  hipStream_t stream) {
   const int64_t N = B * S;
   const f4* ws = static_cast<const f4*>(packed);
@@ -431,7 +432,7 @@ int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const 
 #define AON_LAUNCH_H(M, C)                                                                       \
   hipLaunchKernelGGL((k_mlp_fwd_f16x3<M, C>),                                                    \
                      static_cast<int>((N + GeomH<C>::kRowsPerBlock - 1) / GeomH<C>::kRowsPerBlock), \
-                     GeomH<C>::kThreads, 0, stream, ws, bias, a0, a1, a2, a3, B, S, raw)
+                     GeomH<C>::kThreads, 0, stream, ws, bias, a0, a1, a2, a3, B, S, act, raw)
   if (mode == 0 && ncol == 1) AON_LAUNCH_H(0, 1);
   else if (mode == 0) AON_LAUNCH_H(0, 2);
   else if (ncol == 1) AON_LAUNCH_H(1, 1);

@@ -110,7 +110,7 @@ struct PackArgs {
 // fp16x3 path (mlp_f16x3.hip)
 int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream);
 int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,
-                 const float* a2, const float* a3, int64_t B, int S, float* raw,
+                 const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
                  hipStream_t stream);
 
 }  // namespace mlp

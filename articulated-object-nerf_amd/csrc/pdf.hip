@@ -127,8 +127,13 @@ __global__ __launch_bounds__(64 * kPdfWaves) void k_sample_pdf(
       L.samp[j] = s;
     }
     wave_sync();
-    // ---- bitonic sort of the samples (ascending)
-    for (int k = 2; k <= Ns_pow2; k <<= 1) {
+    // ---- bitonic sort of the samples (ascending), skipped when they already are (sorted u,
+    // e.g. the eval-mode linspace, maps to nondecreasing samples); a NaN compares unordered
+    // and keeps the sort on, as before
+    bool unsorted = false;
+    for (int j = lane; j + 1 < Ns; j += 64) unsorted |= !(L.samp[j] <= L.samp[j + 1]);
+    const bool need_sort = __any(unsorted);
+    for (int k = 2; need_sort && k <= Ns_pow2; k <<= 1) {
       for (int jj = k >> 1; jj > 0; jj >>= 1) {
         for (int i = lane; i < Ns_pow2; i += 64) {
           const int p = i ^ jj;

@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 1
+#define AON_ABI_VERSION 2
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -109,14 +109,18 @@ int aon_mlp_pack(const aon_mlp_params* params, int precision, void* packed,
 
 /* NeRFMLP.forward (model.py:95-120) fused with cast_rays + pos_enc (model.py:175-181):
  * per sample row r = b*S + s: xyz = o[b] + t[r]*d[b], enc = pos_enc(xyz, 0, 10),
- * venc = pos_enc(viewdirs[b], 0, 4); raw (B*S, 4) = [raw_rgb(3), raw_sigma]. */
+ * venc = pos_enc(viewdirs[b], 0, 4); out (B*S, 4) = [rgb(3), sigma].
+ * act = AON_ACT_NONE: the raw head outputs (NeRFMLP.forward);
+ * act = AON_ACT_VANILLA: also rgb_activation / sigma_activation (sigmoid / relu,
+ *       model.py:186-187), so the compositor can run with AON_ACT_NONE;
+ * act = AON_ACT_ARTIC: the articulated model's padded sigmoid / softplus(x - 1). */
 int aon_mlp_fwd(const void* packed, int precision, const float* rays_o, const float* rays_d,
-                const float* viewdirs, const float* t, int64_t B, int S, float* raw,
+                const float* viewdirs, const float* t, int64_t B, int S, int act, float* out,
                 aon_stream_t stream);
 
-/* NeRFMLP.forward on pre-encoded inputs: x (B*S, 63), condition (B, 27) -> raw (B*S, 4). */
+/* NeRFMLP.forward on pre-encoded inputs: x (B*S, 63), condition (B, 27) -> out (B*S, 4). */
 int aon_mlp_fwd_encoded(const void* packed, int precision, const float* x,
-                        const float* condition, int64_t B, int S, float* raw,
+                        const float* condition, int64_t B, int S, int act, float* out,
                         aon_stream_t stream);
 
 /* ---------------------------------------------------------------- compositing */

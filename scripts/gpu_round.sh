@@ -21,6 +21,7 @@ step bench 600 python bench.py "$@"
 tail -1 "$OUT/bench.log" > "$OUT/bench.json"
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@"
+[ "${SKIP_PMC:-0}" = 1 ] && exit 0
 step rocprof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@"
 step rocprof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@"
 echo done

@@ -35,7 +35,7 @@ def test_header_symbols_exported(L):
 
 def test_abi_version_and_sizes(L):
     lib = L.lib()
-    assert lib.aon_abi_version() == 1
+    assert lib.aon_abi_version() == 2
     assert lib.aon_mlp_packed_bytes(0) == 2368 * 1024 + 2464 * 4
     assert lib.aon_mlp_packed_bytes(99) == 0
 
@@ -43,7 +43,7 @@ def test_abi_version_and_sizes(L):
 @pytest.mark.parametrize("name,args", [
     ("aon_composite_fwd", (None, 3, None, 1, None, None, 4, 8, 1, 1, None, None, None, None, None)),
     ("aon_sample_pdf", (None, 0, None, 0, 4, 1, 128, None, 0, None, 0, None, None, None, None, None)),
-    ("aon_mlp_fwd", (None, 0, None, None, None, None, 4, 8, None, None)),
+    ("aon_mlp_fwd", (None, 0, None, None, None, None, 4, 8, 0, None, None)),
     ("aon_pos_enc", (None, 4, 0, 10, None, None)),
     ("aon_frame_rays", (0, 4, 1.0, None, 0, 0, None, None, None, None)),
 ])

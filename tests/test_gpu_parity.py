@@ -178,7 +178,8 @@ def test_composite_levels_from_reference_raw(golden):
         raw = raw.contiguous()
         comp, acc = torch.empty((B, 3), device="cuda"), torch.empty((B,), device="cuda")
         w, depth = torch.empty((B, S), device="cuda"), torch.empty((B,), device="cuda")
-        L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(cuda(g[f"{name}_t"])),
+        t_d = cuda(g[f"{name}_t"])  # keep device operands alive until the kernel has run
+        L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_d),
                L.ptr(d), B, S, 1, L.ACT_VANILLA, L.ptr(comp), L.ptr(acc), L.ptr(w), L.ptr(depth),
                L.stream())
         torch.cuda.synchronize()
@@ -186,6 +187,46 @@ def test_composite_levels_from_reference_raw(golden):
             report(f"{name} composite {k}", npy(v), g[f"{name}_{k}"], 1e-7)
             tol = 1e-5 if k == "depth" else 1e-6  # depth ~ 2..6: a few fp32 ulps
             np.testing.assert_allclose(npy(v), g[f"{name}_{k}"], rtol=0, atol=tol, err_msg=f"{name} {k}")
+
+
+COMP_S = [1, 2, 3, 5, 7, 8, 9, 17, 33, 63, 64, 65, 100, 128, 129, 193, 255, 256, 257, 385, 448, 512]
+
+
+@pytest.mark.parametrize("layout", ["raw4", "split"])
+def test_composite_sample_counts(layout):
+    """Every block count (S = 1..512) and both operand layouts: the weights against the oracle,
+    and the per-ray sums bit-for-bit equal to torch CPU's sums of the GPU's own weights (the
+    reduction order is the reference's, so given equal weights the sums round identically)."""
+    from aonerf import _lib as L
+
+    g = torch.Generator().manual_seed(7)
+    B = 96
+    for S in COMP_S:
+        t = torch.sort(2.0 + 4.0 * torch.rand((B, S), generator=g), -1).values
+        rgb = torch.rand((B, S, 3), generator=g)
+        sigma = 3.0 * torch.rand((B, S, 1), generator=g)
+        dirs = torch.randn((B, 3), generator=g)
+        dirs[:4] = 0.0  # zero-length directions: dists * 0
+        dirs = dirs.contiguous()
+        if layout == "raw4":
+            raw = cuda(torch.cat([rgb, sigma], -1).reshape(-1, 4))
+            prgb, srgb, psig, ssig = L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4
+        else:
+            rgb_d, sig_d = cuda(rgb), cuda(sigma)
+            prgb, srgb, psig, ssig = L.ptr(rgb_d), 3, L.ptr(sig_d), 1
+        comp, acc = torch.empty((B, 3), device="cuda"), torch.empty((B,), device="cuda")
+        w, depth = torch.empty((B, S), device="cuda"), torch.empty((B,), device="cuda")
+        t_d, dirs_d = cuda(t), cuda(dirs)  # keep device operands alive until the kernel has run
+        L.call("aon_composite_fwd", prgb, srgb, psig, ssig, L.ptr(t_d), L.ptr(dirs_d), B, S,
+               0, L.ACT_NONE, L.ptr(comp), L.ptr(acc), L.ptr(w), L.ptr(depth), L.stream())
+        torch.cuda.synchronize()
+        _, _, w_ref, _ = O.volumetric_rendering(rgb, sigma, t, dirs, False)
+        np.testing.assert_allclose(npy(w), w_ref.numpy(), rtol=0, atol=1e-6, err_msg=f"S={S} weights")
+        wc = w.cpu()
+        np.testing.assert_array_equal(npy(acc), wc.sum(-1).numpy(), err_msg=f"S={S} acc")
+        np.testing.assert_array_equal(npy(depth), (wc * t).sum(-1).numpy(), err_msg=f"S={S} depth")
+        np.testing.assert_array_equal(npy(comp), (wc[..., None] * rgb).sum(-2).numpy(),
+                                      err_msg=f"S={S} rgb")
 
 
 def test_pdf_edges(golden):
@@ -235,6 +276,13 @@ def test_mlp_from_reference_inputs(golden, nerf):
         report(f"{name} raw_sigma", raw[:, 3], g[f"{name}_raw_sigma"].reshape(-1), 1e-6)
         np.testing.assert_allclose(raw[:, :3], g[f"{name}_raw_rgb"].reshape(-1, 3), rtol=0, atol=1e-5)
         np.testing.assert_allclose(raw[:, 3], g[f"{name}_raw_sigma"].reshape(-1), rtol=0, atol=1e-5)
+        # fused epilogue activations (model.py:186-187) == torch's sigmoid / relu of the raw
+        from aonerf import _lib as L
+
+        act = npy(mlp.forward_rays(rays["rays_o"], rays["rays_d"], rays["viewdirs"], t, act=L.ACT_VANILLA))
+        raw_t = torch.from_numpy(raw)
+        np.testing.assert_allclose(act[:, :3], torch.sigmoid(raw_t[:, :3]).numpy(), rtol=0, atol=1.2e-7)
+        np.testing.assert_array_equal(act[:, 3], torch.relu(raw_t[:, 3]).numpy())
 
 
 def test_mlp_encoded_api(golden, nerf):
