@@ -24,6 +24,21 @@ class AonMlpParams(ctypes.Structure):
                 ("rgb_w", vp), ("rgb_b", vp)]
 
 
+class AonGemmArgs(ctypes.Structure):
+    _fields_ = [("M", c_i64), ("N", c_i64), ("K", c_i64), ("A", vp), ("lda", c_i64), ("a_kc", c_int),
+                ("A2", vp), ("lda2", c_i64), ("K1", c_i64), ("a2_rdiv", c_i64),
+                ("B", vp), ("ldb", c_i64), ("b_kc", c_int), ("b_rdiv", c_i64),
+                ("C", vp), ("ldc", c_i64), ("bias", vp), ("mask", vp), ("ldm", c_i64),
+                ("relu", c_int), ("accumulate", c_int), ("a_scale", c_float), ("b_scale", c_float),
+                ("k_splits", c_i64)]
+
+
+class AonAdamTensor(ctypes.Structure):
+    _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("numel", c_i64)]
+
+
+ADAM_MAX_TENSORS = 64
+
 _SIGNATURES = {
     "aon_abi_version": (c_int, []),
     "aon_last_error": (ctypes.c_char_p, []),
@@ -32,6 +47,7 @@ _SIGNATURES = {
     "aon_frame_rays": (c_int, [c_int, c_int, c_float, vp, c_i64, c_i64, vp, vp, vp, vp]),
     "aon_sample_along_rays": (c_int, [vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp]),
     "aon_pos_enc": (c_int, [vp, c_i64, c_int, c_int, vp, vp]),
+    "aon_cast_rays": (c_int, [vp, vp, vp, c_i64, c_int, vp, c_int, c_int, vp, vp]),
     "aon_sample_pdf": (c_int, [vp, c_i64, vp, c_i64, c_i64, c_int, c_int, vp, c_i64, vp, c_int,
                                vp, vp, vp, vp, vp]),
     "aon_mlp_packed_bytes": (c_size, [c_int]),
@@ -40,6 +56,15 @@ _SIGNATURES = {
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,
                                   vp, vp, vp, vp]),
+    "aon_gemm_workspace_bytes": (c_size, [ctypes.POINTER(AonGemmArgs)]),
+    "aon_gemm": (c_int, [ctypes.POINTER(AonGemmArgs), vp, c_size, vp]),
+    "aon_composite_bwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp, vp,
+                                  vp, vp, vp, c_i64, vp]),
+    "aon_mse": (c_int, [vp, vp, c_i64, c_float, vp, vp, vp]),
+    "aon_colsum_workspace_bytes": (c_size, [c_i64, c_i64]),
+    "aon_colsum": (c_int, [vp, c_i64, c_i64, c_i64, c_int, vp, vp, c_size, vp]),
+    "aon_adam_step": (c_int, [ctypes.POINTER(AonAdamTensor), c_int, c_float, c_float, c_float,
+                              c_float, c_i64, vp]),
 }
 
 _lib = None

@@ -165,64 +165,100 @@ class NeRF(nn.Module):
             m.precision = precision
         return self
 
-    @torch.no_grad()
     def forward(self, rays, randomized, white_bkgd, near, far, *, u_coarse=None, u_fine=None,
                 return_weights=False, return_intermediates=False, timers=None):
         """reference model.py:147-199 -> [(comp_rgb, acc, depth)_coarse, (...)_fine].
 
         ``u_coarse`` (B, Sc+1) / ``u_fine`` (B, Nf) inject the uniforms of randomized mode;
         ``return_weights`` adds each level's weights (B, S) as a 4th element;
-        ``return_intermediates`` adds a dict(t_vals, weights, rgb_sigma) as the last element
-        (rgb_sigma (B*S, 4): the activated MLP outputs the compositor consumed);
+        ``return_intermediates`` adds a dict(t_vals, weights[, rgb_sigma]) as the last element
+        (rgb_sigma (B*S, 4), inference path only: the activated MLP outputs the compositor
+        consumed);
         ``timers`` (dict) records hip events around each level's MLP / composite launches.
+
+        With autograd enabled and trainable parameters, each level runs the training path
+        (train.RenderLevel: layer GEMMs keeping activations, HIP backward); otherwise the fused
+        inference kernels.
         """
         o, d, v = rays["rays_o"], rays["rays_d"], rays["viewdirs"]
         L.require_gpu(o, d, v)
         o, d, v = L.contig(o), L.contig(d), L.contig(v)
+        training = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         B = o.shape[0]
         dev = o.device
         ret = []
         t_vals = weights = None
         for level in range(2):
-            if level == 0:
-                t_vals, _ = helper.sample_along_rays(o, d, self.num_coarse_samples, near, far,
-                                                     randomized, self.lindisp, u=u_coarse,
-                                                     want_coords=False)
-                mlp = self.coarse_mlp
-            else:
-                Sc = t_vals.shape[1]
-                if randomized:
-                    u = torch.rand((B, self.num_fine_samples), device=dev) if u_fine is None else L.contig(u_fine)
-                    u_stride = self.num_fine_samples
-                else:
-                    u, u_stride = helper.eval_u(self.num_fine_samples, dev), 0
-                t_new = torch.empty((B, Sc + self.num_fine_samples), device=dev)
-                # bins = mids of t (model.py:163), weights[..., 1:-1] as a strided view
-                L.call("aon_sample_pdf", None, 0, L.ptr(weights[:, 1:]), Sc, B, Sc - 1,
-                       self.num_fine_samples, L.ptr(u), u_stride, L.ptr(t_vals), Sc, None, None,
-                       L.ptr(t_new), None, L.stream(dev))
-                t_vals = t_new
-                mlp = self.fine_mlp
+            with torch.no_grad():
+                t_vals = self._level_t(level, o, d, t_vals, weights, randomized, near, far,
+                                       u_coarse, u_fine)
+            mlp = self.coarse_mlp if level == 0 else self.fine_mlp
             S = t_vals.shape[1]
-            # the activations (model.py:186-187) run in the MLP epilogue, unless density noise
-            # must be added to the raw sigma first (model.py:183-184)
-            noisy = self.noise_std > 0 and randomized
-            ev = _events(timers)
-            raw = mlp.forward_rays(o, d, v, t_vals, act=L.ACT_NONE if noisy else L.ACT_VANILLA)
-            _record(timers, ev, f"mlp{level}", B * S)
-            if noisy:
-                raw[:, 3] += torch.rand_like(raw[:, 3]) * self.noise_std
-            comp = torch.empty((B, 3), device=dev)
-            acc = torch.empty((B,), device=dev)
-            weights = torch.empty((B, S), device=dev)
-            depth = torch.empty((B,), device=dev)
-            ev = _events(timers)
-            L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
-                   B, S, int(bool(white_bkgd)), L.ACT_VANILLA if noisy else L.ACT_NONE,
-                   L.ptr(comp), L.ptr(acc), L.ptr(weights), L.ptr(depth), L.stream(dev))
-            _record(timers, ev, f"comp{level}", B * S)
-            out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
-            if return_intermediates:
-                out = out + (dict(t_vals=t_vals, weights=weights, rgb_sigma=raw),)
+            if training:
+                from .train import RenderLevel
+                noise = None
+                if self.noise_std > 0 and randomized:  # model.py:183-184
+                    noise = torch.rand((B * S,), device=dev) * self.noise_std
+                params = [p for m in mlp._layers() for p in (m.weight, m.bias)]
+                comp, acc, depth, weights = RenderLevel.apply(o, d, v, t_vals, bool(white_bkgd),
+                                                              noise, *params)
+                out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
+                if return_intermediates:
+                    out = out + (dict(t_vals=t_vals, weights=weights),)
+                ret.append(out)
+                continue
+            with torch.no_grad():
+                out, weights = self._render_level_fused(mlp, o, d, v, t_vals, randomized,
+                                                        white_bkgd, level, timers)
+            if not return_weights:
+                out = out[:3] + out[4:]
+            if not return_intermediates:
+                out = out[:4] if return_weights else out[:3]
             ret.append(out)
         return ret
+
+    def _level_t(self, level, o, d, t_prev, w_prev, randomized, near, far, u_coarse, u_fine):
+        """Sample positions of a level: stratified (helper.py:106-133) or inverse-CDF resampling
+        of the previous level's weights merged with its samples (model.py:163-172)."""
+        dev = o.device
+        B = o.shape[0]
+        if level == 0:
+            t_vals, _ = helper.sample_along_rays(o, d, self.num_coarse_samples, near, far,
+                                                 randomized, self.lindisp, u=u_coarse,
+                                                 want_coords=False)
+            return t_vals
+        Sc = t_prev.shape[1]
+        if randomized:
+            u = torch.rand((B, self.num_fine_samples), device=dev) if u_fine is None else L.contig(u_fine)
+            u_stride = self.num_fine_samples
+        else:
+            u, u_stride = helper.eval_u(self.num_fine_samples, dev), 0
+        w_prev = L.contig(w_prev.detach())
+        t_new = torch.empty((B, Sc + self.num_fine_samples), device=dev)
+        # bins = mids of t (model.py:163), weights[..., 1:-1] as a strided view
+        L.call("aon_sample_pdf", None, 0, L.ptr(w_prev[:, 1:]), Sc, B, Sc - 1,
+               self.num_fine_samples, L.ptr(u), u_stride, L.ptr(t_prev), Sc, None, None,
+               L.ptr(t_new), None, L.stream(dev))
+        return t_new
+
+    def _render_level_fused(self, mlp, o, d, v, t_vals, randomized, white_bkgd, level, timers):
+        B, S = t_vals.shape
+        dev = o.device
+        # the activations (model.py:186-187) run in the MLP epilogue, unless density noise
+        # must be added to the raw sigma first (model.py:183-184)
+        noisy = self.noise_std > 0 and randomized
+        ev = _events(timers)
+        raw = mlp.forward_rays(o, d, v, t_vals, act=L.ACT_NONE if noisy else L.ACT_VANILLA)
+        _record(timers, ev, f"mlp{level}", B * S)
+        if noisy:
+            raw[:, 3] += torch.rand_like(raw[:, 3]) * self.noise_std
+        comp = torch.empty((B, 3), device=dev)
+        acc = torch.empty((B,), device=dev)
+        weights = torch.empty((B, S), device=dev)
+        depth = torch.empty((B,), device=dev)
+        ev = _events(timers)
+        L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
+               B, S, int(bool(white_bkgd)), L.ACT_VANILLA if noisy else L.ACT_NONE,
+               L.ptr(comp), L.ptr(acc), L.ptr(weights), L.ptr(depth), L.stream(dev))
+        _record(timers, ev, f"comp{level}", B * S)
+        return (comp, acc, depth, weights, dict(t_vals=t_vals, weights=weights, rgb_sigma=raw)), weights

@@ -1,0 +1,288 @@
+"""Training step of the reference (LitNeRF.training_step, model.py:256-282; configure_optimizers /
+optimizer_step, model.py:386-419) on the HIP kernels.
+
+One render level under autograd is ``RenderLevel`` (a torch.autograd.Function):
+
+  forward   pos_enc (aon_pos_enc) -> 11 layer GEMMs keeping every activation (aon_gemm: bias,
+            ReLU, the skip concat cat[h4, enc] and the view concat cat[bottleneck, enc_dir
+            tiled over samples] read in place) -> compositing (aon_composite_fwd, raw outputs +
+            sigmoid/relu as model.py:186-187)
+  backward  aon_composite_bwd (dL/draw) -> per layer, last to first: dW = dY^T X and
+            db = colsum(dY) (split-K, deterministic), dX = (dY W) * relu'(X) (aon_gemm mask)
+
+Gradients land in each parameter's ``.grad`` through autograd, so the reference's own
+optimizer code runs unchanged; ``Adam`` below is the fused replacement (aon_adam_step) with
+the reference's learning-rate schedule.  All arithmetic is in the HIP kernels; torch only
+allocates buffers and routes autograd.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+# power-of-two operand prescales of the fp16 hi/lo split (exact): activations at 2^-8 (fp16
+# range up to 1.6e7, as the fused forward), gradients at 2^10 (dL/d* of a mean loss are small;
+# this keeps their hi parts out of fp16's subnormal range), weights unscaled.
+ACT_SCALE, GRAD_SCALE, W_SCALE = 2.0 ** -8, 2.0 ** 10, 1.0
+
+_ws = {}
+
+
+def _workspace(nbytes, device):
+    key = str(device)
+    buf = _ws.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _ws[key] = buf
+    return buf
+
+
+def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, a2_rdiv=1,
+         b_rdiv=1, bias=None, mask=None, ldm=0, relu=False, accumulate=False, a_scale=1.0,
+         b_scale=1.0, k_splits=0):
+    """aon_gemm on tensor views (each operand's data_ptr carries its own offset)."""
+    a = L.AonGemmArgs(M=M, N=N, K=K, A=A.data_ptr(), lda=lda, a_kc=int(a_kc),
+                      A2=A2.data_ptr() if A2 is not None else None, lda2=lda2, K1=K1,
+                      a2_rdiv=a2_rdiv, B=B.data_ptr(), ldb=ldb, b_kc=int(b_kc), b_rdiv=b_rdiv,
+                      C=C.data_ptr(), ldc=ldc, bias=bias.data_ptr() if bias is not None else None,
+                      mask=mask.data_ptr() if mask is not None else None, ldm=ldm,
+                      relu=int(relu), accumulate=int(accumulate), a_scale=a_scale,
+                      b_scale=b_scale, k_splits=k_splits)
+    nbytes = L.lib().aon_gemm_workspace_bytes(ctypes.byref(a))
+    ws = _workspace(nbytes, C.device) if nbytes else None
+    L.call("aon_gemm", ctypes.byref(a), L.ptr(ws), nbytes, L.stream(C.device))
+
+
+def colsum(out, X, M, N, ldx, accumulate=False):
+    nbytes = L.lib().aon_colsum_workspace_bytes(M, N)
+    ws = _workspace(nbytes, X.device)
+    L.call("aon_colsum", L.ptr(X), ldx, M, N, int(accumulate), L.ptr(out), L.ptr(ws), nbytes,
+           L.stream(X.device))
+
+
+def linear_fwd(out, X, Kx, W, b, *, ldx=None, ldo=None, relu=False, X2=None, K2=0, ld2=0, rdiv2=1,
+               accumulate=False):
+    """out (R x N) (+)= [X | X2] W^T + b (+ReLU); W is the nn.Linear weight (N x (Kx+K2))."""
+    R, N = out.shape[0], W.shape[0]
+    gemm(out, X, W, R, N, Kx + K2, lda=ldx or Kx, a_kc=True, ldb=W.shape[1], b_kc=True,
+         ldc=ldo or out.shape[1], A2=X2, lda2=ld2, K1=Kx if X2 is not None else 0, a2_rdiv=rdiv2,
+         bias=b, relu=relu, accumulate=accumulate, a_scale=ACT_SCALE, b_scale=W_SCALE)
+
+
+# ---------------------------------------------------------------------------- one render level
+def _mlp_params(mlp):
+    """(weight, bias) of pts_linears[0..7], density, bottleneck, views[0], rgb."""
+    return [(m.weight, m.bias) for m in mlp._layers()]
+
+
+def _forward_level(P, enc, venc, S, raw, noise=None):
+    """NeRFMLP.forward (model.py:95-120) layer by layer; returns the kept activations."""
+    R, dev = enc.shape[0], enc.device
+    h = [torch.empty((R, 256), device=dev) for _ in range(8)]
+    linear_fwd(h[0], enc, 63, *P[0], relu=True)
+    for i in range(1, 8):
+        if i == 5:  # cat[h4, enc] (model.py:102-103)
+            linear_fwd(h[5], h[4], 256, *P[5], relu=True, X2=enc, K2=63, ld2=63)
+        else:
+            linear_fwd(h[i], h[i - 1], 256, *P[i], relu=True)
+    if noise is not None:  # raw_sigma + noise (model.py:183-184), added in the GEMM epilogue
+        raw[:, 3].copy_(noise)
+    linear_fwd(raw[:, 3:], h[7], 256, *P[8], ldo=4, accumulate=noise is not None)  # (:105-107)
+    bot = torch.empty((R, 256), device=dev)
+    linear_fwd(bot, h[7], 256, *P[9])                                    # bottleneck, no act
+    hv = torch.empty((R, 128), device=dev)
+    linear_fwd(hv, bot, 256, *P[10], relu=True, X2=venc, K2=27, ld2=27, rdiv2=S)  # (:110-116)
+    linear_fwd(raw, hv, 128, *P[11], ldo=4)                              # rgb (model.py:118)
+    return h, bot, hv
+
+
+def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
+    """Autograd of _forward_level: G[i] = (dW, db) of layer i, from dL/draw (R x 4)."""
+    R, dev = enc.shape[0], enc.device
+    gs, acts = GRAD_SCALE, ACT_SCALE
+
+    def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, ldw=None):
+        # dW[:, col0:col0+n_in] = dY^T X   (K = rows, split over workgroups)
+        gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
+             b_kc=False, b_rdiv=rdiv, ldc=ldw or dW.shape[1], a_scale=gs, b_scale=acts)
+
+    def dinput(dX, dY, ldy, n_out, W, n_in, mask=None, accumulate=False):
+        # dX (R x n_in) = dY W[:, :n_in] (* relu mask)
+        gemm(dX, dY, W, R, n_in, n_out, lda=ldy, a_kc=True, ldb=W.shape[1], b_kc=False,
+             ldc=dX.shape[1], mask=mask, ldm=mask.shape[1] if mask is not None else 0,
+             accumulate=accumulate, a_scale=gs, b_scale=W_SCALE)
+
+    # rgb head (N=3) and view layer
+    dweight(G[11][0], draw, 4, 3, hv, 128, 128)
+    colsum(G[11][1], draw, R, 3, 4)
+    dhv = torch.empty((R, 128), device=dev)
+    dinput(dhv, draw, 4, 3, P[11][0], 128, mask=hv)
+    dweight(G[10][0], dhv, 128, 128, bot, 256, 256)
+    dweight(G[10][0], dhv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
+    colsum(G[10][1], dhv, R, 128, 128)
+    dbot = torch.empty((R, 256), device=dev)
+    dinput(dbot, dhv, 128, 128, P[10][0], 256)
+    del dhv
+    # bottleneck + density heads on h7
+    dweight(G[9][0], dbot, 256, 256, h[7], 256, 256)
+    colsum(G[9][1], dbot, R, 256, 256)
+    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256)
+    colsum(G[8][1], draw[:, 3:], R, 1, 4)
+    dy = torch.empty((R, 256), device=dev)
+    dinput(dy, dbot, 256, 256, P[9][0], 256)
+    dinput(dy, draw[:, 3:], 4, 1, P[8][0], 256, mask=h[7], accumulate=True)
+    del dbot
+    dx = torch.empty((R, 256), device=dev)
+    for i in range(7, -1, -1):  # dy = dL/d(pre-activation of layer i)
+        if i == 5:
+            dweight(G[5][0], dy, 256, 256, h[4], 256, 256)
+            dweight(G[5][0], dy, 256, 256, enc, 63, 63, col0=256)
+        elif i == 0:
+            dweight(G[0][0], dy, 256, 256, enc, 63, 63)
+        else:
+            dweight(G[i][0], dy, 256, 256, h[i - 1], 256, 256)
+        colsum(G[i][1], dy, R, 256, 256)
+        if i > 0:
+            dinput(dx, dy, 256, 256, P[i][0], 256, mask=h[i - 1])
+            dx, dy = dy, dx
+
+
+class RenderLevel(torch.autograd.Function):
+    """cast_rays + pos_enc + NeRFMLP + activations + volumetric_rendering of one level
+    (model.py:175-197) with gradients for the level's 24 MLP parameters."""
+
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise, *params):
+        B, S = t_vals.shape
+        R, dev = B * S, t_vals.device
+        # xyz = o + t d (helper.py:25-26) straight into the encodings (helper.py:136-140)
+        enc = torch.empty((R, 63), device=dev)
+        L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0, 10,
+               L.ptr(enc), L.stream(dev))
+        venc = torch.empty((B, 27), device=dev)
+        L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, 4, L.ptr(venc), L.stream(dev))
+        P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
+        raw = torch.empty((R, 4), device=dev)
+        h, bot, hv = _forward_level(P, enc, venc, S, raw, noise)
+        comp = torch.empty((B, 3), device=dev)
+        acc = torch.empty((B,), device=dev)
+        weights = torch.empty((B, S), device=dev)
+        depth = torch.empty((B,), device=dev)
+        L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals),
+               L.ptr(rays_d), B, S, int(bool(white_bkgd)), L.ACT_VANILLA, L.ptr(comp), L.ptr(acc),
+               L.ptr(weights), L.ptr(depth), L.stream(dev))
+        ctx.save_for_backward(rays_d, t_vals, enc, venc, raw, bot, hv, *h, *params)
+        ctx.meta = (B, S, bool(white_bkgd))
+        ctx.mark_non_differentiable(weights)
+        return comp, acc, depth, weights
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_acc, g_depth, _g_w):
+        B, S, white = ctx.meta
+        saved = ctx.saved_tensors
+        rays_d, t_vals, enc, venc, raw, bot, hv = saved[:7]
+        h = list(saved[7:15])
+        params = saved[15:]
+        dev = raw.device
+        R = B * S
+        draw = torch.empty((R, 4), device=dev)
+        g_rgb = L.contig(g_rgb)
+        L.call("aon_composite_bwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals),
+               L.ptr(rays_d), B, S, int(white), L.ACT_VANILLA, L.ptr(g_rgb),
+               L.ptr(L.contig(g_acc)) if g_acc is not None else None,
+               L.ptr(L.contig(g_depth)) if g_depth is not None else None,
+               L.ptr(draw), L.ptr(draw[:, 3:]), 4, L.stream(dev))
+        P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
+        G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
+        _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
+        grads = [g for pair in G for g in pair]
+        return (None, None, None, None, None, None, *grads)
+
+
+class Mse(torch.autograd.Function):
+    """img2mse (helper.py:17-18) on aon_mse."""
+
+    @staticmethod
+    def forward(ctx, pred, target):
+        L.require_gpu(pred, target)
+        pred, target = L.contig(pred), L.contig(target)
+        loss = torch.empty((), device=pred.device)
+        grad = torch.empty_like(pred)
+        L.call("aon_mse", L.ptr(pred), L.ptr(target), pred.numel(), 1.0, L.ptr(loss), L.ptr(grad),
+               L.stream(pred.device))
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g, None
+
+
+def img2mse(x, y):
+    return Mse.apply(x, y)
+
+
+def mse2psnr(x):
+    """helper.py:21-22 (host-side scalar formula)."""
+    return -10.0 * torch.log(x) / np.log(10.0)
+
+
+def training_step(model, batch, randomized, white_bkgd, near, far, *, u_coarse=None, u_fine=None):
+    """LitNeRF.training_step (model.py:256-282): loss = mse(fine) + mse(coarse) and the psnrs."""
+    ret = model(batch, randomized, white_bkgd, near, far, u_coarse=u_coarse, u_fine=u_fine)
+    target = batch["target"]
+    loss0 = img2mse(ret[0][0], target)
+    loss1 = img2mse(ret[1][0], target)
+    loss = loss1 + loss0
+    return loss, dict(loss0=loss0, loss1=loss1, psnr0=mse2psnr(loss0.detach()),
+                      psnr1=mse2psnr(loss1.detach()))
+
+
+# ---------------------------------------------------------------------------- optimizer
+def learning_rate(step, max_steps, lr_init=5.0e-4, lr_final=5.0e-6, lr_delay_steps=2500,
+                  lr_delay_mult=0.01):
+    """LitNeRF.optimizer_step's schedule (model.py:399-416), host-side like the reference."""
+    if lr_delay_steps > 0:
+        delay_rate = lr_delay_mult + (1 - lr_delay_mult) * np.sin(
+            0.5 * np.pi * np.clip(step / lr_delay_steps, 0, 1))
+    else:
+        delay_rate = 1.0
+    t = np.clip(step / max_steps, 0, 1)
+    scaled_lr = np.exp(np.log(lr_init) * (1 - t) + np.log(lr_final) * t)
+    return float(delay_rate * scaled_lr)
+
+
+class Adam:
+    """torch.optim.Adam(params, lr, betas=(0.9, 0.999)) (model.py:386-389) as one fused
+    aon_adam_step launch over every parameter tensor."""
+
+    def __init__(self, params, lr=5.0e-4, betas=(0.9, 0.999), eps=1e-8):
+        self.params = [p for p in params if p.requires_grad]
+        if len(self.params) > L.ADAM_MAX_TENSORS:
+            raise ValueError(f"at most {L.ADAM_MAX_TENSORS} parameter tensors")
+        L.require_gpu(*self.params)
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.state = [(torch.zeros_like(p), torch.zeros_like(p)) for p in self.params]
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            p.grad = None
+
+    @torch.no_grad()
+    def step(self, lr=None):
+        self.step_count += 1
+        table = (L.AonAdamTensor * len(self.params))()
+        for i, (p, (m, v)) in enumerate(zip(self.params, self.state)):
+            if p.grad is None:
+                raise RuntimeError("Adam.step: a parameter has no gradient")
+            if not p.is_contiguous() or not p.grad.is_contiguous():
+                raise ValueError("Adam.step: parameters and grads must be contiguous")
+            table[i] = L.AonAdamTensor(p.data_ptr(), p.grad.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                       p.numel())
+        L.call("aon_adam_step", table, len(self.params), float(self.lr if lr is None else lr),
+               float(self.betas[0]), float(self.betas[1]), float(self.eps), self.step_count,
+               L.stream(self.params[0].device))

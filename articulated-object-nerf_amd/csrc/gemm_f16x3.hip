@@ -1,0 +1,338 @@
+// General fp32-in / fp32-out GEMM on fp16 MFMA with the 3-product hi/lo split (see
+// mlp_f16x3.hip for the numerics), for the layer-by-layer training path: the forward layers
+// with their activations kept (model.py:95-120), the input-gradient products dX = dY . W and
+// the weight gradients dW = dY^T . X of the reference's autograd backward (model.py:256-282).
+//
+//   C (M x N) = epilogue( A (M x K) . B (K x N) )
+//
+// Workgroup: 256 threads = 4 waves in 2 x 2, C tile 128 x 128, each wave 64 x 64 = 4 x 4
+// MFMA 16x16 tiles with two fp32 accumulators (hi*hi and the 2^11-scaled cross terms).  Per
+// 32-deep k-step the A and B tiles are loaded into registers (global, one step ahead), split
+// into fp16 hi / lo planes and stored to a double-buffered LDS image laid out [row][k] (k
+// contiguous, 80-B rows), from which each lane reads its 8-element MFMA fragments with one
+// ds_read_b128; one barrier per k-step.  Operands stored reduction-major (A as [K][M], B as
+// [K][N]) are transposed in registers while staging (4 x 4 blocks), so every GEMM of the
+// backward pass reads its operands in place.
+#include "aon_common.hpp"
+
+namespace aon {
+namespace gemm {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 32, THREADS = 256;
+constexpr int ROWH = BK + 8;                 // halves per LDS row: 80 B, 16-B aligned
+constexpr int PLANE = BM * ROWH;             // halves per plane (BM == BN)
+constexpr int STAGE = 4 * PLANE;             // A hi, A lo, B hi, B lo
+constexpr float kLo = 2048.0f;               // lo planes carry (x - hi) * 2^11
+constexpr float kInvLo = 1.0f / 2048.0f;
+
+struct Params {
+  int64_t M, N, K;
+  const float* A;
+  int64_t lda;
+  const float* A2;  // a_kc only: columns [K1, K) from A2[(m / a2_rdiv) * lda2 + (k - K1)]
+  int64_t lda2, K1, a2_rdiv;
+  const float* B;
+  int64_t ldb, b_rdiv;  // !b_kc: element (k, n) = B[(k / b_rdiv) * ldb + n]
+  float* C;
+  int64_t ldc;
+  const float* bias;  // per column n
+  const float* mask;  // v *= (mask[m * ldm + n] > 0)
+  int64_t ldm;
+  int relu, accumulate;
+  float sa, sb, inv_s;  // operand prescales (powers of two); result * inv_s
+  int64_t kchunk;       // K rows per blockIdx.z (split-K); == K when not split
+  float* part;          // split-K partials [z][M][N] (unscaled epilogue-free sums * inv_s)
+};
+
+__device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// 4 consecutive k values of one row -> hi / lo halves
+__device__ __forceinline__ void split4(f4 v, float s, h4& hi, h4& lo) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x = v[j] * s;  // power-of-two prescale: exact
+    const _Float16 h = static_cast<_Float16>(x);
+    hi[j] = h;
+    lo[j] = static_cast<_Float16>(__fmul_rn(__fsub_rn(x, static_cast<float>(h)), kLo));
+  }
+}
+
+// ---- tile loaders: 128 rows x 32 k of one operand into 4 f4 registers per thread -------------
+// KC (k-contiguous rows): thread t -> rows (t >> 3) + 32 i, k quad 4 (t & 7).
+// KM (k-major storage, rows contiguous): thread t -> k quad 4 (t >> 5), row quad 4 (t & 31);
+//     register i holds k = kq + i for rows rq..rq+3 (transposed when stored).
+template <bool KC, bool VEC>
+struct TileLoad {
+  f4 r[4];
+
+  // rows/k outside [0,R) x [k0, kend) read as 0.  KC: k >= K1 from p2 (row / rdiv);
+  // KM: storage row k / rdiv.
+  __device__ __forceinline__ void load(const float* p, int64_t ld, const float* p2, int64_t ld2,
+                                       int64_t K1, int64_t rdiv, int64_t row0, int64_t R,
+                                       int64_t k0, int64_t kend, int tid) {
+    if (KC) {
+      const int kq = 4 * (tid & 7);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = row0 + (tid >> 3) + 32 * i;
+        const int64_t k = k0 + kq;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (row < R) {
+          if (VEC && k + 3 < kend && k + 3 < K1) {
+            v = *reinterpret_cast<const f4*>(p + row * ld + k);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int64_t kk = k + j;
+              if (kk < kend) v[j] = kk < K1 ? p[row * ld + kk] : p2[(row / rdiv) * ld2 + (kk - K1)];
+            }
+          }
+        }
+        r[i] = v;
+      }
+    } else {
+      const int kq = 4 * (tid >> 5), rq = 4 * (tid & 31);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t k = k0 + kq + i;
+        const int64_t row = row0 + rq;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (k < kend) {
+          const float* src = p + (rdiv == 1 ? k : k / rdiv) * ld + row;
+          if (VEC && row + 3 < R) {
+            v = *reinterpret_cast<const f4*>(src);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (row + j < R) v[j] = src[j];
+          }
+        }
+        r[i] = v;
+      }
+    }
+  }
+
+  // split and store into the [row][k] hi / lo planes
+  __device__ __forceinline__ void store(_Float16* hi, _Float16* lo, float s, int tid) const {
+    if (KC) {
+      const int kq = 4 * (tid & 7);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = (tid >> 3) + 32 * i;
+        h4 h, l;
+        split4(r[i], s, h, l);
+        *reinterpret_cast<h4*>(hi + row * ROWH + kq) = h;
+        *reinterpret_cast<h4*>(lo + row * ROWH + kq) = l;
+      }
+    } else {
+      const int kq = 4 * (tid >> 5), rq = 4 * (tid & 31);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // row rq + j: k = kq .. kq + 3 from r[0..3][j]
+        const f4 v = {r[0][j], r[1][j], r[2][j], r[3][j]};
+        h4 h, l;
+        split4(v, s, h, l);
+        *reinterpret_cast<h4*>(hi + (rq + j) * ROWH + kq) = h;
+        *reinterpret_cast<h4*>(lo + (rq + j) * ROWH + kq) = l;
+      }
+    }
+  }
+};
+
+template <bool AKC, bool BKC, bool VA, bool VB>
+__global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
+  __shared__ __align__(16) _Float16 smem[2 * STAGE];  // 2 stages x (A hi, A lo, B hi, B lo)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  const int64_t kbeg = (int64_t)blockIdx.z * p.kchunk;
+  const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
+
+  TileLoad<AKC, VA> ta;
+  TileLoad<BKC, VB> tb;
+  f4 acc_h[4][4], acc_x[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc_h[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+      acc_x[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  auto load = [&](int kt) {
+    const int64_t k0 = kbeg + (int64_t)kt * BK;
+    ta.load(p.A, p.lda, p.A2, p.lda2, p.K1, p.a2_rdiv, m0, p.M, k0, kend, tid);
+    tb.load(p.B, p.ldb, nullptr, 0, INT64_MAX, p.b_rdiv, n0, p.N, k0, kend, tid);
+  };
+  auto store = [&](int stage) {
+    _Float16* s = smem + stage * STAGE;
+    ta.store(s, s + PLANE, p.sa, tid);
+    tb.store(s + 2 * PLANE, s + 3 * PLANE, p.sb, tid);
+  };
+
+  if (nk > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load(kt + 1);  // global loads in flight under this step's MFMAs
+    const _Float16* s = smem + (kt & 1) * STAGE;
+    h8 bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wn * 64 + 16 * j + r16;
+      bh[j] = *reinterpret_cast<const h8*>(s + 2 * PLANE + row * ROWH + 8 * g);
+      bl[j] = *reinterpret_cast<const h8*>(s + 3 * PLANE + row * ROWH + 8 * g);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + 16 * i + r16;
+      const h8 ah = *reinterpret_cast<const h8*>(s + row * ROWH + 8 * g);
+      const h8 al = *reinterpret_cast<const h8*>(s + PLANE + row * ROWH + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc_h[i][j] = mfma16(ah, bh[j], acc_h[i][j]);
+        acc_x[i][j] = mfma16(ah, bl[j], acc_x[i][j]);
+        acc_x[i][j] = mfma16(al, bh[j], acc_x[i][j]);
+      }
+    }
+    if (kt + 1 < nk) store((kt + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: D lane layout col = lane & 15, rows 4 (lane >> 4) + r
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + 16 * j + r16;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+        if (m >= p.M) continue;
+        float v = __fmul_rn(__fadd_rn(acc_h[i][j][r], __fmul_rn(acc_x[i][j][r], kInvLo)), p.inv_s);
+        if (split) {
+          p.part[((int64_t)blockIdx.z * p.M + m) * p.N + n] = v;
+          continue;
+        }
+        float* c = p.C + m * p.ldc + n;
+        if (p.accumulate) v = __fadd_rn(*c, v);
+        if (p.bias) v = __fadd_rn(v, p.bias[n]);
+        if (p.relu) v = fmaxf(v, 0.0f);
+        if (p.mask && !(p.mask[m * p.ldm + n] > 0.0f)) v = 0.0f;
+        *c = v;
+      }
+    }
+}
+
+// split-K: C = epilogue(sum_z part[z]) in z order (deterministic)
+__global__ void k_gemm_reduce(Params p, int splits) {
+  const int64_t total = p.M * p.N;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = e / p.N, n = e - m * p.N;
+    float v = p.part[e];
+    for (int z = 1; z < splits; ++z) v = __fadd_rn(v, p.part[(int64_t)z * total + e]);
+    float* c = p.C + m * p.ldc + n;
+    if (p.accumulate) v = __fadd_rn(*c, v);
+    if (p.bias) v = __fadd_rn(v, p.bias[n]);
+    if (p.relu) v = fmaxf(v, 0.0f);
+    if (p.mask && !(p.mask[m * p.ldm + n] > 0.0f)) v = 0.0f;
+    *c = v;
+  }
+}
+
+template <bool AKC, bool BKC, bool VA, bool VB>
+static void launch(const Params& p, dim3 grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_gemm_f16x3<AKC, BKC, VA, VB>), grid, dim3(THREADS), 0, st, p);
+}
+
+template <bool AKC, bool BKC>
+static void launch_v(const Params& p, bool va, bool vb, dim3 grid, hipStream_t st) {
+  if (va && vb) launch<AKC, BKC, true, true>(p, grid, st);
+  else if (va) launch<AKC, BKC, true, false>(p, grid, st);
+  else if (vb) launch<AKC, BKC, false, true>(p, grid, st);
+  else launch<AKC, BKC, false, false>(p, grid, st);
+}
+
+}  // namespace gemm
+}  // namespace aon
+
+using namespace aon;
+using namespace aon::gemm;
+
+static int64_t gemm_splits(const aon_gemm_args* a) {
+  const int64_t tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
+  // split the reduction only when the tile grid alone cannot fill the chip and K is long
+  if (a->k_splits > 0) return a->k_splits;
+  if (tiles >= 512 || a->K < 8 * 1024 || a->A2) return 1;
+  int64_t s = (1024 + tiles - 1) / tiles;
+  const int64_t smax = a->K / 2048;
+  if (s > smax) s = smax;
+  if (s > 256) s = 256;
+  return s < 1 ? 1 : s;
+}
+
+extern "C" size_t aon_gemm_workspace_bytes(const aon_gemm_args* a) {
+  if (!a) return 0;
+  const int64_t s = gemm_splits(a);
+  return s > 1 ? (size_t)s * a->M * a->N * sizeof(float) : 0;
+}
+
+extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
+                        aon_stream_t stream) {
+  AON_REQUIRE(a, "null args");
+  AON_REQUIRE(a->A && a->B && a->C, "null operand");
+  AON_REQUIRE(a->M >= 0 && a->N >= 0 && a->K >= 0, "bad shape");
+  AON_REQUIRE(a->lda >= 1 && a->ldb >= 1 && a->ldc >= a->N, "bad leading dimension");
+  AON_REQUIRE(!a->A2 || (a->a_kc && a->K1 >= 0 && a->K1 <= a->K && a->lda2 >= 1 && a->a2_rdiv >= 1),
+              "A2 needs a_kc, 0 <= K1 <= K, lda2 >= 1, a2_rdiv >= 1");
+  AON_REQUIRE(!a->mask || a->ldm >= a->N, "bad mask leading dimension");
+  AON_REQUIRE(a->b_kc || a->b_rdiv >= 1, "b_rdiv must be >= 1");
+  AON_REQUIRE(a->a_scale > 0.f && a->b_scale > 0.f, "operand scales must be positive");
+  if (a->M == 0 || a->N == 0) return 0;
+  Params p;
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.A = a->A; p.lda = a->lda;
+  p.A2 = a->A2; p.lda2 = a->A2 ? a->lda2 : 0; p.K1 = a->A2 ? a->K1 : INT64_MAX;
+  p.a2_rdiv = a->A2 ? a->a2_rdiv : 1;
+  p.B = a->B; p.ldb = a->ldb; p.b_rdiv = a->b_kc ? 1 : a->b_rdiv;
+  p.C = a->C; p.ldc = a->ldc;
+  p.bias = a->bias; p.mask = a->mask; p.ldm = a->ldm;
+  p.relu = a->relu; p.accumulate = a->accumulate;
+  p.sa = a->a_scale; p.sb = a->b_scale; p.inv_s = 1.0f / (a->a_scale * a->b_scale);
+  const int64_t splits = gemm_splits(a);
+  p.kchunk = splits > 1 ? ((a->K + splits - 1) / splits + BK - 1) / BK * BK : (a->K > 0 ? a->K : 1);
+  const int64_t zs = a->K > 0 ? (a->K + p.kchunk - 1) / p.kchunk : 1;
+  p.part = nullptr;
+  if (zs > 1) {
+    AON_REQUIRE(work && work_bytes >= (size_t)zs * a->M * a->N * sizeof(float),
+                "split-K needs aon_gemm_workspace_bytes() of workspace");
+    p.part = static_cast<float*>(work);
+  }
+  AON_REQUIRE((a->M + BM - 1) / BM < 65536 && (a->N + BN - 1) / BN < (1ll << 31), "too large");
+  const dim3 grid((unsigned)((a->N + BN - 1) / BN), (unsigned)((a->M + BM - 1) / BM), (unsigned)zs);
+  // float4 staging when the 4-element runs are 16-B aligned
+  const bool va = aligned16(a->A) && a->lda % 4 == 0 && (!a->A2 || a->K1 % 4 == 0);
+  const bool vb = aligned16(a->B) && a->ldb % 4 == 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (a->a_kc && a->b_kc) launch_v<true, true>(p, va, vb, grid, st);
+  else if (a->a_kc) launch_v<true, false>(p, va, vb, grid, st);
+  else if (a->b_kc) launch_v<false, true>(p, va, vb, grid, st);
+  else launch_v<false, false>(p, va, vb, grid, st);
+  if (zs > 1) {
+    const int rc = launch_status(__func__);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gemm_reduce, grid_for(a->M * a->N, 256, 4096), 256, 0, st, p, (int)zs);
+  }
+  return launch_status(__func__);
+}

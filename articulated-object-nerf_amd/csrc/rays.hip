@@ -130,6 +130,27 @@ __global__ void k_pos_enc(const float* __restrict__ x, int64_t n, int min_deg, i
   }
 }
 
+// cast_rays (helper.py:25-26) on per-ray t (B, S), optionally straight into pos_enc
+// (helper.py:136-140): one thread per (sample, output feature)
+__global__ void k_cast_rays(const float* __restrict__ ro, const float* __restrict__ rd,
+                            const float* __restrict__ t, int64_t B, int S,
+                            float* __restrict__ xyz, int min_deg, int L, float* __restrict__ enc) {
+  const int C = enc ? 3 + 6 * L : 3;
+  const int64_t total = B * S * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / C;
+    const int f = static_cast<int>(i - r * C);
+    const int64_t b = r / S;
+    const float tv = t[r];
+    const float x0 = __fadd_rn(ro[3 * b], __fmul_rn(tv, rd[3 * b]));
+    const float x1 = __fadd_rn(ro[3 * b + 1], __fmul_rn(tv, rd[3 * b + 1]));
+    const float x2 = __fadd_rn(ro[3 * b + 2], __fmul_rn(tv, rd[3 * b + 2]));
+    if (xyz && f < 3) xyz[3 * r + f] = f == 0 ? x0 : (f == 1 ? x1 : x2);
+    if (enc) enc[i] = pos_enc_feature(x0, x1, x2, f, min_deg, L);
+  }
+}
+
 static Mat34 load_c2w(const float* h) {
   Mat34 m;
   for (int i = 0; i < 12; ++i) m.m[i] = h[i];
@@ -194,5 +215,18 @@ extern "C" int aon_pos_enc(const float* x, int64_t n, int min_deg, int max_deg, 
   const int L = max_deg - min_deg;
   hipLaunchKernelGGL(k_pos_enc, grid_for(n * (3 + 6 * L), 256, 65536), 256, 0, (hipStream_t)stream,
                      x, n, min_deg, L, out);
+  return launch_status(__func__);
+}
+
+extern "C" int aon_cast_rays(const float* rays_o, const float* rays_d, const float* t, int64_t B,
+                             int S, float* xyz, int min_deg, int max_deg, float* enc,
+                             aon_stream_t stream) {
+  AON_REQUIRE(rays_o && rays_d && t && (xyz || enc) && B >= 0 && S >= 1, "bad arguments");
+  AON_REQUIRE(!enc || (max_deg >= min_deg && min_deg >= -126 && max_deg <= 127), "bad degrees");
+  if (B == 0) return 0;
+  const int L = max_deg - min_deg;
+  const int C = enc ? 3 + 6 * L : 3;
+  hipLaunchKernelGGL(k_cast_rays, grid_for(B * S * C, 256, 65536), 256, 0, (hipStream_t)stream,
+                     rays_o, rays_d, t, B, S, xyz, min_deg, L, enc);
   return launch_status(__func__);
 }

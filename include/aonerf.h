@@ -67,6 +67,11 @@ int aon_sample_along_rays(const float* rays_o, const float* rays_d, int64_t B, i
                           const float* t_lower, const float* t_upper, const float* u,
                           float* t_out, float* xyz_out, aon_stream_t stream);
 
+/* cast_rays (helper.py:25-26) on per-ray sample positions t (B, S): xyz (B*S, 3) and/or
+ * enc = pos_enc(xyz, min_deg, max_deg) (B*S, 3 + 6 (max_deg - min_deg)) in one pass. */
+int aon_cast_rays(const float* rays_o, const float* rays_d, const float* t, int64_t B, int S,
+                  float* xyz, int min_deg, int max_deg, float* enc, aon_stream_t stream);
+
 /* pos_enc (helper.py:136-140): out (n, 3 + 6*(max_deg-min_deg)). */
 int aon_pos_enc(const float* x, int64_t n, int min_deg, int max_deg, float* out,
                 aon_stream_t stream);
@@ -131,6 +136,81 @@ int aon_composite_fwd(const float* rgb, int64_t rgb_stride, const float* sigma,
                       int64_t sigma_stride, const float* t, const float* dirs, int64_t B,
                       int S, int white_bkgd, int act, float* comp_rgb, float* acc,
                       float* weights, float* depth, aon_stream_t stream);
+
+/* ---------------------------------------------------------------- training path */
+/* C (M x N) = epilogue(A (M x K) . B (K x N)): fp32 operands, fp16-MFMA hi/lo split
+ * (fp32-class accuracy), the building block of the layer-by-layer training forward
+ * (model.py:95-120 with activations kept) and of its autograd backward (model.py:256-282):
+ *   A: a_kc = 1 -> element (m, k) = A[m*lda + k] for k < K1, and, when A2 != NULL,
+ *                  A2[(m / a2_rdiv)*lda2 + (k - K1)] for k >= K1 (cat[h, enc] of model.py:102,
+ *                  cat[bottleneck, enc_dir tiled over samples] of model.py:110-112);
+ *      a_kc = 0 -> element (m, k) = A[k*lda + m] (dY^T of a weight gradient).
+ *   B: b_kc = 1 -> element (k, n) = B[n*ldb + k] (nn.Linear weight [out][in]: x . W^T);
+ *      b_kc = 0 -> element (k, n) = B[(k / b_rdiv)*ldb + n] (W for dX = dY . W; X for
+ *                  dW = dY^T . X; b_rdiv = S broadcasts a per-ray row over its S samples).
+ *   epilogue per element, in this order: v = sum / (a_scale * b_scale); v += C[m*ldc+n] when
+ *   accumulate; v += bias[n]; relu; v *= (mask[m*ldm+n] > 0).  a_scale / b_scale are
+ *   power-of-two operand prescales that keep |x * scale| < 65504 (fp16 range of the hi part).
+ *   Long reductions (K of a weight gradient = rows) are split over workgroups into
+ *   `work` (aon_gemm_workspace_bytes) and summed in a fixed order (deterministic).
+ *   k_splits = 0 chooses the split automatically. */
+typedef struct aon_gemm_args {
+  int64_t M, N, K;
+  const float* A;
+  int64_t lda;
+  int a_kc;
+  const float* A2;
+  int64_t lda2, K1, a2_rdiv;
+  const float* B;
+  int64_t ldb;
+  int b_kc;
+  int64_t b_rdiv;
+  float* C;
+  int64_t ldc;
+  const float* bias;
+  const float* mask;
+  int64_t ldm;
+  int relu, accumulate;
+  float a_scale, b_scale;
+  int64_t k_splits;
+} aon_gemm_args;
+
+size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);
+int aon_gemm(const aon_gemm_args* args, void* work, size_t work_bytes, aon_stream_t stream);
+
+/* Backward of volumetric_rendering (helper.py:157-195) and of the activations `act` applied to
+ * the raw MLP outputs (model.py:186-187): given dL/dcomp_rgb (B,3) and optionally dL/dacc,
+ * dL/ddepth (B,), writes dL/draw_rgb (3 floats at d_rgb + r*d_stride) and dL/draw_sigma
+ * (d_sigma + r*d_stride) for every sample row r.  Inputs as aon_composite_fwd (raw values). */
+int aon_composite_bwd(const float* rgb, int64_t rgb_stride, const float* sigma,
+                      int64_t sigma_stride, const float* t, const float* dirs, int64_t B, int S,
+                      int white_bkgd, int act, const float* g_rgb, const float* g_acc,
+                      const float* g_depth, float* d_rgb, float* d_sigma, int64_t d_stride,
+                      aon_stream_t stream);
+
+/* img2mse (helper.py:17-18): *loss = mean((pred - target)^2) over n values and
+ * grad = grad_scale * 2 (pred - target) / n (either output may be NULL). */
+int aon_mse(const float* pred, const float* target, int64_t n, float grad_scale, float* loss,
+            float* grad, aon_stream_t stream);
+
+/* out[n] (+)= sum_m X[m*ldx + n] (bias gradients), deterministic order. */
+size_t aon_colsum_workspace_bytes(int64_t M, int64_t N);
+int aon_colsum(const float* X, int64_t ldx, int64_t M, int64_t N, int accumulate, float* out,
+               void* work, size_t work_bytes, aon_stream_t stream);
+
+/* torch.optim.Adam step (model.py:386-389; no weight decay / amsgrad) over up to
+ * AON_ADAM_MAX_TENSORS parameter tensors; `step` counts from 1; lr from optimizer_step's
+ * schedule (model.py:399-416). */
+#define AON_ADAM_MAX_TENSORS 64
+typedef struct aon_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+} aon_adam_tensor;
+int aon_adam_step(const aon_adam_tensor* tensors, int count, float lr, float beta1, float beta2,
+                  float eps, int64_t step, aon_stream_t stream);
 
 #ifdef __cplusplus
 }
