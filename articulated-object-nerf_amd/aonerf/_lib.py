@@ -30,7 +30,7 @@ class AonGemmArgs(ctypes.Structure):
                 ("B", vp), ("ldb", c_i64), ("b_kc", c_int), ("b_rdiv", c_i64),
                 ("C", vp), ("ldc", c_i64), ("bias", vp), ("mask", vp), ("ldm", c_i64),
                 ("relu", c_int), ("accumulate", c_int), ("a_scale", c_float), ("b_scale", c_float),
-                ("k_splits", c_i64)]
+                ("k_splits", c_i64), ("rowsum", vp)]
 
 
 class AonAdamTensor(ctypes.Structure):

@@ -54,3 +54,41 @@ def render_frame_sharded(model, c2w, H, W, focal, near=2.0, far=6.0, white_bkgd=
     if world == 1 or not gather:
         return (local[:n] if world == 1 else None), local
     return gather_frame(local, H, W, dst, group), local
+
+
+# ---------------------------------------------------------------------------- training (DDP)
+class GradAllReduce:
+    """Data-parallel gradient averaging for the training step (run.py:109/151 trains with
+    Lightning DDP: every rank draws its own ray batch, gradients are averaged).
+
+    The gradients of all parameters are packed into ONE flat fp32 bucket (vanilla NeRF:
+    1,191,688 values = 4.77 MB) and averaged with a single all-reduce (RCCL over xGMI; one
+    bucket amortises the per-collective latency, and at this size the ring is latency-, not
+    link-bound), then unpacked into each ``.grad``.
+    """
+
+    def __init__(self, params, group=None):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = group
+        self.sizes = [p.numel() for p in self.params]
+        self.flat = None
+
+    def __call__(self):
+        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        if world == 1:
+            return
+        dev = self.params[0].device
+        if self.flat is None or self.flat.device != dev:
+            self.flat = torch.empty(sum(self.sizes), dtype=torch.float32, device=dev)
+        off = 0
+        for p, n in zip(self.params, self.sizes):
+            if p.grad is None:
+                raise RuntimeError("GradAllReduce: a parameter has no gradient")
+            self.flat[off:off + n].copy_(p.grad.reshape(-1))
+            off += n
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        self.flat.div_(world)
+        off = 0
+        for p, n in zip(self.params, self.sizes):
+            p.grad.copy_(self.flat[off:off + n].view_as(p.grad))
+            off += n

@@ -8,7 +8,8 @@ One render level under autograd is ``RenderLevel`` (a torch.autograd.Function):
             tiled over samples] read in place) -> compositing (aon_composite_fwd, raw outputs +
             sigmoid/relu as model.py:186-187)
   backward  aon_composite_bwd (dL/draw) -> per layer, last to first: dW = dY^T X and
-            db = colsum(dY) (split-K, deterministic), dX = (dY W) * relu'(X) (aon_gemm mask)
+            db = sum_rows dY from the same pass (split-K, deterministic), dX = (dY W) * relu'(X)
+            (aon_gemm mask)
 
 Gradients land in each parameter's ``.grad`` through autograd, so the reference's own
 optimizer code runs unchanged; ``Adam`` below is the fused replacement (aon_adam_step) with
@@ -41,7 +42,7 @@ def _workspace(nbytes, device):
 
 def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, a2_rdiv=1,
          b_rdiv=1, bias=None, mask=None, ldm=0, relu=False, accumulate=False, a_scale=1.0,
-         b_scale=1.0, k_splits=0):
+         b_scale=1.0, k_splits=0, rowsum=None):
     """aon_gemm on tensor views (each operand's data_ptr carries its own offset)."""
     a = L.AonGemmArgs(M=M, N=N, K=K, A=A.data_ptr(), lda=lda, a_kc=int(a_kc),
                       A2=A2.data_ptr() if A2 is not None else None, lda2=lda2, K1=K1,
@@ -49,7 +50,8 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
                       C=C.data_ptr(), ldc=ldc, bias=bias.data_ptr() if bias is not None else None,
                       mask=mask.data_ptr() if mask is not None else None, ldm=ldm,
                       relu=int(relu), accumulate=int(accumulate), a_scale=a_scale,
-                      b_scale=b_scale, k_splits=k_splits)
+                      b_scale=b_scale, k_splits=k_splits,
+                      rowsum=rowsum.data_ptr() if rowsum is not None else None)
     nbytes = L.lib().aon_gemm_workspace_bytes(ctypes.byref(a))
     ws = _workspace(nbytes, C.device) if nbytes else None
     L.call("aon_gemm", ctypes.byref(a), L.ptr(ws), nbytes, L.stream(C.device))
@@ -103,10 +105,12 @@ def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
     R, dev = enc.shape[0], enc.device
     gs, acts = GRAD_SCALE, ACT_SCALE
 
-    def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, ldw=None):
-        # dW[:, col0:col0+n_in] = dY^T X   (K = rows, split over workgroups)
+    def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, ldw=None, db=None):
+        # dW[:, col0:col0+n_in] = dY^T X (K = rows, split over workgroups); db = sum_rows dY
+        # from the same pass over dY
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
-             b_kc=False, b_rdiv=rdiv, ldc=ldw or dW.shape[1], a_scale=gs, b_scale=acts)
+             b_kc=False, b_rdiv=rdiv, ldc=ldw or dW.shape[1], a_scale=gs, b_scale=acts,
+             rowsum=db)
 
     def dinput(dX, dY, ldy, n_out, W, n_in, mask=None, accumulate=False):
         # dX (R x n_in) = dY W[:, :n_in] (* relu mask)
@@ -115,21 +119,17 @@ def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
              accumulate=accumulate, a_scale=gs, b_scale=W_SCALE)
 
     # rgb head (N=3) and view layer
-    dweight(G[11][0], draw, 4, 3, hv, 128, 128)
-    colsum(G[11][1], draw, R, 3, 4)
+    dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1])
     dhv = torch.empty((R, 128), device=dev)
     dinput(dhv, draw, 4, 3, P[11][0], 128, mask=hv)
-    dweight(G[10][0], dhv, 128, 128, bot, 256, 256)
+    dweight(G[10][0], dhv, 128, 128, bot, 256, 256, db=G[10][1])
     dweight(G[10][0], dhv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
-    colsum(G[10][1], dhv, R, 128, 128)
     dbot = torch.empty((R, 256), device=dev)
     dinput(dbot, dhv, 128, 128, P[10][0], 256)
     del dhv
     # bottleneck + density heads on h7
-    dweight(G[9][0], dbot, 256, 256, h[7], 256, 256)
-    colsum(G[9][1], dbot, R, 256, 256)
-    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256)
-    colsum(G[8][1], draw[:, 3:], R, 1, 4)
+    dweight(G[9][0], dbot, 256, 256, h[7], 256, 256, db=G[9][1])
+    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256, db=G[8][1])
     dy = torch.empty((R, 256), device=dev)
     dinput(dy, dbot, 256, 256, P[9][0], 256)
     dinput(dy, draw[:, 3:], 4, 1, P[8][0], 256, mask=h[7], accumulate=True)
@@ -137,13 +137,12 @@ def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
     dx = torch.empty((R, 256), device=dev)
     for i in range(7, -1, -1):  # dy = dL/d(pre-activation of layer i)
         if i == 5:
-            dweight(G[5][0], dy, 256, 256, h[4], 256, 256)
+            dweight(G[5][0], dy, 256, 256, h[4], 256, 256, db=G[5][1])
             dweight(G[5][0], dy, 256, 256, enc, 63, 63, col0=256)
         elif i == 0:
-            dweight(G[0][0], dy, 256, 256, enc, 63, 63)
+            dweight(G[0][0], dy, 256, 256, enc, 63, 63, db=G[0][1])
         else:
-            dweight(G[i][0], dy, 256, 256, h[i - 1], 256, 256)
-        colsum(G[i][1], dy, R, 256, 256)
+            dweight(G[i][0], dy, 256, 256, h[i - 1], 256, 256, db=G[i][1])
         if i > 0:
             dinput(dx, dy, 256, 256, P[i][0], 256, mask=h[i - 1])
             dx, dy = dy, dx

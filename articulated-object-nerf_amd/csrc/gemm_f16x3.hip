@@ -45,7 +45,25 @@ struct Params {
   float sa, sb, inv_s;  // operand prescales (powers of two); result * inv_s
   int64_t kchunk;       // K rows per blockIdx.z (split-K); == K when not split
   float* part;          // split-K partials [z][M][N] (unscaled epilogue-free sums * inv_s)
+  float* rowsum;        // !a_kc: rowsum[m] = sum_k A(m, k) (bias gradient of a dW product)
+  float* rowsum_part;   // split-K partials [z][M]
+  int tiles_m, tiles_n, gm;  // XCD-aware tile order over a 1-D grid.x (see tile_of)
 };
+
+// Workgroups are dispatched round-robin over the 8 XCDs (block L -> XCD L mod 8), each with
+// its own L2.  The tiles (m, 0..tiles_n-1) that share one A row-block are given block ids
+// gm apart -- with gm = 8 the same XCD, dispatched together -- so the A tile is fetched from
+// HBM once per XCD: group g of gm m-tiles x tiles_n n-tiles, L = gm tiles_n g + gm n + (m mod gm).
+// Grids of fewer than 8 m-tiles (weight gradients) use gm = tiles_m: no padding blocks, which
+// would otherwise pile the real tiles onto a few XCDs (measured: 3.5x slower).
+__device__ __forceinline__ bool tile_of(const Params& p, int& tm, int& tn) {
+  const int L = blockIdx.x;
+  const int gsz = p.gm * p.tiles_n;
+  const int g = L / gsz, r = L - g * gsz;
+  tn = r / p.gm;
+  tm = p.gm * g + (r - tn * p.gm);
+  return tm < p.tiles_m;
+}
 
 __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -64,8 +82,10 @@ __device__ __forceinline__ void split4(f4 v, float s, h4& hi, h4& lo) {
 
 // ---- tile loaders: 128 rows x 32 k of one operand into 4 f4 registers per thread -------------
 // KC (k-contiguous rows): thread t -> rows (t >> 3) + 32 i, k quad 4 (t & 7).
-// KM (k-major storage, rows contiguous): thread t -> k quad 4 (t >> 5), row quad 4 (t & 31);
-//     register i holds k = kq + i for rows rq..rq+3 (transposed when stored).
+// KM (k-major storage, rows contiguous): thread t -> rows 16 (t >> 5) + 4 (t & 3) + 0..3, k quad
+//     4 ((t >> 2) & 7); register i holds k = kq + i for those 4 rows (transposed when stored).
+//     Four lanes cover 64 contiguous bytes of a k row; the stores of a 32-lane half hit rows
+//     4 apart in two 16-row groups at 8 k offsets: at most 2-way bank conflicts (80-B rows).
 template <bool KC, bool VEC>
 struct TileLoad {
   f4 r[4];
@@ -96,7 +116,7 @@ struct TileLoad {
         r[i] = v;
       }
     } else {
-      const int kq = 4 * (tid >> 5), rq = 4 * (tid & 31);
+      const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t k = k0 + kq + i;
@@ -117,6 +137,13 @@ struct TileLoad {
     }
   }
 
+  // KM only: per-row sums of this thread's 4 k values (rows rq..rq+3), in k order
+  __device__ __forceinline__ void add_rows(float (&rs)[4]) const {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      rs[j] = __fadd_rn(rs[j], __fadd_rn(__fadd_rn(__fadd_rn(r[0][j], r[1][j]), r[2][j]), r[3][j]));
+  }
+
   // split and store into the [row][k] hi / lo planes
   __device__ __forceinline__ void store(_Float16* hi, _Float16* lo, float s, int tid) const {
     if (KC) {
@@ -130,7 +157,7 @@ struct TileLoad {
         *reinterpret_cast<h4*>(lo + row * ROWH + kq) = l;
       }
     } else {
-      const int kq = 4 * (tid >> 5), rq = 4 * (tid & 31);
+      const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {  // row rq + j: k = kq .. kq + 3 from r[0..3][j]
         const f4 v = {r[0][j], r[1][j], r[2][j], r[3][j]};
@@ -148,7 +175,9 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
   __shared__ __align__(16) _Float16 smem[2 * STAGE];  // 2 stages x (A hi, A lo, B hi, B lo)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  int tm, tn;
+  if (!tile_of(p, tm, tn)) return;  // padding block of the last XCD group (uniform exit)
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kbeg = (int64_t)blockIdx.z * p.kchunk;
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
   const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
@@ -175,14 +204,20 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
     tb.store(s + 2 * PLANE, s + 3 * PLANE, p.sb, tid);
   };
 
+  const bool want_rows = !AKC && p.rowsum && tn == 0;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
   if (nk > 0) {
     load(0);
+    if (!AKC && want_rows) ta.add_rows(rs);
     store(0);
   }
   __syncthreads();
   const int g = lane >> 4, r16 = lane & 15;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load(kt + 1);  // global loads in flight under this step's MFMAs
+    if (kt + 1 < nk) {
+      load(kt + 1);  // global loads in flight under this step's MFMAs
+      if (!AKC && want_rows) ta.add_rows(rs);
+    }
     const _Float16* s = smem + (kt & 1) * STAGE;
     h8 bh[4], bl[4];
 #pragma unroll
@@ -207,8 +242,24 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
     __syncthreads();
   }
 
-  // ---- epilogue: D lane layout col = lane & 15, rows 4 (lane >> 4) + r
   const bool split = gridDim.z > 1;
+  if (!AKC && want_rows) {
+    // combine the 8 k-quad lanes of every row in k order (LDS free after the last barrier)
+    float* red = reinterpret_cast<float*>(smem);  // [8 k quads][128 rows]
+    const int kqi = (tid >> 2) & 7, rq = 16 * (tid >> 5) + 4 * (tid & 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[kqi * BM + rq + j] = rs[j];
+    __syncthreads();
+    if (tid < BM && m0 + tid < p.M) {
+      float v = red[tid];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v = __fadd_rn(v, red[q * BM + tid]);
+      if (split) p.rowsum_part[(int64_t)blockIdx.z * p.M + m0 + tid] = v;
+      else p.rowsum[m0 + tid] = v;
+    }
+  }
+
+  // ---- epilogue: D lane layout col = lane & 15, rows 4 (lane >> 4) + r
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -234,11 +285,19 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
     }
 }
 
-// split-K: C = epilogue(sum_z part[z]) in z order (deterministic)
+// split-K: C = epilogue(sum_z part[z]) in z order (deterministic); rowsum likewise
 __global__ void k_gemm_reduce(Params p, int splits) {
   const int64_t total = p.M * p.N;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+  const int64_t extra = p.rowsum ? p.M : 0;  // rowsum entries ride along as e >= total
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total + extra;
        e += (int64_t)gridDim.x * blockDim.x) {
+    if (e >= total) {
+      const int64_t m = e - total;
+      float v = p.rowsum_part[m];
+      for (int z = 1; z < splits; ++z) v = __fadd_rn(v, p.rowsum_part[(int64_t)z * p.M + m]);
+      p.rowsum[m] = v;
+      continue;
+    }
     const int64_t m = e / p.N, n = e - m * p.N;
     float v = p.part[e];
     for (int z = 1; z < splits; ++z) v = __fadd_rn(v, p.part[(int64_t)z * total + e]);
@@ -285,7 +344,7 @@ static int64_t gemm_splits(const aon_gemm_args* a) {
 extern "C" size_t aon_gemm_workspace_bytes(const aon_gemm_args* a) {
   if (!a) return 0;
   const int64_t s = gemm_splits(a);
-  return s > 1 ? (size_t)s * a->M * a->N * sizeof(float) : 0;
+  return s > 1 ? (size_t)s * (a->M * a->N + a->M) * sizeof(float) : 0;
 }
 
 extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
@@ -313,14 +372,24 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   const int64_t splits = gemm_splits(a);
   p.kchunk = splits > 1 ? ((a->K + splits - 1) / splits + BK - 1) / BK * BK : (a->K > 0 ? a->K : 1);
   const int64_t zs = a->K > 0 ? (a->K + p.kchunk - 1) / p.kchunk : 1;
+  AON_REQUIRE(!a->rowsum || !a->a_kc, "rowsum needs a reduction-major A (a_kc = 0)");
   p.part = nullptr;
+  p.rowsum = a->rowsum;
+  p.rowsum_part = nullptr;
   if (zs > 1) {
-    AON_REQUIRE(work && work_bytes >= (size_t)zs * a->M * a->N * sizeof(float),
+    AON_REQUIRE(work && work_bytes >= (size_t)zs * (a->M * a->N + a->M) * sizeof(float),
                 "split-K needs aon_gemm_workspace_bytes() of workspace");
     p.part = static_cast<float*>(work);
+    p.rowsum_part = p.part + zs * a->M * a->N;
   }
-  AON_REQUIRE((a->M + BM - 1) / BM < 65536 && (a->N + BN - 1) / BN < (1ll << 31), "too large");
-  const dim3 grid((unsigned)((a->N + BN - 1) / BN), (unsigned)((a->M + BM - 1) / BM), (unsigned)zs);
+  const int64_t tiles_m = (a->M + BM - 1) / BM, tiles_n = (a->N + BN - 1) / BN;
+  const int64_t gm = tiles_m < 8 ? tiles_m : 8;
+  const int64_t blocks = (tiles_m + gm - 1) / gm * gm * tiles_n;
+  AON_REQUIRE(blocks < (1ll << 31), "too large");
+  p.tiles_m = (int)tiles_m;
+  p.tiles_n = (int)tiles_n;
+  p.gm = (int)gm;
+  const dim3 grid((unsigned)blocks, 1, (unsigned)zs);
   // float4 staging when the 4-element runs are 16-B aligned
   const bool va = aligned16(a->A) && a->lda % 4 == 0 && (!a->A2 || a->K1 % 4 == 0);
   const bool vb = aligned16(a->B) && a->ldb % 4 == 0;
@@ -332,7 +401,7 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   if (zs > 1) {
     const int rc = launch_status(__func__);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_gemm_reduce, grid_for(a->M * a->N, 256, 4096), 256, 0, st, p, (int)zs);
+    hipLaunchKernelGGL(k_gemm_reduce, grid_for(a->M * a->N + a->M, 256, 4096), 256, 0, st, p, (int)zs);
   }
   return launch_status(__func__);
 }

@@ -151,6 +151,8 @@ int aon_composite_fwd(const float* rgb, int64_t rgb_stride, const float* sigma,
  *   epilogue per element, in this order: v = sum / (a_scale * b_scale); v += C[m*ldc+n] when
  *   accumulate; v += bias[n]; relu; v *= (mask[m*ldm+n] > 0).  a_scale / b_scale are
  *   power-of-two operand prescales that keep |x * scale| < 65504 (fp16 range of the hi part).
+ *   rowsum (optional, a_kc = 0 only): rowsum[m] = sum_k A(m, k) -- the bias gradient
+ *   sum_rows dY that accompanies the weight gradient dY^T . X, from the same operand pass.
  *   Long reductions (K of a weight gradient = rows) are split over workgroups into
  *   `work` (aon_gemm_workspace_bytes) and summed in a fixed order (deterministic).
  *   k_splits = 0 chooses the split automatically. */
@@ -173,6 +175,7 @@ typedef struct aon_gemm_args {
   int relu, accumulate;
   float a_scale, b_scale;
   int64_t k_splits;
+  float* rowsum;
 } aon_gemm_args;
 
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);

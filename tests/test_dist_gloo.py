@@ -79,3 +79,36 @@ def test_gather_frame_gloo_world2(H, W):
     # rank r rendered rows [r * ceil(H/2), ...)
     rows = -(-H // world)
     assert torch.equal(frame[:, 3], (frame[:, 1] // rows).float())
+
+
+def _ddp_worker(rank, world, port, q):
+    from aonerf.parallel import GradAllReduce
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ps = [torch.zeros(s, requires_grad=True) for s in ((4, 3), (5,), (1,))]
+        for i, p in enumerate(ps):
+            p.grad = torch.full(p.shape, float(rank + 1) * (i + 1))
+        GradAllReduce(ps)()
+        q.put((rank, [p.grad.clone() for p in ps]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_gloo_world2():
+    """Training DDP step: the flat-bucket all-reduce averages every parameter's gradient."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for _, grads in got:
+        for i, gr in enumerate(grads):
+            assert torch.equal(gr, torch.full(gr.shape, 1.5 * (i + 1)))

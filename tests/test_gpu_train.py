@@ -94,10 +94,19 @@ def test_gemm_epilogues_segments_split():
     dY = torch.randn((Rb, 128), device="cuda", generator=g) * 1e-3
     V = torch.randn((Rb // 40, 27), device="cuda", generator=g)
     dW = torch.empty((128, 27), device="cuda")
+    db = torch.empty((128,), device="cuda")
     gemm(dW, dY, V, 128, 27, Rb, lda=128, a_kc=False, ldb=27, b_kc=False, b_rdiv=40, ldc=27,
-         a_scale=2.0 ** 10, b_scale=2.0 ** -8, k_splits=7)
+         a_scale=2.0 ** 10, b_scale=2.0 ** -8, k_splits=7, rowsum=db)
     ref = dY.double().t() @ V.double()[torch.arange(Rb, device="cuda") // 40]
     assert (dW.double() - ref).abs().max().item() < 2e-6 * ref.abs().max().item()
+    ref_b = dY.double().sum(0)
+    assert (db.double() - ref_b).abs().max().item() < 1e-5 * ref_b.abs().max().item()
+    # unsplit rowsum, ragged M
+    dW2, db2 = torch.empty((3, 27), device="cuda"), torch.empty((3,), device="cuda")
+    gemm(dW2, dY[:, 5:], V, 3, 27, 200, lda=128, a_kc=False, ldb=27, b_kc=False, b_rdiv=40, ldc=27,
+         k_splits=1, rowsum=db2)
+    ref_b2 = dY[:200, 5:8].double().sum(0)
+    assert (db2.double() - ref_b2).abs().max().item() < 1e-5 * ref_b2.abs().max().item()
 
 
 # ----------------------------------------------------------------------------- compositing bwd

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Training-step throughput (BASELINE configs C5: LitNeRF.training_step on 4096-ray batches,
+randomized sampling, Adam with the reference schedule; DDP over N GPUs = N independent
+batches + one gradient all-reduce per step, weak scaling).
+
+    python tools/bench_train.py [--rays 4096] [--steps 10] [--warmup 3]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_train.py
+
+A step = draw a batch of pixels of a synthetic 640x480 view (8 poses of create_spheric_poses,
+target image PCG64 seed 3), coarse + fine training forward, loss, HIP backward, gradient
+all-reduce, fused Adam.  Rank 0 prints one JSON line; timing is the max over ranks with barrier
++ synchronize on both sides.  Algorithmic FLOP per step = 3 x the forward MLP FLOP (dX and dW
+each cost one forward) = 3 x 2 x 593,408 x 258 per ray.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "articulated-object-nerf_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+H, W = 480, 640
+MAC = 593_408
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rays", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--max-steps", type=int, default=200000, help="schedule length (run_max_steps)")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from aonerf import train
+    from aonerf.model import NeRF
+    from aonerf.parallel import GradAllReduce
+    from aonerf.ray_utils import frame_rays
+    from aonerf.render import create_spheric_poses, sapien_focal
+    from oracle import weights as Wt  # deterministic initial weights (same as bench.py)
+
+    dev = torch.device("cuda", local_rank)
+    net = NeRF().to(dev)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in Wt.nerf_state_dict(0).items()})
+    poses = create_spheric_poses(4.0)
+    focal = sapien_focal(H)
+    rays_all = {k: [] for k in ("rays_o", "rays_d", "viewdirs")}
+    for k in range(8):
+        r = frame_rays(torch.as_tensor(poses[(5 * k) % len(poses)]), H, W, focal)
+        for key in rays_all:
+            rays_all[key].append(r[key])
+    rays_all = {k: torch.cat(v, 0) for k, v in rays_all.items()}
+    rng = np.random.Generator(np.random.PCG64(3))
+    target_all = torch.from_numpy(rng.uniform(0, 1, size=(8 * H * W, 3)).astype(np.float32)).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    opt = train.Adam(net.parameters())
+    sync = GradAllReduce(net.parameters())
+
+    def step(i):
+        idx = torch.randint(0, 8 * H * W, (args.rays,), device=dev, generator=gen)
+        batch = {k: v[idx] for k, v in rays_all.items()}
+        batch["target"] = target_all[idx]
+        opt.zero_grad()
+        loss, _ = train.training_step(net, batch, True, True, 2.0, 6.0)
+        loss.backward()
+        sync()
+        opt.step(lr=train.learning_rate(i, args.max_steps))
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    rays = args.rays * args.steps * world
+    flop = 3 * 2 * MAC * (65 + 193) * rays
+    if rank == 0:
+        print(json.dumps({
+            "metric": "training rays/sec (LitNeRF.training_step, 64c+128f, randomized, Adam)",
+            "value": rays / dt, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000 * dt / args.steps,
+            "higher_is_better": True, "scaling": "weak", "dtype": "f16x3 (fp16 hi/lo split MFMA)",
+            "data": "synthetic", "config": {"workload": "C5 training step", "rays_per_rank": args.rays,
+                                             "parallelism": f"ddp{world}"},
+            "mlp_tflops_algorithmic": flop / dt / 1e12, "final_loss": float(loss.item())}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
