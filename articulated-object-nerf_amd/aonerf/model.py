@@ -142,6 +142,30 @@ def _record(timers, ev, key, rows):
         timers.setdefault(key, []).append((ev[0], ev[1], rows))
 
 
+def level_t_vals(level, o, d, t_prev, w_prev, randomized, near, far, num_coarse_samples,
+                 num_fine_samples, lindisp, u_coarse=None, u_fine=None):
+    """Sample positions of a level: stratified (helper.py:106-133) or inverse-CDF resampling
+    of the previous level's weights merged with its samples (model.py:163-172)."""
+    dev = o.device
+    B = o.shape[0]
+    if level == 0:
+        t_vals, _ = helper.sample_along_rays(o, d, num_coarse_samples, near, far, randomized,
+                                             lindisp, u=u_coarse, want_coords=False)
+        return t_vals
+    Sc = t_prev.shape[1]
+    if randomized:
+        u = torch.rand((B, num_fine_samples), device=dev) if u_fine is None else L.contig(u_fine)
+        u_stride = num_fine_samples
+    else:
+        u, u_stride = helper.eval_u(num_fine_samples, dev), 0
+    w_prev = L.contig(w_prev.detach())
+    t_new = torch.empty((B, Sc + num_fine_samples), device=dev)
+    # bins = mids of t (model.py:163), weights[..., 1:-1] as a strided view
+    L.call("aon_sample_pdf", None, 0, L.ptr(w_prev[:, 1:]), Sc, B, Sc - 1, num_fine_samples,
+           L.ptr(u), u_stride, L.ptr(t_prev), Sc, None, None, L.ptr(t_new), None, L.stream(dev))
+    return t_new
+
+
 class NeRF(nn.Module):
     """reference model.py:123-199 (two-level coarse/fine render)."""
 
@@ -218,28 +242,9 @@ class NeRF(nn.Module):
         return ret
 
     def _level_t(self, level, o, d, t_prev, w_prev, randomized, near, far, u_coarse, u_fine):
-        """Sample positions of a level: stratified (helper.py:106-133) or inverse-CDF resampling
-        of the previous level's weights merged with its samples (model.py:163-172)."""
-        dev = o.device
-        B = o.shape[0]
-        if level == 0:
-            t_vals, _ = helper.sample_along_rays(o, d, self.num_coarse_samples, near, far,
-                                                 randomized, self.lindisp, u=u_coarse,
-                                                 want_coords=False)
-            return t_vals
-        Sc = t_prev.shape[1]
-        if randomized:
-            u = torch.rand((B, self.num_fine_samples), device=dev) if u_fine is None else L.contig(u_fine)
-            u_stride = self.num_fine_samples
-        else:
-            u, u_stride = helper.eval_u(self.num_fine_samples, dev), 0
-        w_prev = L.contig(w_prev.detach())
-        t_new = torch.empty((B, Sc + self.num_fine_samples), device=dev)
-        # bins = mids of t (model.py:163), weights[..., 1:-1] as a strided view
-        L.call("aon_sample_pdf", None, 0, L.ptr(w_prev[:, 1:]), Sc, B, Sc - 1,
-               self.num_fine_samples, L.ptr(u), u_stride, L.ptr(t_prev), Sc, None, None,
-               L.ptr(t_new), None, L.stream(dev))
-        return t_new
+        return level_t_vals(level, o, d, t_prev, w_prev, randomized, near, far,
+                            self.num_coarse_samples, self.num_fine_samples, self.lindisp,
+                            u_coarse, u_fine)
 
     def _render_level_fused(self, mlp, o, d, v, t_vals, randomized, white_bkgd, level, timers):
         B, S = t_vals.shape

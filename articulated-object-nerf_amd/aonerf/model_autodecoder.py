@@ -1,0 +1,248 @@
+"""Drop-in for the articulated ``NeRFMLP`` / ``NeRF_AE_Art`` of the reference
+(models/vanilla_nerf/model_autodecoder.py:60-337; config C3).
+
+Identical constructor keywords, forward signatures and parameter (state_dict) names.  One
+level runs:
+
+    cast_rays (aon_cast_rays: xyz)                                         helper.py:25-26
+    deformation MLP on cat[xyz, shape, articulation]: 4 x (GEMM + ReLU),   model_autodecoder.py:
+      deformation_layer (GEMM)                                             196-205
+    x' = deformation + xyz, pos_enc(x')   (aon_cast_rays offset + enc)     :205-212
+    trunk on cat[pos_enc(x'), shape] with the skip concat, density,        :214-223
+      bottleneck
+    view branch on cat[bottleneck, enc_dir, appearance]: 4 x (GEMM + ReLU) :224-235
+    rgb head; padded sigmoid / softplus(raw - 1) + compositing             :321-333
+      (aon_composite_fwd, AON_ACT_ARTIC)
+
+The latent codes are the same for every sample (the reference repeats (1, C) rows over all
+B*S rows, :186-194), so their products with the weight columns they meet are folded into
+per-call biases (b' = b + W[:, latent cols] . latent, one tiny GEMM each): the per-sample GEMMs
+see K = 3 (deformation input), 63 (trunk input), 256 + 63 (skip) and 256 + 27 (view input).
+Every product runs on the f16x3 MFMA GEMM (aon_gemm); no torch arithmetic on the path.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.init as init
+
+from . import _lib as L
+from .linalg import ACT_SCALE, W_SCALE, gemm, linear_fwd
+from .model import level_t_vals
+
+class NeRFMLP(nn.Module):
+    """reference model_autodecoder.py:60-166 (same nn.Linear layout and init)."""
+
+    def __init__(self, min_deg_point, max_deg_point, deg_view, netdepth: int = 8,
+                 netwidth: int = 256, netdepth_deformation=4, netwidth_deformation: int = 128,
+                 netdepth_condition: int = 4, netwidth_condition: int = 128,
+                 shape_latent_dim=128, appearance_latent_dim=128, articulation_latent_dim=32,
+                 skip_layer: int = 4, input_ch: int = 3, input_ch_view: int = 3,
+                 num_rgb_channels: int = 3, num_density_channels: int = 1,
+                 deformation_mlp: bool = True, enc_after: bool = True, embed_deg: bool = False):
+        super().__init__()
+        cfg = dict(netdepth=netdepth, netwidth=netwidth, netdepth_deformation=netdepth_deformation,
+                   netwidth_deformation=netwidth_deformation, netdepth_condition=netdepth_condition,
+                   netwidth_condition=netwidth_condition, shape_latent_dim=shape_latent_dim,
+                   appearance_latent_dim=appearance_latent_dim,
+                   articulation_latent_dim=articulation_latent_dim, skip_layer=skip_layer,
+                   input_ch=input_ch, input_ch_view=input_ch_view,
+                   num_rgb_channels=num_rgb_channels, num_density_channels=num_density_channels,
+                   deformation_mlp=deformation_mlp, enc_after=enc_after, embed_deg=embed_deg)
+        for k, v in cfg.items():
+            setattr(self, k, v)
+        self.min_deg_point, self.max_deg_point, self.deg_view = min_deg_point, max_deg_point, deg_view
+        if not (deformation_mlp and enc_after and not embed_deg):
+            raise ValueError("aonerf implements the reference's default articulated MLP "
+                             "(deformation_mlp=True, enc_after=True, embed_deg=False)")
+        view_pos_size = (deg_view * 2 + 1) * input_ch_view
+        pos_size_deformation = input_ch + shape_latent_dim + articulation_latent_dim
+        deformations = [nn.Linear(pos_size_deformation, netwidth_deformation)]
+        for _ in range(netdepth_deformation - 1):
+            deformations.append(nn.Linear(netwidth_deformation, netwidth_deformation))
+        for m in deformations:
+            init.xavier_uniform_(m.weight)
+        self.deformations_linear = nn.ModuleList(deformations)
+        self.deformation_layer = nn.Linear(netwidth_deformation, 3)
+        init.xavier_uniform_(self.deformation_layer.weight)
+        pos_size = ((max_deg_point - min_deg_point) * 2 + 1) * input_ch + shape_latent_dim
+        pts = [nn.Linear(pos_size, netwidth)]
+        for idx in range(netdepth - 1):
+            k = netwidth + pos_size if (idx % skip_layer == 0 and idx > 0) else netwidth
+            pts.append(nn.Linear(k, netwidth))
+        for m in pts:
+            init.xavier_uniform_(m.weight)
+        self.pts_linears = nn.ModuleList(pts)
+        views = [nn.Linear(netwidth + view_pos_size + appearance_latent_dim, netwidth_condition)]
+        for _ in range(netdepth_condition - 1):
+            layer = nn.Linear(netwidth_condition, netwidth_condition)
+            init.xavier_uniform_(layer.weight)
+            views.append(layer)
+        self.views_linear = nn.ModuleList(views)
+        self.bottleneck_layer = nn.Linear(netwidth, netwidth)
+        self.density_layer = nn.Linear(netwidth, num_density_channels)
+        self.rgb_layer = nn.Linear(netwidth_condition, num_rgb_channels)
+        for m in (self.bottleneck_layer, self.density_layer, self.rgb_layer):
+            init.xavier_uniform_(m.weight)
+        self.pos_size_enc = pos_size - shape_latent_dim  # 63
+
+    # -- latent folding: b' = b + W[:, c0:c0+n] . latent (one M=1 GEMM with bias epilogue)
+    @staticmethod
+    def _fold(layer, c0, latent):
+        W = layer.weight.detach()
+        out = torch.empty((1, W.shape[0]), device=W.device)
+        n = latent.shape[-1]
+        gemm(out, latent, W[:, c0:], 1, W.shape[0], n, lda=n, a_kc=True, ldb=W.shape[1], b_kc=True,
+             ldc=W.shape[0], bias=layer.bias.detach(), a_scale=1.0, b_scale=W_SCALE)
+        return out.reshape(-1)
+
+    def folded_biases(self, latents):
+        shape = L.contig(latents["density"].detach().reshape(1, -1))
+        app = L.contig(latents["color"].detach().reshape(1, -1))
+        art = L.contig(latents["articulation"].detach().reshape(1, -1))
+        L.require_gpu(shape, app, art)
+        if shape.shape[1] != self.shape_latent_dim or art.shape[1] != self.articulation_latent_dim:
+            raise ValueError("latent code sizes do not match the MLP")
+        lat_def = torch.cat([shape, art], -1)  # the 160 latent columns of cat[pos, shape, art]
+        return {
+            "def0": self._fold(self.deformations_linear[0], self.input_ch, lat_def),
+            "pts0": self._fold(self.pts_linears[0], self.pos_size_enc, shape),
+            "pts_skip": self._fold(self.pts_linears[self.skip_layer + 1],
+                                   self.netwidth + self.pos_size_enc, shape),
+            "view0": self._fold(self.views_linear[0],
+                                self.netwidth + (self.deg_view * 2 + 1) * self.input_ch_view, app),
+        }
+
+    @torch.no_grad()
+    def forward_rays(self, rays_o, rays_d, viewdirs, t_vals, latents):
+        """One level's MLP on samples o + t d -> raw (B*S, 4) = [raw_rgb, raw_sigma]."""
+        L.require_gpu(rays_o, rays_d, viewdirs, t_vals)
+        B, S = t_vals.shape
+        R, dev = B * S, t_vals.device
+        xyz = torch.empty((R, 3), device=dev)
+        L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
+               L.ptr(xyz), 0, 0, None, L.stream(dev))
+        venc = torch.empty((B, (self.deg_view * 2 + 1) * self.input_ch_view), device=dev)
+        L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, self.deg_view, L.ptr(venc), L.stream(dev))
+        return self._mlp(xyz, venc, S, latents)
+
+    @torch.no_grad()
+    def _mlp(self, xyz, venc, S, latents):
+        """The MLP on sample positions xyz (R, 3), view encodings venc (R / S, 27) -> (R, 4)."""
+        R, dev = xyz.shape[0], xyz.device
+        fb = self.folded_biases(latents)
+        W = lambda m: m.weight.detach()  # noqa: E731
+        b = lambda m: m.bias.detach()  # noqa: E731
+        # deformation MLP (model_autodecoder.py:196-205); layer 0 sees only xyz per sample
+        wd = self.netwidth_deformation
+        h = torch.empty((R, wd), device=dev)
+        h2 = torch.empty((R, wd), device=dev)
+        d0 = self.deformations_linear[0]
+        gemm(h, xyz, W(d0), R, wd, 3, lda=3, a_kc=True, ldb=W(d0).shape[1], b_kc=True, ldc=wd,
+             bias=fb["def0"], relu=True, a_scale=ACT_SCALE, b_scale=W_SCALE)
+        for m in list(self.deformations_linear)[1:]:
+            linear_fwd(h2, h, wd, W(m), b(m), relu=True)
+            h, h2 = h2, h
+        delta = torch.empty((R, 3), device=dev)
+        linear_fwd(delta, h, wd, W(self.deformation_layer), b(self.deformation_layer))
+        del h, h2
+        # x' = deformation + xyz, then pos_enc (enc_after, :205-212), points given directly
+        enc = torch.empty((R, self.pos_size_enc), device=dev)
+        L.call("aon_cast_rays", L.ptr(xyz), None, None, R, 1, L.ptr(delta), 3, None,
+               self.min_deg_point, self.max_deg_point, L.ptr(enc), L.stream(dev))
+        # trunk on inputs = cat[enc, shape] (:214-220), shape folded into the biases
+        nw, ne = self.netwidth, self.pos_size_enc
+        x = torch.empty((R, nw), device=dev)
+        y = torch.empty((R, nw), device=dev)
+        p0 = self.pts_linears[0]
+        gemm(x, enc, W(p0), R, nw, ne, lda=ne, a_kc=True, ldb=W(p0).shape[1], b_kc=True, ldc=nw,
+             bias=fb["pts0"], relu=True, a_scale=ACT_SCALE, b_scale=W_SCALE)
+        for idx in range(1, self.netdepth):
+            m = self.pts_linears[idx]
+            if idx == self.skip_layer + 1:  # cat[h, enc, shape]
+                gemm(y, x, W(m), R, nw, nw + ne, lda=nw, a_kc=True, ldb=W(m).shape[1], b_kc=True,
+                     ldc=nw, A2=enc, lda2=ne, K1=nw, bias=fb["pts_skip"], relu=True,
+                     a_scale=ACT_SCALE, b_scale=W_SCALE)
+            else:
+                linear_fwd(y, x, nw, W(m), b(m), relu=True)
+            x, y = y, x
+        raw = torch.empty((R, 4), device=dev)
+        linear_fwd(raw[:, 3:], x, nw, W(self.density_layer), b(self.density_layer), ldo=4)
+        bot = y
+        linear_fwd(bot, x, nw, W(self.bottleneck_layer), b(self.bottleneck_layer))
+        # view branch on cat[bottleneck, enc_dir tiled over samples, appearance] (:224-235)
+        wc, nv = self.netwidth_condition, venc.shape[1]
+        v0 = self.views_linear[0]
+        hv = torch.empty((R, wc), device=dev)
+        hv2 = torch.empty((R, wc), device=dev)
+        gemm(hv, bot, W(v0), R, wc, nw + nv, lda=nw, a_kc=True, ldb=W(v0).shape[1], b_kc=True,
+             ldc=wc, A2=venc, lda2=nv, K1=nw, a2_rdiv=S, bias=fb["view0"], relu=True,
+             a_scale=ACT_SCALE, b_scale=W_SCALE)
+        for m in list(self.views_linear)[1:]:
+            linear_fwd(hv2, hv, wc, W(m), b(m), relu=True)
+            hv, hv2 = hv2, hv
+        linear_fwd(raw, hv, wc, W(self.rgb_layer), b(self.rgb_layer), ldo=4)
+        return raw
+
+    def forward(self, pos, condition, latents):
+        """reference model_autodecoder.py:168-239: pos (B, S, 3) sample positions (enc_after),
+        condition (B, 27) encoded view directions -> (raw_rgb (B, S, 3), raw_density (B, S, 1))."""
+        L.require_gpu(pos, condition)
+        B, S, _ = pos.shape
+        raw = self._mlp(L.contig(pos.reshape(-1, 3)), L.contig(condition), S, latents).view(B, S, 4)
+        return raw[..., :3], raw[..., 3:]
+
+
+class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
+    """reference model_autodecoder.py:242-337 (two-level render with latent codes)."""
+
+    def __init__(self, num_levels: int = 2, min_deg_point: int = 0, max_deg_point: int = 10,
+                 deg_view: int = 4, num_coarse_samples: int = 64, num_fine_samples: int = 128,
+                 use_viewdirs: bool = True, noise_std: float = 0.0, lindisp: bool = False,
+                 rgb_padding: float = 0.001, density_bias: float = -1.0, enc_after=True,
+                 embed_deg=False):
+        super().__init__()
+        if num_levels != 2:
+            raise ValueError("the reference NeRF_AE_Art is two-level (coarse + fine)")
+        if rgb_padding != 0.001 or density_bias != -1.0:
+            raise ValueError("the fused epilogue implements rgb_padding=0.001, density_bias=-1")
+        self.num_levels, self.min_deg_point, self.max_deg_point = num_levels, min_deg_point, max_deg_point
+        self.deg_view, self.num_coarse_samples, self.num_fine_samples = deg_view, num_coarse_samples, num_fine_samples
+        self.use_viewdirs, self.noise_std, self.lindisp = use_viewdirs, noise_std, lindisp
+        self.rgb_padding, self.density_bias = rgb_padding, density_bias
+        self.enc_after, self.embed_deg = enc_after, embed_deg
+        self.coarse_mlp = NeRFMLP(min_deg_point, max_deg_point, deg_view, enc_after=enc_after,
+                                  embed_deg=embed_deg)
+        self.fine_mlp = NeRFMLP(min_deg_point, max_deg_point, deg_view, enc_after=enc_after,
+                                embed_deg=embed_deg)
+
+    @torch.no_grad()
+    def forward(self, rays, randomized, white_bkgd, near, far, latents, train=True, *,
+                u_coarse=None, u_fine=None, return_weights=False, return_intermediates=False):
+        """reference model_autodecoder.py:278-337 -> [(comp_rgb, acc, depth)_coarse, (...)_fine]
+        (``u_coarse`` / ``u_fine`` inject randomized-mode uniforms; the extras as NeRF.forward)."""
+        o, d, v = rays["rays_o"], rays["rays_d"], rays["viewdirs"]
+        L.require_gpu(o, d, v)
+        o, d, v = L.contig(o), L.contig(d), L.contig(v)
+        B, dev = o.shape[0], o.device
+        ret = []
+        t_vals = weights = None
+        for level in range(2):
+            t_vals = level_t_vals(level, o, d, t_vals, weights, randomized, near, far,
+                                  self.num_coarse_samples, self.num_fine_samples, self.lindisp,
+                                  u_coarse, u_fine)
+            mlp = self.coarse_mlp if level == 0 else self.fine_mlp
+            S = t_vals.shape[1]
+            raw = mlp.forward_rays(o, d, v, t_vals, latents)
+            if self.noise_std > 0 and randomized:  # model_autodecoder.py:318-319
+                raw[:, 3].copy_(raw[:, 3] + torch.rand_like(raw[:, 3]) * self.noise_std)
+            comp = torch.empty((B, 3), device=dev)
+            acc = torch.empty((B,), device=dev)
+            weights = torch.empty((B, S), device=dev)
+            depth = torch.empty((B,), device=dev)
+            L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
+                   B, S, int(bool(white_bkgd)), L.ACT_ARTIC, L.ptr(comp), L.ptr(acc),
+                   L.ptr(weights), L.ptr(depth), L.stream(dev))
+            out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
+            if return_intermediates:
+                out = out + (dict(t_vals=t_vals, weights=weights, raw=raw),)
+            ret.append(out)
+        return ret

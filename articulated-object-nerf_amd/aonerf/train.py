@@ -16,62 +16,12 @@ optimizer code runs unchanged; ``Adam`` below is the fused replacement (aon_adam
 the reference's learning-rate schedule.  All arithmetic is in the HIP kernels; torch only
 allocates buffers and routes autograd.
 """
-import ctypes
-
 import numpy as np
 import torch
 
 from . import _lib as L
 
-# power-of-two operand prescales of the fp16 hi/lo split (exact): activations at 2^-8 (fp16
-# range up to 1.6e7, as the fused forward), gradients at 2^10 (dL/d* of a mean loss are small;
-# this keeps their hi parts out of fp16's subnormal range), weights unscaled.
-ACT_SCALE, GRAD_SCALE, W_SCALE = 2.0 ** -8, 2.0 ** 10, 1.0
-
-_ws = {}
-
-
-def _workspace(nbytes, device):
-    key = str(device)
-    buf = _ws.get(key)
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
-        _ws[key] = buf
-    return buf
-
-
-def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, a2_rdiv=1,
-         b_rdiv=1, bias=None, mask=None, ldm=0, relu=False, accumulate=False, a_scale=1.0,
-         b_scale=1.0, k_splits=0, rowsum=None):
-    """aon_gemm on tensor views (each operand's data_ptr carries its own offset)."""
-    a = L.AonGemmArgs(M=M, N=N, K=K, A=A.data_ptr(), lda=lda, a_kc=int(a_kc),
-                      A2=A2.data_ptr() if A2 is not None else None, lda2=lda2, K1=K1,
-                      a2_rdiv=a2_rdiv, B=B.data_ptr(), ldb=ldb, b_kc=int(b_kc), b_rdiv=b_rdiv,
-                      C=C.data_ptr(), ldc=ldc, bias=bias.data_ptr() if bias is not None else None,
-                      mask=mask.data_ptr() if mask is not None else None, ldm=ldm,
-                      relu=int(relu), accumulate=int(accumulate), a_scale=a_scale,
-                      b_scale=b_scale, k_splits=k_splits,
-                      rowsum=rowsum.data_ptr() if rowsum is not None else None)
-    nbytes = L.lib().aon_gemm_workspace_bytes(ctypes.byref(a))
-    ws = _workspace(nbytes, C.device) if nbytes else None
-    L.call("aon_gemm", ctypes.byref(a), L.ptr(ws), nbytes, L.stream(C.device))
-
-
-def colsum(out, X, M, N, ldx, accumulate=False):
-    nbytes = L.lib().aon_colsum_workspace_bytes(M, N)
-    ws = _workspace(nbytes, X.device)
-    L.call("aon_colsum", L.ptr(X), ldx, M, N, int(accumulate), L.ptr(out), L.ptr(ws), nbytes,
-           L.stream(X.device))
-
-
-def linear_fwd(out, X, Kx, W, b, *, ldx=None, ldo=None, relu=False, X2=None, K2=0, ld2=0, rdiv2=1,
-               accumulate=False):
-    """out (R x N) (+)= [X | X2] W^T + b (+ReLU); W is the nn.Linear weight (N x (Kx+K2))."""
-    R, N = out.shape[0], W.shape[0]
-    gemm(out, X, W, R, N, Kx + K2, lda=ldx or Kx, a_kc=True, ldb=W.shape[1], b_kc=True,
-         ldc=ldo or out.shape[1], A2=X2, lda2=ld2, K1=Kx if X2 is not None else 0, a2_rdiv=rdiv2,
-         bias=b, relu=relu, accumulate=accumulate, a_scale=ACT_SCALE, b_scale=W_SCALE)
-
+from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, colsum, gemm, linear_fwd  # noqa: F401
 
 # ---------------------------------------------------------------------------- one render level
 def _mlp_params(mlp):
@@ -158,8 +108,8 @@ class RenderLevel(torch.autograd.Function):
         R, dev = B * S, t_vals.device
         # xyz = o + t d (helper.py:25-26) straight into the encodings (helper.py:136-140)
         enc = torch.empty((R, 63), device=dev)
-        L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0, 10,
-               L.ptr(enc), L.stream(dev))
+        L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0, None,
+               0, 10, L.ptr(enc), L.stream(dev))
         venc = torch.empty((B, 27), device=dev)
         L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, 4, L.ptr(venc), L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]

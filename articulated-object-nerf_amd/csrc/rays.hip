@@ -130,10 +130,12 @@ __global__ void k_pos_enc(const float* __restrict__ x, int64_t n, int min_deg, i
   }
 }
 
-// cast_rays (helper.py:25-26) on per-ray t (B, S), optionally straight into pos_enc
-// (helper.py:136-140): one thread per (sample, output feature)
+// cast_rays (helper.py:25-26) on per-ray t (B, S), optionally displaced by a per-sample offset
+// (the articulated deformation, model_autodecoder.py:205: deformation_layer(x) + pos) and
+// optionally straight into pos_enc (helper.py:136-140): one thread per (sample, feature)
 __global__ void k_cast_rays(const float* __restrict__ ro, const float* __restrict__ rd,
                             const float* __restrict__ t, int64_t B, int S,
+                            const float* __restrict__ off, int64_t off_stride,
                             float* __restrict__ xyz, int min_deg, int L, float* __restrict__ enc) {
   const int C = enc ? 3 + 6 * L : 3;
   const int64_t total = B * S * C;
@@ -142,10 +144,19 @@ __global__ void k_cast_rays(const float* __restrict__ ro, const float* __restric
     const int64_t r = i / C;
     const int f = static_cast<int>(i - r * C);
     const int64_t b = r / S;
-    const float tv = t[r];
-    const float x0 = __fadd_rn(ro[3 * b], __fmul_rn(tv, rd[3 * b]));
-    const float x1 = __fadd_rn(ro[3 * b + 1], __fmul_rn(tv, rd[3 * b + 1]));
-    const float x2 = __fadd_rn(ro[3 * b + 2], __fmul_rn(tv, rd[3 * b + 2]));
+    float x0 = ro[3 * b], x1 = ro[3 * b + 1], x2 = ro[3 * b + 2];
+    if (rd) {  // rays_d == NULL: the points are given directly (rays_o rows)
+      const float tv = t[r];
+      x0 = __fadd_rn(x0, __fmul_rn(tv, rd[3 * b]));
+      x1 = __fadd_rn(x1, __fmul_rn(tv, rd[3 * b + 1]));
+      x2 = __fadd_rn(x2, __fmul_rn(tv, rd[3 * b + 2]));
+    }
+    if (off) {
+      const float* o = off + r * off_stride;
+      x0 = __fadd_rn(o[0], x0);
+      x1 = __fadd_rn(o[1], x1);
+      x2 = __fadd_rn(o[2], x2);
+    }
     if (xyz && f < 3) xyz[3 * r + f] = f == 0 ? x0 : (f == 1 ? x1 : x2);
     if (enc) enc[i] = pos_enc_feature(x0, x1, x2, f, min_deg, L);
   }
@@ -219,14 +230,15 @@ extern "C" int aon_pos_enc(const float* x, int64_t n, int min_deg, int max_deg, 
 }
 
 extern "C" int aon_cast_rays(const float* rays_o, const float* rays_d, const float* t, int64_t B,
-                             int S, float* xyz, int min_deg, int max_deg, float* enc,
-                             aon_stream_t stream) {
-  AON_REQUIRE(rays_o && rays_d && t && (xyz || enc) && B >= 0 && S >= 1, "bad arguments");
+                             int S, const float* offset, int64_t offset_stride, float* xyz,
+                             int min_deg, int max_deg, float* enc, aon_stream_t stream) {
+  AON_REQUIRE(rays_o && (!rays_d || t) && (xyz || enc) && B >= 0 && S >= 1, "bad arguments");
+  AON_REQUIRE(!offset || offset_stride >= 3, "offset rows need >= 3 floats");
   AON_REQUIRE(!enc || (max_deg >= min_deg && min_deg >= -126 && max_deg <= 127), "bad degrees");
   if (B == 0) return 0;
   const int L = max_deg - min_deg;
   const int C = enc ? 3 + 6 * L : 3;
   hipLaunchKernelGGL(k_cast_rays, grid_for(B * S * C, 256, 65536), 256, 0, (hipStream_t)stream,
-                     rays_o, rays_d, t, B, S, xyz, min_deg, L, enc);
+                     rays_o, rays_d, t, B, S, offset, offset_stride, xyz, min_deg, L, enc);
   return launch_status(__func__);
 }

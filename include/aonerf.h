@@ -67,10 +67,13 @@ int aon_sample_along_rays(const float* rays_o, const float* rays_d, int64_t B, i
                           const float* t_lower, const float* t_upper, const float* u,
                           float* t_out, float* xyz_out, aon_stream_t stream);
 
-/* cast_rays (helper.py:25-26) on per-ray sample positions t (B, S): xyz (B*S, 3) and/or
- * enc = pos_enc(xyz, min_deg, max_deg) (B*S, 3 + 6 (max_deg - min_deg)) in one pass. */
+/* cast_rays (helper.py:25-26) on per-ray sample positions t (B, S): x = o + t d, then, when
+ * offset != NULL, x = offset[r] + x (the articulated deformation, model_autodecoder.py:205);
+ * rays_d == NULL (t ignored): x = rays_o[r / S] (points given directly);
+ * writes xyz (B*S, 3) and/or enc = pos_enc(x, min_deg, max_deg) (B*S, 3 + 6 (max - min)). */
 int aon_cast_rays(const float* rays_o, const float* rays_d, const float* t, int64_t B, int S,
-                  float* xyz, int min_deg, int max_deg, float* enc, aon_stream_t stream);
+                  const float* offset, int64_t offset_stride, float* xyz, int min_deg,
+                  int max_deg, float* enc, aon_stream_t stream);
 
 /* pos_enc (helper.py:136-140): out (n, 3 + 6*(max_deg-min_deg)). */
 int aon_pos_enc(const float* x, int64_t n, int min_deg, int max_deg, float* out,

@@ -277,6 +277,89 @@ def render_rays(params, batch, chunk, white_bkgd, near, far, **kw):
     return {k: torch.cat(v, 0) for k, v in out.items()}
 
 
+# ----------------------------------------------------------------------------- articulated
+def _lin(p, name, x):
+    """nn.Linear's own call (F.linear: one addmm on 2-D input)."""
+    return torch.nn.functional.linear(x, p[f"{name}.weight"], p[f"{name}.bias"])
+
+
+def art_mlp_forward(p, pos, condition, latents, netdepth=8, skip_layer=4, netdepth_deformation=4,
+                    netdepth_condition=4, min_deg_point=0, max_deg_point=10):
+    """reference models/vanilla_nerf/model_autodecoder.py:168-239 (deformation_mlp=True,
+    enc_after=True, embed_deg=False).
+
+    pos: (B, S, 3) sample positions; condition: (B, 27) encoded view directions;
+    latents: {density (1,128), color (1,128), articulation (1,32)} repeated over all rows
+    (model_autodecoder.py:186-194).  Returns raw_rgb (B, S, 3), raw_density (B, S, 1).
+    """
+    S = pos.shape[1]
+    pos = pos.reshape(-1, 3)
+    BN = pos.shape[0]
+    shape = latents["density"].repeat(BN, 1)
+    app = latents["color"].repeat(BN, 1)
+    art = latents["articulation"].repeat(BN, 1)
+    x = torch.cat([pos, shape, art], -1)
+    for idx in range(netdepth_deformation):  # model_autodecoder.py:200-203
+        x = torch.relu(_lin(p, f"deformations_linear.{idx}", x))
+    x = _lin(p, "deformation_layer", x) + pos  # :205
+    x = pos_enc(x, min_deg_point, max_deg_point)  # :207-212 (enc_after)
+    x = torch.cat([x, shape], -1)
+    inputs = x
+    for idx in range(netdepth):  # :216-220
+        x = torch.relu(_lin(p, f"pts_linears.{idx}", x))
+        if idx % skip_layer == 0 and idx > 0:
+            x = torch.cat([x, inputs], dim=-1)
+    raw_density = _lin(p, "density_layer", x).reshape(-1, S, 1)
+    bottleneck = _lin(p, "bottleneck_layer", x)
+    cond = torch.tile(condition[:, None, :], (1, S, 1)).reshape(-1, condition.shape[-1])
+    x = torch.cat([bottleneck, cond, app], dim=-1)  # :229-231
+    for idx in range(netdepth_condition):
+        x = torch.relu(_lin(p, f"views_linear.{idx}", x))
+    raw_rgb = _lin(p, "rgb_layer", x).reshape(-1, S, 3)
+    return raw_rgb, raw_density
+
+
+def art_activations(raw_rgb, raw_sigma, rgb_padding=0.001, density_bias=-1.0):
+    """NeRF_AE_Art.forward (model_autodecoder.py:321-323): padded sigmoid, softplus(raw - 1)."""
+    rgb = torch.sigmoid(raw_rgb) * (1 + 2 * rgb_padding) - rgb_padding
+    sigma = torch.nn.functional.softplus(raw_sigma + density_bias)
+    return rgb, sigma
+
+
+def art_nerf_forward(params, rays, randomized, white_bkgd, near, far, latents,
+                     num_coarse_samples=64, num_fine_samples=128, deg_view=4, lindisp=False,
+                     u_coarse=None, u_fine=None, return_intermediates=False):
+    """reference NeRF_AE_Art.forward (model_autodecoder.py:278-337), enc_after=True."""
+    ret, inter = [], []
+    weights = t_vals = None
+    for level in range(2):
+        if level == 0:
+            t_vals, samples = sample_along_rays(rays["rays_o"], rays["rays_d"], num_coarse_samples,
+                                                near, far, randomized, lindisp, u_coarse)
+        else:
+            t_mids = 0.5 * (t_vals[..., 1:] + t_vals[..., :-1])
+            t_vals, samples = sample_pdf(t_mids, weights[..., 1:-1], rays["rays_o"],
+                                         rays["rays_d"], t_vals, num_fine_samples, randomized,
+                                         u_fine)
+        venc = pos_enc(rays["viewdirs"], 0, deg_view)
+        raw_rgb, raw_sigma = art_mlp_forward(params[level], samples, venc, latents)
+        rgb, sigma = art_activations(raw_rgb, raw_sigma)
+        comp_rgb, acc, weights, depth = volumetric_rendering(rgb, sigma, t_vals, rays["rays_d"],
+                                                             white_bkgd)
+        ret.append((comp_rgb, acc, depth))
+        inter.append(dict(t_vals=t_vals, raw_rgb=raw_rgb, raw_sigma=raw_sigma, weights=weights))
+    return (ret, inter) if return_intermediates else ret
+
+
+def art_render_level(params, rays, t_vals, level, white_bkgd, latents, deg_view=4):
+    """One NeRF_AE_Art level on GIVEN sample positions (teacher forcing)."""
+    samples = cast_rays(t_vals, rays["rays_o"], rays["rays_d"])
+    raw_rgb, raw_sigma = art_mlp_forward(params[level], samples,
+                                         pos_enc(rays["viewdirs"], 0, deg_view), latents)
+    rgb, sigma = art_activations(raw_rgb, raw_sigma)
+    return volumetric_rendering(rgb, sigma, t_vals, rays["rays_d"], white_bkgd)
+
+
 # ----------------------------------------------------------------------------- metrics
 def img2mse(x, y):
     """reference helper.py:17-18."""

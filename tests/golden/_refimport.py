@@ -86,6 +86,22 @@ def install_stubs():
         sys.path.insert(0, REF)
 
 
+def load_articulated():
+    """Return the reference's models/vanilla_nerf/model_autodecoder module (NeRF_AE_Art)."""
+    import os
+
+    install_stubs()
+    argv, cwd = sys.argv, os.getcwd()
+    try:
+        sys.argv = ["x"]
+        os.chdir(REF)
+        import models.vanilla_nerf.model_autodecoder as mad
+    finally:
+        sys.argv = argv
+        os.chdir(cwd)
+    return mad
+
+
 def load():
     """Return (helper, model_module, ray_utils, sapien_multi) reference modules."""
     import os

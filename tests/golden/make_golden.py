@@ -95,8 +95,9 @@ def frame_rays(H, W_, pose_idx=5, radius=4.0):
                 viewdirs=viewdirs.contiguous()), c2w, focal, dirs
 
 
-def capture_forward(net, rays, randomized, white_bkgd, near=2.0, far=6.0):
-    """Run reference NeRF.forward and record per-level intermediates via module hooks."""
+def capture_forward(net, rays, randomized, white_bkgd, near=2.0, far=6.0, extra=()):
+    """Run reference NeRF.forward and record per-level intermediates via module hooks
+    (``extra``: further positional arguments, e.g. NeRF_AE_Art's latents)."""
     rec = {"t": [], "raw_rgb": [], "raw_sigma": [], "weights": [], "bins": [], "wpdf": []}
     orig_vr, orig_pdf = helper.volumetric_rendering, helper.sample_pdf
 
@@ -119,7 +120,7 @@ def capture_forward(net, rays, randomized, white_bkgd, near=2.0, far=6.0):
     helper.volumetric_rendering, helper.sample_pdf = vr, pdf
     try:
         with torch.no_grad():
-            ret = net(rays, randomized, white_bkgd, near, far)
+            ret = net(rays, randomized, white_bkgd, near, far, *extra)
     finally:
         helper.volumetric_rendering, helper.sample_pdf = orig_vr, orig_pdf
         for h in hooks:
@@ -316,6 +317,42 @@ def case_train_step():
          psnr0=helper.mse2psnr(loss0).detach().numpy(), **grads)
 
 
+def case_articulated():
+    """NeRF_AE_Art.forward (model_autodecoder.py:278-337) with fixed latents (CodeLibrary
+    rows): eval on 256 rays of a 240x320 (config C3) view, and randomized with recorded
+    uniforms on 128 rays; per-level outputs + intermediates + re-association envelope."""
+    mad = _refimport.load_articulated()
+    net = mad.NeRF_AE_Art()
+    sd = W.art_state_dict(0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    net.eval()
+    lat = {k: torch.from_numpy(v) for k, v in W.art_latents(0).items()}
+    rays, c2w, focal, _ = frame_rays(240, 320, pose_idx=11)
+    out = {"digest": np.array(W.digest(sd))}
+    for tag, sel, randomized in (("eval", torch.arange(0, 76800, 300), False),
+                                 ("rand", torch.arange(17, 76800, 600), True)):
+        r = {k: v[sel].contiguous() for k, v in rays.items()}
+
+        def run():
+            if randomized:
+                with RandQueue(11) as rq:
+                    ret, rec = capture_forward(net, r, True, True, extra=(lat,))
+                run.drawn = rq.drawn
+            else:
+                ret, rec = capture_forward(net, r, False, True, extra=(lat,))
+            return level_arrays(ret, rec)
+
+        arrays = run()
+        env = envelope(run)
+        for k, v in {**{kk: r[kk].numpy() for kk in r}, **arrays, **env}.items():
+            out[f"{tag}_{k}"] = v
+        if randomized:
+            out[f"{tag}_u_coarse"], out[f"{tag}_u_fine"] = run.drawn[0], run.drawn[1]
+    for k, v in W.art_latents(0).items():
+        out[f"latent_{k}"] = v
+    save("articulated.npz", **out)
+
+
 if __name__ == "__main__":
     case_rays()
     case_forward_eval()
@@ -325,3 +362,4 @@ if __name__ == "__main__":
     case_composite_edges()
     case_pos_enc()
     case_train_step()
+    case_articulated()

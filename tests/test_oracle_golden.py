@@ -125,3 +125,25 @@ def test_train_step_loss(golden):
             level, name = key[6:].split(".", 1)
             got = params[0 if level == "coarse_mlp" else 1][name].grad.numpy()
             np.testing.assert_allclose(got, g[key], rtol=1e-4, atol=1e-6, err_msg=key)
+
+
+def test_articulated(golden):
+    """NeRF_AE_Art (model_autodecoder.py:278-337): oracle vs the reference's outputs, eval and
+    randomized (recorded uniforms)."""
+    g = golden("articulated.npz")
+    sd = W.art_state_dict(0)
+    assert W.digest(sd) == str(g["digest"])
+    params = O.split_state_dict(sd)
+    lat = {k: _t(g[f"latent_{k}"]) for k in ("density", "color", "articulation")}
+    for tag, randomized in (("eval", False), ("rand", True)):
+        rays = {k: _t(g[f"{tag}_{k}"]) for k in ("rays_o", "rays_d", "viewdirs")}
+        kw = dict(u_coarse=_t(g[f"{tag}_u_coarse"]), u_fine=_t(g[f"{tag}_u_fine"])) if randomized else {}
+        ret, inter = O.art_nerf_forward(params, rays, randomized, True, 2.0, 6.0, lat,
+                                        return_intermediates=True, **kw)
+        for lv, name in enumerate(("coarse", "fine")):
+            np.testing.assert_array_equal(inter[lv]["t_vals"].numpy(), g[f"{tag}_{name}_t"])
+            for j, k in enumerate(("rgb", "acc", "depth")):
+                np.testing.assert_allclose(ret[lv][j].numpy(), g[f"{tag}_{name}_{k}"], rtol=0,
+                                           atol=1e-6, err_msg=f"{tag} {name} {k}")
+            np.testing.assert_allclose(inter[lv]["raw_rgb"].numpy(), g[f"{tag}_{name}_raw_rgb"],
+                                       rtol=0, atol=1e-6)
