@@ -47,6 +47,8 @@ _SIGNATURES = {
     "aon_frame_rays": (c_int, [c_int, c_int, c_float, vp, c_i64, c_i64, vp, vp, vp, vp]),
     "aon_sample_along_rays": (c_int, [vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp]),
     "aon_pos_enc": (c_int, [vp, c_i64, c_int, c_int, vp, vp]),
+    "aon_sample_rays": (c_int, [vp, vp, c_int, c_i64, c_int, c_int, c_float, vp, c_i64, c_int,
+                                c_float, vp, vp, vp, vp, vp]),
     "aon_cast_rays": (c_int, [vp, vp, vp, c_i64, c_int, vp, c_i64, vp, c_int, c_int, vp, vp]),
     "aon_sample_pdf": (c_int, [vp, c_i64, vp, c_i64, c_i64, c_int, c_int, vp, c_i64, vp, c_int,
                                vp, vp, vp, vp, vp]),

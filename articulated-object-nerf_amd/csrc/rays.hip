@@ -162,6 +162,48 @@ __global__ void k_cast_rays(const float* __restrict__ ro, const float* __restric
   }
 }
 
+// Training-ray batches straight from the device-resident dataset (reference
+// datasets/sapien.py:84-113 / :131-154 and sapien_multi.py:196-238): for flat index
+// g = image * H * W + pixel, the camera ray of that pixel (as k_frame_rays) and its target:
+//   mode 0: rgb = u8 / 255                          (C >= 3)
+//   mode 1: rgb * a + (1 - a), a = alpha / 255      (RGBA onto white, sapien.py:98-99)
+//   mode 2: channel 3 is a segmentation mask: rgb where mask > 0, else bg (sapien_multi.py:186-194)
+__global__ void k_sample_rays(const float* __restrict__ poses, const uint8_t* __restrict__ img,
+                              int C, int64_t N, int H, int W, float focal,
+                              const int64_t* __restrict__ idx, int64_t n, int mode, float bg,
+                              float* __restrict__ ro, float* __restrict__ rd,
+                              float* __restrict__ vd, float* __restrict__ target) {
+  const int64_t hw = static_cast<int64_t>(H) * W;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = idx ? idx[q] : q;
+    const int64_t k = g / hw, p = g - k * hw;
+    Mat34 c;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) c.m[e] = poses[12 * k + e];
+    float x, y, ox, oy, oz, rx, ry, rz;
+    pixel_dir(p, H, W, focal, x, y);
+    rotate_normalize(x, y, -1.0f, c, ox, oy, oz, rx, ry, rz, true);
+    ro[3 * q] = ox; ro[3 * q + 1] = oy; ro[3 * q + 2] = oz;
+    rd[3 * q] = rx; rd[3 * q + 1] = ry; rd[3 * q + 2] = rz;
+    if (vd) { vd[3 * q] = rx; vd[3 * q + 1] = ry; vd[3 * q + 2] = rz; }
+    if (target) {
+      const uint8_t* px = img + g * C;
+      float v[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) v[ch] = __fdiv_rn(static_cast<float>(px[ch]), 255.0f);
+      if (mode == 1) {
+        const float a = __fdiv_rn(static_cast<float>(px[3]), 255.0f);
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) v[ch] = __fadd_rn(__fmul_rn(v[ch], a), __fsub_rn(1.0f, a));
+      } else if (mode == 2 && px[3] == 0) {
+        v[0] = v[1] = v[2] = bg;
+      }
+      target[3 * q] = v[0]; target[3 * q + 1] = v[1]; target[3 * q + 2] = v[2];
+    }
+  }
+}
+
 static Mat34 load_c2w(const float* h) {
   Mat34 m;
   for (int i = 0; i < 12; ++i) m.m[i] = h[i];
@@ -240,5 +282,19 @@ extern "C" int aon_cast_rays(const float* rays_o, const float* rays_d, const flo
   const int C = enc ? 3 + 6 * L : 3;
   hipLaunchKernelGGL(k_cast_rays, grid_for(B * S * C, 256, 65536), 256, 0, (hipStream_t)stream,
                      rays_o, rays_d, t, B, S, offset, offset_stride, xyz, min_deg, L, enc);
+  return launch_status(__func__);
+}
+
+extern "C" int aon_sample_rays(const float* poses, const uint8_t* images, int C, int64_t N, int H,
+                               int W, float focal, const int64_t* idx, int64_t n, int mode,
+                               float bg, float* rays_o, float* rays_d, float* viewdirs,
+                               float* target, aon_stream_t stream) {
+  AON_REQUIRE(poses && rays_o && rays_d && N >= 1 && H > 0 && W > 0 && n >= 0, "bad arguments");
+  AON_REQUIRE(!target || (images && C >= 3 && (mode == 0 || C >= 4)), "bad image layout");
+  AON_REQUIRE(mode >= 0 && mode <= 2, "bad mode");
+  AON_REQUIRE(idx || n <= N * (int64_t)H * W, "n exceeds the dataset");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_sample_rays, grid_for(n, 256, 65536), 256, 0, (hipStream_t)stream, poses,
+                     images, C, N, H, W, focal, idx, n, mode, bg, rays_o, rays_d, viewdirs, target);
   return launch_status(__func__);
 }

@@ -67,6 +67,17 @@ int aon_sample_along_rays(const float* rays_o, const float* rays_d, int64_t B, i
                           const float* t_lower, const float* t_upper, const float* u,
                           float* t_out, float* xyz_out, aon_stream_t stream);
 
+/* Ray batches from a device-resident dataset (datasets/sapien.py:84-113, 131-154;
+ * sapien_multi.py:196-238): poses (N, 3, 4) camera-to-world, images (N, H, W, C) uint8.
+ * For each of n flat indices g = image*H*W + pixel (idx == NULL: g = 0 .. n-1) writes the
+ * pixel's ray (as aon_frame_rays) and, when target != NULL, its target rgb:
+ * mode 0 u8/255; mode 1 RGBA alpha-blended onto white; mode 2 channel 3 is a segmentation
+ * mask, background pixels take `bg`. */
+int aon_sample_rays(const float* poses, const uint8_t* images, int C, int64_t N, int H, int W,
+                    float focal, const int64_t* idx, int64_t n, int mode, float bg,
+                    float* rays_o, float* rays_d, float* viewdirs, float* target,
+                    aon_stream_t stream);
+
 /* cast_rays (helper.py:25-26) on per-ray sample positions t (B, S): x = o + t d, then, when
  * offset != NULL, x = offset[r] + x (the articulated deformation, model_autodecoder.py:205);
  * rays_d == NULL (t ignored): x = rays_o[r / S] (points given directly);

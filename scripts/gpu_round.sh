@@ -19,6 +19,12 @@ step() {  # step <name> <timeout> <cmd...>: run, log, stop the session on crash/
 [ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q -s -p no:cacheprovider
 step bench 600 python bench.py "$@"
 tail -1 "$OUT/bench.log" > "$OUT/bench.json"
+if [ "${EXTRA:-0}" = 1 ]; then
+  step bench_art 600 python tools/bench_articulated.py
+  tail -1 "$OUT/bench_art.log" > "$OUT/bench_art.json"
+  step bench_train 600 python tools/bench_train.py
+  tail -1 "$OUT/bench_train.log" > "$OUT/bench_train.json"
+fi
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@"
 [ "${SKIP_PMC:-0}" = 1 ] && exit 0

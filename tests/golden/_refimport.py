@@ -4,7 +4,10 @@ Test infrastructure only; runs in the build container, never on the GPU box.  On
 fixture generator (make_golden.py) uses it.  The one stub with semantics is
 ``kornia.create_meshgrid(H, W, normalized_coordinates=False)`` which must return (1,H,W,2)
 with [...,0] = column index x in [0, W-1] and [...,1] = row index y (kornia 0.6.1,
-pinned at reference requirements.txt:3; used at datasets/ray_utils.py:84).
+pinned at reference requirements.txt:3; used at datasets/ray_utils.py:84).  The dataset
+fixtures also need ``torchvision.transforms.ToTensor`` with its published semantics (PIL / HWC
+ndarray -> CHW tensor; uint8 -> float32 / 255, other dtypes unchanged; used at
+datasets/sapien.py:119 and sapien_multi.py:209-211); everything else is inert.
 """
 import sys
 import types
@@ -52,6 +55,22 @@ class _Anything:
         return _Anything()
 
 
+class _ToTensor:
+    """torchvision.transforms.ToTensor (PIL.Image or HWC/HW ndarray -> CHW; uint8 -> /255)."""
+
+    def __call__(self, pic):
+        import numpy as np
+        import torch
+
+        a = np.array(pic, copy=True)
+        if a.ndim == 2:
+            a = a[:, :, None]
+        t = torch.from_numpy(a).permute(2, 0, 1).contiguous()
+        if t.dtype == torch.uint8:
+            return t.to(dtype=torch.float32).div(255)
+        return t
+
+
 def install_stubs():
     import torch.nn as nn
 
@@ -73,10 +92,11 @@ def install_stubs():
     _mod("piqa.ssim", SSIM=_Anything)
     _mod("cv2", COLORMAP_JET=2, COLORMAP_HOT=11)
     _mod("imageio")
-    tv = _mod("torchvision", transforms=_Anything(), models=_Anything())
+    tv = _mod("torchvision", models=_Anything())
     _mod("torchvision.ops", masks_to_boxes=_Anything(), box_iou=_Anything())
-    _mod("torchvision.transforms", Compose=_Anything, ToTensor=_Anything, Normalize=_Anything,
+    _mod("torchvision.transforms", Compose=_Anything, ToTensor=_ToTensor, Normalize=_Anything,
          Resize=_Anything)
+    tv.transforms = sys.modules["torchvision.transforms"]
     _mod("torchvision.utils", make_grid=_Anything())
     _mod("torchvision.models", resnet34=_Anything(), resnet18=_Anything())
     tv.ops = sys.modules["torchvision.ops"]
@@ -84,6 +104,23 @@ def install_stubs():
     _mod("torch_optimizer")
     if REF not in sys.path:
         sys.path.insert(0, REF)
+
+
+def load_datasets():
+    """Return the reference's datasets.sapien and datasets.sapien_multi modules."""
+    import os
+
+    install_stubs()
+    argv, cwd = sys.argv, os.getcwd()
+    try:
+        sys.argv = ["x"]
+        os.chdir(REF)
+        import datasets.sapien as sapien
+        import datasets.sapien_multi as sapien_multi
+    finally:
+        sys.argv = argv
+        os.chdir(cwd)
+    return sapien, sapien_multi
 
 
 def load_articulated():

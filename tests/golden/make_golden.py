@@ -8,6 +8,7 @@ from numpy PCG64 by oracle/weights.py (their sha256 is stored with every fixture
 
     python tests/golden/make_golden.py
 """
+import json
 import os
 import sys
 
@@ -353,6 +354,83 @@ def case_articulated():
     save("articulated.npz", **out)
 
 
+def _write_png(path, arr, mode):
+    from PIL import Image
+
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    Image.fromarray(arr, mode).save(path)
+
+
+def make_mini_datasets(root):
+    """Tiny synthetic datasets in the reference's two layouts (data files, committed):
+    sapien_mini/{train,val}/{rgb/r_<i>.png (RGBA 40x30), transforms.json} (sapien.py) and
+    multi_mini/inst1/train/deg0/{rgb (RGB), seg (L)}/r_<i>.png + transforms.json (sapien_multi)."""
+    rng = np.random.Generator(np.random.PCG64(21))
+    poses = sapien_multi.create_spheric_poses(4.0)
+    for split, n in (("train", 3), ("val", 2)):
+        frames = {}
+        for i in range(n):
+            img = rng.integers(0, 256, size=(30, 40, 4), dtype=np.uint8)
+            img[:8, :, 3] = 0          # fully transparent rows
+            img[-6:, :, 3] = 255       # opaque rows
+            _write_png(os.path.join(root, "sapien_mini", split, "rgb", f"r_{i}.png"), img, "RGBA")
+            frames[f"r_{i}"] = np.asarray(poses[3 + 7 * i + (split == "val")]).tolist()
+        with open(os.path.join(root, "sapien_mini", split, "transforms.json"), "w") as f:
+            json.dump({"camera_angle_x": 0.6911112070083618, "frames": frames}, f)
+    base = os.path.join(root, "multi_mini", "inst1", "train", "deg0")
+    frames = {}
+    for i in range(2):
+        img = rng.integers(0, 256, size=(30, 40, 3), dtype=np.uint8)
+        seg = np.zeros((30, 40), dtype=np.uint8)
+        seg[6:22, 9 + 5 * i:30 + 5 * i] = 3
+        _write_png(os.path.join(base, "rgb", f"r_{i}.png"), img, "RGB")
+        _write_png(os.path.join(base, "seg", f"r_{i}.png"), seg, "L")
+        frames[f"r_{i}"] = np.asarray(poses[11 + 5 * i]).tolist()
+    with open(os.path.join(base, "transforms.json"), "w") as f:
+        json.dump({"camera_angle_x": 0.6911112070083618, "frames": frames}, f)
+
+
+def case_datasets():
+    """Reference SapienDataset (train buffers, val samples) and SapienDatasetMulti read_data +
+    get_ray_batch (recorded pixel indices) on the mini datasets, img_wh (32, 24) (LANCZOS
+    resize from 40x30)."""
+    sapien, smulti = _refimport.load_datasets()
+    root = os.path.join(HERE, "data")
+    make_mini_datasets(root)
+    out = {}
+    ds = sapien.SapienDataset(os.path.join(root, "sapien_mini"), "train", img_wh=(32, 24),
+                              white_back=True)
+    files = [f for f in os.listdir(os.path.join(root, "sapien_mini", "train", "rgb"))]
+    out["train_files"] = np.array(files)  # the reference's (listdir) image order
+    out["train_focal"] = np.array(ds.focal)
+    out["train_rays"] = ds.all_rays.numpy()
+    out["train_rays_d"] = ds.all_rays_d.numpy()
+    out["train_rgbs"] = ds.all_rgbs.numpy()
+    dv = sapien.SapienDataset(os.path.join(root, "sapien_mini"), "val", img_wh=(32, 24),
+                              white_back=True)
+    for i in range(2):
+        smp = dv[i] if i == 0 else dv.__getitem__(i)
+        for k in ("rays_o", "rays_d", "viewdirs", "instance_mask", "target"):
+            out[f"val{i}_{k}"] = smp[k].numpy()
+    m = object.__new__(smulti.SapienDatasetMulti)
+    m.root_dir, m.split, m.img_wh, m.white_back = os.path.join(root, "multi_mini"), "train", (32, 24), True
+    m.img_transform = lambda x: x
+    rays_o, view_dirs, rays_d, img, seg = m.read_data("inst1", "deg0", 1)
+    pix = torch.from_numpy(np.random.Generator(np.random.PCG64(5)).integers(0, 768, 97)).long()
+    orig = torch.randint
+    torch.randint = lambda *a, **k: pix
+    try:
+        rays, rd, vd, _, rgbs, msk = m.get_ray_batch(rays_o, view_dirs, rays_d, img, seg, 97)
+    finally:
+        torch.randint = orig
+    out["multi_files"] = np.array(os.listdir(os.path.join(root, "multi_mini", "inst1", "train",
+                                                          "deg0", "rgb")))
+    out["multi_pix"] = pix.numpy()
+    out["multi_rays_o"], out["multi_rays_d"], out["multi_viewdirs"] = rays.numpy(), rd.numpy(), vd.numpy()
+    out["multi_rgbs"], out["multi_mask"] = rgbs.numpy(), msk.numpy()
+    save("datasets.npz", **out)
+
+
 if __name__ == "__main__":
     case_rays()
     case_forward_eval()
@@ -363,3 +441,4 @@ if __name__ == "__main__":
     case_pos_enc()
     case_train_step()
     case_articulated()
+    case_datasets()
