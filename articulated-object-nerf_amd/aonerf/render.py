@@ -22,6 +22,7 @@ def _chunks(B, chunk):
         yield i, min(i + chunk, B)
 
 
+@torch.no_grad()
 def render_rays(model, batch, chunk, white_bkgd, near, far):
     """LitNeRF.render_rays (model.py:295-321): fine-level comp_rgb/acc/depth over all rays and
     psnr_legacy against batch['target'] (returned as 'psnr' instead of being logged)."""
@@ -39,6 +40,7 @@ def render_rays(model, batch, chunk, white_bkgd, near, far):
     return out
 
 
+@torch.no_grad()
 def render_rays_test(model, batch, chunk, white_bkgd, near, far):
     """LitNeRF.render_rays_test (model.py:323-348) -> {target, instance_mask, rgb}."""
     out = render_rays(model, {k: v for k, v in batch.items() if k != "target"}, chunk, white_bkgd,
@@ -50,6 +52,7 @@ def render_rays_test(model, batch, chunk, white_bkgd, near, far):
     return test_output
 
 
+@torch.no_grad()
 def render_frame(model, c2w, H, W, focal, near=2.0, far=6.0, white_bkgd=True, p0=0, n=None,
                  chunk=None, timers=None):
     """Fused ray generation + two-level render of pixels [p0, p0+n) of an H x W frame.

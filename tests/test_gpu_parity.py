@@ -88,7 +88,7 @@ def make_nerf(precision, **kw):
 
     net = NeRF(precision=precision, **kw).cuda()
     net.load_state_dict({k: torch.from_numpy(v) for k, v in W.nerf_state_dict(0).items()})
-    return net
+    return net.requires_grad_(False)  # inference: the fused MLP path (no autograd graph)
 
 
 @pytest.fixture(scope="module", params=PRECISIONS)
