@@ -58,6 +58,8 @@ _SIGNATURES = {
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,
                                   vp, vp, vp, vp]),
+    "aon_image_mse": (c_int, [vp, vp, c_i64, c_i64, vp, c_int, vp, vp, vp]),
+    "aon_to8b": (c_int, [vp, c_i64, vp, vp]),
     "aon_gemm_workspace_bytes": (c_size, [ctypes.POINTER(AonGemmArgs)]),
     "aon_gemm": (c_int, [ctypes.POINTER(AonGemmArgs), vp, c_size, vp]),
     "aon_composite_bwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp, vp,

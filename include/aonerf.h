@@ -151,6 +151,17 @@ int aon_composite_fwd(const float* rgb, int64_t rgb_stride, const float* sigma,
                       int S, int white_bkgd, int act, float* comp_rgb, float* acc,
                       float* weights, float* depth, aon_stream_t stream);
 
+/* ---------------------------------------------------------------- evaluation */
+/* Per-image mean squared error of n_images images of `pixels` rgb pixels ((n, P, 3) fp32):
+ * clip = 1 clips both sides to [0, 1] first (psnr_each, models/interface.py:54-62);
+ * mask (n, P) uint8 != NULL restricts to the masked pixels (the object PSNR of
+ * get_obj_rgbs_from_segmap, models/utils.py:102-109).  psnr (may be NULL) = -10 ln(mse)/ln 10. */
+int aon_image_mse(const float* pred, const float* gt, int64_t n_images, int64_t pixels,
+                  const uint8_t* mask, int clip, float* mse, float* psnr, aon_stream_t stream);
+
+/* to8b (models/utils.py:12-13): out = uint8(255 * clip(x, 0, 1)) (truncating cast). */
+int aon_to8b(const float* x, int64_t n, uint8_t* out, aon_stream_t stream);
+
 /* ---------------------------------------------------------------- training path */
 /* C (M x N) = epilogue(A (M x K) . B (K x N)): fp32 operands, fp16-MFMA hi/lo split
  * (fp32-class accuracy), the building block of the layer-by-layer training forward
