@@ -23,19 +23,35 @@ namespace mlp {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
+#ifndef AON_FMA_MIX
+#define AON_FMA_MIX 1
+#endif
+
 __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ h8 as_h8(f4 v) { return __builtin_bit_cast(h8, v); }
 
-// 8 fp32 values (already at activation scale) -> (hi, lo * 2^11) fp16 fragments
+// fp32 value (already at activation scale) -> (hi, lo) fp16 pair: V2 lo = x - hi (exact in
+// fp32, normal in fp16 for |x| >= 2^-3 at scale); V1 lo = (x - hi) * 2^11
+__device__ __forceinline__ _Float16 lo_of(float v, _Float16 h) {
+#if AON_F16X3_V2
+  // v - hi is exact in fp32; as an fma with the fp16 operand widened in the instruction it can
+  // issue as one v_fma_mix_f32 instead of v_cvt_f32_f16 + v_sub_f32
+  return static_cast<_Float16>(__builtin_fmaf(static_cast<float>(h), -1.0f, v));
+#else
+  return static_cast<_Float16>(__fmul_rn(__fsub_rn(v, static_cast<float>(h)), kLoScale));
+#endif
+}
+
+// 8 fp32 values (already at activation scale) -> (hi, lo) fp16 fragments
 __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const _Float16 h = static_cast<_Float16>(v[j]);
     hi[j] = h;
-    lo[j] = static_cast<_Float16>(__fmul_rn(__fsub_rn(v[j], static_cast<float>(h)), kLoScale));
+    lo[j] = lo_of(v[j], h);
   }
 }
 
@@ -96,18 +112,45 @@ struct Frag {
 // part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
 template <bool RELU, int NCOL, int NO>
 __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
-                                         Frag<NO, NCOL>& out, int pr) {
+                                         const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr) {
   const int uu = q >> 1, r0 = (q & 1) * 2;
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
+    float vv[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
+#if AON_F16X3_V2
+      // one accumulator at scale 2^9 -> activation scale 2^3, plus the (pre-scaled) bias
+      float v = fmaf(hh[uu][c][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
+      (void)xx;
+#else
       float v = fmaf(xx[uu][c][r0 + e], 1.0f / kLoScale, hh[uu][c][r0 + e]);
+      (void)bias;
+#endif
       if (RELU) v = fmaxf(v, 0.0f);
-      const _Float16 h = static_cast<_Float16>(v);
-      out.hi[pr][c][2 * q + e] = h;
-      out.lo[pr][c][2 * q + e] = static_cast<_Float16>(__fmul_rn(__fsub_rn(v, static_cast<float>(h)), kLoScale));
+      vv[e] = v;
     }
+#if AON_F16X3_V2 && AON_FMA_MIX
+    // hi pair by one v_cvt_pk_f16_f32; lo_e = v_e - hi_e by v_fma_mix_f32 reading the fp16 half
+    // in place (exact in fp32), then one more cvt_pk
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 hp = {static_cast<_Float16>(vv[0]), static_cast<_Float16>(vv[1])};
+    const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
+    float d0, d1;
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(vv[0]));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(vv[1]));
+    out.hi[pr][c][2 * q] = hp[0];
+    out.hi[pr][c][2 * q + 1] = hp[1];
+    out.lo[pr][c][2 * q] = static_cast<_Float16>(d0);
+    out.lo[pr][c][2 * q + 1] = static_cast<_Float16>(d1);
+#else
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const _Float16 h = static_cast<_Float16>(vv[e]);
+      out.hi[pr][c][2 * q + e] = h;
+      out.lo[pr][c][2 * q + e] = lo_of(vv[e], h);
+    }
+#endif
   }
 }
 
@@ -122,15 +165,20 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
   constexpr int NP = d.u / 2;
   static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
   f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
+  f4 pbias[2];                     // V2: that pair's biases, added in its epilogue
 #pragma unroll
   for (int pr = 0; pr < NP; ++pr) {
-    f4 hh[2][NCOL], xx[2][NCOL];
+    f4 hh[2][NCOL], xx[2][NCOL], bias[2];
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
-      const f4 bias = *reinterpret_cast<const f4*>(bias_s + d.bias0 + 16 * (2 * pr + uu) + 4 * g);
+      bias[uu] = *reinterpret_cast<const f4*>(bias_s + d.bias0 + 16 * (2 * pr + uu) + 4 * g);
 #pragma unroll
       for (int c = 0; c < NCOL; ++c) {
-        hh[uu][c] = bias;
+#if AON_F16X3_V2
+        hh[uu][c] = f4{0.f, 0.f, 0.f, 0.f};  // bias joins in the epilogue: no LDS read to wait on
+#else
+        hh[uu][c] = bias[uu];
+#endif
         xx[uu][c] = f4{0.f, 0.f, 0.f, 0.f};
       }
     }
@@ -146,27 +194,35 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
           const int ia = k < NA ? k : 0, ib = (k >= d.ka && k - d.ka < NB) ? k - d.ka : 0;
           const h8 xh = k < d.ka ? a.hi[ia][c] : b.hi[ib][c];
           const h8 xl = k < d.ka ? a.lo[ia][c] : b.lo[ib][c];
+#if AON_F16X3_V2
+          hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
+          hh[uu][c] = mfma16(wh, xl, hh[uu][c]);
+          hh[uu][c] = mfma16(wl, xh, hh[uu][c]);
+#else
           hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
           xx[uu][c] = mfma16(wh, xl, xx[uu][c]);
           xx[uu][c] = mfma16(wl, xh, xx[uu][c]);
+#endif
         }
       }
-      if (pr > 0 && k < 4) epi_part<RELU>(k, phh, pxx, out, pr - 1);
+      if (pr > 0 && k < 4) epi_part<RELU>(k, phh, pxx, pbias, out, pr - 1);
     }
     if (pr > 0) {
 #pragma unroll
-      for (int q = K; q < 4; ++q) epi_part<RELU>(q, phh, pxx, out, pr - 1);
+      for (int q = K; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, pr - 1);
     }
 #pragma unroll
-    for (int uu = 0; uu < 2; ++uu)
+    for (int uu = 0; uu < 2; ++uu) {
+      pbias[uu] = bias[uu];
 #pragma unroll
       for (int c = 0; c < NCOL; ++c) {
         phh[uu][c] = hh[uu][c];
         pxx[uu][c] = xx[uu][c];
       }
+    }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) epi_part<RELU>(q, phh, pxx, out, NP - 1);
+  for (int q = 0; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, NP - 1);
 }
 
 // single-tile head (density / rgb): returns the 16-row tile at activation scale
@@ -179,7 +235,11 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
   const f4 bias = *reinterpret_cast<const f4*>(bias_s + d.bias0 + 4 * g);
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
+#if AON_F16X3_V2
+    hh[c] = f4{0.f, 0.f, 0.f, 0.f};
+#else
     hh[c] = bias;
+#endif
     xx[c] = f4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
@@ -189,15 +249,26 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
     p.take(blk, wh, wl);
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
+#if AON_F16X3_V2
+      hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
+      hh[c] = mfma16(wh, a.lo[k][c], hh[c]);
+      hh[c] = mfma16(wl, a.hi[k][c], hh[c]);
+#else
       hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
       xx[c] = mfma16(wh, a.lo[k][c], xx[c]);
       xx[c] = mfma16(wl, a.hi[k][c], xx[c]);
+#endif
     }
   }
 #pragma unroll
   for (int c = 0; c < NCOL; ++c)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) res[c][r] = fmaf(xx[c][r], 1.0f / kLoScale, hh[c][r]);
+    for (int r = 0; r < 4; ++r)
+#if AON_F16X3_V2
+      res[c][r] = fmaf(hh[c][r], 1.0f / (kWS * kActS), bias[r]);  // true scale (head bias unscaled)
+#else
+      res[c][r] = fmaf(xx[c][r], 1.0f / kLoScale, hh[c][r]);
+#endif
 }
 
 #ifndef AON_RING
@@ -300,11 +371,11 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) ev[k][e] *= kActScale;
+      for (int e = 0; e < 8; ++e) ev[k][e] *= (AON_F16X3_V2 ? kActS : kActScale);
       split8(ev[k], enc.hi[k][c], enc.lo[k][c]);
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) vv[e] *= kActScale;
+    for (int e = 0; e < 8; ++e) vv[e] *= (AON_F16X3_V2 ? kActS : kActScale);
     split8(vv, venc.hi[0][c], venc.lo[0][c]);
   }
 
@@ -356,7 +427,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
       if (rows[c] < N) {
-        const float s = 1.0f / kActScale;
+        const float s = AON_F16X3_V2 ? 1.0f : 1.0f / kActScale;  // V2 heads are at true scale
         const f4 o = {act_rgb(rgb[c][0] * s, act), act_rgb(rgb[c][1] * s, act),
                       act_rgb(rgb[c][2] * s, act), act_sigma(dens[c][0] * s, act)};
         *reinterpret_cast<f4*>(raw + 4 * rows[c]) = o;
@@ -404,14 +475,26 @@ __global__ void k_pack_f16x3(PackArgs a, float* __restrict__ out_f) {
         }
         if (o < d.out_real && col >= 0) w = a.w[li][(int64_t)o * (d.len_a + d.len_b) + col];
       }
+#if AON_F16X3_V2
+      w *= kWS;  // exact (power of two)
+      const _Float16 h = static_cast<_Float16>(w);
+      out[e] = lo_part ? static_cast<_Float16>(w - static_cast<float>(h)) : h;
+#else
       const _Float16 h = static_cast<_Float16>(w);
       out[e] = lo_part ? static_cast<_Float16>((w - static_cast<float>(h)) * kLoScale) : h;
+#endif
     } else {
       const int i = static_cast<int>(e - nhalf);
       int li = 0;
       while (li + 1 < kNumLayers && a.layers[li + 1].bias0 <= i) ++li;
       const int o = i - a.layers[li].bias0;
-      bias_out[i] = o < a.layers[li].out_real ? a.b[li][o] * kActScale : 0.f;
+#if AON_F16X3_V2
+      // hidden layers add the bias at activation scale; the 1-tile heads at true scale
+      const float bs = a.layers[li].u == 1 ? 1.0f : kActS;
+#else
+      const float bs = kActScale;
+#endif
+      bias_out[i] = o < a.layers[li].out_real ? a.b[li][o] * bs : 0.f;
     }
   }
 }

@@ -67,6 +67,14 @@ constexpr LayerDesc kLayersH[kNumLayers] = {
 // |x| = 65504 * 256); the lo halves are carried at 2^11 scale
 constexpr float kActScale = 1.0f / 256.0f;
 constexpr float kLoScale = 2048.0f;
+// V2 numerics (AON_F16X3_V2): activations carried at 2^3, weights at 2^6, so the lo parts
+// (x - fp16(x)) stay in fp16's normal range unscaled and hi*hi, hi*lo, lo*hi share ONE fp32
+// accumulator at scale 2^9; the epilogue folds the 2^-6 and the bias into one fma.
+#ifndef AON_F16X3_V2
+#define AON_F16X3_V2 1
+#endif
+constexpr float kActS = 8.0f;
+constexpr float kWS = 64.0f;
 
 constexpr int kBlocks = 2344;                                     // sum of (ka+kb)*u
 constexpr int kStreamBlocks = (kBlocks + 63) / 64 * 64;          // 2368: whole chunks of 16/32/64

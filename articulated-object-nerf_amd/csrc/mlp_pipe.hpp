@@ -9,6 +9,10 @@
 #include "aon_common.hpp"
 #include "mlp_layout.hpp"
 
+#ifndef AON_DMA_ASM
+#define AON_DMA_ASM 1
+#endif
+
 namespace aon {
 namespace mlp {
 
@@ -95,11 +99,29 @@ struct DmaPipe {
 #pragma unroll
     for (int i = 0; i < kCopies; ++i) {
       const int e = i * THREADS + tid;  // 16-B element of the chunk; LDS dst is lane-linear
+#if AON_DMA_ASM
+      // Opaque to the compiler: with a visible LDS-DMA in flight hipcc drains lgkmcnt to 0
+      // before every ds_read (defeating the fragment prefetch); hidden, it keeps counted
+      // lgkmcnt(N) waits.  Ordering is ours: begin() waits vmcnt for this wave's copies and
+      // lgkmcnt(0), then s_barrier, before any wave reads the chunk or reuses its slot.
+      const uint32_t m0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst + e - lane));
+      const f4* g = src + (size_t)c * kChunk * 64 + e;
+      // M0 is reserved to the compiler, which on gfx950 only uses it for LDS-DMA / sendmsg /
+      // GWS -- none of them elsewhere in these kernels (checked in the ISA)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off"
+                   :
+                   : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(g)
+                   : "memory", "m0");
+#pragma clang diagnostic pop
+#else
       __builtin_amdgcn_global_load_lds(
           reinterpret_cast<const void*>(src + (size_t)c * kChunk * 64 + e),
           reinterpret_cast<__attribute__((address_space(3))) void*>(
               reinterpret_cast<uintptr_t>(dst + e - lane)),
           16, 0, 0);
+#endif
     }
   }
   __device__ __forceinline__ void start() {
