@@ -24,6 +24,14 @@ class AonMlpParams(ctypes.Structure):
                 ("rgb_w", vp), ("rgb_b", vp)]
 
 
+class AonMlpArtParams(ctypes.Structure):
+    _fields_ = [("def_w", vp * 4), ("def_b", vp * 4), ("deformation_w", vp), ("deformation_b", vp),
+                ("pts_w", vp * 8), ("pts_b", vp * 8), ("density_w", vp), ("density_b", vp),
+                ("bottleneck_w", vp), ("bottleneck_b", vp), ("views_w", vp * 4),
+                ("views_b", vp * 4), ("rgb_w", vp), ("rgb_b", vp), ("ld_def0", c_i64),
+                ("ld_pts0", c_i64), ("ld_pts5", c_i64), ("ld_view0", c_i64)]
+
+
 class AonGemmArgs(ctypes.Structure):
     _fields_ = [("M", c_i64), ("N", c_i64), ("K", c_i64), ("A", vp), ("lda", c_i64), ("a_kc", c_int),
                 ("A2", vp), ("lda2", c_i64), ("K1", c_i64), ("a2_rdiv", c_i64),
@@ -56,6 +64,10 @@ _SIGNATURES = {
     "aon_mlp_pack": (c_int, [ctypes.POINTER(AonMlpParams), c_int, vp, vp]),
     "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
+    "aon_mlp_art_packed_bytes": (c_size, []),
+    "aon_mlp_art_pack": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
+    "aon_mlp_art_fwd": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
+    "aon_mlp_art_fwd_points": (c_int, [vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,
                                   vp, vp, vp, vp]),
     "aon_image_mse": (c_int, [vp, vp, c_i64, c_i64, vp, c_int, vp, vp, vp]),

@@ -37,8 +37,10 @@ class NeRFMLP(nn.Module):
                  shape_latent_dim=128, appearance_latent_dim=128, articulation_latent_dim=32,
                  skip_layer: int = 4, input_ch: int = 3, input_ch_view: int = 3,
                  num_rgb_channels: int = 3, num_density_channels: int = 1,
-                 deformation_mlp: bool = True, enc_after: bool = True, embed_deg: bool = False):
+                 deformation_mlp: bool = True, enc_after: bool = True, embed_deg: bool = False,
+                 fused: bool = True):
         super().__init__()
+        self.fused = fused  # one fused kernel per level (aon_mlp_art_fwd) vs GEMM per layer
         cfg = dict(netdepth=netdepth, netwidth=netwidth, netdepth_deformation=netdepth_deformation,
                    netwidth_deformation=netwidth_deformation, netdepth_condition=netdepth_condition,
                    netwidth_condition=netwidth_condition, shape_latent_dim=shape_latent_dim,
@@ -112,10 +114,71 @@ class NeRFMLP(nn.Module):
         }
 
     @torch.no_grad()
-    def forward_rays(self, rays_o, rays_d, viewdirs, t_vals, latents):
-        """One level's MLP on samples o + t d -> raw (B*S, 4) = [raw_rgb, raw_sigma]."""
+    def packed_weights(self, latents):
+        """The fused kernel's fp16x3 weight stream with this call's folded biases
+        (aon_mlp_art_pack; re-packed per call: the folded biases follow the latent codes)."""
+        fb = self.folded_biases(latents)
+        W = lambda m: L.contig(m.weight.detach())  # noqa: E731
+        b = lambda m: L.contig(m.bias.detach())  # noqa: E731
+        keep = []  # contiguous copies (if any) must live until the pack is enqueued
+
+        def ptr(t):
+            keep.append(t)
+            return t.data_ptr()
+
+        prm = L.AonMlpArtParams()
+        for i, m in enumerate(self.deformations_linear):
+            prm.def_w[i] = ptr(W(m))
+            prm.def_b[i] = ptr(fb["def0"] if i == 0 else b(m))
+        prm.deformation_w, prm.deformation_b = ptr(W(self.deformation_layer)), ptr(b(self.deformation_layer))
+        for i, m in enumerate(self.pts_linears):
+            prm.pts_w[i] = ptr(W(m))
+            prm.pts_b[i] = ptr(fb["pts0"] if i == 0 else fb["pts_skip"] if i == self.skip_layer + 1
+                               else b(m))
+        prm.density_w, prm.density_b = ptr(W(self.density_layer)), ptr(b(self.density_layer))
+        prm.bottleneck_w, prm.bottleneck_b = ptr(W(self.bottleneck_layer)), ptr(b(self.bottleneck_layer))
+        for i, m in enumerate(self.views_linear):
+            prm.views_w[i] = ptr(W(m))
+            prm.views_b[i] = ptr(fb["view0"] if i == 0 else b(m))
+        prm.rgb_w, prm.rgb_b = ptr(W(self.rgb_layer)), ptr(b(self.rgb_layer))
+        prm.ld_def0 = self.deformations_linear[0].weight.shape[1]
+        prm.ld_pts0 = self.pts_linears[0].weight.shape[1]
+        prm.ld_pts5 = self.pts_linears[self.skip_layer + 1].weight.shape[1]
+        prm.ld_view0 = self.views_linear[0].weight.shape[1]
+        dev = self.rgb_layer.weight.device
+        nbytes = L.lib().aon_mlp_art_packed_bytes()
+        buf = getattr(self, "_art_packed", None)
+        if buf is None or buf.device != dev:
+            buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+            self._art_packed = buf
+        L.call("aon_mlp_art_pack", L.ctypes.byref(prm), L.ptr(buf), L.stream(dev))
+        return buf
+
+    def _fused_ok(self):
+        # the fused kernel is compiled for the default geometry (mlp_layout.hpp kLayersArt)
+        return (self.fused and self.netdepth == 8 and self.netwidth == 256 and self.skip_layer == 4
+                and self.netdepth_deformation == 4 and self.netwidth_deformation == 128
+                and self.netdepth_condition == 4 and self.netwidth_condition == 128
+                and self.input_ch == 3 and self.input_ch_view == 3 and self.min_deg_point == 0
+                and self.max_deg_point == 10 and self.deg_view == 4
+                and self.num_rgb_channels == 3 and self.num_density_channels == 1)
+
+    @torch.no_grad()
+    def forward_rays(self, rays_o, rays_d, viewdirs, t_vals, latents, act=L.ACT_NONE):
+        """One level's MLP on samples o + t d -> raw (B*S, 4) = [raw_rgb, raw_sigma]: one fused
+        kernel (aon_mlp_art_fwd: cast_rays, deformation, both pos_encs, trunk, view branch;
+        ``act=L.ACT_ARTIC`` also applies model_autodecoder.py:321-323), or the layer-by-layer
+        GEMM path when ``fused`` is off."""
         L.require_gpu(rays_o, rays_d, viewdirs, t_vals)
         B, S = t_vals.shape
+        if self._fused_ok():
+            raw = torch.empty((B * S, 4), device=t_vals.device)
+            L.call("aon_mlp_art_fwd", L.ptr(self.packed_weights(latents)), L.ptr(L.contig(rays_o)),
+                   L.ptr(L.contig(rays_d)), L.ptr(L.contig(viewdirs)), L.ptr(L.contig(t_vals)), B,
+                   S, act, L.ptr(raw), L.stream(t_vals.device))
+            return raw
+        if act != L.ACT_NONE:
+            raise ValueError("the layer-by-layer path returns raw outputs only")
         R, dev = B * S, t_vals.device
         xyz = torch.empty((R, 3), device=dev)
         L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
@@ -187,6 +250,13 @@ class NeRFMLP(nn.Module):
         condition (B, 27) encoded view directions -> (raw_rgb (B, S, 3), raw_density (B, S, 1))."""
         L.require_gpu(pos, condition)
         B, S, _ = pos.shape
+        if self._fused_ok():
+            raw = torch.empty((B * S, 4), device=pos.device)
+            L.call("aon_mlp_art_fwd_points", L.ptr(self.packed_weights(latents)),
+                   L.ptr(L.contig(pos.reshape(-1, 3))), L.ptr(L.contig(condition)), B, S,
+                   L.ACT_NONE, L.ptr(raw), L.stream(pos.device))
+            raw = raw.view(B, S, 4)
+            return raw[..., :3], raw[..., 3:]
         raw = self._mlp(L.contig(pos.reshape(-1, 3)), L.contig(condition), S, latents).view(B, S, 4)
         return raw[..., :3], raw[..., 3:]
 

@@ -1,0 +1,247 @@
+// Fused forward of the articulated NeRFMLP (reference models/vanilla_nerf/model_autodecoder.py:
+// 168-239, default geometry: deformation_mlp, enc_after) on the fp16x3 MFMA path of
+// mlp_f16x3.hip, one kernel per level:
+//
+//   xyz = o + t d                                     (helper.py:25-26; or given points)
+//   h = relu(D3 relu(D2 relu(D1 relu(D0 [xyz | shape, art]))))          :196-203
+//   x' = deformation_layer(h) + xyz;  enc = pos_enc(x', 0, 10)          :205-212
+//   trunk on [enc | shape] with the skip concat, density, bottleneck    :214-225
+//   view branch relu(V3 ... relu(V0 [bottleneck | enc_dir | appearance])), rgb head  :226-237
+//   optional padded sigmoid / softplus(raw - 1) (model_autodecoder.py:321-323)
+//
+// The latent columns are folded into per-call biases by the host (NeRFMLP.folded_biases), so
+// the stream (mlp_layout.hpp kLayersArt) holds only per-sample columns.  The deformation head's
+// output lands in lane group 0 (rows 0..2 of its tile, column = sample); it is broadcast to the
+// sample's other three lane groups with ds_bpermute, added to xyz in fp32 and encoded in
+// registers, so nothing leaves the chip between the deformation and the raw outputs.
+#include "mlp_f16x3_core.hpp"
+
+namespace aon {
+namespace mlp {
+
+// MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: points (N, 3), condition (B, 27)
+template <int MODE, int NCOL>
+__global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_art_f16x3(
+    const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
+    const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
+    int64_t B, int S, int act, float* __restrict__ raw) {
+  using G = GeomH<NCOL>;
+  using Net = NetArtH;
+  constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
+  __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + kStash];
+  float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
+  f4* stash = smem + kLdsWeights + Net::kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 6 * NCOL +
+              (threadIdx.x & 63);  // lane-private slots
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int64_t N = B * S;
+
+  WeightPipe<Net, G::kThreads> p;
+  p.wbuf = smem;
+  p.src = wstream;
+  p.tid = tid;
+  p.lane = lane;
+  p.start();
+  for (int i = tid; i < Net::kBiasFloats; i += G::kThreads) bias_s[i] = bias_g[i];
+
+  // deformation input (xyz, natural order: lane group 0 elements 0..2) and enc_dir fragments
+  Frag<1, NCOL> din, venc;
+  int64_t rows[NCOL];
+  float px[NCOL][3];
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    const int64_t row = (int64_t)blockIdx.x * G::kRowsPerBlock + wave * G::kRowsPerWave + 16 * c + j;
+    rows[c] = row;
+    const int64_t rr = row < N ? row : N - 1;
+    const int64_t ray = rr / S;
+    float vv[8];
+    if (MODE == 0) {
+      const float* ro = in0 + 3 * ray;
+      const float* rd = in1 + 3 * ray;
+      const float* vd = in2 + 3 * ray;
+      const float tt = in3[rr];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) px[c][q] = __fadd_rn(ro[q], __fmul_rn(tt, rd[q]));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
+    } else {
+      const float* x = in0 + rr * 3;
+      const float* cd = in1 + ray * 27;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) px[c][q] = x[q];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int f = 8 * g + e;
+        vv[e] = f < 27 ? cd[f] : 0.f;
+      }
+    }
+    float dv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? px[c][e < 3 ? e : 0] * kActS : 0.f;
+    split8(dv, din.hi[0][c], din.lo[0][c]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vv[e] *= kActS;
+    split8(vv, venc.hi[0][c], venc.lo[0][c]);
+    stash[64 * (6 * c + 4)] = __builtin_bit_cast(f4, venc.hi[0][c]);
+    stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
+  }
+
+  FragPipe<WeightPipe<Net, G::kThreads>> fp(p);
+  fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
+  lds_float* bias_l = opaque_lds(bias_s + 4 * g);
+
+  Frag<8, NCOL> x, y;
+  Frag<1, NCOL> none;
+  // deformation MLP (model_autodecoder.py:196-205)
+  layer_h<Net, A_D0, true>(fp, none, din, x, bias_l, g);
+  layer_h<Net, A_D1, true>(fp, x, none, y, bias_l, g);
+  layer_h<Net, A_D2, true>(fp, y, none, x, bias_l, g);
+  layer_h<Net, A_D3, true>(fp, x, none, y, bias_l, g);
+  f4 dlt[NCOL];
+  head_h<Net, A_DOUT>(fp, y, dlt, bias_l, g);
+
+  // x' = deformation + xyz, pos_enc(x') (enc_after, :205-212)
+  Frag<2, NCOL> enc;
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    float q3[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) q3[q] = __fadd_rn(__shfl(dlt[c][q], j, 64), px[c][q]);
+    float ev[2][8];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        ev[k][e] = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10) * kActS;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      split8(ev[k], enc.hi[k][c], enc.lo[k][c]);
+      stash[64 * (6 * c + 2 * k)] = __builtin_bit_cast(f4, enc.hi[k][c]);
+      stash[64 * (6 * c + 2 * k + 1)] = __builtin_bit_cast(f4, enc.lo[k][c]);
+    }
+  }
+
+  // trunk on cat[enc, shape] (:214-220), shape folded into the pts_linears.0 / .5 biases
+  layer_h<Net, A_P0, true>(fp, none, enc, x, bias_l, g);
+  layer_h<Net, A_P1, true>(fp, x, none, y, bias_l, g);
+  layer_h<Net, A_P2, true>(fp, y, none, x, bias_l, g);
+  layer_h<Net, A_P3, true>(fp, x, none, y, bias_l, g);
+  layer_h<Net, A_P4, true>(fp, y, none, x, bias_l, g);
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
+      enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
+    }
+  layer_h<Net, A_P5, true>(fp, x, enc, y, bias_l, g);  // skip: cat[h, enc, shape]
+  layer_h<Net, A_P6, true>(fp, y, none, x, bias_l, g);
+  layer_h<Net, A_P7, true>(fp, x, none, y, bias_l, g);
+  f4 dens[NCOL], rgb[NCOL];
+  head_h<Net, A_DEN>(fp, y, dens, bias_l, g);             // :221-223
+  layer_h<Net, A_BOT, false>(fp, y, none, x, bias_l, g);  // bottleneck, no activation (:225)
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
+    venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
+  }
+  // view branch on cat[bottleneck, enc_dir, appearance] (:226-235)
+  layer_h<Net, A_V0, true>(fp, x, venc, y, bias_l, g);
+  layer_h<Net, A_V1, true>(fp, y, none, x, bias_l, g);
+  layer_h<Net, A_V2, true>(fp, x, none, y, bias_l, g);
+  layer_h<Net, A_V3, true>(fp, y, none, x, bias_l, g);
+  head_h<Net, A_RGB>(fp, x, rgb, bias_l, g);  // :237
+
+  if (g == 0) {
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+      if (rows[c] < N) {
+        const f4 o = {act_rgb(rgb[c][0], act), act_rgb(rgb[c][1], act), act_rgb(rgb[c][2], act),
+                      act_sigma(dens[c][0], act)};
+        *reinterpret_cast<f4*>(raw + 4 * rows[c]) = o;
+      }
+    }
+  }
+}
+
+}  // namespace mlp
+}  // namespace aon
+
+using namespace aon;
+using namespace aon::mlp;
+
+extern "C" size_t aon_mlp_art_packed_bytes(void) { return NetArtH::kPackedBytes; }
+
+extern "C" int aon_mlp_art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream) {
+  AON_REQUIRE(prm && packed, "null pointer");
+  AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
+  PackArgsH a{};
+  for (int i = 0; i < 4; ++i) {
+    a.w[A_D0 + i] = prm->def_w[i];
+    a.b[A_D0 + i] = prm->def_b[i];
+    a.w[A_V0 + i] = prm->views_w[i];
+    a.b[A_V0 + i] = prm->views_b[i];
+  }
+  for (int i = 0; i < 8; ++i) {
+    a.w[A_P0 + i] = prm->pts_w[i];
+    a.b[A_P0 + i] = prm->pts_b[i];
+  }
+  a.w[A_DOUT] = prm->deformation_w; a.b[A_DOUT] = prm->deformation_b;
+  a.w[A_DEN] = prm->density_w;      a.b[A_DEN] = prm->density_b;
+  a.w[A_BOT] = prm->bottleneck_w;   a.b[A_BOT] = prm->bottleneck_b;
+  a.w[A_RGB] = prm->rgb_w;          a.b[A_RGB] = prm->rgb_b;
+  for (int i = 0; i < kNumLayersArt; ++i) {
+    AON_REQUIRE(a.w[i] && a.b[i], "null layer parameter");
+    a.layers[i] = kLayersArt[i];
+    a.ldw[i] = kLayersArt[i].len_a + kLayersArt[i].len_b;
+  }
+  // weights whose rows carry folded latent columns after the per-sample ones
+  AON_REQUIRE(prm->ld_def0 >= 3 && prm->ld_pts0 >= 63 && prm->ld_pts5 >= 319 && prm->ld_view0 >= 283,
+              "latent-carrying weights are narrower than their per-sample columns");
+  a.ldw[A_D0] = prm->ld_def0;
+  a.ldw[A_P0] = prm->ld_pts0;
+  a.ldw[A_P5] = prm->ld_pts5;
+  a.ldw[A_V0] = prm->ld_view0;
+  a.n_layers = kNumLayersArt;
+  a.stream_blocks = NetArtH::kStreamBlocks;
+  a.bias_floats = NetArtH::kBiasFloats;
+  return pack_h(a, packed, (hipStream_t)stream);
+}
+
+static int art_launch(int mode, const void* packed, const float* a0, const float* a1,
+                      const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
+                      aon_stream_t stream) {
+  AON_REQUIRE(packed && raw && a0 && a1, "null pointer");
+  AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
+  AON_REQUIRE(act >= AON_ACT_NONE && act <= AON_ACT_ARTIC, "bad activation");
+  AON_REQUIRE(aligned16(packed) && aligned16(raw), "packed / raw must be 16-byte aligned");
+  const int64_t N = B * S;
+  if (N == 0) return 0;
+  using G = GeomH<1>;
+  const int64_t grid = (N + G::kRowsPerBlock - 1) / G::kRowsPerBlock;
+  AON_REQUIRE(grid < (1ll << 31), "too many rows");
+  const f4* ws = static_cast<const f4*>(packed);
+  const float* bias =
+      reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
+  if (mode == 0)
+    hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1>), (unsigned)grid, G::kThreads, 0,
+                       (hipStream_t)stream, ws, bias, a0, a1, a2, a3, B, S, act, raw);
+  else
+    hipLaunchKernelGGL((k_mlp_art_f16x3<1, 1>), (unsigned)grid, G::kThreads, 0,
+                       (hipStream_t)stream, ws, bias, a0, a1, a2, a3, B, S, act, raw);
+  return launch_status("aon_mlp_art_fwd");
+}
+
+extern "C" int aon_mlp_art_fwd(const void* packed, const float* rays_o, const float* rays_d,
+                               const float* viewdirs, const float* t, int64_t B, int S, int act,
+                               float* out, aon_stream_t stream) {
+  AON_REQUIRE(viewdirs && t, "null pointer");
+  return art_launch(0, packed, rays_o, rays_d, viewdirs, t, B, S, act, out, stream);
+}
+
+extern "C" int aon_mlp_art_fwd_points(const void* packed, const float* pos,
+                                      const float* condition, int64_t B, int S, int act,
+                                      float* out, aon_stream_t stream) {
+  return art_launch(1, packed, pos, condition, nullptr, nullptr, B, S, act, out, stream);
+}

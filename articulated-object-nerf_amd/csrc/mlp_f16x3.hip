@@ -14,291 +14,10 @@
 // epilogue, ARE the next layer's B operand for one 32-feature k-step (lane group g holds rows
 // 4g..4g+3 of both tiles) -- no LDS round trip; the epilogue of pair p overlaps the MFMAs of
 // pair p+1.  Weights stream through the same chunked LDS pipeline (mlp_pipe.hpp).
-#include "aon_common.hpp"
-#include "mlp_layout.hpp"
-#include "mlp_pipe.hpp"
+#include "mlp_f16x3_core.hpp"
 
 namespace aon {
 namespace mlp {
-
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-
-#ifndef AON_FMA_MIX
-#define AON_FMA_MIX 1
-#endif
-
-__device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ h8 as_h8(f4 v) { return __builtin_bit_cast(h8, v); }
-
-// fp32 value (already at activation scale) -> (hi, lo) fp16 pair: V2 lo = x - hi (exact in
-// fp32, normal in fp16 for |x| >= 2^-3 at scale); V1 lo = (x - hi) * 2^11
-__device__ __forceinline__ _Float16 lo_of(float v, _Float16 h) {
-#if AON_F16X3_V2
-  // v - hi is exact in fp32; as an fma with the fp16 operand widened in the instruction it can
-  // issue as one v_fma_mix_f32 instead of v_cvt_f32_f16 + v_sub_f32
-  return static_cast<_Float16>(__builtin_fmaf(static_cast<float>(h), -1.0f, v));
-#else
-  return static_cast<_Float16>(__fmul_rn(__fsub_rn(v, static_cast<float>(h)), kLoScale));
-#endif
-}
-
-// 8 fp32 values (already at activation scale) -> (hi, lo) fp16 fragments
-__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const _Float16 h = static_cast<_Float16>(v[j]);
-    hi[j] = h;
-    lo[j] = lo_of(v[j], h);
-  }
-}
-
-// One-step-ahead fragment prefetch over the weight stream: blocks are consumed strictly in
-// stream order (2 per (u, k-step)), so the step after block b is always b + 2.  The hi/lo pair
-// of the NEXT step is read from LDS before the MFMAs of the current step are issued, hiding the
-// LDS latency behind 3*NCOL MFMAs (hipcc issues ds_read -> lgkmcnt(0) -> MFMA otherwise).
-#ifndef AON_SCHED_MASK
-#define AON_SCHED_MASK 0
-#endif
-
-#ifndef AON_PREFETCH
-#define AON_PREFETCH 2
-#endif
-
-template <typename P, int D = AON_PREFETCH>
-struct FragPipe {
-  P& p;
-  f4 nh[D], nl[D];  // fragments of the next D steps
-  __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
-  __device__ __forceinline__ void fetch_into(int blk, f4& h, f4& l) {
-    if (blk >= kBlocks) return;
-#ifdef AON_ABLATE_LDS  // timing-only build: reuse the first fragments (no LDS reads, wrong results)
-    if (blk >= 2 * D) {
-      if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
-      return;
-    }
-#endif
-    if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
-    h = p.block(blk);
-    l = p.block(blk + 1);
-  }
-  __device__ __forceinline__ void start() {
-#pragma unroll
-    for (int i = 0; i < D; ++i) fetch_into(2 * i, nh[i], nl[i]);
-  }
-  // fragments of block pair `blk` (fetched D steps earlier); prefetches blk + 2D
-  __device__ __forceinline__ void take(int blk, h8& wh, h8& wl) {
-    wh = as_h8(nh[0]);
-    wl = as_h8(nl[0]);
-#pragma unroll
-    for (int i = 0; i + 1 < D; ++i) {
-      nh[i] = nh[i + 1];
-      nl[i] = nl[i + 1];
-    }
-    fetch_into(blk + 2 * D, nh[D - 1], nl[D - 1]);
-    // keep the prefetch reads above this step's MFMAs (hipcc otherwise sinks them to their use)
-    __builtin_amdgcn_sched_barrier(AON_SCHED_MASK);
-  }
-};
-
-template <int N, int NCOL>
-struct Frag {
-  h8 hi[N][NCOL], lo[N][NCOL];
-};
-
-// epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
-// part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
-template <bool RELU, int NCOL, int NO>
-__device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
-                                         const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr) {
-  const int uu = q >> 1, r0 = (q & 1) * 2;
-#pragma unroll
-  for (int c = 0; c < NCOL; ++c) {
-    float vv[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-#if AON_F16X3_V2
-      // one accumulator at scale 2^9 -> activation scale 2^3, plus the (pre-scaled) bias
-      float v = fmaf(hh[uu][c][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
-      (void)xx;
-#else
-      float v = fmaf(xx[uu][c][r0 + e], 1.0f / kLoScale, hh[uu][c][r0 + e]);
-      (void)bias;
-#endif
-      if (RELU) v = fmaxf(v, 0.0f);
-      vv[e] = v;
-    }
-#if AON_F16X3_V2 && AON_FMA_MIX
-    // hi pair by one v_cvt_pk_f16_f32; lo_e = v_e - hi_e by v_fma_mix_f32 reading the fp16 half
-    // in place (exact in fp32), then one more cvt_pk
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    const h2 hp = {static_cast<_Float16>(vv[0]), static_cast<_Float16>(vv[1])};
-    const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
-    float d0, d1;
-    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(vv[0]));
-    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(vv[1]));
-    out.hi[pr][c][2 * q] = hp[0];
-    out.hi[pr][c][2 * q + 1] = hp[1];
-    out.lo[pr][c][2 * q] = static_cast<_Float16>(d0);
-    out.lo[pr][c][2 * q + 1] = static_cast<_Float16>(d1);
-#else
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const _Float16 h = static_cast<_Float16>(vv[e]);
-      out.hi[pr][c][2 * q + e] = h;
-      out.lo[pr][c][2 * q + e] = lo_of(vv[e], h);
-    }
-#endif
-  }
-}
-
-// one layer with U >= 2 output tiles: out = act(W . [a ; b] + bias) as next-layer fragments.
-// Pair p's epilogue is spread over the first k-steps of pair p+1 (compute[cur] || finish[prev]).
-template <int LAYER, bool RELU, typename P, int NCOL, int NA, int NB, int NO>
-__device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
-                                        const Frag<NB, NCOL>& b, Frag<NO, NCOL>& out,
-                                        const float* bias_s, int g) {
-  constexpr LayerDesc d = kLayersH[LAYER];
-  constexpr int K = d.ka + d.kb;
-  constexpr int NP = d.u / 2;
-  static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
-  f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
-  f4 pbias[2];                     // V2: that pair's biases, added in its epilogue
-#pragma unroll
-  for (int pr = 0; pr < NP; ++pr) {
-    f4 hh[2][NCOL], xx[2][NCOL], bias[2];
-#pragma unroll
-    for (int uu = 0; uu < 2; ++uu) {
-      bias[uu] = *reinterpret_cast<const f4*>(bias_s + d.bias0 + 16 * (2 * pr + uu) + 4 * g);
-#pragma unroll
-      for (int c = 0; c < NCOL; ++c) {
-#if AON_F16X3_V2
-        hh[uu][c] = f4{0.f, 0.f, 0.f, 0.f};  // bias joins in the epilogue: no LDS read to wait on
-#else
-        hh[uu][c] = bias[uu];
-#endif
-        xx[uu][c] = f4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-#pragma unroll
-      for (int uu = 0; uu < 2; ++uu) {
-        const int blk = d.blk0 + 2 * ((pr * K + k) * 2 + uu);
-        h8 wh, wl;
-        p.take(blk, wh, wl);
-#pragma unroll
-        for (int c = 0; c < NCOL; ++c) {
-          const int ia = k < NA ? k : 0, ib = (k >= d.ka && k - d.ka < NB) ? k - d.ka : 0;
-          const h8 xh = k < d.ka ? a.hi[ia][c] : b.hi[ib][c];
-          const h8 xl = k < d.ka ? a.lo[ia][c] : b.lo[ib][c];
-#if AON_F16X3_V2
-          hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
-          hh[uu][c] = mfma16(wh, xl, hh[uu][c]);
-          hh[uu][c] = mfma16(wl, xh, hh[uu][c]);
-#else
-          hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
-          xx[uu][c] = mfma16(wh, xl, xx[uu][c]);
-          xx[uu][c] = mfma16(wl, xh, xx[uu][c]);
-#endif
-        }
-      }
-      if (pr > 0 && k < 4) epi_part<RELU>(k, phh, pxx, pbias, out, pr - 1);
-    }
-    if (pr > 0) {
-#pragma unroll
-      for (int q = K; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, pr - 1);
-    }
-#pragma unroll
-    for (int uu = 0; uu < 2; ++uu) {
-      pbias[uu] = bias[uu];
-#pragma unroll
-      for (int c = 0; c < NCOL; ++c) {
-        phh[uu][c] = hh[uu][c];
-        pxx[uu][c] = xx[uu][c];
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, NP - 1);
-}
-
-// single-tile head (density / rgb): returns the 16-row tile at activation scale
-template <int LAYER, typename P, int NCOL, int NA>
-__device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[NCOL],
-                                       const float* bias_s, int g) {
-  constexpr LayerDesc d = kLayersH[LAYER];
-  static_assert(d.u == 1 && d.kb == 0 && d.ka <= NA, "head shape");
-  f4 hh[NCOL], xx[NCOL];
-  const f4 bias = *reinterpret_cast<const f4*>(bias_s + d.bias0 + 4 * g);
-#pragma unroll
-  for (int c = 0; c < NCOL; ++c) {
-#if AON_F16X3_V2
-    hh[c] = f4{0.f, 0.f, 0.f, 0.f};
-#else
-    hh[c] = bias;
-#endif
-    xx[c] = f4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int k = 0; k < d.ka; ++k) {
-    const int blk = d.blk0 + 2 * k;
-    h8 wh, wl;
-    p.take(blk, wh, wl);
-#pragma unroll
-    for (int c = 0; c < NCOL; ++c) {
-#if AON_F16X3_V2
-      hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
-      hh[c] = mfma16(wh, a.lo[k][c], hh[c]);
-      hh[c] = mfma16(wl, a.hi[k][c], hh[c]);
-#else
-      hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
-      xx[c] = mfma16(wh, a.lo[k][c], xx[c]);
-      xx[c] = mfma16(wl, a.hi[k][c], xx[c]);
-#endif
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < NCOL; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#if AON_F16X3_V2
-      res[c][r] = fmaf(hh[c][r], 1.0f / (kWS * kActS), bias[r]);  // true scale (head bias unscaled)
-#else
-      res[c][r] = fmaf(xx[c][r], 1.0f / kLoScale, hh[c][r]);
-#endif
-}
-
-#ifndef AON_RING
-#define AON_RING 3
-#endif
-#ifndef AON_CHUNK_H
-#define AON_CHUNK_H 32
-#endif
-constexpr int kRing = AON_RING;      // LDS-DMA ring depth (chunks in LDS)
-constexpr int kChunkH = AON_CHUNK_H;  // 1-KB blocks per chunk
-// Weight pipeline: the LDS-DMA ring, or (AON_PIPE_REG) the register-staged double buffer.
-// hipcc drains lgkmcnt to 0 before every LDS read while any global_load_lds is in flight, which
-// defeats the fragment prefetch; the register-staged pipe keeps precise lgkmcnt(N) waits.
-#ifdef AON_PIPE_REG
-template <int THREADS>
-using WeightPipe = Pipe<THREADS>;
-constexpr int kLdsWeights = 2 * kChunk * 64;  // f4
-#else
-template <int THREADS>
-using WeightPipe = DmaPipe<THREADS, kRing, kChunkH>;
-constexpr int kLdsWeights = kRing * kChunkH * 64;
-#endif
-
-template <int NCOL>
-struct GeomH {
-  static constexpr int kWaves = NCOL == 1 ? 8 : 4;
-  static constexpr int kThreads = 64 * kWaves;
-  static constexpr int kRowsPerWave = 16 * NCOL;
-  static constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
-};
 
 // MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: encoded x (N, 63), condition (B, 27)
 template <int MODE, int NCOL>
@@ -318,7 +37,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   const int g = lane >> 4, j = lane & 15;
   const int64_t N = B * S;
 
-  WeightPipe<G::kThreads> p;
+  WeightPipe<NetVanillaH, G::kThreads> p;
   p.wbuf = smem;
   p.src = wstream;
   p.tid = tid;
@@ -392,16 +111,17 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
 
-  FragPipe<WeightPipe<G::kThreads>> fp(p);
+  FragPipe<WeightPipe<NetVanillaH, G::kThreads>> fp(p);
   fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
+  lds_float* bias_l = opaque_lds(bias_s + 4 * g);  // this lane group's rows of the bias table
 
   Frag<8, NCOL> x, y;
   Frag<1, NCOL> none;
-  layer_h<L0, true>(fp, none, enc, x, bias_s, g);
-  layer_h<L1, true>(fp, x, none, y, bias_s, g);
-  layer_h<L2, true>(fp, y, none, x, bias_s, g);
-  layer_h<L3, true>(fp, x, none, y, bias_s, g);
-  layer_h<L4, true>(fp, y, none, x, bias_s, g);
+  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g);
+  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g);
+  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g);
+  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g);
+  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g);
 #pragma unroll
   for (int c = 0; c < NCOL; ++c)
 #pragma unroll
@@ -409,19 +129,19 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
       enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
     }
-  layer_h<L5, true>(fp, x, enc, y, bias_s, g);  // skip: cat[h, enc] (model.py:102-103)
-  layer_h<L6, true>(fp, y, none, x, bias_s, g);
-  layer_h<L7, true>(fp, x, none, y, bias_s, g);
+  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g);  // skip: cat[h, enc] (model.py:102-103)
+  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g);
+  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g);
   f4 dens[NCOL], rgb[NCOL];
-  head_h<LDEN>(fp, y, dens, bias_s, g);             // model.py:105-107
-  layer_h<LBOT, false>(fp, y, none, x, bias_s, g);  // bottleneck, no activation (model.py:109)
+  head_h<NetVanillaH, LDEN>(fp, y, dens, bias_l, g);             // model.py:105-107
+  layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g);  // bottleneck, no activation (model.py:109)
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
     venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
     venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
   }
-  layer_h<LVIEW, true>(fp, x, venc, y, bias_s, g);  // cat[bottleneck, enc_dir] + ReLU (:110-116)
-  head_h<LRGB>(fp, y, rgb, bias_s, g);              // model.py:118
+  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g);  // cat[bottleneck, enc_dir] + ReLU (:110-116)
+  head_h<NetVanillaH, LRGB>(fp, y, rgb, bias_l, g);              // model.py:118
 
   if (g == 0) {
 #pragma unroll
@@ -436,12 +156,15 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   }
 }
 
-// ---- packing: torch [out][in] fp32 -> hi/lo fp16 blocks (+ biases at activation scale)
-__global__ void k_pack_f16x3(PackArgs a, float* __restrict__ out_f) {
-  const int64_t nhalf = (int64_t)kStreamBlocks * 512;  // fp16 elements of the stream
+// ---- packing: torch [out][ldw] fp32 -> hi/lo fp16 blocks (+ biases at activation scale), for
+// any NetH layer table (passed by value with each layer's weight row stride)
+__global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
+  const int64_t nhalf = (int64_t)a.stream_blocks * 512;  // fp16 elements of the stream
   _Float16* out = reinterpret_cast<_Float16*>(out_f);
-  float* bias_out = out_f + (int64_t)kStreamBlocks * 256;
-  const int64_t total = nhalf + kBiasFloats;
+  float* bias_out = out_f + (int64_t)a.stream_blocks * 256;
+  const int64_t total = nhalf + a.bias_floats;
+  const LayerDesc& last = a.layers[a.n_layers - 1];
+  const int used_blocks = last.blk0 + (last.ka + last.kb) * last.u * 2;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e < nhalf) {
@@ -449,9 +172,9 @@ __global__ void k_pack_f16x3(PackArgs a, float* __restrict__ out_f) {
       const int l = static_cast<int>((e >> 3) & 63), jj = static_cast<int>(e & 7);
       float w = 0.f;
       bool lo_part = false;
-      if (blk < kBlocks) {
+      if (blk < used_blocks) {
         int li = 0;
-        while (li + 1 < kNumLayers && a.layers[li + 1].blk0 <= blk) ++li;
+        while (li + 1 < a.n_layers && a.layers[li + 1].blk0 <= blk) ++li;
         const LayerDesc d = a.layers[li];
         const int K = d.ka + d.kb;
         const int q = (blk - d.blk0) >> 1;
@@ -473,7 +196,7 @@ __global__ void k_pack_f16x3(PackArgs a, float* __restrict__ out_f) {
           const int f = 32 * (k - d.ka) + 8 * gg + jj;
           col = f < d.len_b ? d.len_a + f : -1;
         }
-        if (o < d.out_real && col >= 0) w = a.w[li][(int64_t)o * (d.len_a + d.len_b) + col];
+        if (o < d.out_real && col >= 0) w = a.w[li][(int64_t)o * a.ldw[li] + col];
       }
 #if AON_F16X3_V2
       w *= kWS;  // exact (power of two)
@@ -486,7 +209,7 @@ __global__ void k_pack_f16x3(PackArgs a, float* __restrict__ out_f) {
     } else {
       const int i = static_cast<int>(e - nhalf);
       int li = 0;
-      while (li + 1 < kNumLayers && a.layers[li + 1].bias0 <= i) ++li;
+      while (li + 1 < a.n_layers && a.layers[li + 1].bias0 <= i) ++li;
       const int o = i - a.layers[li].bias0;
 #if AON_F16X3_V2
       // hidden layers add the bias at activation scale; the 1-tile heads at true scale
@@ -499,11 +222,25 @@ __global__ void k_pack_f16x3(PackArgs a, float* __restrict__ out_f) {
   }
 }
 
-int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream) {
-  const int64_t total = (int64_t)kStreamBlocks * 512 + kBiasFloats;
-  hipLaunchKernelGGL(k_pack_f16x3, grid_for(total, 256, 4096), 256, 0, stream, a,
+int pack_h(PackArgsH a, void* packed, hipStream_t stream) {
+  const int64_t total = (int64_t)a.stream_blocks * 512 + a.bias_floats;
+  hipLaunchKernelGGL(k_pack_h, grid_for(total, 256, 4096), 256, 0, stream, a,
                      static_cast<float*>(packed));
   return launch_status("aon_mlp_pack");
+}
+
+int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream) {
+  PackArgsH h{};
+  for (int i = 0; i < kNumLayers; ++i) {
+    h.w[i] = a.w[i];
+    h.b[i] = a.b[i];
+    h.layers[i] = kLayersH[i];
+    h.ldw[i] = kLayersH[i].len_a + kLayersH[i].len_b;
+  }
+  h.n_layers = kNumLayers;
+  h.stream_blocks = NetVanillaH::kStreamBlocks;
+  h.bias_floats = NetVanillaH::kBiasFloats;
+  return pack_h(h, packed, stream);
 }
 
 int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,

@@ -1,0 +1,286 @@
+// Building blocks of the fused fp16x3 MLP kernels (mlp_f16x3.hip: NeRFMLP of model.py;
+// mlp_art.hip: the articulated NeRFMLP of model_autodecoder.py): operand split, fragment
+// prefetch over the LDS weight ring, and the layer / head MFMA loops over a NetH layer table.
+// Numerics and tiling are described at the top of mlp_f16x3.hip.
+#pragma once
+
+#include "aon_common.hpp"
+#include "mlp_layout.hpp"
+#include "mlp_pipe.hpp"
+
+namespace aon {
+namespace mlp {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+#ifndef AON_FMA_MIX
+#define AON_FMA_MIX 1
+#endif
+
+__device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ h8 as_h8(f4 v) { return __builtin_bit_cast(h8, v); }
+
+// fp32 value (already at activation scale) -> (hi, lo) fp16 pair: V2 lo = x - hi (exact in
+// fp32, normal in fp16 for |x| >= 2^-3 at scale); V1 lo = (x - hi) * 2^11
+__device__ __forceinline__ _Float16 lo_of(float v, _Float16 h) {
+#if AON_F16X3_V2
+  // v - hi is exact in fp32; as an fma with the fp16 operand widened in the instruction it can
+  // issue as one v_fma_mix_f32 instead of v_cvt_f32_f16 + v_sub_f32
+  return static_cast<_Float16>(__builtin_fmaf(static_cast<float>(h), -1.0f, v));
+#else
+  return static_cast<_Float16>(__fmul_rn(__fsub_rn(v, static_cast<float>(h)), kLoScale));
+#endif
+}
+
+// 8 fp32 values (already at activation scale) -> (hi, lo) fp16 fragments
+__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = static_cast<_Float16>(v[j]);
+    hi[j] = h;
+    lo[j] = lo_of(v[j], h);
+  }
+}
+
+// One-step-ahead fragment prefetch over the weight stream: blocks are consumed strictly in
+// stream order (2 per (u, k-step)), so the step after block b is always b + 2.  The hi/lo pair
+// of the NEXT step is read from LDS before the MFMAs of the current step are issued, hiding the
+// LDS latency behind 3*NCOL MFMAs (hipcc issues ds_read -> lgkmcnt(0) -> MFMA otherwise).
+#ifndef AON_SCHED_MASK
+#define AON_SCHED_MASK 0
+#endif
+
+#ifndef AON_PREFETCH
+#define AON_PREFETCH 3
+#endif
+
+template <typename P, int D = AON_PREFETCH>
+struct FragPipe {
+  P& p;
+  f4 nh[D], nl[D];  // fragments of the next D steps
+  __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
+  __device__ __forceinline__ void fetch_into(int blk, f4& h, f4& l) {
+    if (blk >= P::kUsedBlocks) return;
+#ifdef AON_ABLATE_LDS  // timing-only build: reuse the first fragments (no LDS reads, wrong results)
+    if (blk >= 2 * D) {
+      if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
+      return;
+    }
+#endif
+    if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
+    h = p.block(blk);
+    l = p.block(blk + 1);
+  }
+  __device__ __forceinline__ void start() {
+#pragma unroll
+    for (int i = 0; i < D; ++i) fetch_into(2 * i, nh[i], nl[i]);
+  }
+  // fragments of block pair `blk` (fetched D steps earlier); prefetches blk + 2D
+  __device__ __forceinline__ void take(int blk, h8& wh, h8& wl) {
+    wh = as_h8(nh[0]);
+    wl = as_h8(nl[0]);
+#pragma unroll
+    for (int i = 0; i + 1 < D; ++i) {
+      nh[i] = nh[i + 1];
+      nl[i] = nl[i + 1];
+    }
+    fetch_into(blk + 2 * D, nh[D - 1], nl[D - 1]);
+    // keep the prefetch reads above this step's MFMAs (hipcc otherwise sinks them to their use)
+    __builtin_amdgcn_sched_barrier(AON_SCHED_MASK);
+  }
+};
+
+template <int N, int NCOL>
+struct Frag {
+  h8 hi[N][NCOL], lo[N][NCOL];
+};
+
+// epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
+// part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
+template <bool RELU, int NCOL, int NO>
+__device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
+                                         const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr) {
+  const int uu = q >> 1, r0 = (q & 1) * 2;
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    float vv[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+#if AON_F16X3_V2
+      // one accumulator at scale 2^9 -> activation scale 2^3, plus the (pre-scaled) bias
+      float v = fmaf(hh[uu][c][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
+      (void)xx;
+#else
+      float v = fmaf(xx[uu][c][r0 + e], 1.0f / kLoScale, hh[uu][c][r0 + e]);
+      (void)bias;
+#endif
+      if (RELU) v = fmaxf(v, 0.0f);
+      vv[e] = v;
+    }
+#if AON_F16X3_V2 && AON_FMA_MIX
+    // hi pair by one v_cvt_pk_f16_f32; lo_e = v_e - hi_e by v_fma_mix_f32 reading the fp16 half
+    // in place (exact in fp32), then one more cvt_pk
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 hp = {static_cast<_Float16>(vv[0]), static_cast<_Float16>(vv[1])};
+    const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
+    float d0, d1;
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(vv[0]));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(vv[1]));
+    out.hi[pr][c][2 * q] = hp[0];
+    out.hi[pr][c][2 * q + 1] = hp[1];
+    out.lo[pr][c][2 * q] = static_cast<_Float16>(d0);
+    out.lo[pr][c][2 * q + 1] = static_cast<_Float16>(d1);
+#else
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const _Float16 h = static_cast<_Float16>(vv[e]);
+      out.hi[pr][c][2 * q + e] = h;
+      out.lo[pr][c][2 * q + e] = lo_of(vv[e], h);
+    }
+#endif
+  }
+}
+
+// one layer with U >= 2 output tiles: out = act(W . [a ; b] + bias) as next-layer fragments.
+// Pair p's epilogue is spread over the first k-steps of pair p+1 (compute[cur] || finish[prev]).
+template <typename Net, int LAYER, bool RELU, typename P, int NCOL, int NA, int NB, int NO>
+__device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
+                                        const Frag<NB, NCOL>& b, Frag<NO, NCOL>& out,
+                                        lds_float* bias_l, int g) {
+  constexpr LayerDesc d = Net::layer(LAYER);
+  constexpr int K = d.ka + d.kb;
+  constexpr int NP = d.u / 2;
+  static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
+  f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
+  f4 pbias[2];                     // V2: that pair's biases, added in its epilogue
+#pragma unroll
+  for (int pr = 0; pr < NP; ++pr) {
+    f4 hh[2][NCOL], xx[2][NCOL], bias[2];
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) {
+      bias[uu] = *reinterpret_cast<lds_f4*>(bias_l + d.bias0 + 16 * (2 * pr + uu));
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) {
+#if AON_F16X3_V2
+        hh[uu][c] = f4{0.f, 0.f, 0.f, 0.f};  // bias joins in the epilogue: no LDS read to wait on
+#else
+        hh[uu][c] = bias[uu];
+#endif
+        xx[uu][c] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu) {
+        const int blk = d.blk0 + 2 * ((pr * K + k) * 2 + uu);
+        h8 wh, wl;
+        p.take(blk, wh, wl);
+#pragma unroll
+        for (int c = 0; c < NCOL; ++c) {
+          const int ia = k < NA ? k : 0, ib = (k >= d.ka && k - d.ka < NB) ? k - d.ka : 0;
+          const h8 xh = k < d.ka ? a.hi[ia][c] : b.hi[ib][c];
+          const h8 xl = k < d.ka ? a.lo[ia][c] : b.lo[ib][c];
+#if AON_F16X3_V2
+          hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
+          hh[uu][c] = mfma16(wh, xl, hh[uu][c]);
+          hh[uu][c] = mfma16(wl, xh, hh[uu][c]);
+#else
+          hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
+          xx[uu][c] = mfma16(wh, xl, xx[uu][c]);
+          xx[uu][c] = mfma16(wl, xh, xx[uu][c]);
+#endif
+        }
+      }
+      if (pr > 0 && k < 4) epi_part<RELU>(k, phh, pxx, pbias, out, pr - 1);
+    }
+    if (pr > 0) {
+#pragma unroll
+      for (int q = K; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, pr - 1);
+    }
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) {
+      pbias[uu] = bias[uu];
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) {
+        phh[uu][c] = hh[uu][c];
+        pxx[uu][c] = xx[uu][c];
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, NP - 1);
+}
+
+// single-tile head (density / rgb): returns the 16-row tile at activation scale
+template <typename Net, int LAYER, typename P, int NCOL, int NA>
+__device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[NCOL],
+                                       lds_float* bias_l, int g) {
+  constexpr LayerDesc d = Net::layer(LAYER);
+  static_assert(d.u == 1 && d.kb == 0 && d.ka <= NA, "head shape");
+  f4 hh[NCOL], xx[NCOL];
+  const f4 bias = *reinterpret_cast<lds_f4*>(bias_l + d.bias0);
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+#if AON_F16X3_V2
+    hh[c] = f4{0.f, 0.f, 0.f, 0.f};
+#else
+    hh[c] = bias;
+#endif
+    xx[c] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < d.ka; ++k) {
+    const int blk = d.blk0 + 2 * k;
+    h8 wh, wl;
+    p.take(blk, wh, wl);
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+#if AON_F16X3_V2
+      hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
+      hh[c] = mfma16(wh, a.lo[k][c], hh[c]);
+      hh[c] = mfma16(wl, a.hi[k][c], hh[c]);
+#else
+      hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
+      xx[c] = mfma16(wh, a.lo[k][c], xx[c]);
+      xx[c] = mfma16(wl, a.hi[k][c], xx[c]);
+#endif
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#if AON_F16X3_V2
+      res[c][r] = fmaf(hh[c][r], 1.0f / (kWS * kActS), bias[r]);  // true scale (head bias unscaled)
+#else
+      res[c][r] = fmaf(xx[c][r], 1.0f / kLoScale, hh[c][r]);
+#endif
+}
+
+#ifndef AON_RING
+#define AON_RING 3
+#endif
+#ifndef AON_CHUNK_H
+#define AON_CHUNK_H 32
+#endif
+constexpr int kRing = AON_RING;      // LDS-DMA ring depth (chunks in LDS)
+constexpr int kChunkH = AON_CHUNK_H;  // 1-KB blocks per chunk
+// Weight pipeline: the LDS-DMA ring over the network's stream
+template <typename Net, int THREADS>
+using WeightPipe = DmaPipe<THREADS, kRing, kChunkH, Net::kStreamBlocks, Net::kBlocks>;
+constexpr int kLdsWeights = kRing * kChunkH * 64;  // f4
+
+template <int NCOL>
+struct GeomH {
+  static constexpr int kWaves = NCOL == 1 ? 8 : 4;
+  static constexpr int kThreads = 64 * kWaves;
+  static constexpr int kRowsPerWave = 16 * NCOL;
+  static constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
+};
+
+}  // namespace mlp
+}  // namespace aon

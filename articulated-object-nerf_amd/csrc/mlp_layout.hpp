@@ -108,6 +108,71 @@ constexpr bool layout_h_ok() {
 }
 static_assert(layout_h_ok(), "fp16x3 layout must share the block grid");
 
+// ---- the articulated NeRFMLP (reference model_autodecoder.py:60-239, default geometry) on the
+// fp16x3 path, after latent folding: the latent columns of deformations_linear.0,
+// pts_linears.0 / .5 and views_linear.0 meet the same (1, C) code on every sample, so their
+// products are per-call biases (NeRFMLP.folded_biases) and the stream holds only the
+// per-sample columns.  Same block grid rules as kLayersH; ka/kb in 32-feature k-steps.
+enum {
+  A_D0 = 0, A_D1, A_D2, A_D3, A_DOUT,
+  A_P0, A_P1, A_P2, A_P3, A_P4, A_P5, A_P6, A_P7,
+  A_DEN, A_BOT, A_V0, A_V1, A_V2, A_V3, A_RGB, kNumLayersArt
+};
+
+constexpr LayerDesc kLayersArt[kNumLayersArt] = {
+    {0, 1, 8, 0, 3, 128, 0, 0},              // deformations_linear.0  128 x 3 (xyz columns)
+    {4, 0, 8, 128, 0, 128, 16, 128},         // deformations_linear.1
+    {4, 0, 8, 128, 0, 128, 80, 256},         // deformations_linear.2
+    {4, 0, 8, 128, 0, 128, 144, 384},        // deformations_linear.3
+    {4, 0, 1, 128, 0, 3, 208, 512},          // deformation_layer        3 x 128
+    {0, 2, 16, 0, 63, 256, 216, 528},        // pts_linears.0   256 x 63 (enc columns)
+    {8, 0, 16, 256, 0, 256, 280, 784},       // pts_linears.1
+    {8, 0, 16, 256, 0, 256, 536, 1040},      // pts_linears.2
+    {8, 0, 16, 256, 0, 256, 792, 1296},      // pts_linears.3
+    {8, 0, 16, 256, 0, 256, 1048, 1552},     // pts_linears.4
+    {8, 2, 16, 256, 63, 256, 1304, 1808},    // pts_linears.5   256 x (256 + 63)
+    {8, 0, 16, 256, 0, 256, 1624, 2064},     // pts_linears.6
+    {8, 0, 16, 256, 0, 256, 1880, 2320},     // pts_linears.7
+    {8, 0, 1, 256, 0, 1, 2136, 2576},        // density_layer    1 x 256
+    {8, 0, 16, 256, 0, 256, 2152, 2592},     // bottleneck_layer 256 x 256
+    {8, 1, 8, 256, 27, 128, 2408, 2848},     // views_linear.0   128 x (256 + 27)
+    {4, 0, 8, 128, 0, 128, 2552, 2976},      // views_linear.1
+    {4, 0, 8, 128, 0, 128, 2616, 3104},      // views_linear.2
+    {4, 0, 8, 128, 0, 128, 2680, 3232},      // views_linear.3
+    {4, 0, 1, 128, 0, 3, 2744, 3360},        // rgb_layer        3 x 128
+};
+
+// compile-time description of one fp16x3 network: its layer table and stream geometry
+template <const LayerDesc* TABLE, int NLAYERS, int BLOCKS, int STREAM_BLOCKS, int BIAS_FLOATS>
+struct NetH {
+  static constexpr const LayerDesc* kTable = TABLE;
+  static constexpr int kNumLayers = NLAYERS;
+  static constexpr int kBlocks = BLOCKS;               // blocks carrying weights
+  static constexpr int kStreamBlocks = STREAM_BLOCKS;  // padded to whole LDS chunks
+  static constexpr int kBiasFloats = BIAS_FLOATS;
+  static constexpr size_t kStreamBytes = (size_t)STREAM_BLOCKS * 1024;
+  static constexpr size_t kPackedBytes = kStreamBytes + (size_t)BIAS_FLOATS * 4;
+  static constexpr LayerDesc layer(int i) { return TABLE[i]; }
+  static constexpr bool ok() {
+    int blk = 0, bias = 0;
+    for (int i = 0; i < NLAYERS; ++i) {
+      const LayerDesc d = TABLE[i];
+      if (d.blk0 != blk || d.bias0 != bias || d.blk0 % 2) return false;
+      if (!(d.u == 1 || d.u % 2 == 0)) return false;
+      if (d.len_a > 32 * d.ka || d.len_b > 32 * d.kb || d.out_real > 16 * d.u) return false;
+      blk += (d.ka + d.kb) * d.u * 2;
+      bias += d.u * 16;
+    }
+    return blk == BLOCKS && bias == BIAS_FLOATS && STREAM_BLOCKS >= BLOCKS &&
+           STREAM_BLOCKS % 64 == 0;
+  }
+};
+
+using NetVanillaH = NetH<kLayersH, kNumLayers, kBlocks, kStreamBlocks, kBiasFloats>;
+using NetArtH = NetH<kLayersArt, kNumLayersArt, 2752, 2752, 3376>;
+static_assert(NetVanillaH::ok(), "inconsistent vanilla fp16x3 layout");
+static_assert(NetArtH::ok(), "inconsistent articulated fp16x3 layout");
+
 // pack-kernel arguments: per-layer torch parameter pointers + the layout table by value
 struct PackArgs {
   const float* w[kNumLayers];
@@ -115,8 +180,20 @@ struct PackArgs {
   LayerDesc layers[kNumLayers];
 };
 
+// fp16x3 pack: any NetH; ldw = row stride of each torch weight ([out][ldw], the real columns
+// first: latent columns past len_a + len_b are folded into the biases)
+constexpr int kMaxLayersH = 24;
+struct PackArgsH {
+  const float* w[kMaxLayersH];
+  const float* b[kMaxLayersH];
+  int ldw[kMaxLayersH];
+  LayerDesc layers[kMaxLayersH];
+  int n_layers, stream_blocks, bias_floats;
+};
+
 // fp16x3 path (mlp_f16x3.hip)
 int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream);
+int pack_h(PackArgsH a, void* packed, hipStream_t stream);
 int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,
                  const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
                  hipStream_t stream);

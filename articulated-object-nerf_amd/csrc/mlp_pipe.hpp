@@ -19,6 +19,7 @@ namespace mlp {
 template <int THREADS>
 struct Pipe {
   static constexpr int kChunk = mlp::kChunk;
+  static constexpr int kUsedBlocks = kBlocks;
   static constexpr int kStageRegs = kChunk * 64 / THREADS;  // f4 per thread per chunk
   static_assert(kStageRegs * THREADS == kChunk * 64, "chunk must split evenly over threads");
   f4* wbuf;  // [2][kChunk * 64] f4 in LDS
@@ -49,6 +50,18 @@ struct Pipe {
 
 namespace aon {
 namespace mlp {
+
+typedef __attribute__((address_space(3))) const f4 lds_f4;
+typedef __attribute__((address_space(3))) const float lds_float;
+// LDS address of a __shared__ pointer, hidden from the compiler so it stays a base register:
+// ds_read's immediate offset reaches only 64 KB, and past that hipcc rebuilds every address
+// from the kernel's LDS origin with a v_or per read
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) const T* opaque_lds(const T* p) {
+  uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p));
+  asm volatile("" : "+v"(a));
+  return reinterpret_cast<__attribute__((address_space(3))) const T*>(static_cast<uintptr_t>(a));
+}
 
 // s_waitcnt vmcnt(n) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | [15:14], expcnt[6:4], lgkmcnt[11:8]).
 // The builtin wants a literal: after unrolling n is a constant and the switch folds to one case.
@@ -82,40 +95,45 @@ __device__ __forceinline__ void wait_vm_lgkm0(int n) {
 // the buffer of chunk c - 1 (fully read: every wave is past its last use) is refilled with
 // chunk c + NBUF - 1.  All LDS of the kernel lives in ONE __shared__ array (a second object can
 // make hipcc drain vmcnt before every ds_read, cdna_hip_programming.md section 5 item 4a).
-template <int THREADS, int NBUF, int CHUNK>
+template <int THREADS, int NBUF, int CHUNK, int STREAM_BLOCKS = kStreamBlocks,
+          int USED_BLOCKS = kBlocks>
 struct DmaPipe {
   static constexpr int kChunk = CHUNK;  // 1-KB blocks per chunk (shadows the fp32 pipe's)
-  static constexpr int kNumChunks = kStreamBlocks / CHUNK;
-  static_assert(kNumChunks * CHUNK == kStreamBlocks, "stream must be whole chunks");
+  static constexpr int kNumChunks = STREAM_BLOCKS / CHUNK;
+  static constexpr int kUsedBlocks = USED_BLOCKS;  // blocks past this are padding, never read
+  static_assert(kNumChunks * CHUNK == STREAM_BLOCKS, "stream must be whole chunks");
   static constexpr int kCopies = kChunk * 64 / THREADS;  // 16-B copies per thread per chunk
   static_assert(kCopies * THREADS == kChunk * 64, "chunk must split evenly over threads");
   static_assert(NBUF >= 2, "ring needs two buffers");
   f4* wbuf;  // [NBUF][kChunk * 64] f4
   const f4* __restrict__ src;
   int tid, lane;
+  uint32_t voff = 0, m0_wave = 0;  // 16 * tid; LDS byte address of wbuf + this wave's 64 f4
 
   __device__ __forceinline__ void issue(int c) {
-    f4* dst = wbuf + (c % NBUF) * kChunk * 64;
 #pragma unroll
     for (int i = 0; i < kCopies; ++i) {
-      const int e = i * THREADS + tid;  // 16-B element of the chunk; LDS dst is lane-linear
 #if AON_DMA_ASM
       // Opaque to the compiler: with a visible LDS-DMA in flight hipcc drains lgkmcnt to 0
       // before every ds_read (defeating the fragment prefetch); hidden, it keeps counted
       // lgkmcnt(N) waits.  Ordering is ours: begin() waits vmcnt for this wave's copies and
       // lgkmcnt(0), then s_barrier, before any wave reads the chunk or reuses its slot.
-      const uint32_t m0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst + e - lane));
-      const f4* g = src + (size_t)c * kChunk * 64 + e;
+      // Addressing is all scalar: saddr = chunk base + i * THREADS * 16 B (SGPR pair), the
+      // per-lane 32-bit offset 16 * tid is loop-invariant, M0 = this wave's 1-KB LDS slot.
+      const f4* gbase = src + (size_t)c * kChunk * 64 + i * THREADS;
+      const uint32_t m0 = m0_wave + static_cast<uint32_t>(((c % NBUF) * kChunk * 64 + i * THREADS) * 16);
       // M0 is reserved to the compiler, which on gfx950 only uses it for LDS-DMA / sendmsg /
       // GWS -- none of them elsewhere in these kernels (checked in the ISA)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off"
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
                    :
-                   : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(g)
+                   : "s"(m0), "v"(voff), "s"(gbase)
                    : "memory", "m0");
 #pragma clang diagnostic pop
 #else
+      f4* dst = wbuf + (c % NBUF) * kChunk * 64;
+      const int e = i * THREADS + tid;  // 16-B element of the chunk; LDS dst is lane-linear
       __builtin_amdgcn_global_load_lds(
           reinterpret_cast<const void*>(src + (size_t)c * kChunk * 64 + e),
           reinterpret_cast<__attribute__((address_space(3))) void*>(
@@ -125,6 +143,10 @@ struct DmaPipe {
     }
   }
   __device__ __forceinline__ void start() {
+    voff = static_cast<uint32_t>(tid) * 16u;
+    bases();
+    m0_wave = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>(wbuf + (tid & ~63))));
 #pragma unroll
     for (int c = 0; c < NBUF - 1 && c < kNumChunks; ++c) issue(c);
   }
@@ -143,7 +165,17 @@ struct DmaPipe {
 #ifdef AON_ABLATE_RING
     return wbuf[(b % kChunk) * 64 + lane];
 #endif
-    return wbuf[((b / kChunk) % NBUF) * kChunk * 64 + (b % kChunk) * 64 + lane];
+    // ds_read's immediate offset reaches 64 KB: blocks past it read from a second per-lane base
+    // (else hipcc materialises every such address with a v_or)
+    const int off = ((b / kChunk) % NBUF) * kChunk * 64 + (b % kChunk) * 64;
+    return off < kHiOff ? lbase[off] : lbase_hi[off - kHiOff];
+  }
+  static constexpr int kHiOff = 4096;  // f4 = 64 KB
+  const f4* lbase = nullptr;           // wbuf + lane
+  lds_f4* lbase_hi = nullptr;          // wbuf + lane + 64 KB
+  __device__ __forceinline__ void bases() {
+    lbase = wbuf + lane;
+    lbase_hi = opaque_lds(lbase + kHiOff);
   }
 };
 

@@ -8,7 +8,7 @@ N row bands, one per rank, and gathered to rank 0 over RCCL).
 
 A step = generate the frame's rays, coarse sample, coarse MLP, composite, pdf resample, fine
 MLP, composite, gather.  value = 307,200 rays x steps / max-over-ranks wall time.  Rank 0 prints
-ONE JSON line.  Inputs: create_spheric_poses(4)[7] camera, fovy-35 focal, near 2 / far 6,
+random NeRF weights (aonerf.synthetic, PCG64 seed 0; equal to the oracle's test weights, tests/test_synthetic.py).  The CPU baseline is the torch restatement in oracle/ on a
 random NeRF weights (PCG64 seed 0).  The CPU baseline is the torch restatement in oracle/ on a
 bounded ray sample (test infrastructure, never the measured path).
 """
@@ -62,10 +62,9 @@ def main():
     from aonerf.model import NeRF
     from aonerf.parallel import render_frame_sharded
     from aonerf.render import create_spheric_poses, sapien_focal
-    from oracle import weights as Wt
+    from aonerf.synthetic import init_like_reference
 
-    net = NeRF(precision=args.precision).cuda()
-    net.load_state_dict({k: torch.from_numpy(v) for k, v in Wt.nerf_state_dict(0).items()})
+    net = init_like_reference(NeRF(precision=args.precision)).cuda()
     c2w = create_spheric_poses(4.0)[7]
     focal = sapien_focal(H)
 

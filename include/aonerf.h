@@ -142,6 +142,49 @@ int aon_mlp_fwd_encoded(const void* packed, int precision, const float* x,
                         const float* condition, int64_t B, int S, int act, float* out,
                         aon_stream_t stream);
 
+/* ---------------------------------------------------------------- articulated MLP */
+/* Device pointers to one articulated NeRFMLP's nn.Linear parameters in torch layout
+ * (models/vanilla_nerf/model_autodecoder.py:60-166, default geometry: 4 x 128 deformation
+ * layers, 8 x 256 trunk with skip 4, 4 x 128 view layers).  The latent columns of
+ * deformations_linear.0 (after the 3 xyz columns), pts_linears.0 (after 63 enc columns),
+ * pts_linears.5 (after 256 + 63) and views_linear.0 (after 256 + 27) are NOT read: the caller
+ * passes biases with the latent products folded in (b + W[:, latent] . code, the code being
+ * the same for every sample), and each such weight's row stride (ld_*). */
+typedef struct aon_mlp_art_params {
+  const float* def_w[4];
+  const float* def_b[4];
+  const float* deformation_w;
+  const float* deformation_b;
+  const float* pts_w[8];
+  const float* pts_b[8];
+  const float* density_w;
+  const float* density_b;
+  const float* bottleneck_w;
+  const float* bottleneck_b;
+  const float* views_w[4];
+  const float* views_b[4];
+  const float* rgb_w;
+  const float* rgb_b;
+  int64_t ld_def0, ld_pts0, ld_pts5, ld_view0;
+} aon_mlp_art_params;
+
+size_t aon_mlp_art_packed_bytes(void);
+/* Re-lay the parameters (folded biases included) into the fp16x3 weight stream. */
+int aon_mlp_art_pack(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
+
+/* The articulated NeRFMLP.forward (model_autodecoder.py:168-239) fused with cast_rays and
+ * both pos_encs: per sample row r = b*S + s, xyz = o[b] + t[r]*d[b]; deformation MLP;
+ * enc = pos_enc(deformation + xyz, 0, 10); venc = pos_enc(viewdirs[b], 0, 4);
+ * out (B*S, 4) = [rgb(3), sigma], raw (AON_ACT_NONE) or with the articulated activations
+ * (AON_ACT_ARTIC: padded sigmoid, softplus(x - 1), model_autodecoder.py:321-323). */
+int aon_mlp_art_fwd(const void* packed, const float* rays_o, const float* rays_d,
+                    const float* viewdirs, const float* t, int64_t B, int S, int act, float* out,
+                    aon_stream_t stream);
+/* The same on given sample points pos (B*S, 3) and encoded view directions condition (B, 27)
+ * (NeRFMLP.forward(pos, condition, latents)). */
+int aon_mlp_art_fwd_points(const void* packed, const float* pos, const float* condition,
+                           int64_t B, int S, int act, float* out, aon_stream_t stream);
+
 /* ---------------------------------------------------------------- compositing */
 /* volumetric_rendering (helper.py:157-195) with the activations of model.py:186-187.
  * rgb: (B*S) rows of rgb_stride floats (3 = API tensor, 4 = fused raw buffer);

@@ -31,11 +31,10 @@ def main():
     from aonerf.model_autodecoder import NeRF_AE_Art
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, sapien_focal
-    from oracle import weights as Wt
+    from aonerf.synthetic import art_latents, init_like_reference
 
-    net = NeRF_AE_Art().cuda()
-    net.load_state_dict({k: torch.from_numpy(v) for k, v in Wt.art_state_dict(0).items()})
-    lat = {k: torch.from_numpy(v).cuda() for k, v in Wt.art_latents(0).items()}
+    net = init_like_reference(NeRF_AE_Art()).cuda()
+    lat = art_latents(0, device="cuda")
     rays = frame_rays(torch.as_tensor(create_spheric_poses(4.0)[11]), H, W, sapien_focal(H))
 
     def step():

@@ -48,11 +48,10 @@ def main():
     from aonerf.parallel import GradAllReduce
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, sapien_focal
-    from oracle import weights as Wt  # deterministic initial weights (same as bench.py)
+    from aonerf.synthetic import init_like_reference  # same initial weights as bench.py
 
     dev = torch.device("cuda", local_rank)
-    net = NeRF().to(dev)
-    net.load_state_dict({k: torch.from_numpy(v) for k, v in Wt.nerf_state_dict(0).items()})
+    net = init_like_reference(NeRF()).to(dev)
     poses = create_spheric_poses(4.0)
     focal = sapien_focal(H)
     rays_all = {k: [] for k in ("rays_o", "rays_d", "viewdirs")}
