@@ -8,9 +8,10 @@ N row bands, one per rank, and gathered to rank 0 over RCCL).
 
 A step = generate the frame's rays, coarse sample, coarse MLP, composite, pdf resample, fine
 MLP, composite, gather.  value = 307,200 rays x steps / max-over-ranks wall time.  Rank 0 prints
-random NeRF weights (aonerf.synthetic, PCG64 seed 0; equal to the oracle's test weights, tests/test_synthetic.py).  The CPU baseline is the torch restatement in oracle/ on a
-random NeRF weights (PCG64 seed 0).  The CPU baseline is the torch restatement in oracle/ on a
-bounded ray sample (test infrastructure, never the measured path).
+ONE JSON line.  Inputs: create_spheric_poses(4)[7] camera, fovy-35 focal, near 2 / far 6,
+random NeRF weights (aonerf.synthetic, PCG64 seed 0: the oracle's test weights bit for bit,
+tests/test_synthetic.py).  The CPU baseline is the torch restatement in oracle/ on a bounded
+ray sample (test infrastructure, never the measured path).
 """
 import argparse
 import json
