@@ -111,28 +111,27 @@ def test_forward_chain_and_golden(art, tag):
     print(f"art {tag}: mse(gpu fine rgb, reference) = {mse_gpu:.3e}")
 
 
-def test_fused_matches_layerwise_ragged(art):
-    """Fused kernel vs the layer-by-layer GEMM path on a ragged batch (rows not a multiple of
-    the 128-row workgroup, every lane group live), raw and with the articulated activations."""
-    g, net, lat, _, _ = art
+def test_ragged_batch_vs_oracle(art):
+    """Fused kernel and layer-by-layer path vs the oracle MLP on a ragged batch (rows not a
+    multiple of the 128-row workgroup), points off the golden geometry (|x| up to ~6.5, so
+    pos_enc's 2^9 frequency reaches ~3,300 rad): raw outputs >= 99.5% within 1e-5, all within
+    1e-4; the articulated activations of the fused epilogue against float64 formulas."""
+    g, net, lat, lat_cpu, params = art
     mlp = net.fine_mlp
     gen = torch.Generator().manual_seed(7)
     B, S = 77, 65
-    o = (torch.rand(B, 3, generator=gen) - 0.5).cuda()
-    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=gen), dim=-1).cuda()
-    t = (2.0 + 4.0 * torch.rand(B, S, generator=gen)).sort(-1).values.cuda()
-    saved = mlp.fused
-    try:
-        mlp.fused = True
-        fused = npy(mlp.forward_rays(o, d, d, t, lat))
-        act = npy(mlp.forward_rays(o, d, d, t, lat, act=2))
-        mlp.fused = False
-        ref = npy(mlp.forward_rays(o, d, d, t, lat))
-    finally:
-        mlp.fused = saved
-    err = report("art fused vs gemm raw", fused, ref, 1e-5)
-    assert (err <= 1e-5).mean() >= 0.999 and err.max() < 5e-5
-    rgb = 1.0 / (1.0 + np.exp(-fused[:, :3].astype(np.float64))) * 1.002 - 0.001
-    sig = np.logaddexp(0.0, fused[:, 3].astype(np.float64) - 1.0)
-    np.testing.assert_allclose(act[:, :3], rgb, rtol=0, atol=2e-6)
-    np.testing.assert_allclose(act[:, 3], sig, rtol=1e-6, atol=2e-6)
+    o = torch.rand(B, 3, generator=gen) - 0.5
+    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=gen), dim=-1)
+    t = (2.0 + 4.0 * torch.rand(B, S, generator=gen)).sort(-1).values
+    rr, rs = O.art_mlp_forward(params[1], O.cast_rays(t, o, d), O.pos_enc(d, 0, 4), lat_cpu)
+    want = np.concatenate([npy(rr).reshape(-1, 3), npy(rs).reshape(-1, 1)], -1)
+    got = npy(mlp.forward_rays(o.cuda(), d.cuda(), d.cuda(), t.cuda(), lat))
+    err = report(f"art ragged {'fused' if mlp.fused else 'gemm'} vs oracle", got, want, 1e-5)
+    assert (err <= 1e-5).mean() >= 0.995 and err.max() < 1e-4
+    if mlp.fused:
+        act = npy(mlp.forward_rays(o.cuda(), d.cuda(), d.cuda(), t.cuda(), lat, act=2))
+        np.testing.assert_array_equal(act.shape, got.shape)
+        rgb = 1.0 / (1.0 + np.exp(-got[:, :3].astype(np.float64))) * 1.002 - 0.001
+        sig = np.logaddexp(0.0, got[:, 3].astype(np.float64) - 1.0)
+        np.testing.assert_allclose(act[:, :3], rgb, rtol=0, atol=2e-6)
+        np.testing.assert_allclose(act[:, 3], sig, rtol=1e-6, atol=2e-6)
