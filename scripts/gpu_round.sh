@@ -27,7 +27,12 @@ if [ "${EXTRA:-0}" = 1 ]; then
 fi
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@"
+if [ "${EXTRA:-0}" = 1 ]; then
+  step rocprof_kt_art 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_art" -o run -- python3 tools/bench_articulated.py --steps 3 --warmup 1
+fi
 [ "${SKIP_PMC:-0}" = 1 ] && exit 0
 step rocprof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@"
+# effective clock under load (MI355X_MICROARCH.md 'DVFS give-back': GRBM_GUI_ACTIVE / 8 / wall)
+step rocprof_clock 600 rocprofv3 --pmc GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_clock" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@"
 step rocprof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@"
 echo done

@@ -34,6 +34,17 @@ def main():
         p = os.path.join(src, name)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, os.path.basename(name)))
+    trace = os.path.join(src, "kt/run_kernel_trace.csv")
+    if os.path.exists(trace):  # per (kernel, grid) averages: coarse / fine launches share names
+        acc = {}
+        for r in csv.DictReader(open(trace)):
+            key = (r["Kernel_Name"].split("(")[0], int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]))
+            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            acc.setdefault(key, []).append(dur)
+        with open(os.path.join(dst, "kernel_trace_by_grid.csv"), "w") as f:
+            f.write("kernel,grid,calls,avg_ns,total_ns\n")
+            for (k, g), v in sorted(acc.items(), key=lambda kv: -sum(kv[1])):
+                f.write(f"\"{k}\",{g},{len(v)},{sum(v) / len(v):.0f},{sum(v)}\n")
     fetch = load(os.path.join(src, "pmc_fetch/run_counter_collection.csv"), "FETCH_SIZE")
     write = load(os.path.join(src, "pmc_write/run_counter_collection.csv"), "WRITE_SIZE")
     rows = []
