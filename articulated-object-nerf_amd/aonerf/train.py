@@ -98,6 +98,50 @@ def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
             dx, dy = dy, dx
 
 
+# forward of a level under autograd: one fused kernel that also stores the activations
+# (aon_mlp_fwd_train) when True, else the layer-by-layer GEMMs of _forward_level
+FUSED_FORWARD = True
+
+_packed = {}
+
+
+def _pack(P, dev):
+    """The f16x3 weight stream of one level's parameters, re-packed on every call (the
+    optimizer updates the parameters in place behind torch's version counters)."""
+    prm = L.AonMlpParams()
+    for i in range(8):
+        prm.pts_w[i], prm.pts_b[i] = P[i][0].data_ptr(), P[i][1].data_ptr()
+    for name, idx in (("density", 8), ("bottleneck", 9), ("views", 10), ("rgb", 11)):
+        setattr(prm, f"{name}_w", P[idx][0].data_ptr())
+        setattr(prm, f"{name}_b", P[idx][1].data_ptr())
+    prec = L.PREC["f16x3"]
+    nbytes = L.lib().aon_mlp_packed_bytes(prec)
+    key = str(dev)  # one buffer: the pack and its forward are stream-ordered
+    buf = _packed.get(key)
+    if buf is None:
+        buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+        _packed[key] = buf
+    L.call("aon_mlp_pack", L.ctypes.byref(prm), prec, L.ptr(buf), L.stream(dev))
+    return buf
+
+
+def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None):
+    """_forward_level on the fused kernel: raw (R x 4) and the kept activations."""
+    B, S = t_vals.shape
+    R, dev = B * S, t_vals.device
+    hbuf = torch.empty((8, R, 256), device=dev)
+    bot = torch.empty((R, 256), device=dev)
+    hv = torch.empty((R, 128), device=dev)
+    for w, b in P:
+        if not (w.is_contiguous() and b.is_contiguous()):
+            raise ValueError("MLP parameters must be contiguous")
+    packed = _pack(P, dev)
+    L.call("aon_mlp_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
+           L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hbuf),
+           L.ptr(bot), L.ptr(hv), L.ptr(raw), L.stream(dev))
+    return list(hbuf.unbind(0)), bot, hv
+
+
 class RenderLevel(torch.autograd.Function):
     """cast_rays + pos_enc + NeRFMLP + activations + volumetric_rendering of one level
     (model.py:175-197) with gradients for the level's 24 MLP parameters."""
@@ -114,7 +158,12 @@ class RenderLevel(torch.autograd.Function):
         L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, 4, L.ptr(venc), L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
         raw = torch.empty((R, 4), device=dev)
-        h, bot, hv = _forward_level(P, enc, venc, S, raw, noise)
+        if FUSED_FORWARD:
+            noise = L.contig(noise) if noise is not None else None
+            h, bot, hv = _forward_level_fused(P, L.contig(rays_o), L.contig(rays_d),
+                                              L.contig(viewdirs), L.contig(t_vals), raw, noise)
+        else:
+            h, bot, hv = _forward_level(P, enc, venc, S, raw, noise)
         comp = torch.empty((B, 3), device=dev)
         acc = torch.empty((B,), device=dev)
         weights = torch.empty((B, S), device=dev)

@@ -19,12 +19,31 @@
 namespace aon {
 namespace mlp {
 
+template <bool STORE, int NCOL>
+struct StorePick {
+  __device__ __forceinline__ static NoStore make(float*, int, const int64_t (&)[NCOL], int64_t,
+                                                 int) {
+    return {};
+  }
+};
+template <int NCOL>
+struct StorePick<true, NCOL> {
+  __device__ __forceinline__ static RowStore<NCOL> make(float* base, int ld,
+                                                        const int64_t (&rows)[NCOL], int64_t N,
+                                                        int g) {
+    RowStore<NCOL> r;
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + rows[c] * ld + 4 * g : nullptr;
+    return r;
+  }
+};
+
 // MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: encoded x (N, 63), condition (B, 27)
-template <int MODE, int NCOL>
+template <int MODE, int NCOL, bool STORE = false>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_fwd_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
-    int64_t B, int S, int act, float* __restrict__ raw) {
+    int64_t B, int S, int act, float* __restrict__ raw, TrainStore ts = {}) {
   using G = GeomH<NCOL>;
   // ONE __shared__ object: weight ring | bias table | per-lane stash of the encodings
   constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
@@ -117,11 +136,13 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 
   Frag<8, NCOL> x, y;
   Frag<1, NCOL> none;
-  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g);
-  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g);
-  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g);
-  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g);
-  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g);
+  using SP = StorePick<STORE, NCOL>;
+  const int64_t hs = N * 256;  // one pts_linears output in ts.h
+  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g));
+  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 1 * hs, 256, rows, N, g));
+  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g));
+  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g));
+  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c)
 #pragma unroll
@@ -129,18 +150,21 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
       enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
     }
-  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g);  // skip: cat[h, enc] (model.py:102-103)
-  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g);
-  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g);
+  // skip: cat[h, enc] (model.py:102-103)
+  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g));
+  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g));
+  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g));
   f4 dens[NCOL], rgb[NCOL];
   head_h<NetVanillaH, LDEN>(fp, y, dens, bias_l, g);             // model.py:105-107
-  layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g);  // bottleneck, no activation (model.py:109)
+  // bottleneck, no activation (model.py:109)
+  layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g, SP::make(ts.bot, 256, rows, N, g));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
     venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
     venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
   }
-  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g);  // cat[bottleneck, enc_dir] + ReLU (:110-116)
+  // cat[bottleneck, enc_dir] + ReLU (:110-116)
+  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g));
   head_h<NetVanillaH, LRGB>(fp, y, rgb, bias_l, g);              // model.py:118
 
   if (g == 0) {
@@ -148,8 +172,10 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     for (int c = 0; c < NCOL; ++c) {
       if (rows[c] < N) {
         const float s = AON_F16X3_V2 ? 1.0f : 1.0f / kActScale;  // V2 heads are at true scale
+        float sig = dens[c][0] * s;
+        if (STORE && ts.noise) sig = __fadd_rn(sig, ts.noise[rows[c]]);  // raw_sigma + noise
         const f4 o = {act_rgb(rgb[c][0] * s, act), act_rgb(rgb[c][1] * s, act),
-                      act_rgb(rgb[c][2] * s, act), act_sigma(dens[c][0] * s, act)};
+                      act_rgb(rgb[c][2] * s, act), act_sigma(sig, act)};
         *reinterpret_cast<f4*>(raw + 4 * rows[c]) = o;
       }
     }
@@ -245,7 +271,7 @@ int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream) {
 
 int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,
                  const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
-                 hipStream_t stream) {
+                 hipStream_t stream, const TrainStore* ts) {
   const int64_t N = B * S;
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + kStreamBytesF32);
@@ -253,6 +279,12 @@ int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const 
   hipLaunchKernelGGL((k_mlp_fwd_f16x3<M, C>),                                                    \
                      static_cast<int>((N + GeomH<C>::kRowsPerBlock - 1) / GeomH<C>::kRowsPerBlock), \
                      GeomH<C>::kThreads, 0, stream, ws, bias, a0, a1, a2, a3, B, S, act, raw)
+  if (mode == 2) {  // training forward: MODE 0 inputs + activation stores
+    hipLaunchKernelGGL((k_mlp_fwd_f16x3<0, 1, true>),
+                       static_cast<int>((N + GeomH<1>::kRowsPerBlock - 1) / GeomH<1>::kRowsPerBlock),
+                       GeomH<1>::kThreads, 0, stream, ws, bias, a0, a1, a2, a3, B, S, act, raw, *ts);
+    return launch_status("aon_mlp_fwd_train");
+  }
   if (mode == 0 && ncol == 1) AON_LAUNCH_H(0, 1);
   else if (mode == 0) AON_LAUNCH_H(0, 2);
   else if (ncol == 1) AON_LAUNCH_H(1, 1);

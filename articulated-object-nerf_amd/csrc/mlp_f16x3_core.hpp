@@ -98,11 +98,30 @@ struct Frag {
   h8 hi[N][NCOL], lo[N][NCOL];
 };
 
+// Optional copy of a layer's activations to HBM (the training forward keeps them for the
+// backward): NoStore compiles away; RowStore writes the 2 values of an epilogue part as one
+// 8-B store to y[row][16 u + 4 g + r] at true scale (rows past the batch are not stored).
+struct NoStore {
+  __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
+};
+
+template <int NCOL>
+struct RowStore {
+  float* rowp[NCOL];  // y + row * ld + 4 g of each column's sample, nullptr when row >= N
+  __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
+    if (rowp[c]) {
+      constexpr float s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;  // exact
+      *reinterpret_cast<float2*>(rowp[c] + 16 * (2 * pr + uu) + r0) = float2{v0 * s, v1 * s};
+    }
+  }
+};
+
 // epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
 // part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
-template <bool RELU, int NCOL, int NO>
+template <bool RELU, int NCOL, int NO, typename Store = NoStore>
 __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
-                                         const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr) {
+                                         const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr,
+                                         const Store& st = Store{}) {
   const int uu = q >> 1, r0 = (q & 1) * 2;
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
@@ -120,6 +139,7 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
       if (RELU) v = fmaxf(v, 0.0f);
       vv[e] = v;
     }
+    st.put(pr, uu, r0, c, vv[0], vv[1]);
 #if AON_F16X3_V2 && AON_FMA_MIX
     // hi pair by one v_cvt_pk_f16_f32; lo_e = v_e - hi_e by v_fma_mix_f32 reading the fp16 half
     // in place (exact in fp32), then one more cvt_pk
@@ -146,10 +166,11 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
 
 // one layer with U >= 2 output tiles: out = act(W . [a ; b] + bias) as next-layer fragments.
 // Pair p's epilogue is spread over the first k-steps of pair p+1 (compute[cur] || finish[prev]).
-template <typename Net, int LAYER, bool RELU, typename P, int NCOL, int NA, int NB, int NO>
+template <typename Net, int LAYER, bool RELU, typename P, int NCOL, int NA, int NB, int NO,
+          typename Store = NoStore>
 __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
                                         const Frag<NB, NCOL>& b, Frag<NO, NCOL>& out,
-                                        lds_float* bias_l, int g) {
+                                        lds_float* bias_l, int g, const Store& st = Store{}) {
   constexpr LayerDesc d = Net::layer(LAYER);
   constexpr int K = d.ka + d.kb;
   constexpr int NP = d.u / 2;
@@ -195,11 +216,11 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
 #endif
         }
       }
-      if (pr > 0 && k < 4) epi_part<RELU>(k, phh, pxx, pbias, out, pr - 1);
+      if (pr > 0 && k < 4) epi_part<RELU>(k, phh, pxx, pbias, out, pr - 1, st);
     }
     if (pr > 0) {
 #pragma unroll
-      for (int q = K; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, pr - 1);
+      for (int q = K; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, pr - 1, st);
     }
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
@@ -212,7 +233,7 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, NP - 1);
+  for (int q = 0; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, NP - 1, st);
 }
 
 // single-tile head (density / rgb): returns the 16-row tile at activation scale

@@ -191,12 +191,23 @@ struct PackArgsH {
   int n_layers, stream_blocks, bias_floats;
 };
 
+// Training forward of the fused kernel (launch_f16x3 mode 2): every hidden activation goes to
+// HBM for the backward, as the layer-by-layer path keeps them: h (8, N, 256) post-ReLU
+// pts_linears outputs, bot (N, 256), hv (N, 128) post-ReLU views_linear.0; raw_sigma gets
+// + noise[row] when noise is set (model.py:183-184).
+struct TrainStore {
+  float* h;
+  float* bot;
+  float* hv;
+  const float* noise;
+};
+
 // fp16x3 path (mlp_f16x3.hip)
 int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream);
 int pack_h(PackArgsH a, void* packed, hipStream_t stream);
 int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,
                  const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
-                 hipStream_t stream);
+                 hipStream_t stream, const TrainStore* ts = nullptr);
 
 }  // namespace mlp
 }  // namespace aon

@@ -142,6 +142,15 @@ int aon_mlp_fwd_encoded(const void* packed, int precision, const float* x,
                         const float* condition, int64_t B, int S, int act, float* out,
                         aon_stream_t stream);
 
+/* The training forward of one level (model.py:175-184 under autograd) on the fused fp16x3
+ * kernel: as aon_mlp_fwd with AON_ACT_NONE (packed = AON_PREC_F16X3 stream), plus every
+ * hidden activation kept for the backward -- h (8, B*S, 256): post-ReLU pts_linears.0..7,
+ * bot (B*S, 256): bottleneck_layer, hv (B*S, 128): post-ReLU views_linear.0 -- and
+ * raw_sigma + noise[row] when noise (B*S) is not NULL. */
+int aon_mlp_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
+                      const float* viewdirs, const float* t, int64_t B, int S, const float* noise,
+                      float* h, float* bot, float* hv, float* raw, aon_stream_t stream);
+
 /* ---------------------------------------------------------------- articulated MLP */
 /* Device pointers to one articulated NeRFMLP's nn.Linear parameters in torch layout
  * (models/vanilla_nerf/model_autodecoder.py:60-166, default geometry: 4 x 128 deformation

@@ -140,6 +140,54 @@ def test_composite_backward(S, white):
 
 
 # ----------------------------------------------------------------------------- training step
+@pytest.fixture(params=[True, False], ids=["fused_fwd", "gemm_fwd"])
+def fwd_mode(request):
+    """Training forward on the fused kernel with activation stores (aon_mlp_fwd_train) or on
+    the layer-by-layer GEMMs; every training test runs on both."""
+    from aonerf import train
+
+    old = train.FUSED_FORWARD
+    train.FUSED_FORWARD = request.param
+    yield request.param
+    train.FUSED_FORWARD = old
+
+
+def test_fused_train_forward_activations():
+    """aon_mlp_fwd_train's kept activations and raw outputs (with noise) against the
+    layer-by-layer GEMM forward on a ragged batch: the two f16x3 evaluations agree to ~1e-6
+    relative of each tensor's range."""
+    from aonerf import train
+
+    net = _make_trainable(0)
+    gen = torch.Generator().manual_seed(3)
+    B, S = 37, 65
+    o = (torch.rand(B, 3, generator=gen) - 0.5).cuda()
+    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=gen), dim=-1).cuda()
+    t = (2.0 + 4.0 * torch.rand(B, S, generator=gen)).sort(-1).values.cuda()
+    noise = torch.rand(B * S, generator=gen).cuda()
+    P = [(m.weight.detach(), m.bias.detach()) for m in net.fine_mlp._layers()]
+    raw_f = torch.empty((B * S, 4), device="cuda")
+    h_f, bot_f, hv_f = train._forward_level_fused(P, o, d, d, t, raw_f, noise)
+    enc = torch.empty((B * S, 63), device="cuda")
+    L = train.L
+    L.call("aon_cast_rays", L.ptr(o), L.ptr(d), L.ptr(t), B, S, None, 0, None, 0, 10, L.ptr(enc),
+           L.stream(o.device))
+    venc = torch.empty((B, 27), device="cuda")
+    L.call("aon_pos_enc", L.ptr(d), B, 0, 4, L.ptr(venc), L.stream(o.device))
+    raw_g = torch.empty((B * S, 4), device="cuda")
+    h_g, bot_g, hv_g = train._forward_level(P, enc, venc, S, raw_g, noise)
+    for name, a, b in [(f"h{i}", h_f[i], h_g[i]) for i in range(8)] + [
+            ("bot", bot_f, bot_g), ("hv", hv_f, hv_g), ("raw", raw_f, raw_g)]:
+        e = rel_err(a.cpu().numpy(), b.cpu().numpy())
+        print(f"  fused vs gemm forward {name}: max rel err {e:.2e}")
+        assert e < 2e-5, name
+    # relu masks agree wherever the value is not within rounding of zero
+    for i in range(8):
+        a, b = h_f[i].cpu().numpy(), h_g[i].cpu().numpy()
+        tol = 1e-5 * np.abs(b).max()
+        assert np.all(((a > 0) == (b > 0)) | (np.abs(b) < tol))
+
+
 def _make_trainable(seed):
     from aonerf.model import NeRF
 
@@ -171,7 +219,7 @@ def _oracle_grads(g, dtype):
     return grads, inter
 
 
-def test_train_step_golden(golden):
+def test_train_step_golden(golden, fwd_mode):
     """Loss and the recorded gradients of one LitNeRF.training_step (randomized, injected
     uniforms) against the reference.  Gradients w.r.t. the first layer see the encodings'
     sin(2^9 x) features, so a 1e-7 change of a coarse weight, amplified by the inverse CDF into
@@ -207,7 +255,7 @@ def test_train_step_golden(golden):
     print(f"train-step grads vs reference: worst error / allowance {worst:.2f}")
 
 
-def test_train_step_chain(golden):
+def test_train_step_chain(golden, fwd_mode):
     """Teacher-forced per-level gradients: our level-l t_vals through the oracle's autograd."""
     from aonerf import train
 
@@ -236,6 +284,8 @@ def test_train_step_chain(golden):
             got = dict(net.named_parameters())[prefix + name].grad.cpu().numpy()
             want = p.grad.numpy()
             e = rel_err(got, want)
+            if e > 1e-4:
+                print(f"  {prefix + name}: max-rel err {e:.2e}")
             worst = max(worst, e)
             assert e < 1e-3, (prefix + name, e)
     print(f"teacher-forced grads: worst max-rel err {worst:.2e}")
