@@ -65,6 +65,9 @@ _SIGNATURES = {
     "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp]),
+    "aon_mlp_bwd_packed_bytes": (c_size, []),
+    "aon_mlp_bwd_pack": (c_int, [ctypes.POINTER(AonMlpParams), vp, vp]),
+    "aon_mlp_bwd": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp]),
     "aon_mlp_art_packed_bytes": (c_size, []),
     "aon_mlp_art_pack": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
     "aon_mlp_art_fwd": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),

@@ -101,28 +101,85 @@ def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
 # forward of a level under autograd: one fused kernel that also stores the activations
 # (aon_mlp_fwd_train) when True, else the layer-by-layer GEMMs of _forward_level
 FUSED_FORWARD = True
+# backward of a level: input gradients in one fused kernel (aon_mlp_bwd) + weight-gradient GEMMs
+# when True, else every product as a GEMM (_backward_level)
+FUSED_BACKWARD = True
 
 _packed = {}
 
 
-def _pack(P, dev):
-    """The f16x3 weight stream of one level's parameters, re-packed on every call (the
-    optimizer updates the parameters in place behind torch's version counters)."""
+def _params_struct(P):
     prm = L.AonMlpParams()
     for i in range(8):
         prm.pts_w[i], prm.pts_b[i] = P[i][0].data_ptr(), P[i][1].data_ptr()
     for name, idx in (("density", 8), ("bottleneck", 9), ("views", 10), ("rgb", 11)):
         setattr(prm, f"{name}_w", P[idx][0].data_ptr())
         setattr(prm, f"{name}_b", P[idx][1].data_ptr())
-    prec = L.PREC["f16x3"]
-    nbytes = L.lib().aon_mlp_packed_bytes(prec)
-    key = str(dev)  # one buffer: the pack and its forward are stream-ordered
-    buf = _packed.get(key)
+    return prm
+
+
+def _buffer(key, nbytes, dev):
+    # one buffer per kind and device: a pack and the kernel reading it are stream-ordered
+    buf = _packed.get((key, str(dev)))
     if buf is None:
-        buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
-        _packed[key] = buf
-    L.call("aon_mlp_pack", L.ctypes.byref(prm), prec, L.ptr(buf), L.stream(dev))
+        buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
+        _packed[(key, str(dev))] = buf
     return buf
+
+
+def _pack(P, dev):
+    """The f16x3 weight stream of one level's parameters, re-packed on every call (the
+    optimizer updates the parameters in place behind torch's version counters)."""
+    prec = L.PREC["f16x3"]
+    buf = _buffer("fwd", L.lib().aon_mlp_packed_bytes(prec), dev)
+    L.call("aon_mlp_pack", L.ctypes.byref(_params_struct(P)), prec, L.ptr(buf), L.stream(dev))
+    return buf
+
+
+def _pack_bwd(P, dev):
+    """The transposed weight stream of the fused backward chain (aon_mlp_bwd_pack)."""
+    buf = _buffer("bwd", L.lib().aon_mlp_bwd_packed_bytes(), dev)
+    L.call("aon_mlp_bwd_pack", L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
+    return buf
+
+
+def _stacked(h, R):
+    """The 8 kept activations as one (8, R, 256) buffer (a view when they already are one)."""
+    base = h[0].data_ptr()
+    if all(t.is_contiguous() and t.data_ptr() == base + i * R * 256 * 4 for i, t in enumerate(h)):
+        return h[0]
+    return torch.stack(h)
+
+
+def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw):
+    """_backward_level with every input-gradient product in one fused kernel (aon_mlp_bwd);
+    the weight gradients dW = dZ^T X and db = sum_rows dZ stay split-K GEMMs."""
+    R, dev = enc.shape[0], enc.device
+    dzv = torch.empty((R, 128), device=dev)
+    dzb = torch.empty((R, 256), device=dev)
+    dz = torch.empty((8, R, 256), device=dev)
+    work = _buffer("work", 4, dev)
+    L.call("aon_mlp_bwd", L.ptr(_pack_bwd(P, dev)), L.ptr(draw), L.ptr(_stacked(h, R)), L.ptr(hv),
+           R, L.ptr(dzv), L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
+    gs, acts = GRAD_SCALE, ACT_SCALE
+
+    def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None):
+        gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
+             b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=gs, b_scale=acts, rowsum=db)
+
+    dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1])               # rgb_layer
+    dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0
+    dweight(G[10][0], dzv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
+    dweight(G[9][0], dzb, 256, 256, h[7], 256, 256, db=G[9][1])            # bottleneck
+    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256, db=G[8][1])        # density
+    for i in range(7, -1, -1):                                             # pts_linears.i
+        if i == 5:
+            dweight(G[5][0], dz[5], 256, 256, h[4], 256, 256, db=G[5][1])
+            dweight(G[5][0], dz[5], 256, 256, enc, 63, 63, col0=256)
+        elif i == 0:
+            dweight(G[0][0], dz[0], 256, 256, enc, 63, 63, db=G[0][1])
+        else:
+            dweight(G[i][0], dz[i], 256, 256, h[i - 1], 256, 256, db=G[i][1])
 
 
 def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None):
@@ -194,7 +251,10 @@ class RenderLevel(torch.autograd.Function):
                L.ptr(draw), L.ptr(draw[:, 3:]), 4, L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
-        _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
+        if FUSED_BACKWARD:
+            _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw)
+        else:
+            _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
         return (None, None, None, None, None, None, *grads)
 

@@ -1,0 +1,208 @@
+// Fused backward chain of the vanilla NeRFMLP for the training step (reference model.py:95-120
+// under autograd, LitNeRF.training_step model.py:256-282): from dL/d raw (the compositor's
+// backward) down to dL/d pre-activation of pts_linears.0, all input-gradient products
+// dX = dZ W in ONE kernel, each masked by ReLU' of the forward output it flows into, every
+// layer's dZ stored for the weight-gradient GEMMs (dW = dZ^T X runs separately: a reduction
+// over all samples).
+//
+// Same structure and numerics as the forward (mlp_f16x3.hip / mlp_f16x3_core.hpp): feature-
+// major MFMA tiles, W^T streamed through the LDS-DMA ring (kLayersBwd, packed from the forward
+// weights with tr = 1), each finished output pair converted in registers into the next layer's
+// B fragments.  Gradients ride at a power-of-two scale s chosen per call from max|d raw|
+// (|d raw * s| < 2^8: 2^8 of headroom below fp16's 65504 for growth through the chain); the
+// stores undo it exactly.  The ReLU' masks come from the stored forward activations (h > 0,
+// as torch's threshold_backward on the ReLU output), loaded one pair ahead.
+#include "mlp_f16x3_core.hpp"
+
+namespace aon {
+namespace mlp {
+
+struct BwdArgs {
+  const float* draw;              // (N, 4): d raw_rgb (3), d raw_sigma (model.py:183-187 folded)
+  const float* h;                 // (8, N, 256): post-ReLU pts_linears.0..7 outputs
+  const float* hv;                // (N, 128): post-ReLU views_linear.0 output
+  float* dzv;                     // (N, 128): dL/d pre-activation of views_linear.0
+  float* dzb;                     // (N, 256): dL/d bottleneck output
+  float* dz;                      // (8, N, 256): dL/d pre-activation of pts_linears.i
+  const uint32_t* absmax;         // bits of max |draw| (k_absmax)
+  int64_t N;
+};
+
+// max |x| over n floats as uint bits (non-negative floats order like their bit patterns)
+__global__ void k_absmax(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ out) {
+  float m = 0.0f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// |x * s| < 2^8 for the largest |x|: s = 2^(8 - e) with max = m 2^e, m in [0.5, 1)
+__device__ __forceinline__ float grad_scale(uint32_t bits) {
+  const float m = __uint_as_float(bits);
+  if (!(m > 0.0f) || !isfinite(m)) return 1.0f;
+  int e;
+  (void)frexpf(m, &e);
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  return __builtin_ldexpf(1.0f, 8 - e);
+}
+
+template <int NCOL>
+__device__ __forceinline__ MaskStore<NCOL> mask_store(const float* hbase, int ldh, float* obase,
+                                                      int ld, const int64_t (&rows)[NCOL],
+                                                      int64_t N, int g, float s) {
+  MaskStore<NCOL> m;
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    const bool ok = rows[c] < N;
+    m.mrow[c] = ok ? hbase + rows[c] * ldh + 4 * g : nullptr;
+    m.rowp[c] = ok ? obase + rows[c] * ld + 4 * g : nullptr;
+  }
+  m.s = s;
+  return m;
+}
+
+__global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
+    const f4* __restrict__ wstream, const float* __restrict__ bias_g, BwdArgs a) {
+  constexpr int NCOL = 1;
+  using G = GeomH<NCOL>;
+  using Net = NetBwdH;
+  constexpr int kStash = G::kWaves * 64 * 2;  // f4: d raw_sigma fragment, hi & lo
+  __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + kStash];
+  float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
+  f4* stash = smem + kLdsWeights + Net::kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 2 +
+              (threadIdx.x & 63);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int64_t N = a.N;
+
+  WeightPipe<Net, G::kThreads> p;
+  p.wbuf = smem;
+  p.src = wstream;
+  p.tid = tid;
+  p.lane = lane;
+  p.start();
+  for (int i = tid; i < Net::kBiasFloats; i += G::kThreads) bias_s[i] = bias_g[i];
+
+  const float s = grad_scale(*a.absmax);
+  const float inv = 1.0f / s;  // exact: a power of two
+
+  // d raw_rgb -> segment B of rgb_layer^T (lane group 0, elements 0..2); d raw_sigma ->
+  // segment B of [bottleneck | density]^T (lane group 0, element 0)
+  Frag<1, NCOL> drgb, dsig;
+  int64_t rows[NCOL];
+  {
+    const int64_t row = (int64_t)blockIdx.x * G::kRowsPerBlock + wave * G::kRowsPerWave + j;
+    rows[0] = row;
+    const int64_t rr = row < N ? row : N - 1;
+    const f4 d = *reinterpret_cast<const f4*>(a.draw + 4 * rr);
+    float dv[8], sv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      dv[e] = (g == 0 && e < 3) ? d[e < 3 ? e : 0] * s : 0.f;
+      sv[e] = (g == 0 && e == 0) ? d[3] * s : 0.f;
+    }
+    split8(dv, drgb.hi[0][0], drgb.lo[0][0]);
+    split8(sv, dsig.hi[0][0], dsig.lo[0][0]);
+    stash[0] = __builtin_bit_cast(f4, dsig.hi[0][0]);
+    stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
+  }
+
+  FragPipe<WeightPipe<Net, G::kThreads>> fp(p);
+  fp.start();
+  lds_float* bias_l = opaque_lds(bias_s + 4 * g);
+
+  const int64_t hs = N * 256;
+  Frag<8, NCOL> x, y;
+  Frag<1, NCOL> none;
+  // d hv = W_rgb^T d rgb, * ReLU'(hv) -> dZ of views_linear.0
+  layer_h<Net, B_RGB, false>(fp, none, drgb, x, bias_l, g,
+                             mask_store(a.hv, 128, a.dzv, 128, rows, N, g, inv));
+  // d bottleneck = W_view[:, :256]^T dZ_view (linear layer: no mask)
+  {
+    RowStore<NCOL> st;
+    st.rowp[0] = rows[0] < N ? a.dzb + rows[0] * 256 + 4 * g : nullptr;
+    st.s = inv;
+    layer_h<Net, B_VIEW, false>(fp, x, none, y, bias_l, g, st);
+  }
+  dsig.hi[0][0] = __builtin_bit_cast(h8, stash[0]);
+  dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
+  // d h7 = W_bot^T dZ_bot + W_den^T d sigma, * ReLU'(h7) -> dZ_7
+  layer_h<Net, B_BOTDEN, false>(fp, y, dsig, x, bias_l, g,
+                                mask_store(a.h + 7 * hs, 256, a.dz + 7 * hs, 256, rows, N, g, inv));
+  layer_h<Net, B_7, false>(fp, x, none, y, bias_l, g,
+                           mask_store(a.h + 6 * hs, 256, a.dz + 6 * hs, 256, rows, N, g, inv));
+  layer_h<Net, B_6, false>(fp, y, none, x, bias_l, g,
+                           mask_store(a.h + 5 * hs, 256, a.dz + 5 * hs, 256, rows, N, g, inv));
+  // the skip layer's enc columns carry no gradient (positions are not differentiated)
+  layer_h<Net, B_5, false>(fp, x, none, y, bias_l, g,
+                           mask_store(a.h + 4 * hs, 256, a.dz + 4 * hs, 256, rows, N, g, inv));
+  layer_h<Net, B_4, false>(fp, y, none, x, bias_l, g,
+                           mask_store(a.h + 3 * hs, 256, a.dz + 3 * hs, 256, rows, N, g, inv));
+  layer_h<Net, B_3, false>(fp, x, none, y, bias_l, g,
+                           mask_store(a.h + 2 * hs, 256, a.dz + 2 * hs, 256, rows, N, g, inv));
+  layer_h<Net, B_2, false>(fp, y, none, x, bias_l, g,
+                           mask_store(a.h + 1 * hs, 256, a.dz + 1 * hs, 256, rows, N, g, inv));
+  layer_h<Net, B_1, false>(fp, x, none, y, bias_l, g,
+                           mask_store(a.h, 256, a.dz, 256, rows, N, g, inv));
+}
+
+}  // namespace mlp
+}  // namespace aon
+
+using namespace aon;
+using namespace aon::mlp;
+
+extern "C" size_t aon_mlp_bwd_packed_bytes(void) { return NetBwdH::kPackedBytes; }
+
+extern "C" int aon_mlp_bwd_pack(const aon_mlp_params* prm, void* packed, aon_stream_t stream) {
+  AON_REQUIRE(prm && packed, "null pointer");
+  AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
+  PackArgsH a{};
+  const float* w[kNumLayersBwd] = {prm->rgb_w,    prm->views_w,  prm->bottleneck_w,
+                                   prm->pts_w[7], prm->pts_w[6], prm->pts_w[5],
+                                   prm->pts_w[4], prm->pts_w[3], prm->pts_w[2],
+                                   prm->pts_w[1]};
+  // row strides of the forward weights (their in-features): rgb 128, views 256 + 27, skip 256 + 63
+  const int ld[kNumLayersBwd] = {128, 283, 256, 256, 256, 319, 256, 256, 256, 256};
+  for (int i = 0; i < kNumLayersBwd; ++i) {
+    AON_REQUIRE(w[i], "null layer weight");
+    a.w[i] = w[i];
+    a.ldw[i] = ld[i];
+    a.tr[i] = 1;
+    a.layers[i] = kLayersBwd[i];
+  }
+  AON_REQUIRE(prm->density_w, "null layer weight");
+  a.w2[B_BOTDEN] = prm->density_w;  // segment B of d h7: density_layer^T (1 x 256)
+  a.ldw2[B_BOTDEN] = 256;
+  a.n_layers = kNumLayersBwd;
+  a.stream_blocks = NetBwdH::kStreamBlocks;
+  a.bias_floats = NetBwdH::kBiasFloats;
+  return pack_h(a, packed, (hipStream_t)stream);
+}
+
+extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const float* h, const float* hv,
+                           int64_t N, float* dzv, float* dzb, float* dz, void* work,
+                           aon_stream_t stream) {
+  AON_REQUIRE(packed && draw && h && hv && dzv && dzb && dz && work, "null pointer");
+  AON_REQUIRE(N >= 0, "bad shape");
+  AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(h) && aligned16(hv) &&
+                  aligned16(dzv) && aligned16(dzb) && aligned16(dz),
+              "buffers must be 16-byte aligned");
+  if (N == 0) return 0;
+  using G = GeomH<1>;
+  const int64_t grid = (N + G::kRowsPerBlock - 1) / G::kRowsPerBlock;
+  AON_REQUIRE(grid < (1ll << 31), "too many rows");
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* absmax = static_cast<uint32_t*>(work);
+  if (hipMemsetAsync(absmax, 0, sizeof(uint32_t), st) != hipSuccess) return launch_status(__func__);
+  hipLaunchKernelGGL(k_absmax, grid_for(4 * N, 256, 1024), 256, 0, st, draw, 4 * N, absmax);
+  BwdArgs args{draw, h, hv, dzv, dzb, dz, absmax, N};
+  const f4* ws = static_cast<const f4*>(packed);
+  const float* bias =
+      reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetBwdH::kStreamBytes);
+  hipLaunchKernelGGL(k_mlp_bwd_f16x3, (unsigned)grid, G::kThreads, 0, st, ws, bias, args);
+  return launch_status(__func__);
+}

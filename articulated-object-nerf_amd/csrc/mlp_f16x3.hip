@@ -34,6 +34,7 @@ struct StorePick<true, NCOL> {
     RowStore<NCOL> r;
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + rows[c] * ld + 4 * g : nullptr;
+    r.s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;
     return r;
   }
 };
@@ -215,14 +216,21 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
         }
         const int o = 16 * u + (l & 15), gg = l >> 4;
         int col = -1;
+        const float* src = a.w[li];
+        int64_t ld = a.ldw[li];
         if (k < d.ka) {  // previous-layer output fragment order
           const int f = 32 * k + 16 * (jj >> 2) + 4 * gg + (jj & 3);
           col = f < d.len_a ? f : -1;
         } else {  // in-register encodings: natural order
           const int f = 32 * (k - d.ka) + 8 * gg + jj;
-          col = f < d.len_b ? d.len_a + f : -1;
+          col = f < d.len_b ? (a.w2[li] ? f : d.len_a + f) : -1;
+          if (a.w2[li]) {
+            src = a.w2[li];
+            ld = a.ldw2[li];
+          }
         }
-        if (o < d.out_real && col >= 0) w = a.w[li][(int64_t)o * a.ldw[li] + col];
+        if (o < d.out_real && col >= 0)
+          w = a.tr[li] ? src[(int64_t)col * ld + o] : src[(int64_t)o * ld + col];
       }
 #if AON_F16X3_V2
       w *= kWS;  // exact (power of two)
@@ -243,7 +251,7 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
 #else
       const float bs = kActScale;
 #endif
-      bias_out[i] = o < a.layers[li].out_real ? a.b[li][o] * bs : 0.f;
+      bias_out[i] = (o < a.layers[li].out_real && a.b[li]) ? a.b[li][o] * bs : 0.f;
     }
   }
 }

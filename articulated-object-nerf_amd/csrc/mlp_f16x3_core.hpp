@@ -98,21 +98,52 @@ struct Frag {
   h8 hi[N][NCOL], lo[N][NCOL];
 };
 
-// Optional copy of a layer's activations to HBM (the training forward keeps them for the
-// backward): NoStore compiles away; RowStore writes the 2 values of an epilogue part as one
-// 8-B store to y[row][16 u + 4 g + r] at true scale (rows past the batch are not stored).
+// Epilogue policies of layer_h.  begin_pair(pr) runs at the start of output pair pr (before its
+// MFMAs), post() maps a finished value (after the optional ReLU), put() sees the pair's values 2
+// at a time.  NoStore compiles away.  RowStore copies a layer's activations to HBM (the
+// training forward keeps them for the backward): one 8-B store to y[row][16 u + 4 g + r] at
+// true scale (v * s) per part; rows past the batch are not stored.  MaskStore is the backward
+// chain's epilogue: the value is kept where the forward activation h[row][feature] > 0 (ReLU'
+// from the stored output, as torch's threshold_backward), loaded one pair ahead of its use,
+// and the product (true scale) is stored for the weight-gradient GEMMs.
 struct NoStore {
+  __device__ __forceinline__ void begin_pair(int) const {}
+  __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
 };
 
 template <int NCOL>
 struct RowStore {
   float* rowp[NCOL];  // y + row * ld + 4 g of each column's sample, nullptr when row >= N
+  float s;            // to true scale (a power of two: exact)
+  __device__ __forceinline__ void begin_pair(int) const {}
+  __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
-    if (rowp[c]) {
-      constexpr float s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;  // exact
+    if (rowp[c])
       *reinterpret_cast<float2*>(rowp[c] + 16 * (2 * pr + uu) + r0) = float2{v0 * s, v1 * s};
-    }
+  }
+};
+
+template <int NCOL>
+struct MaskStore {
+  const float* mrow[NCOL];  // h + row * ldh + 4 g (mask source), nullptr when row >= N
+  float* rowp[NCOL];        // out + row * ld + 4 g, nullptr when row >= N or no store
+  float s;
+  mutable f4 mk[2][2][NCOL];  // [pair parity][tile of the pair][column]
+  __device__ __forceinline__ void begin_pair(int pr) const {
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu)
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c)
+        mk[pr & 1][uu][c] = mrow[c] ? *reinterpret_cast<const f4*>(mrow[c] + 16 * (2 * pr + uu))
+                                    : f4{0.f, 0.f, 0.f, 0.f};
+  }
+  __device__ __forceinline__ float post(int pr, int uu, int r, int c, float v) const {
+    return mk[pr & 1][uu][c][r] > 0.0f ? v : 0.0f;
+  }
+  __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
+    if (rowp[c])
+      *reinterpret_cast<float2*>(rowp[c] + 16 * (2 * pr + uu) + r0) = float2{v0 * s, v1 * s};
   }
 };
 
@@ -137,7 +168,7 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
       (void)bias;
 #endif
       if (RELU) v = fmaxf(v, 0.0f);
-      vv[e] = v;
+      vv[e] = st.post(pr, uu, r0 + e, c, v);
     }
     st.put(pr, uu, r0, c, vv[0], vv[1]);
 #if AON_F16X3_V2 && AON_FMA_MIX
@@ -179,6 +210,7 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
   f4 pbias[2];                     // V2: that pair's biases, added in its epilogue
 #pragma unroll
   for (int pr = 0; pr < NP; ++pr) {
+    st.begin_pair(pr);
     f4 hh[2][NCOL], xx[2][NCOL], bias[2];
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {

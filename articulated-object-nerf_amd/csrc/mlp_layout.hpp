@@ -142,6 +142,25 @@ constexpr LayerDesc kLayersArt[kNumLayersArt] = {
     {4, 0, 1, 128, 0, 3, 2744, 3360},        // rgb_layer        3 x 128
 };
 
+// ---- backward chain of the vanilla NeRFMLP (training, model.py:95-120 under autograd): the
+// input gradients dL/dX = dZ W (W^T applied feature-major), last layer first, each masked by
+// ReLU' of the forward output it flows into.  Row o of a layer = an INPUT feature of the forward
+// layer, columns = its outputs; packed from the forward weights with tr = 1.
+enum { B_RGB = 0, B_VIEW, B_BOTDEN, B_7, B_6, B_5, B_4, B_3, B_2, B_1, kNumLayersBwd };
+
+constexpr LayerDesc kLayersBwd[kNumLayersBwd] = {
+    {0, 1, 8, 0, 3, 128, 0, 0},             // rgb_layer^T: d hv = W_rgb^T d rgb (3 -> 128)
+    {4, 0, 16, 128, 0, 256, 16, 128},       // views_linear.0^T, bottleneck columns only
+    {8, 1, 16, 256, 1, 256, 144, 384},      // [bottleneck^T | density^T]: d h7
+    {8, 0, 16, 256, 0, 256, 432, 640},      // pts_linears.7^T: d h6
+    {8, 0, 16, 256, 0, 256, 688, 896},      // pts_linears.6^T: d h5
+    {8, 0, 16, 256, 0, 256, 944, 1152},     // pts_linears.5^T, h4 columns only (not enc)
+    {8, 0, 16, 256, 0, 256, 1200, 1408},    // pts_linears.4^T: d h3
+    {8, 0, 16, 256, 0, 256, 1456, 1664},    // pts_linears.3^T: d h2
+    {8, 0, 16, 256, 0, 256, 1712, 1920},    // pts_linears.2^T: d h1
+    {8, 0, 16, 256, 0, 256, 1968, 2176},    // pts_linears.1^T: d h0
+};
+
 // compile-time description of one fp16x3 network: its layer table and stream geometry
 template <const LayerDesc* TABLE, int NLAYERS, int BLOCKS, int STREAM_BLOCKS, int BIAS_FLOATS>
 struct NetH {
@@ -170,8 +189,10 @@ struct NetH {
 
 using NetVanillaH = NetH<kLayersH, kNumLayers, kBlocks, kStreamBlocks, kBiasFloats>;
 using NetArtH = NetH<kLayersArt, kNumLayersArt, 2752, 2752, 3376>;
+using NetBwdH = NetH<kLayersBwd, kNumLayersBwd, 2224, 2240, 2432>;
 static_assert(NetVanillaH::ok(), "inconsistent vanilla fp16x3 layout");
 static_assert(NetArtH::ok(), "inconsistent articulated fp16x3 layout");
+static_assert(NetBwdH::ok(), "inconsistent backward-chain fp16x3 layout");
 
 // pack-kernel arguments: per-layer torch parameter pointers + the layout table by value
 struct PackArgs {
@@ -183,10 +204,15 @@ struct PackArgs {
 // fp16x3 pack: any NetH; ldw = row stride of each torch weight ([out][ldw], the real columns
 // first: latent columns past len_a + len_b are folded into the biases)
 constexpr int kMaxLayersH = 24;
+// tr: the layer applies W^T (the backward chain): stream element (row o, column c) = w[c][o].
+// w2 / ldw2: segment B from its own matrix (else columns len_a.. of w); b may be null (0).
 struct PackArgsH {
   const float* w[kMaxLayersH];
+  const float* w2[kMaxLayersH];
   const float* b[kMaxLayersH];
   int ldw[kMaxLayersH];
+  int ldw2[kMaxLayersH];
+  int tr[kMaxLayersH];
   LayerDesc layers[kMaxLayersH];
   int n_layers, stream_blocks, bias_floats;
 };

@@ -151,6 +151,21 @@ int aon_mlp_fwd_train(const void* packed, const float* rays_o, const float* rays
                       const float* viewdirs, const float* t, int64_t B, int S, const float* noise,
                       float* h, float* bot, float* hv, float* raw, aon_stream_t stream);
 
+/* Backward chain of one level's NeRFMLP for the training step (model.py:95-120 under
+ * autograd): from draw (B*S, 4) = dL/d[raw_rgb, raw_sigma] (aon_composite_bwd), all input-
+ * gradient products dX = dZ W down to pts_linears.0 in one fused kernel, each masked by ReLU'
+ * of the stored forward activation it flows into (h, hv from aon_mlp_fwd_train), writing
+ *   dzv (B*S, 128): dL/d pre-activation of views_linear.0,
+ *   dzb (B*S, 256): dL/d bottleneck_layer output,
+ *   dz  (8, B*S, 256): dL/d pre-activation of pts_linears.i,
+ * the operands of the weight-gradient GEMMs dW = dZ^T X (aon_gemm).  packed: the transposed
+ * weight stream of aon_mlp_bwd_pack (re-pack after every optimizer step); work: >= 4 bytes
+ * of device scratch. */
+size_t aon_mlp_bwd_packed_bytes(void);
+int aon_mlp_bwd_pack(const aon_mlp_params* params, void* packed, aon_stream_t stream);
+int aon_mlp_bwd(const void* packed, const float* draw, const float* h, const float* hv,
+                int64_t N, float* dzv, float* dzb, float* dz, void* work, aon_stream_t stream);
+
 /* ---------------------------------------------------------------- articulated MLP */
 /* Device pointers to one articulated NeRFMLP's nn.Linear parameters in torch layout
  * (models/vanilla_nerf/model_autodecoder.py:60-166, default geometry: 4 x 128 deformation

@@ -140,16 +140,18 @@ def test_composite_backward(S, white):
 
 
 # ----------------------------------------------------------------------------- training step
-@pytest.fixture(params=[True, False], ids=["fused_fwd", "gemm_fwd"])
+@pytest.fixture(params=[(True, True), (False, False), (False, True)],
+                ids=["fused", "gemm", "gemm_fwd_fused_bwd"])
 def fwd_mode(request):
     """Training forward on the fused kernel with activation stores (aon_mlp_fwd_train) or on
-    the layer-by-layer GEMMs; every training test runs on both."""
+    the layer-by-layer GEMMs; backward input gradients in the fused chain (aon_mlp_bwd) or as
+    GEMMs.  Every training test runs on each combination."""
     from aonerf import train
 
-    old = train.FUSED_FORWARD
-    train.FUSED_FORWARD = request.param
+    old = train.FUSED_FORWARD, train.FUSED_BACKWARD
+    train.FUSED_FORWARD, train.FUSED_BACKWARD = request.param
     yield request.param
-    train.FUSED_FORWARD = old
+    train.FUSED_FORWARD, train.FUSED_BACKWARD = old
 
 
 def test_fused_train_forward_activations():
