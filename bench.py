@@ -45,8 +45,8 @@ def composite_bytes(S):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)  # >= 10 timed, 3 warm-up
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_TFLOPS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-chunks", type=int, default=2, help="3840-ray chunks in the CPU sample")
@@ -140,6 +140,16 @@ def main():
                                         "MAC/sample); f16x3 issues 3 fp16 products per MAC, so its "
                                         "peak in those units is 2500/3 TF/s"}},
     }
+    # the MFMA peak measured on random register operands (tools/mfma_peak.py)
+    ppath = os.path.join(ROOT, "profiles", "mfma_peak.json")
+    if achieved and os.path.exists(ppath):
+        mp = json.load(open(ppath))
+        key = "f32_16x16x4_tflops" if args.precision == "fp32" else "f16_16x16x32_tflops"
+        if mp.get(key):
+            iss = out["roofline"]["issued"]
+            iss["measured_dtype_peak_tflops"] = mp[key]
+            iss["frac_of_measured_peak"] = iss["issued_tflops"] / mp[key]
+            iss["measured_peak_source"] = "profiles/mfma_peak.json (tools/mfma_peak.py)"
     if comp_ms:
         cb = composite_bytes(NC + 1 + NF) * (comp_rows // (NC + 1 + NF))
         gbs = cb / (comp_ms * 1e-3) / 1e9
@@ -180,7 +190,14 @@ def cpu_baseline(frame, c2w, focal, nchunks):
     target = torch.from_numpy(np.random.Generator(np.random.PCG64(3)).uniform(0, 1, (n, 3)).astype(np.float32))
     p_ref = O.psnr_each([ref], [target]).item()
     p_gpu = O.psnr_each([gpu], [target]).item()
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": n / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpu_count": os.cpu_count(),
             "sample": f"{nchunks} x 3840-ray chunks (pixels {p0}..{p0 + n}) of the same frame, "
                       f"oracle/nerf_oracle.py torch-CPU restatement, {threads} threads, {dt:.1f} s",
             "max_abs_rgb_diff_vs_gpu": float((ref - gpu).abs().max()),
