@@ -48,6 +48,8 @@ struct Params {
   float* rowsum;        // !a_kc: rowsum[m] = sum_k A(m, k) (bias gradient of a dW product)
   float* rowsum_part;   // split-K partials [z][M]
   int tiles_m, tiles_n, gm;  // XCD-aware tile order over a 1-D grid.x (see tile_of)
+  int zsplit;                // split-K: number of K chunks (1 = not split), see split_of
+  int tblocks;               // blocks of one K chunk's tile grid (tile_of's ids, with padding)
 };
 
 // Workgroups are dispatched round-robin over the 8 XCDs (block L -> XCD L mod 8), each with
@@ -56,8 +58,24 @@ struct Params {
 // HBM once per XCD: group g of gm m-tiles x tiles_n n-tiles, L = gm tiles_n g + gm n + (m mod gm).
 // Grids of fewer than 8 m-tiles (weight gradients) use gm = tiles_m: no padding blocks, which
 // would otherwise pile the real tiles onto a few XCDs (measured: 3.5x slower).
-__device__ __forceinline__ bool tile_of(const Params& p, int& tm, int& tn) {
-  const int L = blockIdx.x;
+// Split-K grids: the tile count T is small (a weight gradient is 2 x 2 tiles) and every K chunk
+// is read by the T tiles that share it.  Chunk z's tiles get block ids 8 apart (L = 8 q + x,
+// z = 8 (q / T) + x, tile = q mod T): one XCD, dispatched together, so each chunk of both
+// operands comes from HBM once and the other tiles hit that XCD's L2.
+__device__ __forceinline__ bool split_of(const Params& p, int& tile, int& z) {
+  if (p.zsplit <= 1) {
+    tile = blockIdx.x;
+    z = 0;
+    return true;
+  }
+  const int T = p.tblocks;
+  const int L = blockIdx.x, x = L & 7, q = L >> 3;
+  z = 8 * (q / T) + x;
+  tile = q - (q / T) * T;
+  return z < p.zsplit;
+}
+
+__device__ __forceinline__ bool tile_of(const Params& p, int L, int& tm, int& tn) {
   const int gsz = p.gm * p.tiles_n;
   const int g = L / gsz, r = L - g * gsz;
   tn = r / p.gm;
@@ -176,9 +194,11 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   int tm, tn;
-  if (!tile_of(p, tm, tn)) return;  // padding block of the last XCD group (uniform exit)
+  int tile, z;
+  if (!split_of(p, tile, z)) return;      // padding block of the last chunk group
+  if (!tile_of(p, tile, tm, tn)) return;  // padding block of the last XCD group (uniform exit)
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int64_t kbeg = (int64_t)blockIdx.z * p.kchunk;
+  const int64_t kbeg = (int64_t)z * p.kchunk;
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
   const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
 
@@ -242,7 +262,7 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
     __syncthreads();
   }
 
-  const bool split = gridDim.z > 1;
+  const bool split = p.zsplit > 1;
   if (!AKC && want_rows) {
     // combine the 8 k-quad lanes of every row in k order (LDS free after the last barrier)
     float* red = reinterpret_cast<float*>(smem);  // [8 k quads][128 rows]
@@ -254,7 +274,7 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
       float v = red[tid];
 #pragma unroll
       for (int q = 1; q < 8; ++q) v = __fadd_rn(v, red[q * BM + tid]);
-      if (split) p.rowsum_part[(int64_t)blockIdx.z * p.M + m0 + tid] = v;
+      if (split) p.rowsum_part[(int64_t)z * p.M + m0 + tid] = v;
       else p.rowsum[m0 + tid] = v;
     }
   }
@@ -272,7 +292,7 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
         if (m >= p.M) continue;
         float v = __fmul_rn(__fadd_rn(acc_h[i][j][r], __fmul_rn(acc_x[i][j][r], kInvLo)), p.inv_s);
         if (split) {
-          p.part[((int64_t)blockIdx.z * p.M + m) * p.N + n] = v;
+          p.part[((int64_t)z * p.M + m) * p.N + n] = v;
           continue;
         }
         float* c = p.C + m * p.ldc + n;
@@ -389,7 +409,12 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   p.tiles_m = (int)tiles_m;
   p.tiles_n = (int)tiles_n;
   p.gm = (int)gm;
-  const dim3 grid((unsigned)blocks, 1, (unsigned)zs);
+  p.tblocks = (int)blocks;
+  p.zsplit = (int)zs;
+  // split-K: one 1-D grid, the tiles of a K chunk on one XCD (split_of)
+  const int64_t gx = zs > 1 ? 8 * blocks * ((zs + 7) / 8) : blocks;
+  AON_REQUIRE(gx < (1ll << 31), "too large");
+  const dim3 grid((unsigned)gx, 1, 1);
   // float4 staging when the 4-element runs are 16-B aligned
   const bool va = aligned16(a->A) && a->lda % 4 == 0 && (!a->A2 || a->K1 % 4 == 0);
   const bool vb = aligned16(a->B) && a->ldb % 4 == 0;
