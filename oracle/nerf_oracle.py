@@ -360,6 +360,40 @@ def art_render_level(params, rays, t_vals, level, white_bkgd, latents, deg_view=
     return volumetric_rendering(rgb, sigma, t_vals, rays["rays_d"], white_bkgd)
 
 
+def code_library_latents(tables, instance_id, articulation_id):
+    """CodeLibraryArticulated.forward, training branch (reference models/code_library.py:36-53):
+    rows of the three embedding tables -> {density, color (1, 128), articulation (1, 32)}."""
+    iid = torch.as_tensor([instance_id])
+    aid = torch.as_tensor([articulation_id])
+    return {"density": torch.nn.functional.embedding(iid, tables["embedding_instance_shape.weight"]),
+            "color": torch.nn.functional.embedding(iid, tables["embedding_instance_appearance.weight"]),
+            "articulation": torch.nn.functional.embedding(
+                aid, tables["embedding_instance_articulation.weight"])}
+
+
+def latent_reg_loss(latents):
+    """The latent-code regulariser of LitNeRF_AutoDecoder.training_step (reference
+    models/vanilla_nerf/model_autodecoder.py:456-466): 1e-4 * sum of mean column norms."""
+    return 1e-4 * (torch.mean(torch.norm(latents["density"], dim=0))
+                   + torch.mean(torch.norm(latents["color"], dim=0))
+                   + torch.mean(torch.norm(latents["articulation"], dim=0)))
+
+
+def art_training_loss(params, tables, rays, target, instance_id, articulation_id, randomized,
+                      white_bkgd, near, far, u_coarse=None, u_fine=None):
+    """LitNeRF_AutoDecoder.training_step (model_autodecoder.py:395-477): loss = mse(fine) +
+    mse(coarse) + the latent regulariser; returns (loss, loss0, loss1, reg)."""
+    latents = code_library_latents(tables, instance_id, articulation_id)
+    ret = art_nerf_forward(params, rays, randomized, white_bkgd, near, far, latents,
+                           u_coarse=u_coarse, u_fine=u_fine)
+    loss0 = img2mse(ret[0][0], target)
+    loss1 = img2mse(ret[1][0], target)
+    reg = latent_reg_loss(latents)
+    loss = loss1 + loss0
+    loss = loss + reg
+    return loss, loss0, loss1, reg
+
+
 # ----------------------------------------------------------------------------- metrics
 def img2mse(x, y):
     """reference helper.py:17-18."""

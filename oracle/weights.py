@@ -117,3 +117,18 @@ def art_latents(seed=0, n_obj_code=128, n_art_code=32):
     return {"density": rng.uniform(-b_obj, b_obj, size=(1, n_obj_code)).astype(np.float32),
             "color": rng.uniform(-b_obj, b_obj, size=(1, n_obj_code)).astype(np.float32),
             "articulation": rng.uniform(-b_art, b_art, size=(1, n_art_code)).astype(np.float32)}
+
+
+def code_library_state_dict(seed=0, n_max_objs=151, n_obj_code=128, n_max_articulations=10,
+                            n_art_code=32):
+    """A ``CodeLibraryArticulated`` state_dict (reference models/code_library.py:12-34): three
+    nn.Embedding tables with xavier_uniform bounds sqrt(6 / (rows + dim)); N_max_objs = 151 and
+    N_obj_code_length = 128 are the reference's opt.py:75,84 defaults."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = {}
+    for name, (n, c) in (("embedding_instance_shape", (n_max_objs, n_obj_code)),
+                         ("embedding_instance_appearance", (n_max_objs, n_obj_code)),
+                         ("embedding_instance_articulation", (n_max_articulations, n_art_code))):
+        b = np.sqrt(6.0 / (n + c))
+        out[f"{name}.weight"] = rng.uniform(-b, b, size=(n, c)).astype(np.float32)
+    return out

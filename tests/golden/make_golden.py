@@ -354,6 +354,59 @@ def case_articulated():
     save("articulated.npz", **out)
 
 
+def case_art_train_step():
+    """LitNeRF_AutoDecoder.training_step (model_autodecoder.py:395-477) run as the reference's
+    own method on a stand-in ``self`` (code library, NeRF_AE_Art, near/far, a recording
+    ``log``): loss = mse(fine) + mse(coarse) + 1e-4 latent regulariser, randomized with recorded
+    uniforms, 64 rays of a 240x320 view; autograd gradients of the MLPs and of the code
+    library's embedding tables."""
+    import types
+
+    mad = _refimport.load_articulated()
+    from models.code_library import CodeLibraryArticulated
+
+    net = mad.NeRF_AE_Art()
+    sd = W.art_state_dict(0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    net.train()
+    lib = CodeLibraryArticulated(types.SimpleNamespace(N_max_objs=151, N_obj_code_length=128))
+    tables = W.code_library_state_dict(0)
+    lib.load_state_dict({k: torch.from_numpy(v) for k, v in tables.items()})
+    logs = {}
+    fake = types.SimpleNamespace(
+        code_library=lib, model=net, white_bkgd=True, randomized=True, near=2.0, far=6.0,
+        log=lambda k, v, **kw: logs.__setitem__(k, float(v)),
+        optimizers=lambda: types.SimpleNamespace(param_groups=[{"lr": 5e-4}]))
+    rays, _, _, _ = frame_rays(240, 320, pose_idx=23)
+    sel = torch.arange(101, 76800, 1200)
+    rays = {k: v[sel].contiguous() for k, v in rays.items()}
+    rng = np.random.Generator(np.random.PCG64(5))
+    target = torch.from_numpy(rng.uniform(0, 1, size=(64, 3)).astype(np.float32))
+    iid, aid = 7, 3
+    batch = {k: v[None] for k, v in rays.items()}
+    batch.update(target=target[None], instance_id=torch.tensor([iid]),
+                 articulation_id=torch.tensor([aid]), deg=torch.tensor([0.25]))
+    with RandQueue(13) as rq:
+        loss = mad.LitNeRF_AutoDecoder.training_step(fake, batch, 0)
+    assert len(rq.drawn) == 2, len(rq.drawn)
+    loss.backward()
+    heavy = ("fine_mlp.deformations_linear.0.weight", "fine_mlp.pts_linears.0.weight",
+             "fine_mlp.pts_linears.5.weight", "fine_mlp.views_linear.0.weight",
+             "coarse_mlp.deformations_linear.0.weight")
+    light = ("bias", "deformation_layer.weight", "density_layer.weight", "rgb_layer.weight")
+    grads = {f"grad::{k}": p.grad.numpy().copy() for k, p in net.named_parameters()
+             if k in heavy or any(k.endswith(s) for s in light)}
+    for k, p in lib.named_parameters():
+        row = iid if "articulation" not in k else aid
+        assert np.count_nonzero(p.grad.numpy().any(axis=1)) == 1  # one row touched
+        grads[f"grad::{k}"] = p.grad.numpy()[row].copy()
+    save("art_train_step.npz", digest=np.array(W.digest(sd)), **{k: v.numpy() for k, v in rays.items()},
+         target=target.numpy(), instance_id=np.array(iid), articulation_id=np.array(aid),
+         u_coarse=rq.drawn[0], u_fine=rq.drawn[1], loss=np.array(loss.item(), dtype=np.float32),
+         reg=np.array(logs["train/loss/reg"], np.float32), psnr0=np.array(logs["train/psnr0"], np.float32),
+         psnr1=np.array(logs["train/psnr1"], np.float32), **grads)
+
+
 def _write_png(path, arr, mode):
     from PIL import Image
 
@@ -432,6 +485,10 @@ def case_datasets():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # e.g. `make_golden.py case_art_train_step`
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     case_rays()
     case_forward_eval()
     case_forward_random()
@@ -442,3 +499,4 @@ if __name__ == "__main__":
     case_train_step()
     case_articulated()
     case_datasets()
+    case_art_train_step()

@@ -147,3 +147,36 @@ def test_articulated(golden):
                                            atol=1e-6, err_msg=f"{tag} {name} {k}")
             np.testing.assert_allclose(inter[lv]["raw_rgb"].numpy(), g[f"{tag}_{name}_raw_rgb"],
                                        rtol=0, atol=1e-6)
+
+
+def test_art_train_step(golden):
+    """LitNeRF_AutoDecoder.training_step (model_autodecoder.py:395-477): the oracle's loss
+    (incl. the latent regulariser) and autograd gradients of both MLPs and of the code
+    library's embedding rows vs the reference run on the same weights / uniforms."""
+    g = golden("art_train_step.npz")
+    sd = W.art_state_dict(0)
+    assert W.digest(sd) == str(g["digest"])
+    params = O.split_state_dict(sd)
+    for p in params:
+        for v in p.values():
+            v.requires_grad_(True)
+    tables = {k: _t(v).requires_grad_(True) for k, v in W.code_library_state_dict(0).items()}
+    rays = {k: _t(g[k]) for k in ("rays_o", "rays_d", "viewdirs")}
+    loss, loss0, loss1, reg = O.art_training_loss(
+        params, tables, rays, _t(g["target"]), int(g["instance_id"]), int(g["articulation_id"]),
+        True, True, 2.0, 6.0, u_coarse=_t(g["u_coarse"]), u_fine=_t(g["u_fine"]))
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-6)
+    np.testing.assert_allclose(reg.item(), g["reg"], rtol=1e-6)
+    np.testing.assert_allclose(O.mse2psnr(loss0).item(), g["psnr0"], rtol=1e-6)
+    for key in g:
+        if not key.startswith("grad::"):
+            continue
+        name = key[6:]
+        if name.startswith("embedding"):
+            row = int(g["articulation_id"] if "articulation" in name else g["instance_id"])
+            got = tables[name].grad.numpy()[row]
+        else:
+            level, pname = name.split(".", 1)
+            got = params[0 if level == "coarse_mlp" else 1][pname].grad.numpy()
+        np.testing.assert_allclose(got, g[key], rtol=1e-4, atol=1e-6, err_msg=key)
