@@ -85,6 +85,8 @@ _SIGNATURES = {
     "aon_colsum": (c_int, [vp, c_i64, c_i64, c_i64, c_int, vp, vp, c_size, vp]),
     "aon_adam_step": (c_int, [ctypes.POINTER(AonAdamTensor), c_int, c_float, c_float, c_float,
                               c_float, c_i64, vp]),
+    "aon_pos_enc_bwd": (c_int, [vp, c_i64, vp, c_i64, c_i64, c_int, c_int, c_int, vp, c_i64, vp]),
+    "aon_latent_reg": (c_int, [vp, c_i64, c_i64, c_float, c_int, vp, vp, vp]),
 }
 
 _lib = None

@@ -284,14 +284,53 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
         self.fine_mlp = NeRFMLP(min_deg_point, max_deg_point, deg_view, enc_after=enc_after,
                                 embed_deg=embed_deg)
 
-    @torch.no_grad()
     def forward(self, rays, randomized, white_bkgd, near, far, latents, train=True, *,
                 u_coarse=None, u_fine=None, return_weights=False, return_intermediates=False):
         """reference model_autodecoder.py:278-337 -> [(comp_rgb, acc, depth)_coarse, (...)_fine]
-        (``u_coarse`` / ``u_fine`` inject randomized-mode uniforms; the extras as NeRF.forward)."""
+        (``u_coarse`` / ``u_fine`` inject randomized-mode uniforms; the extras as NeRF.forward).
+
+        With autograd enabled and trainable parameters or latent codes, each level runs the
+        training path (train_art.ArtRenderLevel: layer GEMMs keeping activations, HIP backward
+        into the MLP parameters and the latent codes); otherwise the fused inference kernel."""
         o, d, v = rays["rays_o"], rays["rays_d"], rays["viewdirs"]
         L.require_gpu(o, d, v)
         o, d, v = L.contig(o), L.contig(d), L.contig(v)
+        training = torch.is_grad_enabled() and (
+            any(p.requires_grad for p in self.parameters())
+            or any(x.requires_grad for x in latents.values()))
+        if training:
+            return self._forward_train(o, d, v, randomized, white_bkgd, near, far, latents,
+                                       u_coarse, u_fine, return_weights, return_intermediates)
+        with torch.no_grad():
+            return self._forward_render(o, d, v, randomized, white_bkgd, near, far, latents,
+                                        u_coarse, u_fine, return_weights, return_intermediates)
+
+    def _forward_train(self, o, d, v, randomized, white_bkgd, near, far, latents, u_coarse,
+                       u_fine, return_weights, return_intermediates):
+        from .train_art import render_level
+
+        B, dev = o.shape[0], o.device
+        ret = []
+        t_vals = weights = None
+        for level in range(2):
+            with torch.no_grad():  # no gradient reaches the sampling (helper.py:246-252)
+                t_vals = level_t_vals(level, o, d, t_vals, weights, randomized, near, far,
+                                      self.num_coarse_samples, self.num_fine_samples,
+                                      self.lindisp, u_coarse, u_fine)
+            mlp = self.coarse_mlp if level == 0 else self.fine_mlp
+            noise = None
+            if self.noise_std > 0 and randomized:  # model_autodecoder.py:318-319
+                noise = torch.rand((B * t_vals.shape[1],), device=dev) * self.noise_std
+            comp, acc, depth, weights = render_level(mlp, o, d, v, t_vals, white_bkgd, latents,
+                                                     noise)
+            out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
+            if return_intermediates:
+                out = out + (dict(t_vals=t_vals, weights=weights),)
+            ret.append(out)
+        return ret
+
+    def _forward_render(self, o, d, v, randomized, white_bkgd, near, far, latents, u_coarse,
+                        u_fine, return_weights, return_intermediates):
         B, dev = o.shape[0], o.device
         ret = []
         t_vals = weights = None

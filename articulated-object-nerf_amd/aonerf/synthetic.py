@@ -42,3 +42,17 @@ def art_latents(seed=0, n_obj_code=128, n_art_code=32, device=None):
            "color": rng.uniform(-b_obj, b_obj, size=(1, n_obj_code)),
            "articulation": rng.uniform(-b_art, b_art, size=(1, n_art_code))}
     return {k: torch.from_numpy(v.astype(np.float32)).to(device) for k, v in out.items()}
+
+
+@torch.no_grad()
+def init_code_library(lib, seed=0):
+    """Fill a CodeLibraryArticulated's three tables in place from PCG64(seed) with their
+    xavier_uniform bounds (reference models/code_library.py:31-33); the same stream as the
+    test-side oracle/weights.py code_library_state_dict."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    for emb in (lib.embedding_instance_shape, lib.embedding_instance_appearance,
+                lib.embedding_instance_articulation):
+        n, c = emb.weight.shape
+        b = np.sqrt(6.0 / (n + c))
+        emb.weight.copy_(torch.from_numpy(rng.uniform(-b, b, size=(n, c)).astype(np.float32)))
+    return lib

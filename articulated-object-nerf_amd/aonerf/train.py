@@ -319,8 +319,6 @@ class Adam:
 
     def __init__(self, params, lr=5.0e-4, betas=(0.9, 0.999), eps=1e-8):
         self.params = [p for p in params if p.requires_grad]
-        if len(self.params) > L.ADAM_MAX_TENSORS:
-            raise ValueError(f"at most {L.ADAM_MAX_TENSORS} parameter tensors")
         L.require_gpu(*self.params)
         self.lr, self.betas, self.eps = lr, betas, eps
         self.state = [(torch.zeros_like(p), torch.zeros_like(p)) for p in self.params]
@@ -333,14 +331,20 @@ class Adam:
     @torch.no_grad()
     def step(self, lr=None):
         self.step_count += 1
-        table = (L.AonAdamTensor * len(self.params))()
-        for i, (p, (m, v)) in enumerate(zip(self.params, self.state)):
+        for p in self.params:
             if p.grad is None:
                 raise RuntimeError("Adam.step: a parameter has no gradient")
             if not p.is_contiguous() or not p.grad.is_contiguous():
                 raise ValueError("Adam.step: parameters and grads must be contiguous")
-            table[i] = L.AonAdamTensor(p.data_ptr(), p.grad.data_ptr(), m.data_ptr(), v.data_ptr(),
-                                       p.numel())
-        L.call("aon_adam_step", table, len(self.params), float(self.lr if lr is None else lr),
-               float(self.betas[0]), float(self.betas[1]), float(self.eps), self.step_count,
-               L.stream(self.params[0].device))
+        # one launch per AON_ADAM_MAX_TENSORS tensors (the articulated model + code library
+        # has 83)
+        n = L.ADAM_MAX_TENSORS
+        for c0 in range(0, len(self.params), n):
+            chunk = list(zip(self.params, self.state))[c0:c0 + n]
+            table = (L.AonAdamTensor * len(chunk))()
+            for i, (p, (m, v)) in enumerate(chunk):
+                table[i] = L.AonAdamTensor(p.data_ptr(), p.grad.data_ptr(), m.data_ptr(),
+                                           v.data_ptr(), p.numel())
+            L.call("aon_adam_step", table, len(chunk), float(self.lr if lr is None else lr),
+                   float(self.betas[0]), float(self.betas[1]), float(self.eps), self.step_count,
+                   L.stream(self.params[0].device))

@@ -1,0 +1,345 @@
+"""Training step of the articulated auto-decoder (reference LitNeRF_AutoDecoder.training_step,
+models/vanilla_nerf/model_autodecoder.py:395-477; configure_optimizers / optimizer_step :599-633)
+on the HIP kernels.
+
+One NeRF_AE_Art level under autograd is ``ArtRenderLevel`` (a torch.autograd.Function) with
+gradients for the level's 40 MLP parameters AND the three latent codes:
+
+  forward   cast_rays -> deformation MLP on cat[xyz, shape, articulation] (4 x GEMM + ReLU,
+            deformation_layer) -> x' = delta + xyz and pos_enc(x') (aon_cast_rays) -> trunk on
+            cat[pos_enc(x'), shape] with the skip concat -> density, bottleneck -> view branch on
+            cat[bottleneck, enc_dir tiled over samples, appearance] -> rgb; every activation kept
+            (model_autodecoder.py:168-239) -> compositing with the padded sigmoid / softplus
+            (aon_composite_fwd, AON_ACT_ARTIC; :321-333)
+  backward  aon_composite_bwd -> per layer, last to first, dW = dZ^T X with db = sum_rows dZ
+            from the same pass and dX = (dZ W) * relu'(X) (aon_gemm) -> the trunk's gradient
+            w.r.t. pos_enc(x') (skip + first layer) through aon_pos_enc_bwd into the
+            deformation MLP.
+
+The latent codes are the same row for every sample (repeated over B*S rows,
+model_autodecoder.py:186-194), so their columns are folded into per-call biases in the
+forward, and in the backward a layer z = W [x; l] + b gives dL/dl = W_l^T db and
+dL/dW_l = db l^T from the bias gradient db alone (aon_gemm with K = 1 / M = 1); the shape code
+collects three such terms (deformation input, trunk input, skip), appearance one, articulation
+one, both levels add through autograd.  The regulariser 1e-4 * sum of mean code norms
+(:456-466) is aon_latent_reg.  All arithmetic is in HIP kernels; torch allocates, routes
+autograd and looks up / scatters the code-library rows (nn.Embedding).
+"""
+import torch
+
+from . import _lib as L
+from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, gemm
+from .train import Adam, img2mse, learning_rate, mse2psnr  # noqa: F401 (the shared loss / optimizer)
+
+# parameter layout of one articulated NeRFMLP in ArtRenderLevel: 20 layers x (weight, bias)
+DEF0, DL, PTS0, DENS, BOT, VIEW0, RGB = 0, 4, 5, 13, 14, 15, 19
+
+
+def art_layers(mlp):
+    """The 20 nn.Linear layers of an articulated NeRFMLP in ArtRenderLevel order."""
+    return (list(mlp.deformations_linear) + [mlp.deformation_layer] + list(mlp.pts_linears)
+            + [mlp.density_layer, mlp.bottleneck_layer] + list(mlp.views_linear) + [mlp.rgb_layer])
+
+
+def _check_geometry(mlp):
+    ok = (mlp.netdepth == 8 and mlp.skip_layer == 4 and mlp.netdepth_deformation == 4
+          and mlp.netdepth_condition == 4 and mlp.input_ch == 3 and mlp.input_ch_view == 3
+          and mlp.num_rgb_channels == 3 and mlp.num_density_channels == 1)
+    if not ok:
+        raise ValueError("the articulated training path implements the reference's default layer "
+                         "counts (netdepth 8, skip 4, 4 deformation / 4 condition layers)")
+
+
+class _Geo:
+    """Widths of one articulated NeRFMLP (model_autodecoder.py:60-166)."""
+
+    def __init__(self, mlp):
+        _check_geometry(mlp)
+        self.wd, self.nw, self.wc = mlp.netwidth_deformation, mlp.netwidth, mlp.netwidth_condition
+        self.ne = mlp.pos_size_enc  # 3 + 6 (max_deg - min_deg)
+        self.min_deg, self.max_deg, self.deg_view = mlp.min_deg_point, mlp.max_deg_point, mlp.deg_view
+        self.nv = (mlp.deg_view * 2 + 1) * mlp.input_ch_view
+        self.n_shape, self.n_app = mlp.shape_latent_dim, mlp.appearance_latent_dim
+        self.n_art = mlp.articulation_latent_dim
+
+
+def _fold(W, b, c0, lat):
+    """b + W[:, c0:c0+n] . lat (the latent columns of a layer as a per-call bias)."""
+    N, n = W.shape[0], lat.shape[1]
+    out = torch.empty((1, N), device=W.device)
+    gemm(out, lat, W[:, c0:], 1, N, n, lda=n, a_kc=True, ldb=W.stride(0), b_kc=True, ldc=N,
+         bias=b, a_scale=1.0, b_scale=W_SCALE)
+    return out.reshape(-1)
+
+
+def _linear(out, X, ldx, W, bias, K, *, relu=False, X2=None, K2=0, ld2=0, rdiv2=1, ldo=None,
+            accumulate=False):
+    """out (R x N) (+)= [X | X2] W[:, :K+K2]^T + bias (+ReLU)."""
+    R, N = out.shape[0], W.shape[0]
+    gemm(out, X, W, R, N, K + K2, lda=ldx, a_kc=True, ldb=W.stride(0), b_kc=True,
+         ldc=ldo or out.stride(0), A2=X2, lda2=ld2, K1=K if X2 is not None else 0, a2_rdiv=rdiv2,
+         bias=bias, relu=relu, accumulate=accumulate, a_scale=ACT_SCALE, b_scale=W_SCALE)
+
+
+def _forward_level(geo, P, lat, xyz, venc, S, raw, noise=None):
+    """NeRFMLP.forward (model_autodecoder.py:168-239) layer by layer, keeping activations."""
+    R, dev = xyz.shape[0], xyz.device
+    shape, app, art = lat
+    wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
+    # deformation MLP on cat[xyz, shape, art] (:196-203), the latent columns folded
+    hd = torch.empty((4, R, wd), device=dev)
+    _linear(hd[0], xyz, 3, P[DEF0][0], _fold(*P[DEF0], 3, torch.cat([shape, art], -1)), 3,
+            relu=True)
+    for i in range(1, 4):
+        _linear(hd[i], hd[i - 1], wd, *P[DEF0 + i], wd, relu=True)
+    delta = torch.empty((R, 3), device=dev)
+    _linear(delta, hd[3], wd, *P[DL], wd)  # deformation_layer (:205)
+    # x' = delta + xyz -> pos_enc (enc_after, :205-212); enc[:, :3] is x' itself
+    enc = torch.empty((R, ne), device=dev)
+    L.call("aon_cast_rays", L.ptr(xyz), None, None, R, 1, L.ptr(delta), 3, None, geo.min_deg,
+           geo.max_deg, L.ptr(enc), L.stream(dev))
+    # trunk on cat[enc, shape] with the skip concat cat[h4, enc, shape] (:214-220)
+    h = torch.empty((8, R, nw), device=dev)
+    W0 = P[PTS0][0]
+    _linear(h[0], enc, ne, W0, _fold(W0, P[PTS0][1], ne, shape), ne, relu=True)
+    for i in range(1, 8):
+        W_, b_ = P[PTS0 + i]
+        if i == 5:
+            _linear(h[5], h[4], nw, W_, _fold(W_, b_, nw + ne, shape), nw, relu=True, X2=enc,
+                    K2=ne, ld2=ne)
+        else:
+            _linear(h[i], h[i - 1], nw, W_, b_, nw, relu=True)
+    if noise is not None:  # raw_sigma + noise (:318-319), added in the GEMM epilogue
+        raw[:, 3].copy_(noise)
+    _linear(raw[:, 3:], h[7], nw, *P[DENS], nw, ldo=4, accumulate=noise is not None)
+    bot = torch.empty((R, nw), device=dev)
+    _linear(bot, h[7], nw, *P[BOT], nw)  # bottleneck, no activation (:225)
+    # view branch on cat[bottleneck, enc_dir tiled over samples, appearance] (:226-235)
+    hv = torch.empty((4, R, wc), device=dev)
+    Wv = P[VIEW0][0]
+    _linear(hv[0], bot, nw, Wv, _fold(Wv, P[VIEW0][1], nw + nv, app), nw, relu=True, X2=venc,
+            K2=nv, ld2=nv, rdiv2=S)
+    for i in range(1, 4):
+        _linear(hv[i], hv[i - 1], wc, *P[VIEW0 + i], wc, relu=True)
+    _linear(raw, hv[3], wc, *P[RGB], wc, ldo=4)  # rgb_layer (:237)
+    return hd, enc, h, bot, hv
+
+
+def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw):
+    """Autograd of _forward_level from dL/draw (R x 4): G[i] = (dW, db) of layer i; dlat =
+    (dshape, dapp, dart) (1 x n each) receive the latent-code gradients."""
+    R, dev = xyz.shape[0], xyz.device
+    wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
+    shape, app, art = lat
+    dshape, dapp, dart = dlat
+    gs, acts = GRAD_SCALE, ACT_SCALE
+
+    def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True):
+        # dW_i[:, col0:col0+n_in] = dY^T X (K = rows, split-K); db_i = sum_rows dY, same pass
+        dW = G[i][0]
+        n_out = dW.shape[0]
+        gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
+             b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0), a_scale=gs, b_scale=acts,
+             rowsum=G[i][1] if bias else None)
+
+    def dinput(dX, dY, ldy, i, col0, n_in, mask=None, accumulate=False):
+        # dX (R x n_in) (+)= dY W_i[:, col0:col0+n_in] (* relu'(mask))
+        W = P[i][0]
+        gemm(dX, dY, W[:, col0:] if col0 else W, R, n_in, W.shape[0], lda=ldy, a_kc=True,
+             ldb=W.stride(0), b_kc=False, ldc=dX.stride(0), mask=mask,
+             ldm=mask.stride(0) if mask is not None else 0, accumulate=accumulate, a_scale=gs,
+             b_scale=W_SCALE)
+
+    def dlatent(i, col0, l, dl, accumulate):
+        # z = W [x; l] + b with l on every row: dW[:, col0:col0+n] = db l^T, dl (+)= db^T W_l
+        dW, db = G[i]
+        W = P[i][0]
+        n_out, n = W.shape[0], l.shape[1]
+        gemm(dW[:, col0:], db, l, n_out, n, 1, lda=1, a_kc=True, ldb=n, b_kc=False,
+             ldc=dW.stride(0), a_scale=gs, b_scale=1.0)
+        gemm(dl, db, W[:, col0:], 1, n, n_out, lda=n_out, a_kc=True, ldb=W.stride(0), b_kc=False,
+             ldc=n, accumulate=accumulate, a_scale=gs, b_scale=W_SCALE)
+
+    # rgb head and the view branch
+    dweight(RGB, draw, 4, hv[3], wc, wc)
+    dz = torch.empty((R, wc), device=dev)
+    dz2 = torch.empty((R, wc), device=dev)
+    dinput(dz, draw, 4, RGB, 0, wc, mask=hv[3])
+    for i in range(3, 0, -1):
+        dweight(VIEW0 + i, dz, wc, hv[i - 1], wc, wc)
+        dinput(dz2, dz, wc, VIEW0 + i, 0, wc, mask=hv[i - 1])
+        dz, dz2 = dz2, dz
+    dweight(VIEW0, dz, wc, bot, nw, nw)
+    dweight(VIEW0, dz, wc, venc, nv, nv, col0=nw, rdiv=S, bias=False)
+    dlatent(VIEW0, nw + nv, app, dapp, False)
+    dbot = torch.empty((R, nw), device=dev)
+    dinput(dbot, dz, wc, VIEW0, 0, nw)  # the bottleneck has no activation
+    del dz, dz2
+    # bottleneck + density heads on h7
+    dweight(BOT, dbot, nw, h[7], nw, nw)
+    dweight(DENS, draw[:, 3:], 4, h[7], nw, nw)
+    dy = torch.empty((R, nw), device=dev)
+    dinput(dy, dbot, nw, BOT, 0, nw)
+    dinput(dy, draw[:, 3:], 4, DENS, 0, nw, mask=h[7], accumulate=True)
+    del dbot
+    # trunk; the gradient w.r.t. enc = pos_enc(x') collects the skip and the first layer
+    denc = torch.empty((R, ne), device=dev)
+    dx = torch.empty((R, nw), device=dev)
+    for i in range(7, -1, -1):  # dy = dL/d(pre-activation of pts_linears.i)
+        if i == 5:
+            dweight(PTS0 + 5, dy, nw, h[4], nw, nw)
+            dweight(PTS0 + 5, dy, nw, enc, ne, ne, col0=nw, bias=False)
+            dlatent(PTS0 + 5, nw + ne, shape, dshape, False)
+            dinput(denc, dy, nw, PTS0 + 5, nw, ne)
+        elif i == 0:
+            dweight(PTS0, dy, nw, enc, ne, ne)
+            dlatent(PTS0, ne, shape, dshape, True)
+            dinput(denc, dy, nw, PTS0, 0, ne, accumulate=True)
+        else:
+            dweight(PTS0 + i, dy, nw, h[i - 1], nw, nw)
+        if i > 0:
+            dinput(dx, dy, nw, PTS0 + i, 0, nw, mask=h[i - 1])
+            dx, dy = dy, dx
+    del dx, dy
+    # x' = deformation_layer(hd3) + xyz, enc = pos_enc(x') (:205-212)
+    dxp = torch.empty((R, 3), device=dev)
+    L.call("aon_pos_enc_bwd", L.ptr(enc), ne, L.ptr(denc), ne, R, geo.min_deg, geo.max_deg, 0,
+           L.ptr(dxp), 3, L.stream(dev))
+    del denc
+    dweight(DL, dxp, 3, hd[3], wd, wd)
+    dz = torch.empty((R, wd), device=dev)
+    dz2 = torch.empty((R, wd), device=dev)
+    dinput(dz, dxp, 3, DL, 0, wd, mask=hd[3])
+    for i in range(3, 0, -1):
+        dweight(DEF0 + i, dz, wd, hd[i - 1], wd, wd)
+        dinput(dz2, dz, wd, DEF0 + i, 0, wd, mask=hd[i - 1])
+        dz, dz2 = dz2, dz
+    # deformations_linear.0 on cat[xyz, shape, art]
+    dweight(DEF0, dz, wd, xyz, 3, 3)
+    dlatent(DEF0, 3, shape, dshape, True)
+    dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
+
+
+class ArtRenderLevel(torch.autograd.Function):
+    """cast_rays + articulated NeRFMLP + activations + volumetric_rendering of one level
+    (model_autodecoder.py:296-333) with gradients for the level's 40 MLP parameters and the
+    three latent codes (density = shape, color = appearance, articulation)."""
+
+    @staticmethod
+    def forward(ctx, geo, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise, shape, app, art,
+                *params):
+        B, S = t_vals.shape
+        R, dev = B * S, t_vals.device
+        lat = tuple(L.contig(x.detach().reshape(1, -1)) for x in (shape, app, art))
+        L.require_gpu(rays_o, rays_d, viewdirs, t_vals, *lat)
+        if lat[0].shape[1] != geo.n_shape or lat[1].shape[1] != geo.n_app or lat[2].shape[1] != geo.n_art:
+            raise ValueError("latent code sizes do not match the MLP")
+        for p in params:
+            if not p.is_contiguous():
+                raise ValueError("MLP parameters must be contiguous")
+        xyz = torch.empty((R, 3), device=dev)
+        L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
+               L.ptr(xyz), 0, 0, None, L.stream(dev))
+        venc = torch.empty((B, geo.nv), device=dev)
+        L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, geo.deg_view, L.ptr(venc), L.stream(dev))
+        P = [(params[2 * i], params[2 * i + 1]) for i in range(20)]
+        raw = torch.empty((R, 4), device=dev)
+        noise = L.contig(noise) if noise is not None else None
+        hd, enc, h, bot, hv = _forward_level(geo, P, lat, xyz, venc, S, raw, noise)
+        comp = torch.empty((B, 3), device=dev)
+        acc = torch.empty((B,), device=dev)
+        weights = torch.empty((B, S), device=dev)
+        depth = torch.empty((B,), device=dev)
+        L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals),
+               L.ptr(rays_d), B, S, int(bool(white_bkgd)), L.ACT_ARTIC, L.ptr(comp), L.ptr(acc),
+               L.ptr(weights), L.ptr(depth), L.stream(dev))
+        ctx.save_for_backward(rays_d, t_vals, xyz, enc, venc, raw, hd, h, bot, hv, *lat, *params)
+        ctx.meta = (geo, B, S, bool(white_bkgd), tuple(x.shape for x in (shape, app, art)))
+        ctx.mark_non_differentiable(weights)
+        return comp, acc, depth, weights
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_acc, g_depth, _g_w):
+        geo, B, S, white, lat_shapes = ctx.meta
+        saved = ctx.saved_tensors
+        rays_d, t_vals, xyz, enc, venc, raw, hd, h, bot, hv = saved[:10]
+        lat = saved[10:13]
+        params = saved[13:]
+        dev = raw.device
+        R = B * S
+        draw = torch.empty((R, 4), device=dev)
+        L.call("aon_composite_bwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals),
+               L.ptr(rays_d), B, S, int(white), L.ACT_ARTIC, L.ptr(L.contig(g_rgb)),
+               L.ptr(L.contig(g_acc)) if g_acc is not None else None,
+               L.ptr(L.contig(g_depth)) if g_depth is not None else None,
+               L.ptr(draw), L.ptr(draw[:, 3:]), 4, L.stream(dev))
+        P = [(params[2 * i], params[2 * i + 1]) for i in range(20)]
+        G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
+        dlat = tuple(torch.empty_like(x) for x in lat)
+        _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
+        grads = [g for pair in G for g in pair]
+        dlat = [d.reshape(s) for d, s in zip(dlat, lat_shapes)]
+        return (None, None, None, None, None, None, None, *dlat, *grads)
+
+
+def render_level(mlp, rays_o, rays_d, viewdirs, t_vals, white_bkgd, latents, noise=None):
+    """One NeRF_AE_Art level under autograd -> (comp_rgb, acc, depth, weights)."""
+    params = [p for m in art_layers(mlp) for p in (m.weight, m.bias)]
+    geo = getattr(mlp, "_geo", None)
+    if geo is None:
+        geo = mlp._geo = _Geo(mlp)
+    return ArtRenderLevel.apply(geo, rays_o, rays_d, viewdirs, t_vals, bool(white_bkgd), noise,
+                                latents["density"], latents["color"], latents["articulation"],
+                                *params)
+
+
+class LatentReg(torch.autograd.Function):
+    """The latent regulariser of training_step (model_autodecoder.py:456-466):
+    1e-4 * (mean ||shape||_0 + mean ||appearance||_0 + mean ||articulation||_0), norms over
+    dim 0 (aon_latent_reg)."""
+
+    @staticmethod
+    def forward(ctx, shape, app, art):
+        codes = [L.contig(x.detach()) for x in (shape, app, art)]
+        L.require_gpu(*codes)
+        loss = torch.empty((), device=shape.device)
+        grads = []
+        for i, c in enumerate(codes):
+            c2 = c.reshape(c.shape[0], -1)  # norm over dim 0: (1, C) -> |x|, (C,) -> ||x||
+            g = torch.empty_like(c)
+            L.call("aon_latent_reg", L.ptr(c2), c2.shape[0], c2.shape[1], 1e-4, int(i > 0),
+                   L.ptr(loss), L.ptr(g), L.stream(shape.device))
+            grads.append(g)
+        ctx.save_for_backward(*grads)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        # the regulariser is a leaf term of the loss: g is dL/dreg = 1 (a scalar multiply by
+        # a non-unit g would be the only torch arithmetic; training_step always passes 1)
+        return tuple(x * g for x in ctx.saved_tensors)
+
+
+def training_step(model, code_library, batch, randomized, white_bkgd, near, far, *,
+                  u_coarse=None, u_fine=None):
+    """LitNeRF_AutoDecoder.training_step (model_autodecoder.py:395-477) ->
+    (loss, logs{loss0, loss1, reg, psnr0, psnr1}).  ``batch`` holds rays_o / rays_d / viewdirs /
+    target (B, 3) and instance_id / articulation_id (1,) as the reference's loader gives them
+    after its squeeze (model_autodecoder.py:396-399)."""
+    latents = code_library(batch)
+    ret = model(batch, randomized, white_bkgd, near, far, latents, u_coarse=u_coarse,
+                u_fine=u_fine)
+    target = batch["target"]
+    loss0 = img2mse(ret[0][0], target)
+    loss1 = img2mse(ret[1][0], target)
+    reg = LatentReg.apply(latents["density"], latents["color"], latents["articulation"])
+    loss = loss1 + loss0 + reg
+    return loss, dict(loss0=loss0, loss1=loss1, reg=reg, psnr0=mse2psnr(loss0.detach()),
+                      psnr1=mse2psnr(loss1.detach()))
+
+
+def configure_optimizers(model, code_library, lr_init=5.0e-4):
+    """configure_optimizers (model_autodecoder.py:599-601): Adam over the MLPs and the code
+    library (the fused aon_adam_step, betas (0.9, 0.999))."""
+    return Adam(list(model.parameters()) + list(code_library.parameters()), lr=lr_init,
+                betas=(0.9, 0.999))

@@ -307,6 +307,22 @@ typedef struct aon_adam_tensor {
 int aon_adam_step(const aon_adam_tensor* tensors, int count, float lr, float beta1, float beta2,
                   float eps, int64_t step, aon_stream_t stream);
 
+/* ---------------------------------------------------------------- articulated training */
+/* Autograd of pos_enc (helper.py:136-140) on the deformed points of the articulated MLP
+ * (model_autodecoder.py:205-212): dx (n x 3, row stride lddx) (+)= dL/dx given the points x
+ * (row stride ldx; the encodings' identity channels serve, ldx = 3 + 6L) and dL/denc (n x
+ * (3 + 6L), row stride ldg), L = max_deg - min_deg.  Replaces torch autograd through
+ * model_autodecoder.py:205-212 (SinBackward / CatBackward / MulBackward). */
+int aon_pos_enc_bwd(const float* x, int64_t ldx, const float* g_enc, int64_t ldg, int64_t n,
+                    int min_deg, int max_deg, int accumulate, float* dx, int64_t lddx,
+                    aon_stream_t stream);
+
+/* One term of the latent-code regulariser of LitNeRF_AutoDecoder.training_step
+ * (model_autodecoder.py:456-466, weight 1e-4): *loss (+)= weight * mean_c ||code[:, c]||_2 over
+ * an (n x c) code; grad (n x c) = weight / c * code / ||code[:, c]|| (0 on a zero column). */
+int aon_latent_reg(const float* code, int64_t n, int64_t c, float weight, int accumulate,
+                   float* loss, float* grad, aon_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

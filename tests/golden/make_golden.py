@@ -404,7 +404,8 @@ def case_art_train_step():
          target=target.numpy(), instance_id=np.array(iid), articulation_id=np.array(aid),
          u_coarse=rq.drawn[0], u_fine=rq.drawn[1], loss=np.array(loss.item(), dtype=np.float32),
          reg=np.array(logs["train/loss/reg"], np.float32), psnr0=np.array(logs["train/psnr0"], np.float32),
-         psnr1=np.array(logs["train/psnr1"], np.float32), **grads)
+         psnr1=np.array(logs["train/psnr1"], np.float32),
+         art_interp=lib.get_interpolated_articulations(2, "cpu").detach().numpy(), **grads)
 
 
 def _write_png(path, arr, mode):

@@ -1,0 +1,239 @@
+"""GPU parity of the articulated training path (reference LitNeRF_AutoDecoder.training_step,
+models/vanilla_nerf/model_autodecoder.py:395-477): the pos_enc backward and the latent
+regulariser kernels against torch autograd through the CPU oracle, the whole training step
+(loss, both MLPs' gradients, the code-library rows' gradients) against the reference's golden
+vectors, teacher-forced per-level gradients, and an Adam step over all 83 parameter tensors.
+
+Tolerances: pos_enc backward 1e-5 of each tensor's gradient scale (fp32 sin' = cos at the same
+fp32 arguments, ulp-level differences of cosf at |arg| <= 5120); regulariser 1e-6 relative;
+loss rtol 1e-5; gradients vs the reference within max(4 x the reference's own fp32-vs-fp64
+spread, 1e-4) of each tensor's max (as tests/test_gpu_train.py); teacher-forced gradients vs
+the fp32 oracle within max(2 x its distance from the fp64 oracle, 1e-3) (measured values
+printed).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+from oracle import weights as W
+
+pytestmark = pytest.mark.gpu
+
+
+def cuda(a):
+    return torch.as_tensor(np.ascontiguousarray(a)).cuda()
+
+
+def rel_err(got, want):
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    scale = np.abs(want).max() if want.size else 1.0
+    return float(np.abs(got - want).max() / max(scale, 1e-30)) if want.size else 0.0
+
+
+@pytest.mark.parametrize("n,L", [(1000, 10), (37, 4), (1, 10)])
+def test_pos_enc_backward(n, L):
+    from aonerf import _lib
+
+    gen = torch.Generator().manual_seed(n + L)
+    x = (torch.rand(n, 3, generator=gen) - 0.5) * 20
+    x[0] = torch.tensor([0.0, -3.1415927, 10.0])
+    g = torch.randn(n, 3 + 6 * L, generator=gen)
+    xr = x.clone().requires_grad_(True)
+    O.pos_enc(xr, 0, L).backward(g)
+    enc = torch.empty((n, 3 + 6 * L), device="cuda")
+    xd, gd = x.cuda(), g.cuda()
+    _lib.call("aon_pos_enc", _lib.ptr(xd), n, 0, L, _lib.ptr(enc), _lib.stream())
+    dx = torch.full((n, 3), 0.5, device="cuda")
+    # identity channels of the encoding as the points (ldx = 3 + 6L), accumulate into dx
+    _lib.call("aon_pos_enc_bwd", _lib.ptr(enc), 3 + 6 * L, _lib.ptr(gd), 3 + 6 * L, n, 0, L, 1,
+              _lib.ptr(dx), 3, _lib.stream())
+    got = dx.cpu().numpy() - 0.5
+    e = rel_err(got, xr.grad.numpy())
+    print(f"pos_enc backward n={n} L={L}: max rel err {e:.2e}")
+    assert e < 1e-5
+
+
+def test_latent_reg():
+    from aonerf.train_art import LatentReg
+
+    lat = {k: cuda(v) for k, v in W.art_latents(3).items()}
+    lat["density"][0, 5] = 0.0  # zero entry: torch's norm backward gives 0
+    codes = [lat[k].clone().requires_grad_(True) for k in ("density", "color", "articulation")]
+    loss = LatentReg.apply(*codes)
+    loss.backward()
+    ref_codes = [lat[k].cpu().clone().requires_grad_(True) for k in ("density", "color", "articulation")]
+    ref = O.latent_reg_loss(dict(zip(("density", "color", "articulation"), ref_codes)))
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-6)
+    for c, r in zip(codes, ref_codes):
+        np.testing.assert_allclose(c.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-6, atol=0)
+
+
+def _make(seed=0):
+    import types
+
+    from aonerf.code_library import CodeLibraryArticulated
+    from aonerf.model_autodecoder import NeRF_AE_Art
+
+    net = NeRF_AE_Art().cuda()
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.art_state_dict(seed).items()})
+    lib = CodeLibraryArticulated(types.SimpleNamespace(N_max_objs=151, N_obj_code_length=128)).cuda()
+    lib.load_state_dict({k: torch.from_numpy(v) for k, v in W.code_library_state_dict(seed).items()})
+    return net, lib
+
+
+def _batch(g):
+    b = {k: cuda(g[k]) for k in ("rays_o", "rays_d", "viewdirs", "target")}
+    b["instance_id"] = torch.tensor([int(g["instance_id"])], device="cuda")
+    b["articulation_id"] = torch.tensor([int(g["articulation_id"])], device="cuda")
+    return b
+
+
+def _oracle_grads(g, dtype):
+    params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
+              for p in O.split_state_dict(W.art_state_dict(0))]
+    tables = {k: torch.from_numpy(v).to(dtype).requires_grad_(True)
+              for k, v in W.code_library_state_dict(0).items()}
+    rays = {k: torch.from_numpy(g[k]).to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
+    loss, *_ = O.art_training_loss(params, tables, rays, torch.from_numpy(g["target"]).to(dtype),
+                                   int(g["instance_id"]), int(g["articulation_id"]), True, True,
+                                   2.0, 6.0, u_coarse=torch.from_numpy(g["u_coarse"]).to(dtype),
+                                   u_fine=torch.from_numpy(g["u_fine"]).to(dtype))
+    loss.backward()
+    grads = {f"{lv}.{k}": v.grad.double().numpy() for lv, p in zip(("coarse_mlp", "fine_mlp"), params)
+             for k, v in p.items()}
+    grads.update({k: v.grad.double().numpy() for k, v in tables.items()})
+    return grads
+
+
+def _named_grad(net, lib, name, g):
+    if name.startswith("embedding"):
+        row = int(g["articulation_id"] if "articulation" in name else g["instance_id"])
+        return dict(lib.named_parameters())[name].grad[row].cpu().numpy()
+    return dict(net.named_parameters())[name].grad.cpu().numpy()
+
+
+def test_art_train_step_golden(golden):
+    """Loss (incl. the latent regulariser) and the recorded gradients of one
+    LitNeRF_AutoDecoder.training_step (randomized, injected uniforms) vs the reference."""
+    from aonerf import train_art
+
+    g = golden("art_train_step.npz")
+    assert W.digest(W.art_state_dict(0)) == str(g["digest"])
+    net, lib = _make(0)
+    loss, logs = train_art.training_step(net, lib, _batch(g), True, True, 2.0, 6.0,
+                                         u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]))
+    loss.backward()
+    torch.cuda.synchronize()
+    print(f"loss gpu {loss.item():.8f} ref {float(g['loss']):.8f}")
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-5)
+    np.testing.assert_allclose(logs["reg"].item(), g["reg"], rtol=1e-5)
+    np.testing.assert_allclose(logs["psnr0"].item(), g["psnr0"], rtol=1e-5)
+    g64 = _oracle_grads(g, torch.float64)
+    worst = 0.0
+    for key in g:
+        if not key.startswith("grad::"):
+            continue
+        name = key[6:]
+        ref = g[key]
+        ref64 = g64[name]
+        if name.startswith("embedding"):
+            ref64 = ref64[int(g["articulation_id"] if "articulation" in name else g["instance_id"])]
+        env = rel_err(ref, ref64)
+        e = rel_err(_named_grad(net, lib, name, g), ref)
+        print(f"  {name:45s} ours {e:.2e}  reference fp32-vs-fp64 envelope {env:.2e}")
+        worst = max(worst, e / max(4 * env, 1e-4))
+        assert e <= max(4 * env, 1e-4), (key, e, env)
+    # the code library's untouched rows get exactly zero gradient
+    for name, p in lib.named_parameters():
+        row = int(g["articulation_id"] if "articulation" in name else g["instance_id"])
+        gr = p.grad.clone()
+        gr[row] = 0
+        assert not gr.any(), name
+    print(f"articulated train-step grads vs reference: worst error / allowance {worst:.2f}")
+
+
+@pytest.mark.parametrize("loss_scale", [1.0, 1.0 / 64], ids=["64rays", "grad_mag_4096rays"])
+def test_art_train_step_chain(golden, loss_scale):
+    """Teacher-forced: our level-l sample positions through the oracle's autograd; gradients of
+    every MLP parameter and of the three latent codes against the fp32 oracle (the reference's
+    arithmetic), each within max(2 x its own distance from the fp64 oracle, 1e-3) of the
+    tensor's max.  ``loss_scale``
+    1/64 gives the per-row gradient magnitudes of a 4096-ray batch (the mean over 64x more
+    rays)."""
+    from aonerf import train_art
+
+    g = golden("art_train_step.npz")
+    net, lib = _make(0)
+    batch = _batch(g)
+    latents = lib(batch)
+    ret = net(batch, True, True, 2.0, 6.0, latents, u_coarse=cuda(g["u_coarse"]),
+              u_fine=cuda(g["u_fine"]), return_intermediates=True)
+    target = batch["target"]
+    loss = (train_art.img2mse(ret[1][0], target) + train_art.img2mse(ret[0][0], target)) * loss_scale
+    for x in latents.values():
+        x.retain_grad()
+    loss.backward()
+    # the oracle at our sample positions, in fp32 and in fp64: the deformation gradients pass
+    # through pos_enc's sin(2^9 x') (model_autodecoder.py:205-212), so a 1e-7 relative change
+    # of x' moves them by ~1e-3 -- the reference's own fp32 evaluation is that far from fp64
+    ref = {}
+    for dtype in (torch.float32, torch.float64):
+        rays = {k: torch.from_numpy(g[k]).to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
+        params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
+                  for p in O.split_state_dict(W.art_state_dict(0))]
+        lat = {k: v.detach().cpu().to(dtype).requires_grad_(True) for k, v in latents.items()}
+        tgt = torch.from_numpy(g["target"]).to(dtype)
+        ref_loss = 0.0
+        for level in range(2):
+            t = ret[level][3]["t_vals"].cpu().to(dtype)
+            comp, acc, w, depth = O.art_render_level(params, rays, t, level, True, lat)
+            ref_loss = ref_loss + O.img2mse(comp, tgt)
+            np.testing.assert_allclose(ret[level][0].detach().cpu().numpy(), comp.detach().numpy(),
+                                       rtol=0, atol=1e-5)
+        (ref_loss * loss_scale).backward()
+        ref[dtype] = {f"{pre}{n}": v.grad.double().numpy() for lv, pre in ((0, "coarse_mlp."), (1, "fine_mlp."))
+                      for n, v in params[lv].items()}
+        ref[dtype].update({f"latent {k}": v.grad.double().numpy() for k, v in lat.items()})
+    ours = {n: p.grad.cpu().numpy() for n, p in net.named_parameters()}
+    ours.update({f"latent {k}": v.grad.cpu().numpy() for k, v in latents.items()})
+    worst = 0.0
+    for name, want in ref[torch.float32].items():
+        env = rel_err(want, ref[torch.float64][name])
+        e = rel_err(ours[name], want)
+        allow = max(2 * env, 1e-3)
+        if e > 1e-4 or name.startswith("latent"):
+            print(f"  {name:45s} ours {e:.2e}  oracle fp32-vs-fp64 {env:.2e}")
+        worst = max(worst, e / allow)
+        assert e <= allow, (name, e, env)
+    print(f"articulated teacher-forced grads vs fp32 oracle: worst error / allowance {worst:.2f}")
+
+
+def test_art_adam_all_tensors(golden):
+    """configure_optimizers (model_autodecoder.py:599-601): one Adam over the 80 MLP tensors and
+    the 3 embedding tables (two aon_adam_step launches) matches torch.optim.Adam."""
+    from aonerf import train_art
+
+    g = golden("art_train_step.npz")
+    net, lib = _make(0)
+    ref_net, ref_lib = _make(0)
+    opt = train_art.configure_optimizers(net, lib)
+    ref_opt = torch.optim.Adam(list(ref_net.parameters()) + list(ref_lib.parameters()), lr=5e-4,
+                               betas=(0.9, 0.999), foreach=False)
+    assert len(opt.params) == 83
+    kw = dict(u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]))
+    loss, _ = train_art.training_step(net, lib, _batch(g), True, True, 2.0, 6.0, **kw)
+    loss.backward()
+    for p, q in zip(list(net.parameters()) + list(lib.parameters()),
+                    list(ref_net.parameters()) + list(ref_lib.parameters())):
+        q.grad = p.grad.clone()
+    lr = train_art.learning_rate(1, 1000)
+    opt.step(lr=lr)
+    for pg in ref_opt.param_groups:
+        pg["lr"] = lr
+    ref_opt.step()
+    for (name, p), q in zip(list(net.named_parameters()) + list(lib.named_parameters()),
+                            list(ref_net.parameters()) + list(ref_lib.parameters())):
+        d = (p.detach() - q.detach()).abs().max().item()
+        assert d <= 1e-6, (name, d)

@@ -28,3 +28,17 @@ def test_articulated_weights_and_latents_match_oracle():
     for k in lat_o:
         np.testing.assert_array_equal(lat[k].numpy(), lat_o[k])
         assert lat[k].dtype == torch.float32
+
+
+def test_code_library_matches_oracle():
+    import types
+
+    from aonerf.code_library import CodeLibraryArticulated
+    from aonerf.synthetic import init_code_library
+
+    lib = CodeLibraryArticulated(types.SimpleNamespace(N_max_objs=151, N_obj_code_length=128))
+    sd = init_code_library(lib).state_dict()
+    want = W.code_library_state_dict(0)
+    assert set(sd) == set(want)
+    for k in want:
+        np.testing.assert_array_equal(sd[k].numpy(), want[k])

@@ -1,16 +1,20 @@
 #!/usr/bin/env python3
 """Training-step throughput (BASELINE configs C5: LitNeRF.training_step on 4096-ray batches,
 randomized sampling, Adam with the reference schedule; DDP over N GPUs = N independent
-batches + one gradient all-reduce per step, weak scaling).
+batches + one gradient all-reduce per step, weak scaling).  ``--model art`` times the
+articulated auto-decoder's step instead (LitNeRF_AutoDecoder.training_step,
+model_autodecoder.py:395-477: NeRF_AE_Art + CodeLibraryArticulated, latent regulariser, Adam
+over the MLPs and the code tables).
 
-    python tools/bench_train.py [--rays 4096] [--steps 10] [--warmup 3]
+    python tools/bench_train.py [--model vanilla|art] [--rays 4096] [--steps 10] [--warmup 3]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_train.py
 
 A step = draw a batch of pixels of a synthetic 640x480 view (8 poses of create_spheric_poses,
 target image PCG64 seed 3), coarse + fine training forward, loss, HIP backward, gradient
 all-reduce, fused Adam.  Rank 0 prints one JSON line; timing is the max over ranks with barrier
 + synchronize on both sides.  Algorithmic FLOP per step = 3 x the forward MLP FLOP (dX and dW
-each cost one forward) = 3 x 2 x 593,408 x 258 per ray.
+each cost one forward) = 3 x 2 x 593,408 x 258 per ray (articulated: 794,880 MAC per sample,
+latent columns unfolded, as the reference computes them).
 """
 import argparse
 import json
@@ -26,11 +30,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 H, W = 480, 640
-MAC = 593_408
+MAC = {"vanilla": 593_408, "art": 794_880}
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--model", choices=("vanilla", "art"), default="vanilla")
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -51,7 +56,22 @@ def main():
     from aonerf.synthetic import init_like_reference  # same initial weights as bench.py
 
     dev = torch.device("cuda", local_rank)
-    net = init_like_reference(NeRF()).to(dev)
+    art = args.model == "art"
+    if art:
+        import types
+
+        from aonerf import train_art
+        from aonerf.code_library import CodeLibraryArticulated
+        from aonerf.model_autodecoder import NeRF_AE_Art
+        from aonerf.synthetic import init_code_library
+
+        net = init_like_reference(NeRF_AE_Art()).to(dev)
+        lib = init_code_library(CodeLibraryArticulated(
+            types.SimpleNamespace(N_max_objs=151, N_obj_code_length=128))).to(dev)
+        ids = {"instance_id": torch.tensor([7], device=dev),
+               "articulation_id": torch.tensor([3], device=dev)}
+    else:
+        net = init_like_reference(NeRF()).to(dev)
     poses = create_spheric_poses(4.0)
     focal = sapien_focal(H)
     rays_all = {k: [] for k in ("rays_o", "rays_d", "viewdirs")}
@@ -63,15 +83,20 @@ def main():
     rng = np.random.Generator(np.random.PCG64(3))
     target_all = torch.from_numpy(rng.uniform(0, 1, size=(8 * H * W, 3)).astype(np.float32)).to(dev)
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    opt = train.Adam(net.parameters())
-    sync = GradAllReduce(net.parameters())
+    params = list(net.parameters()) + (list(lib.parameters()) if art else [])
+    opt = train.Adam(params)
+    sync = GradAllReduce(params)
 
     def step(i):
         idx = torch.randint(0, 8 * H * W, (args.rays,), device=dev, generator=gen)
         batch = {k: v[idx] for k, v in rays_all.items()}
         batch["target"] = target_all[idx]
         opt.zero_grad()
-        loss, _ = train.training_step(net, batch, True, True, 2.0, 6.0)
+        if art:
+            batch.update(ids)
+            loss, _ = train_art.training_step(net, lib, batch, True, True, 2.0, 6.0)
+        else:
+            loss, _ = train.training_step(net, batch, True, True, 2.0, 6.0)
         loss.backward()
         sync()
         opt.step(lr=train.learning_rate(i, args.max_steps))
@@ -94,14 +119,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     rays = args.rays * args.steps * world
-    flop = 3 * 2 * MAC * (65 + 193) * rays
+    flop = 3 * 2 * MAC[args.model] * (65 + 193) * rays
     if rank == 0:
         print(json.dumps({
-            "metric": "training rays/sec (LitNeRF.training_step, 64c+128f, randomized, Adam)",
+            "metric": ("training rays/sec (LitNeRF_AutoDecoder.training_step, NeRF_AE_Art, 64c+128f, "
+                       "randomized, Adam)" if art else
+                       "training rays/sec (LitNeRF.training_step, 64c+128f, randomized, Adam)"),
             "value": rays / dt, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1000 * dt / args.steps,
             "higher_is_better": True, "scaling": "weak", "dtype": "f16x3 (fp16 hi/lo split MFMA)",
-            "data": "synthetic", "config": {"workload": "C5 training step", "rays_per_rank": args.rays,
+            "data": "synthetic", "config": {"workload": "C5 training step" + (" (articulated)" if art else ""),
+                                             "rays_per_rank": args.rays,
                                              "parallelism": f"ddp{world}"},
             "mlp_tflops_algorithmic": flop / dt / 1e12, "final_loss": float(loss.item())}))
     if world > 1:
