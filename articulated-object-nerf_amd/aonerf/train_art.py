@@ -5,11 +5,13 @@ on the HIP kernels.
 One NeRF_AE_Art level under autograd is ``ArtRenderLevel`` (a torch.autograd.Function) with
 gradients for the level's 40 MLP parameters AND the three latent codes:
 
-  forward   cast_rays -> deformation MLP on cat[xyz, shape, articulation] (4 x GEMM + ReLU,
-            deformation_layer) -> x' = delta + xyz and pos_enc(x') (aon_cast_rays) -> trunk on
-            cat[pos_enc(x'), shape] with the skip concat -> density, bottleneck -> view branch on
-            cat[bottleneck, enc_dir tiled over samples, appearance] -> rgb; every activation kept
-            (model_autodecoder.py:168-239) -> compositing with the padded sigmoid / softplus
+  forward   one fused kernel per level (aon_mlp_art_fwd_train, the inference kernel with
+            activation stores): cast_rays -> deformation MLP on cat[xyz, shape, articulation] ->
+            x' = delta + xyz, pos_enc(x') -> trunk on cat[pos_enc(x'), shape] with the skip
+            concat -> density, bottleneck -> view branch on cat[bottleneck, enc_dir tiled over
+            samples, appearance] -> rgb, every activation, pos_enc(x') and the points kept
+            (model_autodecoder.py:168-239); or the same layer by layer on aon_gemm
+            (FUSED_FORWARD = False) -> compositing with the padded sigmoid / softplus
             (aon_composite_fwd, AON_ACT_ARTIC; :321-333)
   backward  aon_composite_bwd -> per layer, last to first, dW = dZ^T X with db = sum_rows dZ
             from the same pass and dX = (dZ W) * relu'(X) (aon_gemm) -> the trunk's gradient
@@ -125,6 +127,70 @@ def _forward_level(geo, P, lat, xyz, venc, S, raw, noise=None):
     return hd, enc, h, bot, hv
 
 
+# forward of a level under autograd: one fused kernel that also stores the activations
+# (aon_mlp_art_fwd_train) when True, else the layer-by-layer GEMMs of _forward_level
+FUSED_FORWARD = True
+
+_packed = {}
+
+
+def _pack(geo, P, lat):
+    """The fused kernel's fp16x3 weight stream (aon_mlp_art_pack) of one level's parameters with
+    this call's latent codes folded into the biases; re-packed on every call (the optimizer
+    updates the parameters in place)."""
+    shape, app, art = lat
+    dev = shape.device
+    fb = {DEF0: _fold(*P[DEF0], 3, torch.cat([shape, art], -1)),
+          PTS0: _fold(*P[PTS0], geo.ne, shape),
+          PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
+          VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
+    b = lambda i: (fb.get(i, P[i][1])).data_ptr()  # noqa: E731
+    prm = L.AonMlpArtParams()
+    for i in range(4):
+        prm.def_w[i], prm.def_b[i] = P[DEF0 + i][0].data_ptr(), b(DEF0 + i)
+        prm.views_w[i], prm.views_b[i] = P[VIEW0 + i][0].data_ptr(), b(VIEW0 + i)
+    for i in range(8):
+        prm.pts_w[i], prm.pts_b[i] = P[PTS0 + i][0].data_ptr(), b(PTS0 + i)
+    prm.deformation_w, prm.deformation_b = P[DL][0].data_ptr(), b(DL)
+    prm.density_w, prm.density_b = P[DENS][0].data_ptr(), b(DENS)
+    prm.bottleneck_w, prm.bottleneck_b = P[BOT][0].data_ptr(), b(BOT)
+    prm.rgb_w, prm.rgb_b = P[RGB][0].data_ptr(), b(RGB)
+    prm.ld_def0, prm.ld_pts0 = P[DEF0][0].shape[1], P[PTS0][0].shape[1]
+    prm.ld_pts5, prm.ld_view0 = P[PTS0 + 5][0].shape[1], P[VIEW0][0].shape[1]
+    buf = _packed.get(str(dev))
+    if buf is None:
+        buf = torch.empty(L.lib().aon_mlp_art_packed_bytes() // 4, dtype=torch.float32, device=dev)
+        _packed[str(dev)] = buf
+    # the folded biases are stream-ordered before the pack reads them; keep them alive until then
+    L.call("aon_mlp_art_pack", L.ctypes.byref(prm), L.ptr(buf), L.stream(dev))
+    buf._keep = fb
+    return buf
+
+
+def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None):
+    """_forward_level on the fused kernel (aon_mlp_art_fwd_train): raw (R x 4) and the kept
+    activations, plus the sample points and pos_enc(x')."""
+    B, S = t_vals.shape
+    R, dev = B * S, t_vals.device
+    hd = torch.empty((4, R, geo.wd), device=dev)
+    h = torch.empty((8, R, geo.nw), device=dev)
+    bot = torch.empty((R, geo.nw), device=dev)
+    hv = torch.empty((4, R, geo.wc), device=dev)
+    enc = torch.empty((R, geo.ne), device=dev)
+    xyz = torch.empty((R, 3), device=dev)
+    packed = _pack(geo, P, lat)
+    L.call("aon_mlp_art_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
+           L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h),
+           L.ptr(bot), L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.stream(dev))
+    return xyz, hd, enc, h, bot, hv
+
+
+def _fused_ok(geo):
+    # the fused kernel is compiled for the default widths (mlp_layout.hpp kLayersArt)
+    return (geo.wd == 128 and geo.nw == 256 and geo.wc == 128 and geo.ne == 63 and geo.nv == 27
+            and geo.min_deg == 0)
+
+
 def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw):
     """Autograd of _forward_level from dL/draw (R x 4): G[i] = (dW, db) of layer i; dlat =
     (dshape, dapp, dart) (1 x n each) receive the latent-code gradients."""
@@ -237,15 +303,20 @@ class ArtRenderLevel(torch.autograd.Function):
         for p in params:
             if not p.is_contiguous():
                 raise ValueError("MLP parameters must be contiguous")
-        xyz = torch.empty((R, 3), device=dev)
-        L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
-               L.ptr(xyz), 0, 0, None, L.stream(dev))
         venc = torch.empty((B, geo.nv), device=dev)
         L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, geo.deg_view, L.ptr(venc), L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(20)]
         raw = torch.empty((R, 4), device=dev)
         noise = L.contig(noise) if noise is not None else None
-        hd, enc, h, bot, hv = _forward_level(geo, P, lat, xyz, venc, S, raw, noise)
+        if FUSED_FORWARD and _fused_ok(geo):
+            xyz, hd, enc, h, bot, hv = _forward_level_fused(
+                geo, P, lat, L.contig(rays_o), L.contig(rays_d), L.contig(viewdirs),
+                L.contig(t_vals), raw, noise)
+        else:
+            xyz = torch.empty((R, 3), device=dev)
+            L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
+                   L.ptr(xyz), 0, 0, None, L.stream(dev))
+            hd, enc, h, bot, hv = _forward_level(geo, P, lat, xyz, venc, S, raw, noise)
         comp = torch.empty((B, 3), device=dev)
         acc = torch.empty((B,), device=dev)
         weights = torch.empty((B, S), device=dev)

@@ -19,12 +19,14 @@
 namespace aon {
 namespace mlp {
 
-// MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: points (N, 3), condition (B, 27)
-template <int MODE, int NCOL>
+// MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: points (N, 3), condition (B, 27).
+// STORE: the training forward -- every layer's activations, the encodings of x' and the
+// sample points are kept for the backward (TrainStoreArt), raw_sigma gets the noise.
+template <int MODE, int NCOL, bool STORE = false>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_art_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
-    int64_t B, int S, int act, float* __restrict__ raw) {
+    int64_t B, int S, int act, float* __restrict__ raw, TrainStoreArt ts = {}) {
   using G = GeomH<NCOL>;
   using Net = NetArtH;
   constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
@@ -76,6 +78,10 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
         vv[e] = f < 27 ? cd[f] : 0.f;
       }
     }
+    if (STORE && g == 0 && row < N) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) ts.xyz[3 * row + q] = px[c][q];
+    }
     float dv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? px[c][e < 3 ? e : 0] * kActS : 0.f;
@@ -93,11 +99,13 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 
   Frag<8, NCOL> x, y;
   Frag<1, NCOL> none;
+  using SP = StorePick<STORE, NCOL>;
+  const int64_t hds = N * 128, hs = N * 256;  // one deformation / pts_linears output
   // deformation MLP (model_autodecoder.py:196-205)
-  layer_h<Net, A_D0, true>(fp, none, din, x, bias_l, g);
-  layer_h<Net, A_D1, true>(fp, x, none, y, bias_l, g);
-  layer_h<Net, A_D2, true>(fp, y, none, x, bias_l, g);
-  layer_h<Net, A_D3, true>(fp, x, none, y, bias_l, g);
+  layer_h<Net, A_D0, true>(fp, none, din, x, bias_l, g, SP::make(ts.hd, 128, rows, N, g));
+  layer_h<Net, A_D1, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + hds, 128, rows, N, g));
+  layer_h<Net, A_D2, true>(fp, y, none, x, bias_l, g, SP::make(ts.hd + 2 * hds, 128, rows, N, g));
+  layer_h<Net, A_D3, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + 3 * hds, 128, rows, N, g));
   f4 dlt[NCOL];
   head_h<Net, A_DOUT>(fp, y, dlt, bias_l, g);
 
@@ -112,8 +120,11 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        ev[k][e] = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10) * kActS;
+      for (int e = 0; e < 8; ++e) {
+        const float f = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10);
+        if (STORE && rows[c] < N && 32 * k + 8 * g + e < 63) ts.enc[63 * rows[c] + 32 * k + 8 * g + e] = f;
+        ev[k][e] = f * kActS;
+      }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       split8(ev[k], enc.hi[k][c], enc.lo[k][c]);
@@ -123,11 +134,11 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   }
 
   // trunk on cat[enc, shape] (:214-220), shape folded into the pts_linears.0 / .5 biases
-  layer_h<Net, A_P0, true>(fp, none, enc, x, bias_l, g);
-  layer_h<Net, A_P1, true>(fp, x, none, y, bias_l, g);
-  layer_h<Net, A_P2, true>(fp, y, none, x, bias_l, g);
-  layer_h<Net, A_P3, true>(fp, x, none, y, bias_l, g);
-  layer_h<Net, A_P4, true>(fp, y, none, x, bias_l, g);
+  layer_h<Net, A_P0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g));
+  layer_h<Net, A_P1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + hs, 256, rows, N, g));
+  layer_h<Net, A_P2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g));
+  layer_h<Net, A_P3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g));
+  layer_h<Net, A_P4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c)
 #pragma unroll
@@ -135,30 +146,34 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
       enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
     }
-  layer_h<Net, A_P5, true>(fp, x, enc, y, bias_l, g);  // skip: cat[h, enc, shape]
-  layer_h<Net, A_P6, true>(fp, y, none, x, bias_l, g);
-  layer_h<Net, A_P7, true>(fp, x, none, y, bias_l, g);
+  // skip: cat[h, enc, shape]
+  layer_h<Net, A_P5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g));
+  layer_h<Net, A_P6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g));
+  layer_h<Net, A_P7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g));
   f4 dens[NCOL], rgb[NCOL];
-  head_h<Net, A_DEN>(fp, y, dens, bias_l, g);             // :221-223
-  layer_h<Net, A_BOT, false>(fp, y, none, x, bias_l, g);  // bottleneck, no activation (:225)
+  head_h<Net, A_DEN>(fp, y, dens, bias_l, g);  // :221-223
+  // bottleneck, no activation (:225)
+  layer_h<Net, A_BOT, false>(fp, y, none, x, bias_l, g, SP::make(ts.bot, 256, rows, N, g));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
     venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
     venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
   }
   // view branch on cat[bottleneck, enc_dir, appearance] (:226-235)
-  layer_h<Net, A_V0, true>(fp, x, venc, y, bias_l, g);
-  layer_h<Net, A_V1, true>(fp, y, none, x, bias_l, g);
-  layer_h<Net, A_V2, true>(fp, x, none, y, bias_l, g);
-  layer_h<Net, A_V3, true>(fp, y, none, x, bias_l, g);
+  layer_h<Net, A_V0, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g));
+  layer_h<Net, A_V1, true>(fp, y, none, x, bias_l, g, SP::make(ts.hv + hds, 128, rows, N, g));
+  layer_h<Net, A_V2, true>(fp, x, none, y, bias_l, g, SP::make(ts.hv + 2 * hds, 128, rows, N, g));
+  layer_h<Net, A_V3, true>(fp, y, none, x, bias_l, g, SP::make(ts.hv + 3 * hds, 128, rows, N, g));
   head_h<Net, A_RGB>(fp, x, rgb, bias_l, g);  // :237
 
   if (g == 0) {
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
       if (rows[c] < N) {
+        float sig = dens[c][0];
+        if (STORE && ts.noise) sig = __fadd_rn(sig, ts.noise[rows[c]]);  // :318-319
         const f4 o = {act_rgb(rgb[c][0], act), act_rgb(rgb[c][1], act), act_rgb(rgb[c][2], act),
-                      act_sigma(dens[c][0], act)};
+                      act_sigma(sig, act)};
         *reinterpret_cast<f4*>(raw + 4 * rows[c]) = o;
       }
     }
@@ -238,6 +253,33 @@ extern "C" int aon_mlp_art_fwd(const void* packed, const float* rays_o, const fl
                                float* out, aon_stream_t stream) {
   AON_REQUIRE(viewdirs && t, "null pointer");
   return art_launch(0, packed, rays_o, rays_d, viewdirs, t, B, S, act, out, stream);
+}
+
+extern "C" int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
+                                     const float* viewdirs, const float* t, int64_t B, int S,
+                                     const float* noise, float* hd, float* h, float* bot,
+                                     float* hv, float* enc, float* xyz, float* raw,
+                                     aon_stream_t stream) {
+  AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && raw, "null pointer");
+  AON_REQUIRE(hd && h && bot && hv && enc && xyz, "null activation buffer");
+  AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
+  AON_REQUIRE(aligned16(packed) && aligned16(raw), "packed / raw must be 16-byte aligned");
+  AON_REQUIRE(((reinterpret_cast<uintptr_t>(hd) | reinterpret_cast<uintptr_t>(h) |
+                reinterpret_cast<uintptr_t>(bot) | reinterpret_cast<uintptr_t>(hv)) & 7) == 0,
+              "activation buffers must be 8-byte aligned");
+  const int64_t N = B * S;
+  if (N == 0) return 0;
+  using G = GeomH<1>;
+  const int64_t grid = (N + G::kRowsPerBlock - 1) / G::kRowsPerBlock;
+  AON_REQUIRE(grid < (1ll << 31), "too many rows");
+  const f4* ws = static_cast<const f4*>(packed);
+  const float* bias =
+      reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
+  const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise};
+  hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true>), (unsigned)grid, G::kThreads, 0,
+                     (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
+                     (int)AON_ACT_NONE, raw, ts);
+  return launch_status(__func__);
 }
 
 extern "C" int aon_mlp_art_fwd_points(const void* packed, const float* pos,

@@ -19,26 +19,6 @@
 namespace aon {
 namespace mlp {
 
-template <bool STORE, int NCOL>
-struct StorePick {
-  __device__ __forceinline__ static NoStore make(float*, int, const int64_t (&)[NCOL], int64_t,
-                                                 int) {
-    return {};
-  }
-};
-template <int NCOL>
-struct StorePick<true, NCOL> {
-  __device__ __forceinline__ static RowStore<NCOL> make(float* base, int ld,
-                                                        const int64_t (&rows)[NCOL], int64_t N,
-                                                        int g) {
-    RowStore<NCOL> r;
-#pragma unroll
-    for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + rows[c] * ld + 4 * g : nullptr;
-    r.s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;
-    return r;
-  }
-};
-
 // MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: encoded x (N, 63), condition (B, 27)
 template <int MODE, int NCOL, bool STORE = false>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_fwd_f16x3(

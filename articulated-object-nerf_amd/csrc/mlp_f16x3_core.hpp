@@ -147,6 +147,27 @@ struct MaskStore {
   }
 };
 
+// NoStore (STORE = false) or a RowStore at y + row * ld (true scale) for the training forward
+template <bool STORE, int NCOL>
+struct StorePick {
+  __device__ __forceinline__ static NoStore make(float*, int, const int64_t (&)[NCOL], int64_t,
+                                                 int) {
+    return {};
+  }
+};
+template <int NCOL>
+struct StorePick<true, NCOL> {
+  __device__ __forceinline__ static RowStore<NCOL> make(float* base, int ld,
+                                                        const int64_t (&rows)[NCOL], int64_t N,
+                                                        int g) {
+    RowStore<NCOL> r;
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + rows[c] * ld + 4 * g : nullptr;
+    r.s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;
+    return r;
+  }
+};
+
 // epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
 // part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
 template <bool RELU, int NCOL, int NO, typename Store = NoStore>

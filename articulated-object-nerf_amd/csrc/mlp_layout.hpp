@@ -228,6 +228,17 @@ struct TrainStore {
   const float* noise;
 };
 
+// activations the articulated training forward keeps (aon_mlp_art_fwd_train)
+struct TrainStoreArt {
+  float* hd;    // (4, N, 128) deformation layers
+  float* h;     // (8, N, 256) pts_linears
+  float* bot;   // (N, 256)
+  float* hv;    // (4, N, 128) views_linear
+  float* enc;   // (N, 63) pos_enc(x'); enc[:, :3] = x'
+  float* xyz;   // (N, 3) the sample points (deformation input)
+  const float* noise;  // (N) added to raw_sigma, or nullptr
+};
+
 // fp16x3 path (mlp_f16x3.hip)
 int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream);
 int pack_h(PackArgsH a, void* packed, hipStream_t stream);

@@ -204,6 +204,17 @@ int aon_mlp_art_pack(const aon_mlp_art_params* params, void* packed, aon_stream_
 int aon_mlp_art_fwd(const void* packed, const float* rays_o, const float* rays_d,
                     const float* viewdirs, const float* t, int64_t B, int S, int act, float* out,
                     aon_stream_t stream);
+/* Training forward of one articulated level (reference model_autodecoder.py:168-239 under
+ * autograd): aon_mlp_art_fwd (MODE 0 inputs, raw outputs, no activation) that also keeps what
+ * the backward needs -- hd (4, B*S, 128) deformation layers, h (8, B*S, 256) pts_linears, bot
+ * (B*S, 256), hv (4, B*S, 128) views_linear, enc (B*S, 63) = pos_enc(x') and xyz (B*S, 3) the
+ * sample points; raw_sigma += noise[r] when noise != NULL (:318-319).  Activation buffers 8-byte
+ * aligned, raw 16-byte aligned. */
+int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
+                          const float* viewdirs, const float* t, int64_t B, int S,
+                          const float* noise, float* hd, float* h, float* bot, float* hv,
+                          float* enc, float* xyz, float* raw, aon_stream_t stream);
+
 /* The same on given sample points pos (B*S, 3) and encoded view directions condition (B, 27)
  * (NeRFMLP.forward(pos, condition, latents)). */
 int aon_mlp_art_fwd_points(const void* packed, const float* pos, const float* condition,

@@ -70,6 +70,60 @@ def test_latent_reg():
         np.testing.assert_allclose(c.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-6, atol=0)
 
 
+@pytest.fixture(params=[True, False], ids=["fused_fwd", "gemm_fwd"])
+def art_fwd_mode(request):
+    """Articulated training forward on the fused kernel with activation stores
+    (aon_mlp_art_fwd_train) or layer by layer on aon_gemm."""
+    from aonerf import train_art
+
+    old = train_art.FUSED_FORWARD
+    train_art.FUSED_FORWARD = request.param
+    yield request.param
+    train_art.FUSED_FORWARD = old
+
+
+def test_fused_art_train_forward_activations():
+    """aon_mlp_art_fwd_train's kept tensors and raw outputs (with noise) against the
+    layer-by-layer GEMM forward on a ragged batch: the points bit-exact, the deformation layers
+    ~1e-6 of each tensor's range (both f16x3), pos_enc(x') and the layers after it within the
+    sin(2^9 x') amplification of that (measured ~4e-5)."""
+    from aonerf import train_art
+    from aonerf import _lib as L
+
+    net, _ = _make(0)
+    mlp = net.fine_mlp
+    geo = train_art._Geo(mlp)
+    gen = torch.Generator().manual_seed(4)
+    B, S = 37, 65
+    o = (torch.rand(B, 3, generator=gen) - 0.5).cuda()
+    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=gen), dim=-1).cuda()
+    t = (2.0 + 4.0 * torch.rand(B, S, generator=gen)).sort(-1).values.cuda()
+    noise = torch.rand(B * S, generator=gen).cuda()
+    lat = tuple(cuda(v) for v in W.art_latents(1).values())
+    P = [(m.weight.detach(), m.bias.detach()) for m in train_art.art_layers(mlp)]
+    raw_f = torch.empty((B * S, 4), device="cuda")
+    xyz_f, hd_f, enc_f, h_f, bot_f, hv_f = train_art._forward_level_fused(geo, P, lat, o, d, d, t,
+                                                                         raw_f, noise)
+    xyz = torch.empty((B * S, 3), device="cuda")
+    L.call("aon_cast_rays", L.ptr(o), L.ptr(d), L.ptr(t), B, S, None, 0, L.ptr(xyz), 0, 0, None,
+           L.stream())
+    venc = torch.empty((B, 27), device="cuda")
+    L.call("aon_pos_enc", L.ptr(d), B, 0, 4, L.ptr(venc), L.stream())
+    raw_g = torch.empty((B * S, 4), device="cuda")
+    hd_g, enc_g, h_g, bot_g, hv_g = train_art._forward_level(geo, P, lat, xyz, venc, S, raw_g, noise)
+    np.testing.assert_array_equal(xyz_f.cpu().numpy(), xyz.cpu().numpy())
+    pairs = ([(f"hd{i}", hd_f[i], hd_g[i]) for i in range(4)] + [("enc", enc_f, enc_g)]
+             + [(f"h{i}", h_f[i], h_g[i]) for i in range(8)]
+             + [("bot", bot_f, bot_g)] + [(f"hv{i}", hv_f[i], hv_g[i]) for i in range(4)]
+             + [("raw", raw_f, raw_g)])
+    for name, a, b in pairs:
+        e = rel_err(a.cpu().numpy(), b.cpu().numpy())
+        print(f"  fused vs gemm forward {name}: max rel err {e:.2e}")
+        # enc carries sin(2^9 x'): a 1e-7 change of x' (the two deformation evaluations differ
+        # by that) moves it by ~1e-4, and everything after it inherits that
+        assert e < (2e-5 if name.startswith("hd") else 5e-4), name
+
+
 def _make(seed=0):
     import types
 
@@ -114,7 +168,7 @@ def _named_grad(net, lib, name, g):
     return dict(net.named_parameters())[name].grad.cpu().numpy()
 
 
-def test_art_train_step_golden(golden):
+def test_art_train_step_golden(golden, art_fwd_mode):
     """Loss (incl. the latent regulariser) and the recorded gradients of one
     LitNeRF_AutoDecoder.training_step (randomized, injected uniforms) vs the reference."""
     from aonerf import train_art
@@ -155,7 +209,7 @@ def test_art_train_step_golden(golden):
 
 
 @pytest.mark.parametrize("loss_scale", [1.0, 1.0 / 64], ids=["64rays", "grad_mag_4096rays"])
-def test_art_train_step_chain(golden, loss_scale):
+def test_art_train_step_chain(golden, art_fwd_mode, loss_scale):
     """Teacher-forced: our level-l sample positions through the oracle's autograd; gradients of
     every MLP parameter and of the three latent codes against the fp32 oracle (the reference's
     arithmetic), each within max(2 x its own distance from the fp64 oracle, 1e-3) of the
