@@ -72,6 +72,9 @@ _SIGNATURES = {
     "aon_mlp_art_pack": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
     "aon_mlp_art_fwd": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_art_fwd_points": (c_int, [vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
+    "aon_mlp_art_bwd_packed_bytes": (c_size, []),
+    "aon_mlp_art_bwd_pack": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
+    "aon_mlp_art_bwd": (c_int, [vp, vp, vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp, vp, vp]),
     "aon_mlp_art_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp,
                                       vp, vp]),
     "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,

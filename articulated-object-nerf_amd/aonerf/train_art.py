@@ -13,10 +13,11 @@ gradients for the level's 40 MLP parameters AND the three latent codes:
             (model_autodecoder.py:168-239); or the same layer by layer on aon_gemm
             (FUSED_FORWARD = False) -> compositing with the padded sigmoid / softplus
             (aon_composite_fwd, AON_ACT_ARTIC; :321-333)
-  backward  aon_composite_bwd -> per layer, last to first, dW = dZ^T X with db = sum_rows dZ
-            from the same pass and dX = (dZ W) * relu'(X) (aon_gemm) -> the trunk's gradient
-            w.r.t. pos_enc(x') (skip + first layer) through aon_pos_enc_bwd into the
-            deformation MLP.
+  backward  aon_composite_bwd -> every input gradient dX = (dZ W) * relu'(X) in one fused
+            kernel (aon_mlp_art_bwd): view branch, heads, trunk, the gradient w.r.t.
+            pos_enc(x') (skip + first layer) through pos_enc's backward into the deformation
+            head and MLP -> per layer dW = dZ^T X with db = sum_rows dZ from the same pass
+            (aon_gemm); or the whole chain as GEMMs + aon_pos_enc_bwd (FUSED_BACKWARD = False).
 
 The latent codes are the same row for every sample (repeated over B*S rows,
 model_autodecoder.py:186-194), so their columns are folded into per-call biases in the
@@ -130,20 +131,16 @@ def _forward_level(geo, P, lat, xyz, venc, S, raw, noise=None):
 # forward of a level under autograd: one fused kernel that also stores the activations
 # (aon_mlp_art_fwd_train) when True, else the layer-by-layer GEMMs of _forward_level
 FUSED_FORWARD = True
+# backward of a level: every input gradient in one fused kernel (aon_mlp_art_bwd) + the
+# weight-gradient GEMMs when True, else every product as a GEMM (_backward_level)
+FUSED_BACKWARD = True
 
 _packed = {}
 
 
-def _pack(geo, P, lat):
-    """The fused kernel's fp16x3 weight stream (aon_mlp_art_pack) of one level's parameters with
-    this call's latent codes folded into the biases; re-packed on every call (the optimizer
-    updates the parameters in place)."""
-    shape, app, art = lat
-    dev = shape.device
-    fb = {DEF0: _fold(*P[DEF0], 3, torch.cat([shape, art], -1)),
-          PTS0: _fold(*P[PTS0], geo.ne, shape),
-          PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
-          VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
+def _params_struct(P, fb=None):
+    """AonMlpArtParams of one level's parameters (``fb``: folded biases by layer index)."""
+    fb = fb or {}
     b = lambda i: (fb.get(i, P[i][1])).data_ptr()  # noqa: E731
     prm = L.AonMlpArtParams()
     for i in range(4):
@@ -157,13 +154,37 @@ def _pack(geo, P, lat):
     prm.rgb_w, prm.rgb_b = P[RGB][0].data_ptr(), b(RGB)
     prm.ld_def0, prm.ld_pts0 = P[DEF0][0].shape[1], P[PTS0][0].shape[1]
     prm.ld_pts5, prm.ld_view0 = P[PTS0 + 5][0].shape[1], P[VIEW0][0].shape[1]
-    buf = _packed.get(str(dev))
+    return prm
+
+
+def _buffer(key, nbytes, dev):
+    # one buffer per kind and device: a pack and the kernel reading it are stream-ordered
+    buf = _packed.get((key, str(dev)))
     if buf is None:
-        buf = torch.empty(L.lib().aon_mlp_art_packed_bytes() // 4, dtype=torch.float32, device=dev)
-        _packed[str(dev)] = buf
-    # the folded biases are stream-ordered before the pack reads them; keep them alive until then
-    L.call("aon_mlp_art_pack", L.ctypes.byref(prm), L.ptr(buf), L.stream(dev))
-    buf._keep = fb
+        buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
+        _packed[(key, str(dev))] = buf
+    return buf
+
+
+def _pack(geo, P, lat):
+    """The fused kernel's fp16x3 weight stream (aon_mlp_art_pack) of one level's parameters with
+    this call's latent codes folded into the biases; re-packed on every call (the optimizer
+    updates the parameters in place)."""
+    shape, app, art = lat
+    dev = shape.device
+    fb = {DEF0: _fold(*P[DEF0], 3, torch.cat([shape, art], -1)),
+          PTS0: _fold(*P[PTS0], geo.ne, shape),
+          PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
+          VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
+    buf = _buffer("fwd", L.lib().aon_mlp_art_packed_bytes(), dev)
+    L.call("aon_mlp_art_pack", L.ctypes.byref(_params_struct(P, fb)), L.ptr(buf), L.stream(dev))
+    return buf
+
+
+def _pack_bwd(P, dev):
+    """The transposed weight stream of the fused backward chain (aon_mlp_art_bwd_pack)."""
+    buf = _buffer("bwd", L.lib().aon_mlp_art_bwd_packed_bytes(), dev)
+    L.call("aon_mlp_art_bwd_pack", L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
     return buf
 
 
@@ -286,6 +307,62 @@ def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, dra
     dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
 
 
+def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw):
+    """_backward_level with every input-gradient product (and pos_enc's backward) in one fused
+    kernel (aon_mlp_art_bwd); the weight gradients dW = dZ^T X, db = sum_rows dZ and the latent
+    terms stay GEMMs."""
+    R, dev = xyz.shape[0], xyz.device
+    wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
+    shape, app, art = lat
+    dshape, dapp, dart = dlat
+    dzv = torch.empty((4, R, wc), device=dev)
+    dbot = torch.empty((R, nw), device=dev)
+    dz = torch.empty((8, R, nw), device=dev)
+    dxp = torch.empty((R, 3), device=dev)
+    dzd = torch.empty((4, R, wd), device=dev)
+    work = _buffer("work", 4, dev)
+    L.call("aon_mlp_art_bwd", L.ptr(_pack_bwd(P, dev)), L.ptr(draw), L.ptr(hd), L.ptr(h),
+           L.ptr(hv), L.ptr(enc), R, L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd),
+           L.ptr(work), L.stream(dev))
+    gs, acts = GRAD_SCALE, ACT_SCALE
+
+    def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True):
+        dW = G[i][0]
+        gemm(dW[:, col0:] if col0 else dW, dY, X, dW.shape[0], n_in, R, lda=ldy, a_kc=False,
+             ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0), a_scale=gs, b_scale=acts,
+             rowsum=G[i][1] if bias else None)
+
+    def dlatent(i, col0, l, dl, accumulate):
+        dW, db = G[i]
+        W = P[i][0]
+        n_out, n = W.shape[0], l.shape[1]
+        gemm(dW[:, col0:], db, l, n_out, n, 1, lda=1, a_kc=True, ldb=n, b_kc=False,
+             ldc=dW.stride(0), a_scale=gs, b_scale=1.0)
+        gemm(dl, db, W[:, col0:], 1, n, n_out, lda=n_out, a_kc=True, ldb=W.stride(0), b_kc=False,
+             ldc=n, accumulate=accumulate, a_scale=gs, b_scale=W_SCALE)
+
+    dweight(RGB, draw, 4, hv[3], wc, wc)                                  # rgb_layer
+    for i in range(3, 0, -1):                                             # views_linear.i
+        dweight(VIEW0 + i, dzv[i], wc, hv[i - 1], wc, wc)
+    dweight(VIEW0, dzv[0], wc, bot, nw, nw)                               # views_linear.0
+    dweight(VIEW0, dzv[0], wc, venc, nv, nv, col0=nw, rdiv=S, bias=False)
+    dlatent(VIEW0, nw + nv, app, dapp, False)
+    dweight(BOT, dbot, nw, h[7], nw, nw)                                  # bottleneck
+    dweight(DENS, draw[:, 3:], 4, h[7], nw, nw)                           # density
+    for i in range(7, 0, -1):                                             # pts_linears.i
+        dweight(PTS0 + i, dz[i], nw, h[i - 1], nw, nw)
+    dweight(PTS0 + 5, dz[5], nw, enc, ne, ne, col0=nw, bias=False)
+    dlatent(PTS0 + 5, nw + ne, shape, dshape, False)
+    dweight(PTS0, dz[0], nw, enc, ne, ne)                                 # pts_linears.0
+    dlatent(PTS0, ne, shape, dshape, True)
+    dweight(DL, dxp, 3, hd[3], wd, wd)                                    # deformation_layer
+    for i in range(3, 0, -1):                                             # deformations_linear.i
+        dweight(DEF0 + i, dzd[i], wd, hd[i - 1], wd, wd)
+    dweight(DEF0, dzd[0], wd, xyz, 3, 3)                                  # deformations_linear.0
+    dlatent(DEF0, 3, shape, dshape, True)
+    dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
+
+
 class ArtRenderLevel(torch.autograd.Function):
     """cast_rays + articulated NeRFMLP + activations + volumetric_rendering of one level
     (model_autodecoder.py:296-333) with gradients for the level's 40 MLP parameters and the
@@ -347,7 +424,10 @@ class ArtRenderLevel(torch.autograd.Function):
         P = [(params[2 * i], params[2 * i + 1]) for i in range(20)]
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
         dlat = tuple(torch.empty_like(x) for x in lat)
-        _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
+        if FUSED_BACKWARD and _fused_ok(geo):
+            _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
+        else:
+            _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
         dlat = [d.reshape(s) for d, s in zip(dlat, lat_shapes)]
         return (None, None, None, None, None, None, None, *dlat, *grads)

@@ -1,0 +1,288 @@
+// Fused backward chain of the articulated NeRFMLP for the training step (reference
+// models/vanilla_nerf/model_autodecoder.py:168-239 under autograd, LitNeRF_AutoDecoder.training_step
+// :395-477): from dL/d raw (the compositor's backward) through the view branch, the heads and
+// the trunk to dL/d pos_enc(x'), through pos_enc's backward (helper.py:136-140) to dL/dx', then
+// through the deformation head and the deformation MLP -- every input-gradient product
+// dX = dZ W in ONE kernel, each masked by ReLU' of the forward output it flows into, every dZ
+// stored for the weight-gradient GEMMs (dW = dZ^T X, train_art.py).
+//
+// Structure and numerics as mlp_bwd.hip (the vanilla chain): feature-major MFMA tiles, W^T
+// streamed through the LDS-DMA ring (kLayersArtBwd, packed from the forward weights with tr = 1),
+// each finished output pair converted in registers into the next layer's B fragments, gradients
+// at a per-call power-of-two scale s from max |d raw|.  The enc columns of the skip layer give
+// 64 values per sample, parked lane-private in LDS; those of pts_linears.0 join them in the
+// epilogue, where pos_enc's backward runs on the fly -- sin' = cos at the forward's fp32
+// arguments (x' 2^d and x' 2^d + pi/2f), summed over degrees -- and the four lane groups of a
+// sample are reduced with two shuffles.  dL/dx' then re-enters fp16 at a per-sample power-of-two
+// scale (it carries the 2^9 factors of pos_enc's top degree).
+#include "mlp_f16x3_core.hpp"
+
+namespace aon {
+namespace mlp {
+
+struct ArtBwdArgs {
+  const float* draw;       // (N, 4): d raw_rgb (3), d raw_sigma
+  const float* hd;         // (4, N, 128) post-ReLU deformations_linear.i outputs
+  const float* h;          // (8, N, 256) post-ReLU pts_linears.i outputs
+  const float* hv;         // (4, N, 128) post-ReLU views_linear.i outputs
+  const float* enc;        // (N, 63) pos_enc(x'), enc[:, :3] = x'
+  float* dzv;              // (4, N, 128): dL/d pre-activation of views_linear.i
+  float* dbot;             // (N, 256): dL/d bottleneck output
+  float* dz;               // (8, N, 256): dL/d pre-activation of pts_linears.i
+  float* dxp;              // (N, 3): dL/dx' = dL/d deformation_layer output
+  float* dzd;              // (4, N, 128): dL/d pre-activation of deformations_linear.i
+  const uint32_t* absmax;  // bits of max |draw|
+  int64_t N;
+};
+
+// Epilogue policy of the skip layer's enc columns: park each value (scale s) in this lane's LDS
+// slots [tile][reg]; nothing goes to the output fragments' consumer.
+struct EncStash {
+  float* slot;  // lane-private: float index (t * 64) * 4 + r of the lane's f4 slot t
+  __device__ __forceinline__ void begin_pair(int) const {}
+  __device__ __forceinline__ float post(int pr, int uu, int r, int, float v) const {
+    slot[(2 * pr + uu) * 256 + r] = v;
+    return v;
+  }
+  __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
+};
+
+// Epilogue policy of pts_linears.0's enc columns: total d enc_f = this value + the parked skip
+// value, then pos_enc's backward accumulated per x' component (feature f = 16 t + 4 g + r):
+// f < 3 identity; 3 <= f < 33 sin(x_c 2^d); 33 <= f < 63 sin(x_c 2^d + pi/2f), (f - 3) mod 30 =
+// 3 d + c.
+struct EncBwd {
+  const float* slot;
+  float x0, x1, x2;  // x' of this lane's sample
+  int g;
+  mutable float dx0 = 0.f, dx1 = 0.f, dx2 = 0.f;
+  __device__ __forceinline__ void begin_pair(int) const {}
+  __device__ __forceinline__ float post(int pr, int uu, int r, int, float v) const {
+    const int t = 2 * pr + uu;
+    const float tot = __fadd_rn(slot[t * 256 + r], v);
+    const int f = 16 * t + 4 * g + r;
+    float a = 0.f;
+    int comp;
+    if (f < 3) {
+      a = tot;
+      comp = f;
+    } else if (f < 63) {
+      const bool cosine = f >= 33;
+      const int q = cosine ? f - 33 : f - 3;
+      const int d = q / 3;
+      comp = q - 3 * d;
+      const float sc = __builtin_ldexpf(1.0f, d);
+      const float xc = comp == 0 ? x0 : (comp == 1 ? x1 : x2);
+      const float xb = __fmul_rn(xc, sc);  // exact
+      a = __fmul_rn(__fmul_rn(tot, cosf(cosine ? __fadd_rn(xb, kHalfPi) : xb)), sc);
+    } else {
+      comp = 3;  // padding row
+    }
+    dx0 = comp == 0 ? __fadd_rn(dx0, a) : dx0;
+    dx1 = comp == 1 ? __fadd_rn(dx1, a) : dx1;
+    dx2 = comp == 2 ? __fadd_rn(dx2, a) : dx2;
+    return v;
+  }
+  __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
+};
+
+__global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
+    const f4* __restrict__ wstream, const float* __restrict__ bias_g, ArtBwdArgs a) {
+  constexpr int NCOL = 1;
+  using G = GeomH<NCOL>;
+  using Net = NetArtBwdH;
+  // per lane: d raw_sigma fragment (hi, lo) + 4 f4 of parked skip-enc gradients
+  constexpr int kSlots = 6;
+  __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + G::kWaves * 64 * kSlots];
+  float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
+  f4* stash = smem + kLdsWeights + Net::kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * kSlots +
+              (threadIdx.x & 63);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int64_t N = a.N;
+
+  WeightPipe<Net, G::kThreads> p;
+  p.wbuf = smem;
+  p.src = wstream;
+  p.tid = tid;
+  p.lane = lane;
+  p.start();
+  for (int i = tid; i < Net::kBiasFloats; i += G::kThreads) bias_s[i] = bias_g[i];
+
+  const float s = grad_scale(*a.absmax);
+  const float inv = 1.0f / s;  // exact: a power of two
+
+  Frag<1, NCOL> drgb, dsig;
+  int64_t rows[NCOL];
+  const int64_t row = (int64_t)blockIdx.x * G::kRowsPerBlock + wave * G::kRowsPerWave + j;
+  rows[0] = row;
+  const int64_t rr = row < N ? row : N - 1;
+  {
+    const f4 d = *reinterpret_cast<const f4*>(a.draw + 4 * rr);
+    float dv[8], sv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      dv[e] = (g == 0 && e < 3) ? d[e < 3 ? e : 0] * s : 0.f;
+      sv[e] = (g == 0 && e == 0) ? d[3] * s : 0.f;
+    }
+    split8(dv, drgb.hi[0][0], drgb.lo[0][0]);
+    split8(sv, dsig.hi[0][0], dsig.lo[0][0]);
+    stash[0] = __builtin_bit_cast(f4, dsig.hi[0][0]);
+    stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
+  }
+
+  FragPipe<WeightPipe<Net, G::kThreads>> fp(p);
+  fp.start();
+  lds_float* bias_l = opaque_lds(bias_s + 4 * g);
+
+  const int64_t hs = N * 256, ws = N * 128;
+  Frag<8, NCOL> x, y;
+  Frag<2, NCOL> junk;  // output fragments of the enc-column layers (consumed in the epilogue)
+  Frag<1, NCOL> none;
+  // view branch: d hv3 = W_rgb^T d rgb, then views_linear.3 .. 1, each * ReLU'
+  layer_h<Net, AB_RGB, false>(fp, none, drgb, x, bias_l, g,
+                              mask_store(a.hv + 3 * ws, 128, a.dzv + 3 * ws, 128, rows, N, g, inv));
+  layer_h<Net, AB_V3, false>(fp, x, none, y, bias_l, g,
+                             mask_store(a.hv + 2 * ws, 128, a.dzv + 2 * ws, 128, rows, N, g, inv));
+  layer_h<Net, AB_V2, false>(fp, y, none, x, bias_l, g,
+                             mask_store(a.hv + 1 * ws, 128, a.dzv + 1 * ws, 128, rows, N, g, inv));
+  layer_h<Net, AB_V1, false>(fp, x, none, y, bias_l, g,
+                             mask_store(a.hv, 128, a.dzv, 128, rows, N, g, inv));
+  // d bottleneck = W_view0[:, :256]^T dZ_view0 (linear layer: no mask)
+  {
+    RowStore<NCOL> st;
+    st.rowp[0] = row < N ? a.dbot + row * 256 + 4 * g : nullptr;
+    st.s = inv;
+    layer_h<Net, AB_V0, false>(fp, y, none, x, bias_l, g, st);
+  }
+  dsig.hi[0][0] = __builtin_bit_cast(h8, stash[0]);
+  dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
+  // d h7 = W_bot^T d bottleneck + W_den^T d sigma, * ReLU'(h7) -> dZ_7
+  layer_h<Net, AB_BOTDEN, false>(fp, x, dsig, y, bias_l, g,
+                                 mask_store(a.h + 7 * hs, 256, a.dz + 7 * hs, 256, rows, N, g, inv));
+  layer_h<Net, AB_P7, false>(fp, y, none, x, bias_l, g,
+                             mask_store(a.h + 6 * hs, 256, a.dz + 6 * hs, 256, rows, N, g, inv));
+  layer_h<Net, AB_P6, false>(fp, x, none, y, bias_l, g,
+                             mask_store(a.h + 5 * hs, 256, a.dz + 5 * hs, 256, rows, N, g, inv));
+  // skip layer: its h4 columns continue the chain, its enc columns are parked for the encoding's
+  // gradient (y = dZ_5 feeds both)
+  layer_h<Net, AB_P5, false>(fp, y, none, x, bias_l, g,
+                             mask_store(a.h + 4 * hs, 256, a.dz + 4 * hs, 256, rows, N, g, inv));
+  float* slot = reinterpret_cast<float*>(stash + 2 * 64);
+  layer_h<Net, AB_P5E, false>(fp, y, none, junk, bias_l, g, EncStash{slot});
+  layer_h<Net, AB_P4, false>(fp, x, none, y, bias_l, g,
+                             mask_store(a.h + 3 * hs, 256, a.dz + 3 * hs, 256, rows, N, g, inv));
+  layer_h<Net, AB_P3, false>(fp, y, none, x, bias_l, g,
+                             mask_store(a.h + 2 * hs, 256, a.dz + 2 * hs, 256, rows, N, g, inv));
+  layer_h<Net, AB_P2, false>(fp, x, none, y, bias_l, g,
+                             mask_store(a.h + 1 * hs, 256, a.dz + 1 * hs, 256, rows, N, g, inv));
+  layer_h<Net, AB_P1, false>(fp, y, none, x, bias_l, g,
+                             mask_store(a.h, 256, a.dz, 256, rows, N, g, inv));
+  // d enc = W_0[:, :63]^T dZ_0 + the parked skip part, and pos_enc's backward (:205-212)
+  EncBwd eb;
+  eb.slot = slot;
+  eb.x0 = a.enc[63 * rr];
+  eb.x1 = a.enc[63 * rr + 1];
+  eb.x2 = a.enc[63 * rr + 2];
+  eb.g = g;
+  layer_h<Net, AB_P0E, false>(fp, x, none, junk, bias_l, g, eb);
+  float dx[3] = {eb.dx0, eb.dx1, eb.dx2};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    dx[q] = __fadd_rn(dx[q], __shfl_xor(dx[q], 16, 64));
+    dx[q] = __fadd_rn(dx[q], __shfl_xor(dx[q], 32, 64));
+    dx[q] *= inv;  // true dL/dx' (identical in the sample's four lane groups)
+  }
+  if (g == 0 && row < N) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) a.dxp[3 * row + q] = dx[q];
+  }
+  // dL/dx' carries pos_enc's 2^d factors: back into fp16 at this sample's own scale
+  const float sd = grad_scale(__float_as_uint(fmaxf(fabsf(dx[0]), fmaxf(fabsf(dx[1]), fabsf(dx[2])))));
+  const float invd = 1.0f / sd;
+  Frag<1, NCOL> ddx;
+  {
+    float dv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? dx[e < 3 ? e : 0] * sd : 0.f;
+    split8(dv, ddx.hi[0][0], ddx.lo[0][0]);
+  }
+  // deformation head and MLP: d hd3 = W_dl^T dL/dx', then deformations_linear.3 .. 1
+  layer_h<Net, AB_DL, false>(fp, none, ddx, y, bias_l, g,
+                             mask_store(a.hd + 3 * ws, 128, a.dzd + 3 * ws, 128, rows, N, g, invd));
+  layer_h<Net, AB_D3, false>(fp, y, none, x, bias_l, g,
+                             mask_store(a.hd + 2 * ws, 128, a.dzd + 2 * ws, 128, rows, N, g, invd));
+  layer_h<Net, AB_D2, false>(fp, x, none, y, bias_l, g,
+                             mask_store(a.hd + 1 * ws, 128, a.dzd + 1 * ws, 128, rows, N, g, invd));
+  layer_h<Net, AB_D1, false>(fp, y, none, x, bias_l, g,
+                             mask_store(a.hd, 128, a.dzd, 128, rows, N, g, invd));
+}
+
+}  // namespace mlp
+}  // namespace aon
+
+using namespace aon;
+using namespace aon::mlp;
+
+extern "C" size_t aon_mlp_art_bwd_packed_bytes(void) { return NetArtBwdH::kPackedBytes; }
+
+extern "C" int aon_mlp_art_bwd_pack(const aon_mlp_art_params* prm, void* packed,
+                                    aon_stream_t stream) {
+  AON_REQUIRE(prm && packed, "null pointer");
+  AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
+  AON_REQUIRE(prm->ld_pts0 >= 63 && prm->ld_pts5 >= 319 && prm->ld_view0 >= 283,
+              "latent-carrying weights are narrower than their per-sample columns");
+  PackArgsH a{};
+  const float* w[kNumLayersArtBwd] = {
+      prm->rgb_w,     prm->views_w[3], prm->views_w[2], prm->views_w[1], prm->views_w[0],
+      prm->bottleneck_w, prm->pts_w[7], prm->pts_w[6], prm->pts_w[5],
+      prm->pts_w[5] ? prm->pts_w[5] + 256 : nullptr,  // enc columns of the skip layer
+      prm->pts_w[4], prm->pts_w[3], prm->pts_w[2], prm->pts_w[1], prm->pts_w[0],
+      prm->deformation_w, prm->def_w[3], prm->def_w[2], prm->def_w[1]};
+  // row strides of the forward weights (their in-features, latent columns included)
+  const int ld[kNumLayersArtBwd] = {128, 128, 128, 128, (int)prm->ld_view0, 256, 256, 256,
+                                    (int)prm->ld_pts5, (int)prm->ld_pts5, 256, 256, 256, 256,
+                                    (int)prm->ld_pts0, 128, 128, 128, 128};
+  for (int i = 0; i < kNumLayersArtBwd; ++i) {
+    AON_REQUIRE(w[i], "null layer weight");
+    a.w[i] = w[i];
+    a.ldw[i] = ld[i];
+    a.tr[i] = 1;
+    a.layers[i] = kLayersArtBwd[i];
+  }
+  AON_REQUIRE(prm->density_w, "null layer weight");
+  a.w2[AB_BOTDEN] = prm->density_w;  // segment B of d h7: density_layer^T (1 x 256)
+  a.ldw2[AB_BOTDEN] = 256;
+  a.n_layers = kNumLayersArtBwd;
+  a.stream_blocks = NetArtBwdH::kStreamBlocks;
+  a.bias_floats = NetArtBwdH::kBiasFloats;
+  return pack_h(a, packed, (hipStream_t)stream);
+}
+
+extern "C" int aon_mlp_art_bwd(const void* packed, const float* draw, const float* hd,
+                               const float* h, const float* hv, const float* enc, int64_t N,
+                               float* dzv, float* dbot, float* dz, float* dxp, float* dzd,
+                               void* work, aon_stream_t stream) {
+  AON_REQUIRE(packed && draw && hd && h && hv && enc && dzv && dbot && dz && dxp && dzd && work,
+              "null pointer");
+  AON_REQUIRE(N >= 0, "bad shape");
+  AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(hd) && aligned16(h) &&
+                  aligned16(hv) && aligned16(dzv) && aligned16(dbot) && aligned16(dz) &&
+                  aligned16(dzd),
+              "buffers must be 16-byte aligned");
+  if (N == 0) return 0;
+  using G = GeomH<1>;
+  const int64_t grid = (N + G::kRowsPerBlock - 1) / G::kRowsPerBlock;
+  AON_REQUIRE(grid < (1ll << 31), "too many rows");
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* amax = static_cast<uint32_t*>(work);
+  const int rc = absmax(draw, 4 * N, amax, st);
+  if (rc) return rc;
+  const ArtBwdArgs args{draw, hd, h, hv, enc, dzv, dbot, dz, dxp, dzd, amax, N};
+  const f4* wsp = static_cast<const f4*>(packed);
+  const float* bias =
+      reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtBwdH::kStreamBytes);
+  hipLaunchKernelGGL(k_mlp_art_bwd_f16x3, (unsigned)grid, G::kThreads, 0, st, wsp, bias, args);
+  return launch_status(__func__);
+}

@@ -38,29 +38,10 @@ __global__ void k_absmax(const float* __restrict__ x, int64_t n, uint32_t* __res
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-// |x * s| < 2^8 for the largest |x|: s = 2^(8 - e) with max = m 2^e, m in [0.5, 1)
-__device__ __forceinline__ float grad_scale(uint32_t bits) {
-  const float m = __uint_as_float(bits);
-  if (!(m > 0.0f) || !isfinite(m)) return 1.0f;
-  int e;
-  (void)frexpf(m, &e);
-  e = e < -100 ? -100 : (e > 100 ? 100 : e);
-  return __builtin_ldexpf(1.0f, 8 - e);
-}
-
-template <int NCOL>
-__device__ __forceinline__ MaskStore<NCOL> mask_store(const float* hbase, int ldh, float* obase,
-                                                      int ld, const int64_t (&rows)[NCOL],
-                                                      int64_t N, int g, float s) {
-  MaskStore<NCOL> m;
-#pragma unroll
-  for (int c = 0; c < NCOL; ++c) {
-    const bool ok = rows[c] < N;
-    m.mrow[c] = ok ? hbase + rows[c] * ldh + 4 * g : nullptr;
-    m.rowp[c] = ok ? obase + rows[c] * ld + 4 * g : nullptr;
-  }
-  m.s = s;
-  return m;
+int absmax(const float* x, int64_t n, uint32_t* out, hipStream_t stream) {
+  if (hipMemsetAsync(out, 0, sizeof(uint32_t), stream) != hipSuccess) return launch_status("absmax");
+  hipLaunchKernelGGL(k_absmax, grid_for(n, 256, 1024), 256, 0, stream, x, n, out);
+  return launch_status("absmax");
 }
 
 __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
@@ -196,10 +177,10 @@ extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const float* h
   const int64_t grid = (N + G::kRowsPerBlock - 1) / G::kRowsPerBlock;
   AON_REQUIRE(grid < (1ll << 31), "too many rows");
   hipStream_t st = (hipStream_t)stream;
-  uint32_t* absmax = static_cast<uint32_t*>(work);
-  if (hipMemsetAsync(absmax, 0, sizeof(uint32_t), st) != hipSuccess) return launch_status(__func__);
-  hipLaunchKernelGGL(k_absmax, grid_for(4 * N, 256, 1024), 256, 0, st, draw, 4 * N, absmax);
-  BwdArgs args{draw, h, hv, dzv, dzb, dz, absmax, N};
+  uint32_t* amax = static_cast<uint32_t*>(work);
+  const int rc = absmax(draw, 4 * N, amax, st);
+  if (rc) return rc;
+  BwdArgs args{draw, h, hv, dzv, dzb, dz, amax, N};
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetBwdH::kStreamBytes);

@@ -168,6 +168,32 @@ struct StorePick<true, NCOL> {
   }
 };
 
+// ---- backward chains (mlp_bwd.hip, mlp_art_bwd.hip)
+// |x * s| < 2^8 for the largest |x|: s = 2^(8 - e) with max = m 2^e, m in [0.5, 1)
+__device__ __forceinline__ float grad_scale(uint32_t bits) {
+  const float m = __uint_as_float(bits);
+  if (!(m > 0.0f) || !isfinite(m)) return 1.0f;
+  int e;
+  (void)frexpf(m, &e);
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  return __builtin_ldexpf(1.0f, 8 - e);
+}
+
+template <int NCOL>
+__device__ __forceinline__ MaskStore<NCOL> mask_store(const float* hbase, int ldh, float* obase,
+                                                      int ld, const int64_t (&rows)[NCOL],
+                                                      int64_t N, int g, float s) {
+  MaskStore<NCOL> m;
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    const bool ok = rows[c] < N;
+    m.mrow[c] = ok ? hbase + rows[c] * ldh + 4 * g : nullptr;
+    m.rowp[c] = ok ? obase + rows[c] * ld + 4 * g : nullptr;
+  }
+  m.s = s;
+  return m;
+}
+
 // epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
 // part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
 template <bool RELU, int NCOL, int NO, typename Store = NoStore>

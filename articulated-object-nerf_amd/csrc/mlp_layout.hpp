@@ -161,6 +161,39 @@ constexpr LayerDesc kLayersBwd[kNumLayersBwd] = {
     {8, 0, 16, 256, 0, 256, 1968, 2176},    // pts_linears.1^T: d h0
 };
 
+// ---- backward chain of the articulated NeRFMLP (training, model_autodecoder.py:168-239 under
+// autograd), same conventions as kLayersBwd: the view branch, the bottleneck / density heads,
+// the trunk, the enc columns of pts_linears.5 (the skip) and of pts_linears.0 (256 -> 63: the
+// gradient w.r.t. pos_enc(x'), reduced in registers through pos_enc's backward to dL/dx'), the
+// deformation head and the deformation MLP.  Latent columns carry no per-sample gradient (their
+// codes' gradients come from the bias gradients, train_art.py).
+enum {
+  AB_RGB = 0, AB_V3, AB_V2, AB_V1, AB_V0, AB_BOTDEN, AB_P7, AB_P6, AB_P5, AB_P5E, AB_P4, AB_P3,
+  AB_P2, AB_P1, AB_P0E, AB_DL, AB_D3, AB_D2, AB_D1, kNumLayersArtBwd
+};
+
+constexpr LayerDesc kLayersArtBwd[kNumLayersArtBwd] = {
+    {0, 1, 8, 0, 3, 128, 0, 0},             // rgb_layer^T: d hv3 (3 -> 128)
+    {4, 0, 8, 128, 0, 128, 16, 128},        // views_linear.3^T: d hv2
+    {4, 0, 8, 128, 0, 128, 80, 256},        // views_linear.2^T: d hv1
+    {4, 0, 8, 128, 0, 128, 144, 384},       // views_linear.1^T: d hv0
+    {4, 0, 16, 128, 0, 256, 208, 512},      // views_linear.0^T, bottleneck columns: d bottleneck
+    {8, 1, 16, 256, 1, 256, 336, 768},      // [bottleneck^T | density^T]: d h7
+    {8, 0, 16, 256, 0, 256, 624, 1024},     // pts_linears.7^T: d h6
+    {8, 0, 16, 256, 0, 256, 880, 1280},     // pts_linears.6^T: d h5
+    {8, 0, 16, 256, 0, 256, 1136, 1536},    // pts_linears.5^T, h4 columns: d h4
+    {8, 0, 4, 256, 0, 63, 1392, 1792},      // pts_linears.5^T, enc columns: d enc (skip)
+    {8, 0, 16, 256, 0, 256, 1456, 1856},    // pts_linears.4^T: d h3
+    {8, 0, 16, 256, 0, 256, 1712, 2112},    // pts_linears.3^T: d h2
+    {8, 0, 16, 256, 0, 256, 1968, 2368},    // pts_linears.2^T: d h1
+    {8, 0, 16, 256, 0, 256, 2224, 2624},    // pts_linears.1^T: d h0
+    {8, 0, 4, 256, 0, 63, 2480, 2880},      // pts_linears.0^T, enc columns: d enc
+    {0, 1, 8, 0, 3, 128, 2544, 2944},       // deformation_layer^T: d hd3 (3 -> 128)
+    {4, 0, 8, 128, 0, 128, 2560, 3072},     // deformations_linear.3^T: d hd2
+    {4, 0, 8, 128, 0, 128, 2624, 3200},     // deformations_linear.2^T: d hd1
+    {4, 0, 8, 128, 0, 128, 2688, 3328},     // deformations_linear.1^T: d hd0
+};
+
 // compile-time description of one fp16x3 network: its layer table and stream geometry
 template <const LayerDesc* TABLE, int NLAYERS, int BLOCKS, int STREAM_BLOCKS, int BIAS_FLOATS>
 struct NetH {
@@ -190,9 +223,11 @@ struct NetH {
 using NetVanillaH = NetH<kLayersH, kNumLayers, kBlocks, kStreamBlocks, kBiasFloats>;
 using NetArtH = NetH<kLayersArt, kNumLayersArt, 2752, 2752, 3376>;
 using NetBwdH = NetH<kLayersBwd, kNumLayersBwd, 2224, 2240, 2432>;
+using NetArtBwdH = NetH<kLayersArtBwd, kNumLayersArtBwd, 2752, 2752, 3456>;
 static_assert(NetVanillaH::ok(), "inconsistent vanilla fp16x3 layout");
 static_assert(NetArtH::ok(), "inconsistent articulated fp16x3 layout");
 static_assert(NetBwdH::ok(), "inconsistent backward-chain fp16x3 layout");
+static_assert(NetArtBwdH::ok(), "inconsistent articulated backward-chain fp16x3 layout");
 
 // pack-kernel arguments: per-layer torch parameter pointers + the layout table by value
 struct PackArgs {
@@ -242,6 +277,9 @@ struct TrainStoreArt {
 // fp16x3 path (mlp_f16x3.hip)
 int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream);
 int pack_h(PackArgsH a, void* packed, hipStream_t stream);
+// *out = bits of max |x| over n floats (memset + k_absmax, mlp_bwd.hip): the backward chains'
+// per-call gradient scale
+int absmax(const float* x, int64_t n, uint32_t* out, hipStream_t stream);
 int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,
                  const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
                  hipStream_t stream, const TrainStore* ts = nullptr);

@@ -215,6 +215,19 @@ int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* 
                           const float* noise, float* hd, float* h, float* bot, float* hv,
                           float* enc, float* xyz, float* raw, aon_stream_t stream);
 
+/* Backward chain of one articulated level (autograd of model_autodecoder.py:168-239): from
+ * dL/d raw (N, 4) and the forward's kept tensors (aon_mlp_art_fwd_train: hd, h, hv, enc) to
+ * every layer's dL/d pre-activation -- dzv (4, N, 128) views_linear.i, dbot (N, 256) the
+ * bottleneck output, dz (8, N, 256) pts_linears.i, dxp (N, 3) = dL/dx' (the deformation head's
+ * output, through pos_enc's backward), dzd (4, N, 128) deformations_linear.i -- the operands of
+ * the weight-gradient GEMMs.  packed: aon_mlp_art_bwd_pack of the forward weights (layout
+ * kLayersArtBwd); work: >= 4 bytes.  Buffers 16-byte aligned (dxp: 4). */
+size_t aon_mlp_art_bwd_packed_bytes(void);
+int aon_mlp_art_bwd_pack(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
+int aon_mlp_art_bwd(const void* packed, const float* draw, const float* hd, const float* h,
+                    const float* hv, const float* enc, int64_t N, float* dzv, float* dbot,
+                    float* dz, float* dxp, float* dzd, void* work, aon_stream_t stream);
+
 /* The same on given sample points pos (B*S, 3) and encoded view directions condition (B, 27)
  * (NeRFMLP.forward(pos, condition, latents)). */
 int aon_mlp_art_fwd_points(const void* packed, const float* pos, const float* condition,

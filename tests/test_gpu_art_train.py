@@ -70,16 +70,18 @@ def test_latent_reg():
         np.testing.assert_allclose(c.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-6, atol=0)
 
 
-@pytest.fixture(params=[True, False], ids=["fused_fwd", "gemm_fwd"])
+@pytest.fixture(params=[(True, True), (False, False), (True, False)],
+                ids=["fused", "gemm", "fused_fwd_gemm_bwd"])
 def art_fwd_mode(request):
     """Articulated training forward on the fused kernel with activation stores
-    (aon_mlp_art_fwd_train) or layer by layer on aon_gemm."""
+    (aon_mlp_art_fwd_train) or layer by layer on aon_gemm; input gradients in the fused chain
+    (aon_mlp_art_bwd) or as GEMMs + aon_pos_enc_bwd."""
     from aonerf import train_art
 
-    old = train_art.FUSED_FORWARD
-    train_art.FUSED_FORWARD = request.param
+    old = train_art.FUSED_FORWARD, train_art.FUSED_BACKWARD
+    train_art.FUSED_FORWARD, train_art.FUSED_BACKWARD = request.param
     yield request.param
-    train_art.FUSED_FORWARD = old
+    train_art.FUSED_FORWARD, train_art.FUSED_BACKWARD = old
 
 
 def test_fused_art_train_forward_activations():
@@ -122,6 +124,44 @@ def test_fused_art_train_forward_activations():
         # enc carries sin(2^9 x'): a 1e-7 change of x' (the two deformation evaluations differ
         # by that) moves it by ~1e-4, and everything after it inherits that
         assert e < (2e-5 if name.startswith("hd") else 5e-4), name
+
+
+def test_fused_art_backward_chain():
+    """aon_mlp_art_bwd (+ the weight-gradient GEMMs) against the all-GEMM backward on the same
+    kept activations and d raw (ragged batch): every parameter and latent gradient within
+    2e-5 of its tensor's max (two f16x3 evaluations of the same products)."""
+    from aonerf import train_art
+
+    net, _ = _make(0)
+    mlp = net.fine_mlp
+    geo = train_art._Geo(mlp)
+    gen = torch.Generator().manual_seed(6)
+    B, S = 29, 65
+    R = B * S
+    o = (torch.rand(B, 3, generator=gen) - 0.5).cuda()
+    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=gen), dim=-1).cuda()
+    t = (2.0 + 4.0 * torch.rand(B, S, generator=gen)).sort(-1).values.cuda()
+    lat = tuple(cuda(v) for v in W.art_latents(2).values())
+    P = [(m.weight.detach(), m.bias.detach()) for m in train_art.art_layers(mlp)]
+    raw = torch.empty((R, 4), device="cuda")
+    xyz, hd, enc, h, bot, hv = train_art._forward_level_fused(geo, P, lat, o, d, d, t, raw)
+    venc = torch.empty((B, 27), device="cuda")
+    L = train_art.L
+    L.call("aon_pos_enc", L.ptr(d), B, 0, 4, L.ptr(venc), L.stream())
+    draw = (torch.randn(R, 4, generator=gen) * 1e-3).cuda()
+    out = {}
+    for mode, fn in (("fused", train_art._backward_level_fused), ("gemm", train_art._backward_level)):
+        G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
+        dlat = tuple(torch.empty_like(x) for x in lat)
+        fn(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
+        out[mode] = [g for pair in G for g in pair] + list(dlat)
+    names = [f"{i}.{k}" for i in range(20) for k in ("w", "b")] + ["shape", "app", "art"]
+    worst = 0.0
+    for name, a, b in zip(names, out["fused"], out["gemm"]):
+        e = rel_err(a.cpu().numpy(), b.cpu().numpy())
+        worst = max(worst, e)
+        assert e < 2e-5, (name, e)
+    print(f"fused vs GEMM articulated backward: worst max-rel err {worst:.2e}")
 
 
 def _make(seed=0):
