@@ -6,14 +6,18 @@
 //   C (M x N) = epilogue( A (M x K) . B (K x N) )
 //
 // Workgroup: 256 threads = 4 waves in 2 x 2, C tile 128 x 128, each wave 64 x 64 = 4 x 4
-// MFMA 16x16 tiles with two fp32 accumulators (hi*hi and the 2^11-scaled cross terms).  Per
-// 32-deep k-step the A and B tiles are loaded into registers (global, one step ahead), split
-// into fp16 hi / lo planes and stored to a double-buffered LDS image laid out [row][k] (k
-// contiguous, 80-B rows), from which each lane reads its 8-element MFMA fragments with one
-// ds_read_b128; one barrier per k-step.  Operands stored reduction-major (A as [K][M], B as
+// MFMA 16x16 tiles with two fp32 accumulators (hi*hi and the 2^11-scaled cross terms: the lo
+// parts stay normal in fp16 down to |x * scale| = 2^-14, so a fixed operand scale covers
+// gradients over many orders of magnitude).  Per 32-deep k-step the A and B tiles are loaded
+// into registers PF steps ahead (the loads fly under the MFMAs; the bias-gradient row sums read
+// them only when they are published), split into fp16 hi / lo planes and stored to a
+// double-buffered LDS image laid out [row][k] (k contiguous, 80-B rows), from which each lane
+// reads its 8-element MFMA fragments with one ds_read_b128; one barrier per k-step.  Operands stored reduction-major (A as [K][M], B as
 // [K][N]) are transposed in registers while staging (4 x 4 blocks), so every GEMM of the
 // backward pass reads its operands in place.
 #include "aon_common.hpp"
+
+#include <type_traits>
 
 namespace aon {
 namespace gemm {
@@ -27,6 +31,10 @@ constexpr int PLANE = BM * ROWH;             // halves per plane (BM == BN)
 constexpr int STAGE = 4 * PLANE;             // A hi, A lo, B hi, B lo
 constexpr float kLo = 2048.0f;               // lo planes carry (x - hi) * 2^11
 constexpr float kInvLo = 1.0f / 2048.0f;
+#ifndef AON_GEMM_PF
+#define AON_GEMM_PF 1
+#endif
+constexpr int PF = AON_GEMM_PF;              // k-tiles loaded ahead (register sets)
 
 struct Params {
   int64_t M, N, K;
@@ -202,8 +210,9 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
   const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
 
-  TileLoad<AKC, VA> ta;
-  TileLoad<BKC, VB> tb;
+  // PF register sets: tile kt + 1 waits in one while later tiles' loads fly into the others
+  TileLoad<AKC, VA> ta[PF];
+  TileLoad<BKC, VB> tb[PF];
   f4 acc_h[4][4], acc_x[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -213,32 +222,43 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
       acc_x[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     }
 
-  auto load = [&](int kt) {
+  auto load = [&](int kt, auto set) {
+    constexpr int S = decltype(set)::value;
     const int64_t k0 = kbeg + (int64_t)kt * BK;
-    ta.load(p.A, p.lda, p.A2, p.lda2, p.K1, p.a2_rdiv, m0, p.M, k0, kend, tid);
-    tb.load(p.B, p.ldb, nullptr, 0, INT64_MAX, p.b_rdiv, n0, p.N, k0, kend, tid);
+    ta[S].load(p.A, p.lda, p.A2, p.lda2, p.K1, p.a2_rdiv, m0, p.M, k0, kend, tid);
+    tb[S].load(p.B, p.ldb, nullptr, 0, INT64_MAX, p.b_rdiv, n0, p.N, k0, kend, tid);
   };
-  auto store = [&](int stage) {
-    _Float16* s = smem + stage * STAGE;
-    ta.store(s, s + PLANE, p.sa, tid);
-    tb.store(s + 2 * PLANE, s + 3 * PLANE, p.sb, tid);
-  };
-
   const bool want_rows = !AKC && p.rowsum && tn == 0;
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  // publish a landed register set to LDS stage `stage` (and add its rows to the row sums, in
+  // k-tile order)
+  auto store = [&](int stage, auto set) {
+    constexpr int S = decltype(set)::value;
+    if (!AKC && want_rows) ta[S].add_rows(rs);
+    _Float16* s = smem + stage * STAGE;
+    ta[S].store(s, s + PLANE, p.sa, tid);
+    tb[S].store(s + 2 * PLANE, s + 3 * PLANE, p.sb, tid);
+  };
+  using Set0 = std::integral_constant<int, 0>;
+  using Set1 = std::integral_constant<int, 1>;
+
+  using SetN = std::integral_constant<int, PF - 1>;
   if (nk > 0) {
-    load(0);
-    if (!AKC && want_rows) ta.add_rows(rs);
-    store(0);
+    load(0, Set0{});
+    if (PF == 2 && nk > 1) load(1, SetN{});
+    store(0, Set0{});
   }
   __syncthreads();
   const int g = lane >> 4, r16 = lane & 15;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) {
-      load(kt + 1);  // global loads in flight under this step's MFMAs
-      if (!AKC && want_rows) ta.add_rows(rs);
-    }
-    const _Float16* s = smem + (kt & 1) * STAGE;
+  // step kt: tile kt is in LDS stage kt & 1 and tile kt + 1 in register set (kt + 1) % PF
+  // (PF = 2: loaded last step; PF = 1: loaded now, under this step's MFMAs); tile kt + PF goes
+  // into set kt % PF, free since tile kt was published
+  auto step = [&](int kt, auto par) {
+    constexpr int P = decltype(par)::value;
+    using Cur = std::integral_constant<int, P % PF>;
+    using Nxt = std::integral_constant<int, (P + 1) % PF>;
+    if (kt + PF < nk) load(kt + PF, Cur{});  // global loads in flight under PF steps of MFMAs
+    const _Float16* s = smem + P * STAGE;
     h8 bh[4], bl[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -258,8 +278,12 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
         acc_x[i][j] = mfma16(al, bh[j], acc_x[i][j]);
       }
     }
-    if (kt + 1 < nk) store((kt + 1) & 1);
+    if (kt + 1 < nk) store(1 - P, Nxt{});
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, Set0{});
+    if (kt + 1 < nk) step(kt + 1, Set1{});
   }
 
   const bool split = p.zsplit > 1;
@@ -305,7 +329,23 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
     }
 }
 
-// split-K: C = epilogue(sum_z part[z]) in z order (deterministic); rowsum likewise
+// split-K: C = epilogue(sum_z part[z]) in z order (deterministic); rowsum likewise.  The loads
+// of 8 consecutive z are issued before their (in-order) adds: a thread walks up to 256 partials
+// spaced M*N apart, and one load at a time left this kernel latency-bound (~50 us at any size).
+__device__ __forceinline__ float sum_z(const float* src, int64_t stride, int splits) {
+  float v = src[0];
+  int z = 1;
+  for (; z + 8 <= splits; z += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = src[(int64_t)(z + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v = __fadd_rn(v, t[u]);
+  }
+  for (; z < splits; ++z) v = __fadd_rn(v, src[(int64_t)z * stride]);
+  return v;
+}
+
 __global__ void k_gemm_reduce(Params p, int splits) {
   const int64_t total = p.M * p.N;
   const int64_t extra = p.rowsum ? p.M : 0;  // rowsum entries ride along as e >= total
@@ -313,14 +353,11 @@ __global__ void k_gemm_reduce(Params p, int splits) {
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e >= total) {
       const int64_t m = e - total;
-      float v = p.rowsum_part[m];
-      for (int z = 1; z < splits; ++z) v = __fadd_rn(v, p.rowsum_part[(int64_t)z * p.M + m]);
-      p.rowsum[m] = v;
+      p.rowsum[m] = sum_z(p.rowsum_part + m, p.M, splits);
       continue;
     }
     const int64_t m = e / p.N, n = e - m * p.N;
-    float v = p.part[e];
-    for (int z = 1; z < splits; ++z) v = __fadd_rn(v, p.part[(int64_t)z * total + e]);
+    float v = sum_z(p.part + e, total, splits);
     float* c = p.C + m * p.ldc + n;
     if (p.accumulate) v = __fadd_rn(*c, v);
     if (p.bias) v = __fadd_rn(v, p.bias[n]);
