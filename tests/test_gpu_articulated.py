@@ -85,7 +85,9 @@ def test_forward_chain_and_golden(art, tag):
     randomized = tag == "rand"
     rays = {k: cuda(g[f"{tag}_{k}"]) for k in ("rays_o", "rays_d", "viewdirs")}
     kw = dict(u_coarse=cuda(g[f"{tag}_u_coarse"]), u_fine=cuda(g[f"{tag}_u_fine"])) if randomized else {}
-    ret = net(rays, randomized, True, 2.0, 6.0, lat, return_weights=True, return_intermediates=True, **kw)
+    with torch.no_grad():  # the render path (with autograd on, forward takes the training path)
+        ret = net(rays, randomized, True, 2.0, 6.0, lat, return_weights=True,
+                  return_intermediates=True, **kw)
     rc = {k: v.cpu() for k, v in rays.items()}
     # (1) coarse level (sample positions equal the reference's)
     np.testing.assert_array_equal(npy(ret[0][4]["t_vals"]), g[f"{tag}_coarse_t"])

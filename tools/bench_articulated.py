@@ -40,6 +40,7 @@ def main():
     net.coarse_mlp.fused = net.fine_mlp.fused = not args.layerwise
     rays = frame_rays(torch.as_tensor(create_spheric_poses(4.0)[11]), H, W, sapien_focal(H))
 
+    @torch.no_grad()  # a render (Lightning's eval steps run without autograd)
     def step():
         return net(rays, False, True, 2.0, 6.0, lat)
 
