@@ -64,19 +64,20 @@ _SIGNATURES = {
     "aon_mlp_pack": (c_int, [ctypes.POINTER(AonMlpParams), c_int, vp, vp]),
     "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
-    "aon_mlp_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp]),
+    "aon_mlp_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp]),
+    "aon_relu_masks": (c_int, [vp, c_i64, c_int, vp, vp]),
     "aon_mlp_bwd_packed_bytes": (c_size, []),
     "aon_mlp_bwd_pack": (c_int, [ctypes.POINTER(AonMlpParams), vp, vp]),
-    "aon_mlp_bwd": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp]),
+    "aon_mlp_bwd": (c_int, [vp, vp, vp, c_i64, vp, vp, vp, vp, vp]),
     "aon_mlp_art_packed_bytes": (c_size, []),
     "aon_mlp_art_pack": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
     "aon_mlp_art_fwd": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_art_fwd_points": (c_int, [vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_art_bwd_packed_bytes": (c_size, []),
     "aon_mlp_art_bwd_pack": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
-    "aon_mlp_art_bwd": (c_int, [vp, vp, vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp, vp, vp]),
+    "aon_mlp_art_bwd": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp, vp, vp]),
     "aon_mlp_art_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp,
-                                      vp, vp]),
+                                      vp, vp, vp]),
     "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,
                                   vp, vp, vp, vp]),
     "aon_image_mse": (c_int, [vp, vp, c_i64, c_i64, vp, c_int, vp, vp, vp]),
@@ -109,7 +110,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.aon_abi_version() != 2:
+        if handle.aon_abi_version() != 3:
             raise ImportError("aonerf: ABI version mismatch")
         _lib = handle
     return _lib

@@ -151,16 +151,30 @@ def _stacked(h, R):
     return torch.stack(h)
 
 
-def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw):
+def relu_masks(acts, R):
+    """ReLU' bits (len(acts), R, 4) x 64-bit words (aon_relu_masks) of stored activations, in the
+    layout the fused training forwards write: the masks of the fused backward chains after a
+    layer-by-layer forward."""
+    dev = acts[0].device
+    masks = torch.empty((len(acts), R, 8), dtype=torch.int32, device=dev)
+    for i, a in enumerate(acts):
+        L.call("aon_relu_masks", L.ptr(L.contig(a)), R, a.shape[-1], L.ptr(masks[i]), L.stream(dev))
+    return masks
+
+
+def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
     """_backward_level with every input-gradient product in one fused kernel (aon_mlp_bwd);
-    the weight gradients dW = dZ^T X and db = sum_rows dZ stay split-K GEMMs."""
+    the weight gradients dW = dZ^T X and db = sum_rows dZ stay split-K GEMMs.  ``masks``: the
+    ReLU' bits of h0..h7, hv from the fused forward (built from the activations when None)."""
     R, dev = enc.shape[0], enc.device
+    if masks is None:
+        masks = relu_masks(list(h) + [hv], R)
     dzv = torch.empty((R, 128), device=dev)
     dzb = torch.empty((R, 256), device=dev)
     dz = torch.empty((8, R, 256), device=dev)
     work = _buffer("work", 4, dev)
-    L.call("aon_mlp_bwd", L.ptr(_pack_bwd(P, dev)), L.ptr(draw), L.ptr(_stacked(h, R)), L.ptr(hv),
-           R, L.ptr(dzv), L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
+    L.call("aon_mlp_bwd", L.ptr(_pack_bwd(P, dev)), L.ptr(draw), L.ptr(masks), R, L.ptr(dzv),
+           L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
     gs, acts = GRAD_SCALE, ACT_SCALE
 
     def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None):
@@ -182,10 +196,13 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw):
             dweight(G[i][0], dz[i], 256, 256, h[i - 1], 256, 256, db=G[i][1])
 
 
-def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None):
-    """_forward_level on the fused kernel: raw (R x 4) and the kept activations."""
+def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, masks=None):
+    """_forward_level on the fused kernel: raw (R x 4) and the kept activations; ``masks``
+    ((9, R, 8) int32) receives their ReLU' bits for the backward chain."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
+    if masks is None:
+        masks = torch.empty((9, R, 8), dtype=torch.int32, device=dev)
     hbuf = torch.empty((8, R, 256), device=dev)
     bot = torch.empty((R, 256), device=dev)
     hv = torch.empty((R, 128), device=dev)
@@ -195,7 +212,7 @@ def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None):
     packed = _pack(P, dev)
     L.call("aon_mlp_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
            L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hbuf),
-           L.ptr(bot), L.ptr(hv), L.ptr(raw), L.stream(dev))
+           L.ptr(bot), L.ptr(hv), L.ptr(raw), L.ptr(masks), L.stream(dev))
     return list(hbuf.unbind(0)), bot, hv
 
 
@@ -215,10 +232,13 @@ class RenderLevel(torch.autograd.Function):
         L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, 4, L.ptr(venc), L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
         raw = torch.empty((R, 4), device=dev)
+        masks = None  # ReLU' bits for the fused backward chain (built there when None)
         if FUSED_FORWARD:
             noise = L.contig(noise) if noise is not None else None
+            masks = torch.empty((9, R, 8), dtype=torch.int32, device=dev)
             h, bot, hv = _forward_level_fused(P, L.contig(rays_o), L.contig(rays_d),
-                                              L.contig(viewdirs), L.contig(t_vals), raw, noise)
+                                              L.contig(viewdirs), L.contig(t_vals), raw, noise,
+                                              masks)
         else:
             h, bot, hv = _forward_level(P, enc, venc, S, raw, noise)
         comp = torch.empty((B, 3), device=dev)
@@ -229,6 +249,7 @@ class RenderLevel(torch.autograd.Function):
                L.ptr(rays_d), B, S, int(bool(white_bkgd)), L.ACT_VANILLA, L.ptr(comp), L.ptr(acc),
                L.ptr(weights), L.ptr(depth), L.stream(dev))
         ctx.save_for_backward(rays_d, t_vals, enc, venc, raw, bot, hv, *h, *params)
+        ctx.masks = masks
         ctx.meta = (B, S, bool(white_bkgd))
         ctx.mark_non_differentiable(weights)
         return comp, acc, depth, weights
@@ -252,7 +273,7 @@ class RenderLevel(torch.autograd.Function):
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
         if FUSED_BACKWARD:
-            _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw)
+            _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, ctx.masks)
         else:
             _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]

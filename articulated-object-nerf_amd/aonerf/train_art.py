@@ -32,7 +32,7 @@ import torch
 
 from . import _lib as L
 from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, gemm
-from .train import Adam, img2mse, learning_rate, mse2psnr  # noqa: F401 (the shared loss / optimizer)
+from .train import Adam, img2mse, learning_rate, mse2psnr, relu_masks  # noqa: F401 (shared)
 
 # parameter layout of one articulated NeRFMLP in ArtRenderLevel: 20 layers x (weight, bias)
 DEF0, DL, PTS0, DENS, BOT, VIEW0, RGB = 0, 4, 5, 13, 14, 15, 19
@@ -188,11 +188,15 @@ def _pack_bwd(P, dev):
     return buf
 
 
-def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None):
+def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None,
+                         masks=None):
     """_forward_level on the fused kernel (aon_mlp_art_fwd_train): raw (R x 4) and the kept
-    activations, plus the sample points and pos_enc(x')."""
+    activations, plus the sample points and pos_enc(x'); ``masks`` ((16, R, 8) int32) receives
+    the ReLU' bits of hd0..3, h0..7, hv0..3 for the backward chain."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
+    if masks is None:
+        masks = torch.empty((16, R, 8), dtype=torch.int32, device=dev)
     hd = torch.empty((4, R, geo.wd), device=dev)
     h = torch.empty((8, R, geo.nw), device=dev)
     bot = torch.empty((R, geo.nw), device=dev)
@@ -202,7 +206,7 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     packed = _pack(geo, P, lat)
     L.call("aon_mlp_art_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
            L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h),
-           L.ptr(bot), L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.stream(dev))
+           L.ptr(bot), L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks), L.stream(dev))
     return xyz, hd, enc, h, bot, hv
 
 
@@ -307,11 +311,15 @@ def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, dra
     dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
 
 
-def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw):
+def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
+                          masks=None):
     """_backward_level with every input-gradient product (and pos_enc's backward) in one fused
     kernel (aon_mlp_art_bwd); the weight gradients dW = dZ^T X, db = sum_rows dZ and the latent
-    terms stay GEMMs."""
+    terms stay GEMMs.  ``masks``: the fused forward's ReLU' bits (built from the activations
+    when None)."""
     R, dev = xyz.shape[0], xyz.device
+    if masks is None:
+        masks = relu_masks(list(hd) + list(h) + list(hv), R)
     wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
     shape, app, art = lat
     dshape, dapp, dart = dlat
@@ -321,9 +329,8 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     dxp = torch.empty((R, 3), device=dev)
     dzd = torch.empty((4, R, wd), device=dev)
     work = _buffer("work", 4, dev)
-    L.call("aon_mlp_art_bwd", L.ptr(_pack_bwd(P, dev)), L.ptr(draw), L.ptr(hd), L.ptr(h),
-           L.ptr(hv), L.ptr(enc), R, L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd),
-           L.ptr(work), L.stream(dev))
+    L.call("aon_mlp_art_bwd", L.ptr(_pack_bwd(P, dev)), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
+           L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
     gs, acts = GRAD_SCALE, ACT_SCALE
 
     def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True):
@@ -385,10 +392,12 @@ class ArtRenderLevel(torch.autograd.Function):
         P = [(params[2 * i], params[2 * i + 1]) for i in range(20)]
         raw = torch.empty((R, 4), device=dev)
         noise = L.contig(noise) if noise is not None else None
+        masks = None  # ReLU' bits for the fused backward chain (built there when None)
         if FUSED_FORWARD and _fused_ok(geo):
+            masks = torch.empty((16, R, 8), dtype=torch.int32, device=dev)
             xyz, hd, enc, h, bot, hv = _forward_level_fused(
                 geo, P, lat, L.contig(rays_o), L.contig(rays_d), L.contig(viewdirs),
-                L.contig(t_vals), raw, noise)
+                L.contig(t_vals), raw, noise, masks)
         else:
             xyz = torch.empty((R, 3), device=dev)
             L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
@@ -402,6 +411,7 @@ class ArtRenderLevel(torch.autograd.Function):
                L.ptr(rays_d), B, S, int(bool(white_bkgd)), L.ACT_ARTIC, L.ptr(comp), L.ptr(acc),
                L.ptr(weights), L.ptr(depth), L.stream(dev))
         ctx.save_for_backward(rays_d, t_vals, xyz, enc, venc, raw, hd, h, bot, hv, *lat, *params)
+        ctx.masks = masks
         ctx.meta = (geo, B, S, bool(white_bkgd), tuple(x.shape for x in (shape, app, art)))
         ctx.mark_non_differentiable(weights)
         return comp, acc, depth, weights
@@ -425,7 +435,8 @@ class ArtRenderLevel(torch.autograd.Function):
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
         dlat = tuple(torch.empty_like(x) for x in lat)
         if FUSED_BACKWARD and _fused_ok(geo):
-            _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
+            _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
+                                  ctx.masks)
         else:
             _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]

@@ -331,15 +331,17 @@ extern "C" int aon_mlp_fwd_encoded(const void* packed, int precision, const floa
 extern "C" int aon_mlp_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
                                  const float* viewdirs, const float* t, int64_t B, int S,
                                  const float* noise, float* h, float* bot, float* hv, float* raw,
-                                 aon_stream_t stream) {
-  AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && h && bot && hv && raw, "null pointer");
+                                 uint32_t* masks, aon_stream_t stream) {
+  AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && h && bot && hv && raw && masks,
+              "null pointer");
+  AON_REQUIRE(aligned16(masks), "masks must be 16-byte aligned");
   AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
   AON_REQUIRE(aligned16(packed) && aligned16(raw) && aligned16(h) && aligned16(bot) && aligned16(hv),
               "packed / output buffers must be 16-byte aligned");
   const int64_t N = B * S;
   if (N == 0) return 0;
   AON_REQUIRE((N + 127) / 128 < (1ll << 31), "too many rows");
-  const TrainStore ts{h, bot, hv, noise};
+  const TrainStore ts{h, bot, hv, noise, reinterpret_cast<uint2*>(masks)};
   return launch_f16x3(2, 1, packed, rays_o, rays_d, viewdirs, t, B, S, AON_ACT_NONE, raw,
                       (hipStream_t)stream, &ts);
 }

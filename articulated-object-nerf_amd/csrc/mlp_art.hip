@@ -101,11 +101,12 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   Frag<1, NCOL> none;
   using SP = StorePick<STORE, NCOL>;
   const int64_t hds = N * 128, hs = N * 256;  // one deformation / pts_linears output
+  const int64_t ms = N * 4;  // one layer's ReLU' bits: hd0..3, h0..7, hv0..3 in ts.masks
   // deformation MLP (model_autodecoder.py:196-205)
-  layer_h<Net, A_D0, true>(fp, none, din, x, bias_l, g, SP::make(ts.hd, 128, rows, N, g));
-  layer_h<Net, A_D1, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + hds, 128, rows, N, g));
-  layer_h<Net, A_D2, true>(fp, y, none, x, bias_l, g, SP::make(ts.hd + 2 * hds, 128, rows, N, g));
-  layer_h<Net, A_D3, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + 3 * hds, 128, rows, N, g));
+  layer_h<Net, A_D0, true>(fp, none, din, x, bias_l, g, SP::make(ts.hd, 128, rows, N, g, ts.masks));
+  layer_h<Net, A_D1, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + hds, 128, rows, N, g, ts.masks + 1 * ms));
+  layer_h<Net, A_D2, true>(fp, y, none, x, bias_l, g, SP::make(ts.hd + 2 * hds, 128, rows, N, g, ts.masks + 2 * ms));
+  layer_h<Net, A_D3, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + 3 * hds, 128, rows, N, g, ts.masks + 3 * ms));
   f4 dlt[NCOL];
   head_h<Net, A_DOUT>(fp, y, dlt, bias_l, g);
 
@@ -134,11 +135,11 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   }
 
   // trunk on cat[enc, shape] (:214-220), shape folded into the pts_linears.0 / .5 biases
-  layer_h<Net, A_P0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g));
-  layer_h<Net, A_P1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + hs, 256, rows, N, g));
-  layer_h<Net, A_P2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g));
-  layer_h<Net, A_P3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g));
-  layer_h<Net, A_P4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g));
+  layer_h<Net, A_P0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g, ts.masks + 4 * ms));
+  layer_h<Net, A_P1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + hs, 256, rows, N, g, ts.masks + 5 * ms));
+  layer_h<Net, A_P2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g, ts.masks + 6 * ms));
+  layer_h<Net, A_P3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g, ts.masks + 7 * ms));
+  layer_h<Net, A_P4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g, ts.masks + 8 * ms));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c)
 #pragma unroll
@@ -147,9 +148,9 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
     }
   // skip: cat[h, enc, shape]
-  layer_h<Net, A_P5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g));
-  layer_h<Net, A_P6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g));
-  layer_h<Net, A_P7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g));
+  layer_h<Net, A_P5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g, ts.masks + 9 * ms));
+  layer_h<Net, A_P6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g, ts.masks + 10 * ms));
+  layer_h<Net, A_P7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g, ts.masks + 11 * ms));
   f4 dens[NCOL], rgb[NCOL];
   head_h<Net, A_DEN>(fp, y, dens, bias_l, g);  // :221-223
   // bottleneck, no activation (:225)
@@ -160,10 +161,10 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
   }
   // view branch on cat[bottleneck, enc_dir, appearance] (:226-235)
-  layer_h<Net, A_V0, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g));
-  layer_h<Net, A_V1, true>(fp, y, none, x, bias_l, g, SP::make(ts.hv + hds, 128, rows, N, g));
-  layer_h<Net, A_V2, true>(fp, x, none, y, bias_l, g, SP::make(ts.hv + 2 * hds, 128, rows, N, g));
-  layer_h<Net, A_V3, true>(fp, y, none, x, bias_l, g, SP::make(ts.hv + 3 * hds, 128, rows, N, g));
+  layer_h<Net, A_V0, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g, ts.masks + 12 * ms));
+  layer_h<Net, A_V1, true>(fp, y, none, x, bias_l, g, SP::make(ts.hv + hds, 128, rows, N, g, ts.masks + 13 * ms));
+  layer_h<Net, A_V2, true>(fp, x, none, y, bias_l, g, SP::make(ts.hv + 2 * hds, 128, rows, N, g, ts.masks + 14 * ms));
+  layer_h<Net, A_V3, true>(fp, y, none, x, bias_l, g, SP::make(ts.hv + 3 * hds, 128, rows, N, g, ts.masks + 15 * ms));
   head_h<Net, A_RGB>(fp, x, rgb, bias_l, g);  // :237
 
   if (g == 0) {
@@ -259,9 +260,10 @@ extern "C" int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, co
                                      const float* viewdirs, const float* t, int64_t B, int S,
                                      const float* noise, float* hd, float* h, float* bot,
                                      float* hv, float* enc, float* xyz, float* raw,
-                                     aon_stream_t stream) {
+                                     uint32_t* masks, aon_stream_t stream) {
   AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && raw, "null pointer");
-  AON_REQUIRE(hd && h && bot && hv && enc && xyz, "null activation buffer");
+  AON_REQUIRE(hd && h && bot && hv && enc && xyz && masks, "null activation buffer");
+  AON_REQUIRE(aligned16(masks), "masks must be 16-byte aligned");
   AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
   AON_REQUIRE(aligned16(packed) && aligned16(raw), "packed / raw must be 16-byte aligned");
   AON_REQUIRE(((reinterpret_cast<uintptr_t>(hd) | reinterpret_cast<uintptr_t>(h) |
@@ -275,7 +277,7 @@ extern "C" int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, co
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
-  const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise};
+  const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise, reinterpret_cast<uint2*>(masks)};
   hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true>), (unsigned)grid, G::kThreads, 0,
                      (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
                      (int)AON_ACT_NONE, raw, ts);

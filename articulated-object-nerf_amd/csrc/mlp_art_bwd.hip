@@ -22,9 +22,7 @@ namespace mlp {
 
 struct ArtBwdArgs {
   const float* draw;       // (N, 4): d raw_rgb (3), d raw_sigma
-  const float* hd;         // (4, N, 128) post-ReLU deformations_linear.i outputs
-  const float* h;          // (8, N, 256) post-ReLU pts_linears.i outputs
-  const float* hv;         // (4, N, 128) post-ReLU views_linear.i outputs
+  const uint2* masks;      // (16, N, 4) ReLU' bits of hd0..3, h0..7, hv0..3
   const float* enc;        // (N, 63) pos_enc(x'), enc[:, :3] = x'
   float* dzv;              // (4, N, 128): dL/d pre-activation of views_linear.i
   float* dbot;             // (N, 256): dL/d bottleneck output
@@ -136,19 +134,19 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   fp.start();
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 
-  const int64_t hs = N * 256, ws = N * 128;
+  const int64_t hs = N * 256, ws = N * 128, ms = N * 4;  // ms: one layer's ReLU' bits
   Frag<8, NCOL> x, y;
   Frag<2, NCOL> junk;  // output fragments of the enc-column layers (consumed in the epilogue)
   Frag<1, NCOL> none;
   // view branch: d hv3 = W_rgb^T d rgb, then views_linear.3 .. 1, each * ReLU'
   layer_h<Net, AB_RGB, false>(fp, none, drgb, x, bias_l, g,
-                              mask_store(a.hv + 3 * ws, 128, a.dzv + 3 * ws, 128, rows, N, g, inv));
+                              mask_bits(a.masks + 15 * ms, a.dzv + 3 * ws, 128, rows, N, g, inv));
   layer_h<Net, AB_V3, false>(fp, x, none, y, bias_l, g,
-                             mask_store(a.hv + 2 * ws, 128, a.dzv + 2 * ws, 128, rows, N, g, inv));
+                             mask_bits(a.masks + 14 * ms, a.dzv + 2 * ws, 128, rows, N, g, inv));
   layer_h<Net, AB_V2, false>(fp, y, none, x, bias_l, g,
-                             mask_store(a.hv + 1 * ws, 128, a.dzv + 1 * ws, 128, rows, N, g, inv));
+                             mask_bits(a.masks + 13 * ms, a.dzv + 1 * ws, 128, rows, N, g, inv));
   layer_h<Net, AB_V1, false>(fp, x, none, y, bias_l, g,
-                             mask_store(a.hv, 128, a.dzv, 128, rows, N, g, inv));
+                             mask_bits(a.masks + 12 * ms, a.dzv, 128, rows, N, g, inv));
   // d bottleneck = W_view0[:, :256]^T dZ_view0 (linear layer: no mask)
   {
     RowStore<NCOL> st;
@@ -160,25 +158,25 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
   // d h7 = W_bot^T d bottleneck + W_den^T d sigma, * ReLU'(h7) -> dZ_7
   layer_h<Net, AB_BOTDEN, false>(fp, x, dsig, y, bias_l, g,
-                                 mask_store(a.h + 7 * hs, 256, a.dz + 7 * hs, 256, rows, N, g, inv));
+                                 mask_bits(a.masks + 11 * ms, a.dz + 7 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P7, false>(fp, y, none, x, bias_l, g,
-                             mask_store(a.h + 6 * hs, 256, a.dz + 6 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 10 * ms, a.dz + 6 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P6, false>(fp, x, none, y, bias_l, g,
-                             mask_store(a.h + 5 * hs, 256, a.dz + 5 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 9 * ms, a.dz + 5 * hs, 256, rows, N, g, inv));
   // skip layer: its h4 columns continue the chain, its enc columns are parked for the encoding's
   // gradient (y = dZ_5 feeds both)
   layer_h<Net, AB_P5, false>(fp, y, none, x, bias_l, g,
-                             mask_store(a.h + 4 * hs, 256, a.dz + 4 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 8 * ms, a.dz + 4 * hs, 256, rows, N, g, inv));
   float* slot = reinterpret_cast<float*>(stash + 2 * 64);
   layer_h<Net, AB_P5E, false>(fp, y, none, junk, bias_l, g, EncStash{slot});
   layer_h<Net, AB_P4, false>(fp, x, none, y, bias_l, g,
-                             mask_store(a.h + 3 * hs, 256, a.dz + 3 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 7 * ms, a.dz + 3 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P3, false>(fp, y, none, x, bias_l, g,
-                             mask_store(a.h + 2 * hs, 256, a.dz + 2 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 6 * ms, a.dz + 2 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P2, false>(fp, x, none, y, bias_l, g,
-                             mask_store(a.h + 1 * hs, 256, a.dz + 1 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 5 * ms, a.dz + 1 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P1, false>(fp, y, none, x, bias_l, g,
-                             mask_store(a.h, 256, a.dz, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 4 * ms, a.dz, 256, rows, N, g, inv));
   // d enc = W_0[:, :63]^T dZ_0 + the parked skip part, and pos_enc's backward (:205-212)
   EncBwd eb;
   eb.slot = slot;
@@ -210,13 +208,13 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   }
   // deformation head and MLP: d hd3 = W_dl^T dL/dx', then deformations_linear.3 .. 1
   layer_h<Net, AB_DL, false>(fp, none, ddx, y, bias_l, g,
-                             mask_store(a.hd + 3 * ws, 128, a.dzd + 3 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 3 * ms, a.dzd + 3 * ws, 128, rows, N, g, invd));
   layer_h<Net, AB_D3, false>(fp, y, none, x, bias_l, g,
-                             mask_store(a.hd + 2 * ws, 128, a.dzd + 2 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 2 * ms, a.dzd + 2 * ws, 128, rows, N, g, invd));
   layer_h<Net, AB_D2, false>(fp, x, none, y, bias_l, g,
-                             mask_store(a.hd + 1 * ws, 128, a.dzd + 1 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 1 * ms, a.dzd + 1 * ws, 128, rows, N, g, invd));
   layer_h<Net, AB_D1, false>(fp, y, none, x, bias_l, g,
-                             mask_store(a.hd, 128, a.dzd, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 0 * ms, a.dzd, 128, rows, N, g, invd));
 }
 
 }  // namespace mlp
@@ -260,16 +258,14 @@ extern "C" int aon_mlp_art_bwd_pack(const aon_mlp_art_params* prm, void* packed,
   return pack_h(a, packed, (hipStream_t)stream);
 }
 
-extern "C" int aon_mlp_art_bwd(const void* packed, const float* draw, const float* hd,
-                               const float* h, const float* hv, const float* enc, int64_t N,
-                               float* dzv, float* dbot, float* dz, float* dxp, float* dzd,
-                               void* work, aon_stream_t stream) {
-  AON_REQUIRE(packed && draw && hd && h && hv && enc && dzv && dbot && dz && dxp && dzd && work,
+extern "C" int aon_mlp_art_bwd(const void* packed, const float* draw, const uint32_t* masks,
+                               const float* enc, int64_t N, float* dzv, float* dbot, float* dz,
+                               float* dxp, float* dzd, void* work, aon_stream_t stream) {
+  AON_REQUIRE(packed && draw && masks && enc && dzv && dbot && dz && dxp && dzd && work,
               "null pointer");
   AON_REQUIRE(N >= 0, "bad shape");
-  AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(hd) && aligned16(h) &&
-                  aligned16(hv) && aligned16(dzv) && aligned16(dbot) && aligned16(dz) &&
-                  aligned16(dzd),
+  AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(masks) && aligned16(dzv) &&
+                  aligned16(dbot) && aligned16(dz) && aligned16(dzd),
               "buffers must be 16-byte aligned");
   if (N == 0) return 0;
   using G = GeomH<1>;
@@ -279,7 +275,8 @@ extern "C" int aon_mlp_art_bwd(const void* packed, const float* draw, const floa
   uint32_t* amax = static_cast<uint32_t*>(work);
   const int rc = absmax(draw, 4 * N, amax, st);
   if (rc) return rc;
-  const ArtBwdArgs args{draw, hd, h, hv, enc, dzv, dbot, dz, dxp, dzd, amax, N};
+  const ArtBwdArgs args{draw, reinterpret_cast<const uint2*>(masks), enc, dzv, dbot, dz, dxp, dzd,
+                        amax, N};
   const f4* wsp = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtBwdH::kStreamBytes);

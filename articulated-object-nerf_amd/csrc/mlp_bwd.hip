@@ -19,8 +19,7 @@ namespace mlp {
 
 struct BwdArgs {
   const float* draw;              // (N, 4): d raw_rgb (3), d raw_sigma (model.py:183-187 folded)
-  const float* h;                 // (8, N, 256): post-ReLU pts_linears.0..7 outputs
-  const float* hv;                // (N, 128): post-ReLU views_linear.0 output
+  const uint2* masks;             // (9, N, 4): ReLU' bits of pts_linears.0..7, views_linear.0
   float* dzv;                     // (N, 128): dL/d pre-activation of views_linear.0
   float* dzb;                     // (N, 256): dL/d bottleneck output
   float* dz;                      // (8, N, 256): dL/d pre-activation of pts_linears.i
@@ -95,12 +94,12 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   fp.start();
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 
-  const int64_t hs = N * 256;
+  const int64_t hs = N * 256, ms = N * 4;
   Frag<8, NCOL> x, y;
   Frag<1, NCOL> none;
   // d hv = W_rgb^T d rgb, * ReLU'(hv) -> dZ of views_linear.0
   layer_h<Net, B_RGB, false>(fp, none, drgb, x, bias_l, g,
-                             mask_store(a.hv, 128, a.dzv, 128, rows, N, g, inv));
+                             mask_bits(a.masks + 8 * ms, a.dzv, 128, rows, N, g, inv));
   // d bottleneck = W_view[:, :256]^T dZ_view (linear layer: no mask)
   {
     RowStore<NCOL> st;
@@ -112,22 +111,22 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
   // d h7 = W_bot^T dZ_bot + W_den^T d sigma, * ReLU'(h7) -> dZ_7
   layer_h<Net, B_BOTDEN, false>(fp, y, dsig, x, bias_l, g,
-                                mask_store(a.h + 7 * hs, 256, a.dz + 7 * hs, 256, rows, N, g, inv));
+                                mask_bits(a.masks + 7 * ms, a.dz + 7 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_7, false>(fp, x, none, y, bias_l, g,
-                           mask_store(a.h + 6 * hs, 256, a.dz + 6 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 6 * ms, a.dz + 6 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_6, false>(fp, y, none, x, bias_l, g,
-                           mask_store(a.h + 5 * hs, 256, a.dz + 5 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 5 * ms, a.dz + 5 * hs, 256, rows, N, g, inv));
   // the skip layer's enc columns carry no gradient (positions are not differentiated)
   layer_h<Net, B_5, false>(fp, x, none, y, bias_l, g,
-                           mask_store(a.h + 4 * hs, 256, a.dz + 4 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 4 * ms, a.dz + 4 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_4, false>(fp, y, none, x, bias_l, g,
-                           mask_store(a.h + 3 * hs, 256, a.dz + 3 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 3 * ms, a.dz + 3 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_3, false>(fp, x, none, y, bias_l, g,
-                           mask_store(a.h + 2 * hs, 256, a.dz + 2 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 2 * ms, a.dz + 2 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_2, false>(fp, y, none, x, bias_l, g,
-                           mask_store(a.h + 1 * hs, 256, a.dz + 1 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 1 * ms, a.dz + 1 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_1, false>(fp, x, none, y, bias_l, g,
-                           mask_store(a.h, 256, a.dz, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 0 * ms, a.dz, 256, rows, N, g, inv));
 }
 
 }  // namespace mlp
@@ -164,13 +163,13 @@ extern "C" int aon_mlp_bwd_pack(const aon_mlp_params* prm, void* packed, aon_str
   return pack_h(a, packed, (hipStream_t)stream);
 }
 
-extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const float* h, const float* hv,
+extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const uint32_t* masks,
                            int64_t N, float* dzv, float* dzb, float* dz, void* work,
                            aon_stream_t stream) {
-  AON_REQUIRE(packed && draw && h && hv && dzv && dzb && dz && work, "null pointer");
+  AON_REQUIRE(packed && draw && masks && dzv && dzb && dz && work, "null pointer");
   AON_REQUIRE(N >= 0, "bad shape");
-  AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(h) && aligned16(hv) &&
-                  aligned16(dzv) && aligned16(dzb) && aligned16(dz),
+  AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(masks) && aligned16(dzv) &&
+                  aligned16(dzb) && aligned16(dz),
               "buffers must be 16-byte aligned");
   if (N == 0) return 0;
   using G = GeomH<1>;
@@ -180,10 +179,38 @@ extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const float* h
   uint32_t* amax = static_cast<uint32_t*>(work);
   const int rc = absmax(draw, 4 * N, amax, st);
   if (rc) return rc;
-  BwdArgs args{draw, h, hv, dzv, dzb, dz, amax, N};
+  BwdArgs args{draw, reinterpret_cast<const uint2*>(masks), dzv, dzb, dz, amax, N};
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetBwdH::kStreamBytes);
   hipLaunchKernelGGL(k_mlp_bwd_f16x3, (unsigned)grid, G::kThreads, 0, st, ws, bias, args);
+  return launch_status(__func__);
+}
+
+// ReLU' bits of an activation tensor h (N x width, width = 32 x pairs <= 256) in the layout
+// RowStoreBits writes (the layer-by-layer forward's masks for the fused chains): word (row, g)
+// bit 4 t + r = h[row][16 t + 4 g + r] > 0.
+__global__ void k_relu_masks(const float* __restrict__ h, int64_t N, int width,
+                             uint2* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < 4 * N; i += stride) {
+    const int64_t row = i >> 2;
+    const int g = static_cast<int>(i & 3);
+    uint32_t b[2] = {0u, 0u};
+    for (int t = 0; t < width / 16; ++t)
+      for (int r = 0; r < 4; ++r)
+        if (h[row * width + 16 * t + 4 * g + r] > 0.0f) b[t >> 3] |= 1u << ((4 * t + r) & 31);
+    out[i] = uint2{b[0], b[1]};
+  }
+}
+
+extern "C" int aon_relu_masks(const float* h, int64_t N, int width, uint32_t* masks,
+                              aon_stream_t stream) {
+  AON_REQUIRE(h && masks, "null pointer");
+  AON_REQUIRE(N >= 0 && width >= 32 && width <= 256 && width % 32 == 0, "bad shape");
+  AON_REQUIRE(aligned16(masks), "masks must be 16-byte aligned");
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(k_relu_masks, grid_for(4 * N, 256, 65536), 256, 0, (hipStream_t)stream, h, N,
+                     width, reinterpret_cast<uint2*>(masks));
   return launch_status(__func__);
 }

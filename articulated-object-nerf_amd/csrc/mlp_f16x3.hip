@@ -119,11 +119,12 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   Frag<1, NCOL> none;
   using SP = StorePick<STORE, NCOL>;
   const int64_t hs = N * 256;  // one pts_linears output in ts.h
-  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g));
-  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 1 * hs, 256, rows, N, g));
-  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g));
-  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g));
-  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g));
+  const int64_t ms = N * 4;    // one layer's ReLU' bits in ts.masks
+  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g, ts.masks));
+  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 1 * hs, 256, rows, N, g, ts.masks + 1 * ms));
+  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g, ts.masks + 2 * ms));
+  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g, ts.masks + 3 * ms));
+  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g, ts.masks + 4 * ms));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c)
 #pragma unroll
@@ -132,9 +133,9 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
     }
   // skip: cat[h, enc] (model.py:102-103)
-  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g));
-  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g));
-  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g));
+  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g, ts.masks + 5 * ms));
+  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g, ts.masks + 6 * ms));
+  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g, ts.masks + 7 * ms));
   f4 dens[NCOL], rgb[NCOL];
   head_h<NetVanillaH, LDEN>(fp, y, dens, bias_l, g);             // model.py:105-107
   // bottleneck, no activation (model.py:109)
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
   }
   // cat[bottleneck, enc_dir] + ReLU (:110-116)
-  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g));
+  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g, ts.masks + 8 * ms));
   head_h<NetVanillaH, LRGB>(fp, y, rgb, bias_l, g);              // model.py:118
 
   if (g == 0) {

@@ -124,22 +124,43 @@ struct RowStore {
   }
 };
 
+#ifndef AON_MASK_AHEAD
+#define AON_MASK_AHEAD 1
+#endif
 template <int NCOL>
 struct MaskStore {
+  // a pair's masks are loaded kAhead pairs before its MFMAs start (its epilogue runs during the
+  // next pair's), in a ring of kAhead + 1 slots
+  static constexpr int kAhead = AON_MASK_AHEAD;
   const float* mrow[NCOL];  // h + row * ldh + 4 g (mask source), nullptr when row >= N
   float* rowp[NCOL];        // out + row * ld + 4 g, nullptr when row >= N or no store
   float s;
-  mutable f4 mk[2][2][NCOL];  // [pair parity][tile of the pair][column]
-  __device__ __forceinline__ void begin_pair(int pr) const {
+  int nf;                   // features per mask row (32 x the layer's output pairs)
+  mutable f4 mk[kAhead + 1][2][NCOL];  // [pair mod (kAhead + 1)][tile of the pair][column]
+  __device__ __forceinline__ void load(int q) const {
+    if (32 * q >= nf) return;  // past the layer's last pair
+#ifdef AON_ABLATE_MASK  // timing-only build: no mask loads (wrong results)
+    for (int uu = 0; uu < 2; ++uu)
+      for (int c = 0; c < NCOL; ++c) mk[q % (kAhead + 1)][uu][c] = f4{1.f, 1.f, 1.f, 1.f};
+    return;
+#endif
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu)
 #pragma unroll
       for (int c = 0; c < NCOL; ++c)
-        mk[pr & 1][uu][c] = mrow[c] ? *reinterpret_cast<const f4*>(mrow[c] + 16 * (2 * pr + uu))
-                                    : f4{0.f, 0.f, 0.f, 0.f};
+        mk[q % (kAhead + 1)][uu][c] = mrow[c] ? *reinterpret_cast<const f4*>(mrow[c] + 16 * (2 * q + uu))
+                                              : f4{0.f, 0.f, 0.f, 0.f};
+  }
+  __device__ __forceinline__ void begin_pair(int pr) const {
+    if (pr == 0) {
+#pragma unroll
+      for (int q = 0; q < kAhead; ++q) load(q);
+    } else {
+      load(pr + kAhead - 1);
+    }
   }
   __device__ __forceinline__ float post(int pr, int uu, int r, int c, float v) const {
-    return mk[pr & 1][uu][c][r] > 0.0f ? v : 0.0f;
+    return mk[pr % (kAhead + 1)][uu][c][r] > 0.0f ? v : 0.0f;
   }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     if (rowp[c])
@@ -147,11 +168,77 @@ struct MaskStore {
   }
 };
 
+// ReLU' as bits: the training forward records, per sample and lane group g, one 64-bit word
+// whose bit 4 t + r is (h[16 t + 4 g + r] > 0) for output tile t (32 B per sample and layer,
+// layout [layer][N][4] of uint2), so the backward chains read 1/32 of the bytes of the fp32
+// activations for their masks.  Written a byte per output pair (the pair's 2 tiles x 4 rows),
+// so nothing is carried across pairs.
+template <int NCOL>
+struct RowStoreBits : RowStore<NCOL> {
+  uint8_t* mrow[NCOL];  // bytes of word (row, g), nullptr when row >= N
+  bool narrow;          // 4-pair (128-wide) layer: bytes 4..7 of the word are written as 0
+  mutable uint32_t b[NCOL];  // the current pair's 8 bits (byte pr of the word)
+  __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
+    RowStore<NCOL>::put(pr, uu, r0, c, v0, v1);
+    const uint32_t m = (v0 > 0.0f ? 1u : 0u) | (v1 > 0.0f ? 2u : 0u);  // v: post-ReLU, s > 0
+    const int bit = 4 * uu + r0;  // within the pair's byte (compile-time after unrolling)
+    b[c] = bit == 0 ? m : (b[c] | (m << bit));
+    if (uu == 1 && r0 == 2 && mrow[c]) {
+      mrow[c][pr] = static_cast<uint8_t>(b[c]);
+      if (narrow) mrow[c][pr + 4] = 0;
+    }
+  }
+};
+
+// Backward-chain epilogue with ReLU' from those bits (MaskStore's job without reading the
+// activations): the layer's word is loaded when its first pair starts.
+template <int NCOL>
+struct MaskBits {
+  const uint2* mrow[NCOL];  // masks + row * 4 + g, nullptr when row >= N
+  float* rowp[NCOL];        // out + row * ld + 4 g, nullptr when row >= N
+  float s;
+  mutable uint2 m[NCOL];
+  __device__ __forceinline__ void begin_pair(int pr) const {
+    if (pr == 0) {
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) m[c] = mrow[c] ? *mrow[c] : uint2{0u, 0u};
+    }
+  }
+  __device__ __forceinline__ float post(int pr, int uu, int r, int c, float v) const {
+    const int bit = 4 * (2 * pr + uu) + r;
+    const uint32_t w = bit < 32 ? m[c].x : m[c].y;
+    return (w >> (bit & 31)) & 1u ? v : 0.0f;
+  }
+  __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
+    if (rowp[c])
+      *reinterpret_cast<float2*>(rowp[c] + 16 * (2 * pr + uu) + r0) = float2{v0 * s, v1 * s};
+  }
+};
+
+template <int NCOL>
+__device__ __forceinline__ MaskBits<NCOL> mask_bits(const uint2* mbase, float* obase, int ld,
+                                                    const int64_t (&rows)[NCOL], int64_t N, int g,
+                                                    float s) {
+  MaskBits<NCOL> mb;
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    const bool ok = rows[c] < N;
+    mb.mrow[c] = ok ? mbase + rows[c] * 4 + g : nullptr;
+    mb.rowp[c] = ok ? obase + rows[c] * ld + 4 * g : nullptr;
+  }
+  mb.s = s;
+  return mb;
+}
+
 // NoStore (STORE = false) or a RowStore at y + row * ld (true scale) for the training forward
 template <bool STORE, int NCOL>
 struct StorePick {
   __device__ __forceinline__ static NoStore make(float*, int, const int64_t (&)[NCOL], int64_t,
                                                  int) {
+    return {};
+  }
+  __device__ __forceinline__ static NoStore make(float*, int, const int64_t (&)[NCOL], int64_t,
+                                                 int, uint2*) {
     return {};
   }
 };
@@ -164,6 +251,20 @@ struct StorePick<true, NCOL> {
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + rows[c] * ld + 4 * g : nullptr;
     r.s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;
+    return r;
+  }
+  // a ReLU layer: also its ReLU' bits at mbase ([N][4] uint2); ld / 32 output pairs
+  __device__ __forceinline__ static RowStoreBits<NCOL> make(float* base, int ld,
+                                                            const int64_t (&rows)[NCOL], int64_t N,
+                                                            int g, uint2* mbase) {
+    RowStoreBits<NCOL> r;
+    static_cast<RowStore<NCOL>&>(r) = make(base, ld, rows, N, g);
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+      r.mrow[c] = rows[c] < N ? reinterpret_cast<uint8_t*>(mbase + rows[c] * 4 + g) : nullptr;
+      r.b[c] = 0u;
+    }
+    r.narrow = ld == 128;
     return r;
   }
 };
@@ -191,6 +292,7 @@ __device__ __forceinline__ MaskStore<NCOL> mask_store(const float* hbase, int ld
     m.rowp[c] = ok ? obase + rows[c] * ld + 4 * g : nullptr;
   }
   m.s = s;
+  m.nf = ldh;
   return m;
 }
 

@@ -261,6 +261,7 @@ struct TrainStore {
   float* bot;
   float* hv;
   const float* noise;
+  uint2* masks;  // (9, N, 4) ReLU' bits of h0..h7, hv (RowStoreBits)
 };
 
 // activations the articulated training forward keeps (aon_mlp_art_fwd_train)
@@ -272,6 +273,7 @@ struct TrainStoreArt {
   float* enc;   // (N, 63) pos_enc(x'); enc[:, :3] = x'
   float* xyz;   // (N, 3) the sample points (deformation input)
   const float* noise;  // (N) added to raw_sigma, or nullptr
+  uint2* masks;        // (16, N, 4) ReLU' bits of hd0..3, h0..7, hv0..3 (RowStoreBits)
 };
 
 // fp16x3 path (mlp_f16x3.hip)

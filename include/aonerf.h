@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 2
+#define AON_ABI_VERSION 3
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -146,15 +146,23 @@ int aon_mlp_fwd_encoded(const void* packed, int precision, const float* x,
  * kernel: as aon_mlp_fwd with AON_ACT_NONE (packed = AON_PREC_F16X3 stream), plus every
  * hidden activation kept for the backward -- h (8, B*S, 256): post-ReLU pts_linears.0..7,
  * bot (B*S, 256): bottleneck_layer, hv (B*S, 128): post-ReLU views_linear.0 -- and
- * raw_sigma + noise[row] when noise (B*S) is not NULL. */
+ * raw_sigma + noise[row] when noise (B*S) is not NULL.  masks (9, B*S, 4) pairs of uint32:
+ * the ReLU' bits of h0..h7, hv for the backward chain (word (row, g), bit 4 t + r = output
+ * feature 16 t + 4 g + r > 0; aon_relu_masks builds the same from stored activations). */
 int aon_mlp_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
                       const float* viewdirs, const float* t, int64_t B, int S, const float* noise,
-                      float* h, float* bot, float* hv, float* raw, aon_stream_t stream);
+                      float* h, float* bot, float* hv, float* raw, uint32_t* masks,
+                      aon_stream_t stream);
+
+/* ReLU' bits of an activation tensor h (N x width, width a multiple of 32 up to 256) in the
+ * layout of aon_mlp_fwd_train's masks (N, 4) pairs of uint32 -- for the fused backward chains
+ * after a layer-by-layer forward (threshold_backward of model.py:95-120's ReLUs). */
+int aon_relu_masks(const float* h, int64_t N, int width, uint32_t* masks, aon_stream_t stream);
 
 /* Backward chain of one level's NeRFMLP for the training step (model.py:95-120 under
  * autograd): from draw (B*S, 4) = dL/d[raw_rgb, raw_sigma] (aon_composite_bwd), all input-
  * gradient products dX = dZ W down to pts_linears.0 in one fused kernel, each masked by ReLU'
- * of the stored forward activation it flows into (h, hv from aon_mlp_fwd_train), writing
+ * of the forward output it flows into (masks: the ReLU' bits of aon_mlp_fwd_train), writing
  *   dzv (B*S, 128): dL/d pre-activation of views_linear.0,
  *   dzb (B*S, 256): dL/d bottleneck_layer output,
  *   dz  (8, B*S, 256): dL/d pre-activation of pts_linears.i,
@@ -163,8 +171,8 @@ int aon_mlp_fwd_train(const void* packed, const float* rays_o, const float* rays
  * of device scratch. */
 size_t aon_mlp_bwd_packed_bytes(void);
 int aon_mlp_bwd_pack(const aon_mlp_params* params, void* packed, aon_stream_t stream);
-int aon_mlp_bwd(const void* packed, const float* draw, const float* h, const float* hv,
-                int64_t N, float* dzv, float* dzb, float* dz, void* work, aon_stream_t stream);
+int aon_mlp_bwd(const void* packed, const float* draw, const uint32_t* masks, int64_t N,
+                float* dzv, float* dzb, float* dz, void* work, aon_stream_t stream);
 
 /* ---------------------------------------------------------------- articulated MLP */
 /* Device pointers to one articulated NeRFMLP's nn.Linear parameters in torch layout
@@ -208,15 +216,18 @@ int aon_mlp_art_fwd(const void* packed, const float* rays_o, const float* rays_d
  * autograd): aon_mlp_art_fwd (MODE 0 inputs, raw outputs, no activation) that also keeps what
  * the backward needs -- hd (4, B*S, 128) deformation layers, h (8, B*S, 256) pts_linears, bot
  * (B*S, 256), hv (4, B*S, 128) views_linear, enc (B*S, 63) = pos_enc(x') and xyz (B*S, 3) the
- * sample points; raw_sigma += noise[r] when noise != NULL (:318-319).  Activation buffers 8-byte
- * aligned, raw 16-byte aligned. */
+ * sample points; raw_sigma += noise[r] when noise != NULL (:318-319); masks (16, B*S, 4) pairs
+ * of uint32: the ReLU' bits of hd0..3, h0..7, hv0..3 (layout of aon_mlp_fwd_train's).  Activation
+ * buffers 8-byte aligned, raw and masks 16-byte aligned. */
 int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
                           const float* viewdirs, const float* t, int64_t B, int S,
                           const float* noise, float* hd, float* h, float* bot, float* hv,
-                          float* enc, float* xyz, float* raw, aon_stream_t stream);
+                          float* enc, float* xyz, float* raw, uint32_t* masks,
+                          aon_stream_t stream);
 
 /* Backward chain of one articulated level (autograd of model_autodecoder.py:168-239): from
- * dL/d raw (N, 4) and the forward's kept tensors (aon_mlp_art_fwd_train: hd, h, hv, enc) to
+ * dL/d raw (N, 4), the ReLU' bits (16, N, 4) of hd0..3, h0..7, hv0..3 and pos_enc(x') (enc) kept
+ * by aon_mlp_art_fwd_train, to
  * every layer's dL/d pre-activation -- dzv (4, N, 128) views_linear.i, dbot (N, 256) the
  * bottleneck output, dz (8, N, 256) pts_linears.i, dxp (N, 3) = dL/dx' (the deformation head's
  * output, through pos_enc's backward), dzd (4, N, 128) deformations_linear.i -- the operands of
@@ -224,9 +235,9 @@ int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* 
  * kLayersArtBwd); work: >= 4 bytes.  Buffers 16-byte aligned (dxp: 4). */
 size_t aon_mlp_art_bwd_packed_bytes(void);
 int aon_mlp_art_bwd_pack(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
-int aon_mlp_art_bwd(const void* packed, const float* draw, const float* hd, const float* h,
-                    const float* hv, const float* enc, int64_t N, float* dzv, float* dbot,
-                    float* dz, float* dxp, float* dzd, void* work, aon_stream_t stream);
+int aon_mlp_art_bwd(const void* packed, const float* draw, const uint32_t* masks,
+                    const float* enc, int64_t N, float* dzv, float* dbot, float* dz, float* dxp,
+                    float* dzd, void* work, aon_stream_t stream);
 
 /* The same on given sample points pos (B*S, 3) and encoded view directions condition (B, 27)
  * (NeRFMLP.forward(pos, condition, latents)). */

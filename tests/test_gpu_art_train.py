@@ -104,8 +104,11 @@ def test_fused_art_train_forward_activations():
     lat = tuple(cuda(v) for v in W.art_latents(1).values())
     P = [(m.weight.detach(), m.bias.detach()) for m in train_art.art_layers(mlp)]
     raw_f = torch.empty((B * S, 4), device="cuda")
+    masks = torch.empty((16, B * S, 8), dtype=torch.int32, device="cuda")
     xyz_f, hd_f, enc_f, h_f, bot_f, hv_f = train_art._forward_level_fused(geo, P, lat, o, d, d, t,
-                                                                         raw_f, noise)
+                                                                         raw_f, noise, masks)
+    # the ReLU' bits written by the forward == those built from its stored activations
+    assert torch.equal(masks, train_art.relu_masks(list(hd_f) + list(h_f) + list(hv_f), B * S))
     xyz = torch.empty((B * S, 3), device="cuda")
     L.call("aon_cast_rays", L.ptr(o), L.ptr(d), L.ptr(t), B, S, None, 0, L.ptr(xyz), 0, 0, None,
            L.stream())

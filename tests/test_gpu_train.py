@@ -169,7 +169,10 @@ def test_fused_train_forward_activations():
     noise = torch.rand(B * S, generator=gen).cuda()
     P = [(m.weight.detach(), m.bias.detach()) for m in net.fine_mlp._layers()]
     raw_f = torch.empty((B * S, 4), device="cuda")
-    h_f, bot_f, hv_f = train._forward_level_fused(P, o, d, d, t, raw_f, noise)
+    masks = torch.empty((9, B * S, 8), dtype=torch.int32, device="cuda")
+    h_f, bot_f, hv_f = train._forward_level_fused(P, o, d, d, t, raw_f, noise, masks)
+    # the ReLU' bits written by the forward == those built from its stored activations
+    assert torch.equal(masks, train.relu_masks(list(h_f) + [hv_f], B * S))
     enc = torch.empty((B * S, 63), device="cuda")
     L = train.L
     L.call("aon_cast_rays", L.ptr(o), L.ptr(d), L.ptr(t), B, S, None, 0, None, 0, 10, L.ptr(enc),
