@@ -102,10 +102,10 @@ struct Frag {
 // MFMAs), post() maps a finished value (after the optional ReLU), put() sees the pair's values 2
 // at a time.  NoStore compiles away.  RowStore copies a layer's activations to HBM (the
 // training forward keeps them for the backward): one 8-B store to y[row][16 u + 4 g + r] at
-// true scale (v * s) per part; rows past the batch are not stored.  MaskStore is the backward
-// chain's epilogue: the value is kept where the forward activation h[row][feature] > 0 (ReLU'
-// from the stored output, as torch's threshold_backward), loaded one pair ahead of its use,
-// and the product (true scale) is stored for the weight-gradient GEMMs.
+// true scale (v * s) per part; rows past the batch are not stored.  RowStoreBits also records
+// the ReLU' bits; MaskBits is the backward chains' epilogue: the value is kept where the forward
+// output it flows into was > 0 (torch's threshold_backward on the ReLU output) and the product
+// (true scale) is stored for the weight-gradient GEMMs.
 struct NoStore {
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
@@ -118,50 +118,6 @@ struct RowStore {
   float s;            // to true scale (a power of two: exact)
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
-  __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
-    if (rowp[c])
-      *reinterpret_cast<float2*>(rowp[c] + 16 * (2 * pr + uu) + r0) = float2{v0 * s, v1 * s};
-  }
-};
-
-#ifndef AON_MASK_AHEAD
-#define AON_MASK_AHEAD 1
-#endif
-template <int NCOL>
-struct MaskStore {
-  // a pair's masks are loaded kAhead pairs before its MFMAs start (its epilogue runs during the
-  // next pair's), in a ring of kAhead + 1 slots
-  static constexpr int kAhead = AON_MASK_AHEAD;
-  const float* mrow[NCOL];  // h + row * ldh + 4 g (mask source), nullptr when row >= N
-  float* rowp[NCOL];        // out + row * ld + 4 g, nullptr when row >= N or no store
-  float s;
-  int nf;                   // features per mask row (32 x the layer's output pairs)
-  mutable f4 mk[kAhead + 1][2][NCOL];  // [pair mod (kAhead + 1)][tile of the pair][column]
-  __device__ __forceinline__ void load(int q) const {
-    if (32 * q >= nf) return;  // past the layer's last pair
-#ifdef AON_ABLATE_MASK  // timing-only build: no mask loads (wrong results)
-    for (int uu = 0; uu < 2; ++uu)
-      for (int c = 0; c < NCOL; ++c) mk[q % (kAhead + 1)][uu][c] = f4{1.f, 1.f, 1.f, 1.f};
-    return;
-#endif
-#pragma unroll
-    for (int uu = 0; uu < 2; ++uu)
-#pragma unroll
-      for (int c = 0; c < NCOL; ++c)
-        mk[q % (kAhead + 1)][uu][c] = mrow[c] ? *reinterpret_cast<const f4*>(mrow[c] + 16 * (2 * q + uu))
-                                              : f4{0.f, 0.f, 0.f, 0.f};
-  }
-  __device__ __forceinline__ void begin_pair(int pr) const {
-    if (pr == 0) {
-#pragma unroll
-      for (int q = 0; q < kAhead; ++q) load(q);
-    } else {
-      load(pr + kAhead - 1);
-    }
-  }
-  __device__ __forceinline__ float post(int pr, int uu, int r, int c, float v) const {
-    return mk[pr % (kAhead + 1)][uu][c][r] > 0.0f ? v : 0.0f;
-  }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     if (rowp[c])
       *reinterpret_cast<float2*>(rowp[c] + 16 * (2 * pr + uu) + r0) = float2{v0 * s, v1 * s};
@@ -280,21 +236,6 @@ __device__ __forceinline__ float grad_scale(uint32_t bits) {
   return __builtin_ldexpf(1.0f, 8 - e);
 }
 
-template <int NCOL>
-__device__ __forceinline__ MaskStore<NCOL> mask_store(const float* hbase, int ldh, float* obase,
-                                                      int ld, const int64_t (&rows)[NCOL],
-                                                      int64_t N, int g, float s) {
-  MaskStore<NCOL> m;
-#pragma unroll
-  for (int c = 0; c < NCOL; ++c) {
-    const bool ok = rows[c] < N;
-    m.mrow[c] = ok ? hbase + rows[c] * ldh + 4 * g : nullptr;
-    m.rowp[c] = ok ? obase + rows[c] * ld + 4 * g : nullptr;
-  }
-  m.s = s;
-  m.nf = ldh;
-  return m;
-}
 
 // epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
 // part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
