@@ -146,7 +146,7 @@ struct RowStoreBits : RowStore<NCOL> {
   }
 };
 
-// Backward-chain epilogue with ReLU' from those bits (MaskStore's job without reading the
+// Backward-chain epilogue with ReLU' from those bits (no reads of the fp32
 // activations): the layer's word is loaded when its first pair starts.
 template <int NCOL>
 struct MaskBits {
