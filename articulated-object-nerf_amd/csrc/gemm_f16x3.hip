@@ -391,10 +391,13 @@ static int64_t gemm_splits(const aon_gemm_args* a) {
   // split the reduction only when the tile grid alone cannot fill the chip and K is long
   if (a->k_splits > 0) return a->k_splits;
   if (tiles >= 512 || a->K < 8 * 1024 || a->A2) return 1;
-  int64_t s = (1024 + tiles - 1) / tiles;
-  const int64_t smax = a->K / 2048;
-  if (s > smax) s = smax;
-  if (s > 256) s = 256;
+  // whole rounds of 512 workgroups (2 per CU): two rounds when K is long enough, else one --
+  // a grid a few workgroups past a round runs its tail as a second, nearly empty round (a
+  // 266k-row weight gradient on 544 workgroups took as long as one on 1024)
+  int64_t cap = a->K / 2048;
+  if (cap > 256) cap = 256;
+  int64_t s = cap * tiles >= 1024 ? 1024 / tiles : (cap < 512 / tiles ? cap : 512 / tiles);
+  if (s >= 8) s = s / 8 * 8;  // split_of places chunks in groups of 8 (one per XCD)
   return s < 1 ? 1 : s;
 }
 
