@@ -32,9 +32,12 @@ def gather_frame(local, H, W, dst=0, group=None):
     """Gather every rank's band payload (n_max, C) to `dst` -> (H*W, C) there, None elsewhere."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    dev = local.device
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        local = local.cpu()  # gloo is a host transport (CPU-only gather); RCCL gathers in HBM
     parts = [torch.empty_like(local) for _ in range(world)] if rank == dst else None
     dist.gather(local, parts, dst=dst, group=group)
-    return assemble(parts, H, W) if rank == dst else None
+    return assemble(parts, H, W).to(dev) if rank == dst else None
 
 
 def render_frame_sharded(model, c2w, H, W, focal, near=2.0, far=6.0, white_bkgd=True, dst=0,

@@ -1,0 +1,103 @@
+"""The multi-GPU paths with the real HIP kernels: two processes on the one GPU of the test box
+(gloo process group; on a node, bench.py / tools/bench_train.py run one process per GPU over
+RCCL with the same code).  (1) The row-band frame render + gather (aonerf.parallel,
+BASELINE config C4) equals the single-process render bit for bit.  (2) A DDP training step
+(tools/bench_train.py): after GradAllReduce every rank holds the average of the two ranks'
+gradients, bit for bit as computed from each batch alone."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+H, W = 24, 32
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _net():
+    from aonerf.model import NeRF
+    from aonerf.synthetic import init_like_reference
+
+    return init_like_reference(NeRF()).cuda()
+
+
+def _batch(seed, n=96):
+    from aonerf.ray_utils import frame_rays
+    from aonerf.render import create_spheric_poses, sapien_focal
+
+    rays = frame_rays(torch.as_tensor(create_spheric_poses(4.0)[3 + seed]), H, W, sapien_focal(H))
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.randperm(H * W, generator=g)[:n].cuda()
+    b = {k: v[idx].contiguous() for k, v in rays.items()}
+    b["target"] = torch.rand(n, 3, generator=g).cuda()
+    u = (torch.rand(n, 65, generator=g).cuda(), torch.rand(n, 128, generator=g).cuda())
+    return b, u
+
+
+def _grads(net, seed):
+    from aonerf import train
+
+    b, (uc, uf) = _batch(seed)
+    for p in net.parameters():
+        p.grad = None
+    loss, _ = train.training_step(net, b, True, True, 2.0, 6.0, u_coarse=uc, u_fine=uf)
+    loss.backward()
+    return [p.grad.clone() for p in net.parameters()]
+
+
+def _worker(rank, world, port, q):
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from aonerf.parallel import GradAllReduce, render_frame_sharded
+        from aonerf.render import create_spheric_poses, sapien_focal
+
+        net = _net()
+        frame, _ = render_frame_sharded(net, create_spheric_poses(4.0)[7], H, W, sapien_focal(H))
+        grads = _grads(net, rank)
+        GradAllReduce(net.parameters())()
+        # numpy arrays: pickled by value (a tensor would travel as a shared-memory handle that
+        # dies with this process)
+        q.put((rank, frame.cpu().numpy() if frame is not None else None,
+               [p.grad.cpu().numpy() for p in net.parameters()]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_render_and_ddp_step_two_ranks():
+    from aonerf.render import create_spheric_poses, render_frame, sapien_focal
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (f, g)) for r, f, g in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # (1) frame: bands of 12 rows rendered by two processes == one process, bit for bit
+    net = _net()
+    ref = render_frame(net, create_spheric_poses(4.0)[7], H, W, sapien_focal(H)).cpu()
+    assert got[0][0] is not None and got[1][0] is None
+    np.testing.assert_array_equal(got[0][0], ref.numpy())
+    # (2) DDP: every rank holds (g_rank0 + g_rank1) / 2 of the single-batch gradients
+    g0, g1 = _grads(net, 0), _grads(net, 1)
+    for r in range(world):
+        for a, b, c in zip(got[r][1], g0, g1):
+            np.testing.assert_array_equal(a, ((b + c) / 2).cpu().numpy())
