@@ -19,6 +19,10 @@
 namespace aon {
 namespace mlp {
 
+#ifndef AON_STASH_REGS
+#define AON_STASH_REGS 0  // 1: keep the encodings in VGPRs instead of parking them in LDS
+#endif
+
 // MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: encoded x (N, 63), condition (B, 27)
 template <int MODE, int NCOL, bool STORE = false>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_fwd_f16x3(
@@ -27,7 +31,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     int64_t B, int S, int act, float* __restrict__ raw, TrainStore ts = {}) {
   using G = GeomH<NCOL>;
   // ONE __shared__ object: weight ring | bias table | per-lane stash of the encodings
-  constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
+  constexpr int kStash = AON_STASH_REGS ? 0 : G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
   __shared__ f4 smem[kLdsWeights + kBiasFloats / 4 + kStash];
   float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
   f4* stash = smem + kLdsWeights + kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 6 * NCOL +
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   // park the encodings in LDS until the skip / view layers need them (frees 24 VGPRs for the
   // fragment prefetch); only the owning lane ever touches its slots
 #pragma unroll
-  for (int c = 0; c < NCOL; ++c) {
+  for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       stash[64 * (6 * c + 2 * k)] = __builtin_bit_cast(f4, enc.hi[k][c]);
@@ -113,6 +117,9 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 
   FragPipe<WeightPipe<NetVanillaH, G::kThreads>> fp(p);
   fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
+#if AON_PRIO_HALF
+  if (wave >= G::kWaves / 2) __builtin_amdgcn_s_setprio(AON_PRIO_HALF);
+#endif
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);  // this lane group's rows of the bias table
 
   Frag<8, NCOL> x, y;
@@ -126,7 +133,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g, ts.masks + 3 * ms));
   layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g, ts.masks + 4 * ms));
 #pragma unroll
-  for (int c = 0; c < NCOL; ++c)
+  for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
@@ -141,7 +148,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   // bottleneck, no activation (model.py:109)
   layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g, SP::make(ts.bot, 256, rows, N, g));
 #pragma unroll
-  for (int c = 0; c < NCOL; ++c) {
+  for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c) {
     venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
     venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
   }

@@ -412,14 +412,22 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
 #endif
 constexpr int kRing = AON_RING;      // LDS-DMA ring depth (chunks in LDS)
 constexpr int kChunkH = AON_CHUNK_H;  // 1-KB blocks per chunk
+#ifndef AON_RING_LEAD
+#define AON_RING_LEAD (AON_RING - 1)
+#endif
+constexpr int kRingLead = AON_RING_LEAD;  // chunks in flight ahead of the one in use
 // Weight pipeline: the LDS-DMA ring over the network's stream
 template <typename Net, int THREADS>
-using WeightPipe = DmaPipe<THREADS, kRing, kChunkH, Net::kStreamBlocks, Net::kBlocks>;
+using WeightPipe = DmaPipe<THREADS, kRing, kChunkH, Net::kStreamBlocks, Net::kBlocks, kRingLead>;
 constexpr int kLdsWeights = kRing * kChunkH * 64;  // f4
+
+#ifndef AON_WAVES_H
+#define AON_WAVES_H 8  // waves per workgroup at 16 samples per wave (2 waves per SIMD either way)
+#endif
 
 template <int NCOL>
 struct GeomH {
-  static constexpr int kWaves = NCOL == 1 ? 8 : 4;
+  static constexpr int kWaves = NCOL == 1 ? AON_WAVES_H : 4;
   static constexpr int kThreads = 64 * kWaves;
   static constexpr int kRowsPerWave = 16 * NCOL;
   static constexpr int kRowsPerBlock = kRowsPerWave * kWaves;

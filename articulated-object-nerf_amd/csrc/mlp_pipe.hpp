@@ -65,8 +65,12 @@ __device__ __forceinline__ __attribute__((address_space(3))) const T* opaque_lds
 
 // s_waitcnt vmcnt(n) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | [15:14], expcnt[6:4], lgkmcnt[11:8]).
 // The builtin wants a literal: after unrolling n is a constant and the switch folds to one case.
-#define AON_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4))
-__device__ __forceinline__ void wait_vm_lgkm0(int n) {
+// (vmcnt has 6 bits; the switch covers the 0..31 the pipelines can need.)
+// LGKM = 0 also drains the LDS reads, LGKM = 15 leaves them alone.
+#define AON_WAIT_VM(n) \
+  __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (LGKM << 8))
+template <int LGKM>
+__device__ __forceinline__ void wait_vm(int n) {
   switch (n) {
     case 0: AON_WAIT_VM(0); break;
     case 1: AON_WAIT_VM(1); break;
@@ -83,10 +87,27 @@ __device__ __forceinline__ void wait_vm_lgkm0(int n) {
     case 12: AON_WAIT_VM(12); break;
     case 13: AON_WAIT_VM(13); break;
     case 14: AON_WAIT_VM(14); break;
-    default: AON_WAIT_VM(15); break;
+    case 15: AON_WAIT_VM(15); break;
+    case 16: AON_WAIT_VM(16); break;
+    case 17: AON_WAIT_VM(17); break;
+    case 18: AON_WAIT_VM(18); break;
+    case 19: AON_WAIT_VM(19); break;
+    case 20: AON_WAIT_VM(20); break;
+    case 21: AON_WAIT_VM(21); break;
+    case 22: AON_WAIT_VM(22); break;
+    case 23: AON_WAIT_VM(23); break;
+    case 24: AON_WAIT_VM(24); break;
+    case 25: AON_WAIT_VM(25); break;
+    case 26: AON_WAIT_VM(26); break;
+    case 27: AON_WAIT_VM(27); break;
+    case 28: AON_WAIT_VM(28); break;
+    case 29: AON_WAIT_VM(29); break;
+    case 30: AON_WAIT_VM(30); break;
+    default: AON_WAIT_VM(31); break;
   }
 }
 #undef AON_WAIT_VM
+__device__ __forceinline__ void wait_vm_lgkm0(int n) { wait_vm<0>(n); }
 
 // LDS-DMA ring: chunk c is copied HBM/L2 -> LDS buffer c % NBUF by global_load_lds (16 B per
 // lane, no VGPR staging), NBUF - 1 chunks ahead of its first use.  At the first use of chunk c
@@ -95,8 +116,13 @@ __device__ __forceinline__ void wait_vm_lgkm0(int n) {
 // the buffer of chunk c - 1 (fully read: every wave is past its last use) is refilled with
 // chunk c + NBUF - 1.  All LDS of the kernel lives in ONE __shared__ array (a second object can
 // make hipcc drain vmcnt before every ds_read, cdna_hip_programming.md section 5 item 4a).
+//
+// LEAD < NBUF - 1 (chunks in flight ahead of the one in use) refills the buffer of chunk
+// c + LEAD - NBUF <= c - 2 instead: every wave finished reading it before it could reach chunk
+// c - 1's fragments (LDS reads complete in order and the prefetch reaches less than a chunk
+// ahead), so begin() need not drain the wave's LDS reads before the barrier.
 template <int THREADS, int NBUF, int CHUNK, int STREAM_BLOCKS = kStreamBlocks,
-          int USED_BLOCKS = kBlocks>
+          int USED_BLOCKS = kBlocks, int LEAD = NBUF - 1>
 struct DmaPipe {
   static constexpr int kChunk = CHUNK;  // 1-KB blocks per chunk (shadows the fp32 pipe's)
   static constexpr int kNumChunks = STREAM_BLOCKS / CHUNK;
@@ -105,6 +131,7 @@ struct DmaPipe {
   static constexpr int kCopies = kChunk * 64 / THREADS;  // 16-B copies per thread per chunk
   static_assert(kCopies * THREADS == kChunk * 64, "chunk must split evenly over threads");
   static_assert(NBUF >= 2, "ring needs two buffers");
+  static_assert(LEAD >= 1 && LEAD <= NBUF - 1, "chunks ahead");
   f4* wbuf;  // [NBUF][kChunk * 64] f4
   const f4* __restrict__ src;
   int tid, lane;
@@ -148,18 +175,22 @@ struct DmaPipe {
     m0_wave = __builtin_amdgcn_readfirstlane(
         static_cast<uint32_t>(reinterpret_cast<uintptr_t>(wbuf + (tid & ~63))));
 #pragma unroll
-    for (int c = 0; c < NBUF - 1 && c < kNumChunks; ++c) issue(c);
+    for (int c = 0; c < LEAD && c < kNumChunks; ++c) issue(c);
   }
   __device__ __forceinline__ void begin(int c) {
 #ifdef AON_ABLATE_RING  // timing-only build: every chunk reads buffer 0 (wrong results)
     if (c > 0) return;
 #endif
-    // copies issued after chunk c's: chunks c+1 .. min(c+NBUF-2, last)
-    const int ahead = (c + NBUF - 2 < kNumChunks - 1 ? c + NBUF - 2 : kNumChunks - 1) - c;
-    static_assert((NBUF - 2) * kCopies <= 15, "vmcnt budget");
-    wait_vm_lgkm0(ahead * kCopies);
+    // copies issued after chunk c's: chunks c+1 .. min(c+LEAD-1, last)
+    const int ahead = (c + LEAD - 1 < kNumChunks - 1 ? c + LEAD - 1 : kNumChunks - 1) - c;
+    static_assert((LEAD - 1) * kCopies <= 31, "vmcnt budget");
+    // chunk 0's barrier also publishes what the kernel staged in LDS before the loop
+    if (LEAD == NBUF - 1 || c == 0)
+      wait_vm<0>(ahead * kCopies);
+    else
+      wait_vm<15>(ahead * kCopies);
     __builtin_amdgcn_s_barrier();
-    if (c + NBUF - 1 < kNumChunks) issue(c + NBUF - 1);
+    if (c + LEAD < kNumChunks) issue(c + LEAD);
   }
   __device__ __forceinline__ f4 block(int b) const {
 #ifdef AON_ABLATE_RING
