@@ -6,7 +6,9 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 
 #include "aonerf.h"
 
@@ -41,6 +43,30 @@ inline int grid_for(int64_t work, int per_block, int cap = 1 << 20) {
   if (g < 1) g = 1;
   if (g > cap) g = cap;
   return static_cast<int>(g);
+}
+
+// Workgroups of `kernel` the device keeps resident at once (occupancy x CUs), queried once per
+// kernel.  A grid-stride kernel that software-pipelines over its items launches at most this
+// many: a second, partial round of workgroups would add a tail of one workgroup's duration.
+inline int64_t resident_blocks(const void* kernel, int threads) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int64_t> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  int dev = 0, cus = 0, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0);
+  const int64_t r = static_cast<int64_t>(cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  cache.emplace(kernel, r);
+  return r;
+}
+
+template <typename Kernel>
+inline int resident_grid(Kernel kernel, int threads, int64_t work_blocks) {
+  const int64_t r = resident_blocks(reinterpret_cast<const void*>(kernel), threads);
+  return grid_for(work_blocks, 1, static_cast<int>(r));
 }
 
 // torch.nan_to_num(x, nan=nan_val) with default posinf/neginf (float max / lowest)

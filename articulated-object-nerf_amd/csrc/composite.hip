@@ -56,13 +56,16 @@ __device__ __forceinline__ double wave_incl_prod(double x) {
 // fp64) carried across blocks, and the per-ray sums are evaluated in torch's CPU order by the
 // whole wave (wave_row_sums) from planar LDS arrays w, w*t, w*r, w*g, w*b.
 // RAW4: rgb and sigma interleaved as one (.., 4) fp32 row, 16-B aligned -> one dwordx4 load.
-template <int NB, bool RAW4>
+// SC > 0: the sample count as a compile-time constant (the render's 65 and 193), so the
+// torch-order sum schedule (task split, chunk counts, tails) folds to constants.
+template <int NB, bool RAW4, int SC = 0>
 __global__ __launch_bounds__(64 * kCompWaves) void k_composite_fwd(
     const float* __restrict__ rgb, int64_t rgb_stride, const float* __restrict__ sig,
     int64_t sig_stride, const float* __restrict__ tv, const float* __restrict__ dirs, int64_t B,
-    int S, int white, int act, float* __restrict__ out_rgb, float* __restrict__ out_acc,
+    int S_rt, int white, int act, float* __restrict__ out_rgb, float* __restrict__ out_acc,
     float* __restrict__ out_w, float* __restrict__ out_depth) {
   constexpr int SM = 64 * NB;
+  const int S = SC > 0 ? SC : S_rt;
   __shared__ float lds_all[kCompWaves][5 * SM + kCompScratch + 32];
   float* P = lds_all[threadIdx.x >> 6];  // P[q * SM + i]: q = 0 w, 1 w*t, 2..4 w*rgb
   float* scratch = P + 5 * SM;
@@ -179,16 +182,16 @@ __global__ __launch_bounds__(64 * kCompWaves) void k_composite_fwd(
   }
 }
 
-template <int NB>
+template <int NB, int SC = 0>
 static void launch_composite(bool raw4, int grid, hipStream_t st, const float* rgb,
                              int64_t rgb_stride, const float* sig, int64_t sig_stride,
                              const float* t, const float* dirs, int64_t B, int S, int white,
                              int act, float* comp, float* acc, float* w, float* depth) {
   if (raw4)
-    hipLaunchKernelGGL((k_composite_fwd<NB, true>), grid, 64 * kCompWaves, 0, st, rgb, rgb_stride,
-                       sig, sig_stride, t, dirs, B, S, white, act, comp, acc, w, depth);
+    hipLaunchKernelGGL((k_composite_fwd<NB, true, SC>), grid, 64 * kCompWaves, 0, st, rgb,
+                       rgb_stride, sig, sig_stride, t, dirs, B, S, white, act, comp, acc, w, depth);
   else
-    hipLaunchKernelGGL((k_composite_fwd<NB, false>), grid, 64 * kCompWaves, 0, st, rgb,
+    hipLaunchKernelGGL((k_composite_fwd<NB, false, SC>), grid, 64 * kCompWaves, 0, st, rgb,
                        rgb_stride, sig, sig_stride, t, dirs, B, S, white, act, comp, acc, w,
                        depth);
 }
@@ -209,6 +212,15 @@ extern "C" int aon_composite_fwd(const float* rgb, int64_t rgb_stride, const flo
   const bool raw4 = rgb_stride == 4 && sigma_stride == 4 && sigma == rgb + 3 && aligned16(rgb);
   const int grid = grid_for(B, kCompWaves, 1 << 16);
   hipStream_t st = (hipStream_t)stream;
+  if (S == 193 || S == 65) {  // the render's levels (64 + 1 coarse, 64 + 1 + 128 fine)
+    if (S == 193)
+      launch_composite<4, 193>(raw4, grid, st, rgb, rgb_stride, sigma, sigma_stride, t, dirs, B,
+                               S, white_bkgd, act, comp_rgb, acc, weights, depth);
+    else
+      launch_composite<2, 65>(raw4, grid, st, rgb, rgb_stride, sigma, sigma_stride, t, dirs, B,
+                              S, white_bkgd, act, comp_rgb, acc, weights, depth);
+    return launch_status(__func__);
+  }
   switch ((S + 63) / 64) {
 #define AON_COMP_CASE(nb)                                                                       \
   case nb:                                                                                      \

@@ -46,35 +46,63 @@ __device__ __forceinline__ int count_lt(const float* a, int n, float x) {
   return lo;
 }
 
+// per-wave LDS, sized for rows of up to 64 * NBX entries (bins, weights, samples, t_merge)
+template <int NBX>
 struct PdfLds {
-  float bins[kMaxBins];
-  float cdf[kMaxBins];
-  float samp[kMaxNs];
-  float tm[kMaxNt];
+  float bins[64 * NBX];
+  float cdf[64 * NBX];
+  float w[64 * NBX];
+  float samp[64 * NBX];
+  float tm[64 * NBX];
 };
 
+// A ray's inputs -- its t_merge row (or bins), weights and u, NBX 64-entry blocks of each -- are
+// read by coalesced wave-wide loads into registers ONE RAY AHEAD: the wave loops over rays (a
+// resident grid) and issues ray r + 1's loads before ray r's math, so the weight sum, scan and
+// searches never wait on HBM.
+template <int NBX>
 __global__ __launch_bounds__(64 * kPdfWaves) void k_sample_pdf(
     const float* __restrict__ bins_g, int64_t bins_stride, const float* __restrict__ w_g,
     int64_t w_stride, int64_t B, int nb, int Ns, int Ns_pow2, const float* __restrict__ u_g,
     int64_t u_stride, const float* __restrict__ tm_g, int Nt, const float* __restrict__ ro,
     const float* __restrict__ rd, float* __restrict__ out, float* __restrict__ xyz) {
-  __shared__ PdfLds lds_all[kPdfWaves];
+  __shared__ PdfLds<NBX> lds_all[kPdfWaves];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  PdfLds& L = lds_all[wid];
+  PdfLds<NBX>& L = lds_all[wid];
   const int nw = nb - 1;
   const int64_t nwaves = (int64_t)gridDim.x * kPdfWaves;
-  for (int64_t ray = (int64_t)blockIdx.x * kPdfWaves + wid; ray < B; ray += nwaves) {
-    // ---- stage t_merge and bins
-    if (tm_g) {
-      for (int i = lane; i < Nt; i += 64) L.tm[i] = tm_g[ray * Nt + i];
+  // this lane's entries 64 b + lane of t_merge, bins, weights and u: current ray, next ray
+  float ct[NBX], cb[NBX], cw[NBX], cu[NBX];
+  float pt[NBX], pb[NBX], pw[NBX], pu[NBX];
+  auto load_ray = [&](int64_t r, float(&tv)[NBX], float(&bv)[NBX], float(&wv)[NBX],
+                      float(&uv)[NBX]) {
+#pragma unroll
+    for (int b = 0; b < NBX; ++b) {
+      const int i = 64 * b + lane;
+      tv[b] = tm_g && i < Nt ? tm_g[r * Nt + i] : 0.f;
+      bv[b] = bins_g && i < nb ? bins_g[r * bins_stride + i] : 0.f;
+      wv[b] = i < nw ? w_g[r * w_stride + i] : 0.f;
+      uv[b] = i < Ns ? u_g[r * u_stride + i] : 0.f;
+    }
+  };
+  int64_t ray = (int64_t)blockIdx.x * kPdfWaves + wid;
+  if (ray < B) load_ray(ray, ct, cb, cw, cu);
+  for (; ray < B; ray += nwaves) {
+    if (ray + nwaves < B) load_ray(ray + nwaves, pt, pb, pw, pu);
+    // ---- stage t_merge, bins and the weights
+#pragma unroll
+    for (int b = 0; b < NBX; ++b) {
+      const int i = 64 * b + lane;
+      if (tm_g && i < Nt) L.tm[i] = ct[b];
+      if (bins_g && i < nb) L.bins[i] = cb[b];
+      if (i < nw) L.w[i] = cw[b];
     }
     wave_sync();
-    for (int k = lane; k < nb; k += 64) {
-      L.bins[k] = bins_g ? bins_g[ray * bins_stride + k]
-                         : __fmul_rn(0.5f, __fadd_rn(L.tm[k + 1], L.tm[k]));
+    if (!bins_g) {  // bins = mids of t_merge (model.py:163)
+      for (int k = lane; k < nb; k += 64) L.bins[k] = __fmul_rn(0.5f, __fadd_rn(L.tm[k + 1], L.tm[k]));
     }
     // ---- weight sum (torch CPU order, torch_sum.hpp) + padding (helper.py:206-212)
-    const float* w = w_g + ray * w_stride;
+    const float* w = L.w;
     float part = 0.f;
     if (nw >= 8) {
       if (lane < 8) part = inner_sum_lane([&](int e) { return w[e]; }, nw, lane);
@@ -110,11 +138,13 @@ __global__ __launch_bounds__(64 * kPdfWaves) void k_sample_pdf(
     }
     wave_sync();
     // ---- inverse cdf (helper.py:232-241)
-    const float* u = u_g + ray * u_stride;
-    for (int j = lane; j < Ns_pow2; j += 64) {
+#pragma unroll
+    for (int b = 0; b < NBX; ++b) {
+      const int j = 64 * b + lane;
+      if (j >= Ns_pow2) break;
       float s = __builtin_inff();  // sort padding
       if (j < Ns) {
-        const float uj = u[j];
+        const float uj = cu[b];
         const int idx = count_le(L.cdf, nb, uj);
         const int i0 = idx - 1 < 0 ? 0 : (idx - 1 > nb - 1 ? nb - 1 : idx - 1);
         const int i1 = idx > nb - 1 ? nb - 1 : idx;
@@ -181,7 +211,24 @@ __global__ __launch_bounds__(64 * kPdfWaves) void k_sample_pdf(
       }
     }
     wave_sync();  // LDS reuse by the next ray of this wave
+#pragma unroll
+    for (int b = 0; b < NBX; ++b) {
+      ct[b] = pt[b];
+      cb[b] = pb[b];
+      cw[b] = pw[b];
+      cu[b] = pu[b];
+    }
   }
+}
+
+template <int NBX>
+static void launch_pdf(hipStream_t st, const float* bins, int64_t bins_stride, const float* w,
+                       int64_t w_stride, int64_t B, int nb, int Ns, int p2, const float* u,
+                       int64_t u_stride, const float* tm, int Nt, const float* ro,
+                       const float* rd, float* out, float* xyz) {
+  const int grid = resident_grid(k_sample_pdf<NBX>, 64 * kPdfWaves, (B + kPdfWaves - 1) / kPdfWaves);
+  hipLaunchKernelGGL(k_sample_pdf<NBX>, grid, 64 * kPdfWaves, 0, st, bins, bins_stride, w,
+                     w_stride, B, nb, Ns, p2, u, u_stride, tm, Nt, ro, rd, out, xyz);
 }
 
 }  // namespace aon
@@ -201,8 +248,17 @@ extern "C" int aon_sample_pdf(const float* bins, int64_t bins_stride, const floa
   if (B == 0) return 0;
   int p2 = 1;
   while (p2 < Ns) p2 <<= 1;
-  hipLaunchKernelGGL(k_sample_pdf, grid_for(B, kPdfWaves, 1 << 16), 64 * kPdfWaves, 0,
-                     (hipStream_t)stream, bins, bins_stride, weights, w_stride, B, nb, Ns, p2, u,
-                     u_stride, t_merge, t_merge ? Nt : 0, rays_o, rays_d, out, xyz);
+  // LDS rows of 64 * NBX entries hold the bins, t_merge and the (power-of-two padded) samples
+  int need = nb > p2 ? nb : p2;
+  if (t_merge && Nt > need) need = Nt;
+  const int nbx = need <= 64 ? 1 : (need <= 128 ? 2 : (need <= 256 ? 4 : 8));
+  hipStream_t st = (hipStream_t)stream;
+  const int nt = t_merge ? Nt : 0;
+  switch (nbx) {
+    case 1: launch_pdf<1>(st, bins, bins_stride, weights, w_stride, B, nb, Ns, p2, u, u_stride, t_merge, nt, rays_o, rays_d, out, xyz); break;
+    case 2: launch_pdf<2>(st, bins, bins_stride, weights, w_stride, B, nb, Ns, p2, u, u_stride, t_merge, nt, rays_o, rays_d, out, xyz); break;
+    case 4: launch_pdf<4>(st, bins, bins_stride, weights, w_stride, B, nb, Ns, p2, u, u_stride, t_merge, nt, rays_o, rays_d, out, xyz); break;
+    default: launch_pdf<8>(st, bins, bins_stride, weights, w_stride, B, nb, Ns, p2, u, u_stride, t_merge, nt, rays_o, rays_d, out, xyz); break;
+  }
   return launch_status(__func__);
 }

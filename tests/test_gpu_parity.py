@@ -229,6 +229,60 @@ def test_composite_sample_counts(layout):
                                       err_msg=f"S={S} rgb")
 
 
+def test_pipelined_ray_loop_equals_one_ray_per_wave():
+    """The compositor and the pdf sampler run a resident grid whose waves loop over many rays with
+    the next ray's loads in flight.  A 60,000-ray launch (tens of rays per wave) must equal
+    launches of 900 rays (one ray per wave) bit for bit, and a slice of it the oracle."""
+    from aonerf import _lib as L
+    from aonerf import helper
+
+    g = torch.Generator().manual_seed(11)
+    B, S, Sc = 60000, 193, 65
+    t = torch.sort(2.0 + 4.0 * torch.rand((B, S), generator=g), -1).values
+    raw = torch.cat([torch.rand((B, S, 3), generator=g), 3.0 * torch.rand((B, S, 1), generator=g)],
+                    -1).reshape(-1, 4)
+    dirs = torch.nn.functional.normalize(torch.randn((B, 3), generator=g), dim=-1)
+    raw_d, t_d, dirs_d = cuda(raw), cuda(t), cuda(dirs)
+
+    def composite(lo, hi):
+        n = hi - lo
+        outs = [torch.empty(s, device="cuda") for s in ((n, 3), (n,), (n, S), (n,))]
+        L.call("aon_composite_fwd", L.ptr(raw_d[lo * S:]), 4, L.ptr(raw_d[lo * S:, 3:]), 4,
+               L.ptr(t_d[lo:]), L.ptr(dirs_d[lo:]), n, S, 1, L.ACT_VANILLA,
+               *[L.ptr(o) for o in outs], L.stream())
+        return outs
+
+    whole = composite(0, B)
+    parts = [composite(lo, min(lo + 900, B)) for lo in range(0, B, 900)]
+    torch.cuda.synchronize()
+    for k, name in enumerate(("rgb", "acc", "weights", "depth")):
+        assert torch.equal(whole[k], torch.cat([p[k] for p in parts])), f"composite {name}"
+    rgb_c = torch.sigmoid(raw[:512 * S, :3].reshape(512, S, 3))
+    sig_c = torch.relu(raw[:512 * S, 3:].reshape(512, S, 1))
+    _, _, w_ref, _ = O.volumetric_rendering(rgb_c, sig_c, t[:512], dirs[:512], True)
+    np.testing.assert_allclose(npy(whole[2][:512]), w_ref.numpy(), rtol=0, atol=1e-6)
+
+    tc = cuda(torch.sort(2.0 + 4.0 * torch.rand((B, Sc), generator=g), -1).values)
+    wc = cuda(torch.rand((B, Sc), generator=g) * (torch.rand((B, Sc), generator=g) > 0.3))
+    u = cuda(torch.rand((B, 128), generator=g))
+    o, d = cuda(torch.randn((B, 3), generator=g)), dirs_d
+    mids = 0.5 * (tc[..., 1:] + tc[..., :-1])
+    for rnd in (False, True):
+        uu = u if rnd else None
+        t_all, x_all = helper.sample_pdf(mids, wc[..., 1:-1], o, d, tc, 128, rnd, u=uu)
+        chunks = [helper.sample_pdf(mids[lo:lo + 900], wc[lo:lo + 900, 1:-1], o[lo:lo + 900],
+                                    d[lo:lo + 900], tc[lo:lo + 900], 128, rnd,
+                                    u=None if uu is None else uu[lo:lo + 900])
+                  for lo in range(0, B, 900)]
+        torch.cuda.synchronize()
+        assert torch.equal(t_all, torch.cat([c[0] for c in chunks])), f"pdf t (randomized={rnd})"
+        assert torch.equal(x_all, torch.cat([c[1] for c in chunks])), f"pdf xyz (randomized={rnd})"
+        t_ref, _ = O.sample_pdf(mids[:256].cpu(), wc[:256, 1:-1].cpu(), o[:256].cpu(),
+                                d[:256].cpu(), tc[:256].cpu(), 128, rnd,
+                                **({"u": u[:256].cpu()} if rnd else {}))
+        np.testing.assert_array_equal(npy(t_all[:256]), t_ref.numpy())
+
+
 def test_pdf_edges(golden):
     from aonerf import helper
 
