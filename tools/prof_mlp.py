@@ -18,6 +18,7 @@ ap.add_argument("--rays", type=int, default=307200 // 4)
 ap.add_argument("--samples", type=int, default=193)
 ap.add_argument("--precision", default="all")
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--dump", default="", help="write the last raw output's sha256 here (A/B bit-identity)")
 a = ap.parse_args()
 g = torch.Generator(device="cuda").manual_seed(0)
 B, S = a.rays, a.samples
@@ -36,3 +37,8 @@ for p in precs:
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1)
         print(f"{p}: {B * S} rows {ms:.2f} ms -> {2 * 593408 * B * S / ms / 1e9:.1f} TFLOP/s algorithmic")
+    if a.dump:
+        import hashlib
+        h = hashlib.sha256(raw.detach().cpu().numpy().tobytes()).hexdigest()
+        with open(a.dump, "a") as f:
+            f.write(f"{os.environ.get('AONERF_LIB', 'default')} {p} {h}\n")
