@@ -12,9 +12,20 @@
 
 namespace aon {
 
+#ifndef AON_COMP_OCC_FINE
+#define AON_COMP_OCC_FINE 6  // waves per SIMD the fine-level (S = 193) instantiation is built for (7: 72 VGPRs, 8: spills; both no faster)
+#endif
+
 constexpr int kCompWaves = 4;
 constexpr int kCompMaxS = 512;
 constexpr int kCompScratch = 256;  // wave_row_sums task partials (<= 236 at S = 512)
+
+// wave_row_sums task partials the compositor's sums need at S samples (3 rgb sums over S terms,
+// 16 vector-lane sums over S/8 terms; torch_sum.hpp)
+constexpr int comp_scratch(int S) {
+  return S < 8 ? 256
+               : 3 * 4 * ((S >> 2 >> 4) + 1) + 16 * 4 * (((S / 8) >> 2 >> 4) + 1);
+}
 
 __device__ __forceinline__ void wave_sync_c() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -59,17 +70,20 @@ __device__ __forceinline__ double wave_incl_prod(double x) {
 // SC > 0: the sample count as a compile-time constant (the render's 65 and 193), so the
 // torch-order sum schedule (task split, chunk counts, tails) folds to constants.
 template <int NB, bool RAW4, int SC = 0>
-__global__ __launch_bounds__(64 * kCompWaves) void k_composite_fwd(
+__global__ __launch_bounds__(64 * kCompWaves, SC > 0 ? (SC > 128 ? AON_COMP_OCC_FINE : 8) : 1) void k_composite_fwd(
     const float* __restrict__ rgb, int64_t rgb_stride, const float* __restrict__ sig,
     int64_t sig_stride, const float* __restrict__ tv, const float* __restrict__ dirs, int64_t B,
     int S_rt, int white, int act, float* __restrict__ out_rgb, float* __restrict__ out_acc,
     float* __restrict__ out_w, float* __restrict__ out_depth) {
-  constexpr int SM = 64 * NB;
+  // LDS rows of SM floats; with the sample count known at compile time they are S long and the
+  // scratch is exactly the sums' task count, so more waves fit per CU (LDS bounds occupancy)
+  constexpr int SM = SC > 0 ? SC : 64 * NB;
+  constexpr int kScratch = SC > 0 ? comp_scratch(SC) : kCompScratch;
   const int S = SC > 0 ? SC : S_rt;
-  __shared__ float lds_all[kCompWaves][5 * SM + kCompScratch + 32];
+  __shared__ float lds_all[kCompWaves][5 * SM + kScratch + 32];
   float* P = lds_all[threadIdx.x >> 6];  // P[q * SM + i]: q = 0 w, 1 w*t, 2..4 w*rgb
   float* scratch = P + 5 * SM;
-  float* sums = scratch + kCompScratch;
+  float* sums = scratch + kScratch;
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * kCompWaves;
   const bool inner8 = S >= 8;
