@@ -283,6 +283,39 @@ def test_pipelined_ray_loop_equals_one_ray_per_wave():
         np.testing.assert_array_equal(npy(t_all[:256]), t_ref.numpy())
 
 
+def test_render_replays_from_a_graph():
+    """The C ABI neither allocates nor synchronises (include/aonerf.h), so a whole two-level
+    render -- ray generation, both MLP levels, compositing, pdf resampling -- captures into one
+    HIP graph; its replay equals the eager launches bit for bit."""
+    from aonerf.ray_utils import frame_rays
+    from aonerf.render import create_spheric_poses, sapien_focal
+
+    net = make_nerf("f16x3")
+    H, Wd = 24, 40
+    c2w = create_spheric_poses(4.0)[3]
+
+    def render():
+        rays = frame_rays(c2w, H, Wd, sapien_focal(H))
+        out = net(rays, False, True, 2.0, 6.0)
+        return torch.cat([out[1][0], out[1][1][:, None], out[1][2][:, None]], -1)
+
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):  # warm-up: schedules cached, workspace sizes and grids known
+        eager = render()
+        render()
+    torch.cuda.current_stream().wait_stream(st)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        captured = render()
+    for _ in range(2):
+        captured.zero_()
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(captured, eager)
+
+
 def test_pdf_edges(golden):
     from aonerf import helper
 
