@@ -231,9 +231,12 @@ class NeRF(nn.Module):
                     out = out + (dict(t_vals=t_vals, weights=weights),)
                 ret.append(out)
                 continue
+            # the last level's weights are an output only when asked for: otherwise the
+            # compositor skips writing them (4 B of its 24 B per sample)
+            keep_w = level == 0 or return_weights or return_intermediates
             with torch.no_grad():
                 out, weights = self._render_level_fused(mlp, o, d, v, t_vals, randomized,
-                                                        white_bkgd, level, timers)
+                                                        white_bkgd, level, timers, keep_w)
             if not return_weights:
                 out = out[:3] + out[4:]
             if not return_intermediates:
@@ -246,7 +249,8 @@ class NeRF(nn.Module):
                             self.num_coarse_samples, self.num_fine_samples, self.lindisp,
                             u_coarse, u_fine)
 
-    def _render_level_fused(self, mlp, o, d, v, t_vals, randomized, white_bkgd, level, timers):
+    def _render_level_fused(self, mlp, o, d, v, t_vals, randomized, white_bkgd, level, timers,
+                            keep_weights=True):
         B, S = t_vals.shape
         dev = o.device
         # the activations (model.py:186-187) run in the MLP epilogue, unless density noise
@@ -259,7 +263,7 @@ class NeRF(nn.Module):
             raw[:, 3] += torch.rand_like(raw[:, 3]) * self.noise_std
         comp = torch.empty((B, 3), device=dev)
         acc = torch.empty((B,), device=dev)
-        weights = torch.empty((B, S), device=dev)
+        weights = torch.empty((B, S), device=dev) if keep_weights else None
         depth = torch.empty((B,), device=dev)
         ev = _events(timers)
         L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),

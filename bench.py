@@ -37,9 +37,10 @@ ISSUED_PEAK = {"fp32": ("v_mfma_f32_16x16x4_f32", 157.3, 1), "f16x3": ("v_mfma_f
 PEAK_HBM_GBS = 8000.0
 
 
-def composite_bytes(S):
-    # per ray: raw (S,4) + t (S) + dirs (3) read; rgb(3) + acc + depth + weights (S) written
-    return 16 * S + 4 * S + 12 + 20 + 4 * S
+def composite_bytes(S, weights_out=True):
+    # per ray: raw (S,4) + t (S) + dirs (3) read; rgb(3) + acc + depth (+ weights (S)) written.
+    # The frame render does not ask for the fine level's weights, so that launch skips them.
+    return 16 * S + 4 * S + 12 + 20 + (4 * S if weights_out else 0)
 
 
 def main():
@@ -151,7 +152,7 @@ def main():
             iss["frac_of_measured_peak"] = iss["issued_tflops"] / mp[key]
             iss["measured_peak_source"] = "profiles/mfma_peak.json (tools/mfma_peak.py)"
     if comp_ms:
-        cb = composite_bytes(NC + 1 + NF) * (comp_rows // (NC + 1 + NF))
+        cb = composite_bytes(NC + 1 + NF, weights_out=False) * (comp_rows // (NC + 1 + NF))
         gbs = cb / (comp_ms * 1e-3) / 1e9
         out["roofline_composite"] = {"bound": "hbm", "kernel": "k_composite_fwd (fine level)",
                                      "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
