@@ -229,15 +229,15 @@ def test_composite_sample_counts(layout):
                                       err_msg=f"S={S} rgb")
 
 
-def test_pipelined_ray_loop_equals_one_ray_per_wave():
-    """The compositor and the pdf sampler run a resident grid whose waves loop over many rays with
-    the next ray's loads in flight.  A 60,000-ray launch (tens of rays per wave) must equal
-    launches of 900 rays (one ray per wave) bit for bit, and a slice of it the oracle."""
+def test_ray_loop_equals_one_ray_per_wave():
+    """The compositor and the pdf sampler cap their grids at 65,536 workgroups (262,144 waves)
+    and loop: a 270,000-ray launch, where some waves take two rays, must equal launches of 900
+    rays (one ray per wave) bit for bit, and a slice of it the oracle."""
     from aonerf import _lib as L
     from aonerf import helper
 
     g = torch.Generator().manual_seed(11)
-    B, S, Sc = 60000, 193, 65
+    B, S, Sc = 270000, 65, 65
     t = torch.sort(2.0 + 4.0 * torch.rand((B, S), generator=g), -1).values
     raw = torch.cat([torch.rand((B, S, 3), generator=g), 3.0 * torch.rand((B, S, 1), generator=g)],
                     -1).reshape(-1, 4)
