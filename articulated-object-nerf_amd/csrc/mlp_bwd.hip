@@ -28,18 +28,34 @@ struct BwdArgs {
 };
 
 // max |x| over n floats as uint bits (non-negative floats order like their bit patterns)
+// (16-B loads over the aligned body, scalar loads for the ragged head / tail)
 __global__ void k_absmax(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ out) {
   float m = 0.0f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(x[i]));
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  const int64_t head = ((16 - (reinterpret_cast<uintptr_t>(x) & 15)) & 15) / 4;  // floats to 16 B
+  const int64_t h = head < n ? head : n;
+  const int64_t nv = (n - h) / 4;
+  const f4* xv = reinterpret_cast<const f4*>(x + h);
+  for (int64_t i = tid; i < nv; i += nthreads) {
+    const f4 v = xv[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  for (int64_t i = tid; i < h; i += nthreads) m = fmaxf(m, fabsf(x[i]));
+  for (int64_t i = h + 4 * nv + tid; i < n; i += nthreads) m = fmaxf(m, fabsf(x[i]));
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+  // one atomic per workgroup: same-address atomics serialise in one L2 channel (one per wave
+  // took 50 us on the training step's 3.2 M values)
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(out, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
 
 int absmax(const float* x, int64_t n, uint32_t* out, hipStream_t stream) {
   if (hipMemsetAsync(out, 0, sizeof(uint32_t), stream) != hipSuccess) return launch_status("absmax");
-  hipLaunchKernelGGL(k_absmax, grid_for(n, 256, 1024), 256, 0, stream, x, n, out);
+  hipLaunchKernelGGL(k_absmax, grid_for(n / 4 + 1, 256, 512), 256, 0, stream, x, n, out);
   return launch_status("absmax");
 }
 

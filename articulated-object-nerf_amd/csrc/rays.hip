@@ -133,17 +133,20 @@ __global__ void k_pos_enc(const float* __restrict__ x, int64_t n, int min_deg, i
 // cast_rays (helper.py:25-26) on per-ray t (B, S), optionally displaced by a per-sample offset
 // (the articulated deformation, model_autodecoder.py:205: deformation_layer(x) + pos) and
 // optionally straight into pos_enc (helper.py:136-140): one thread per (sample, feature)
+// Idx: the element index type -- 32-bit when the launch has < 2^31 elements (the training
+// step's 50 M), so the two index divisions per element are 32-bit, not 64-bit, sequences.
+template <typename Idx>
 __global__ void k_cast_rays(const float* __restrict__ ro, const float* __restrict__ rd,
                             const float* __restrict__ t, int64_t B, int S,
                             const float* __restrict__ off, int64_t off_stride,
                             float* __restrict__ xyz, int min_deg, int L, float* __restrict__ enc) {
   const int C = enc ? 3 + 6 * L : 3;
-  const int64_t total = B * S * C;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / C;
-    const int f = static_cast<int>(i - r * C);
-    const int64_t b = r / S;
+  const Idx total = static_cast<Idx>(B * S * C);
+  for (Idx i = blockIdx.x * (Idx)blockDim.x + threadIdx.x; i < total;
+       i += (Idx)gridDim.x * blockDim.x) {
+    const Idx r = i / static_cast<Idx>(C);
+    const int f = static_cast<int>(i - r * static_cast<Idx>(C));
+    const Idx b = r / static_cast<Idx>(S);
     float x0 = ro[3 * b], x1 = ro[3 * b + 1], x2 = ro[3 * b + 2];
     if (rd) {  // rays_d == NULL: the points are given directly (rays_o rows)
       const float tv = t[r];
@@ -280,8 +283,14 @@ extern "C" int aon_cast_rays(const float* rays_o, const float* rays_d, const flo
   if (B == 0) return 0;
   const int L = max_deg - min_deg;
   const int C = enc ? 3 + 6 * L : 3;
-  hipLaunchKernelGGL(k_cast_rays, grid_for(B * S * C, 256, 65536), 256, 0, (hipStream_t)stream,
-                     rays_o, rays_d, t, B, S, offset, offset_stride, xyz, min_deg, L, enc);
+  if (B * S * C < (int64_t(1) << 31))
+    hipLaunchKernelGGL(k_cast_rays<uint32_t>, grid_for(B * S * C, 256, 65536), 256, 0,
+                       (hipStream_t)stream, rays_o, rays_d, t, B, S, offset, offset_stride, xyz,
+                       min_deg, L, enc);
+  else
+    hipLaunchKernelGGL(k_cast_rays<int64_t>, grid_for(B * S * C, 256, 65536), 256, 0,
+                       (hipStream_t)stream, rays_o, rays_d, t, B, S, offset, offset_stride, xyz,
+                       min_deg, L, enc);
   return launch_status(__func__);
 }
 
