@@ -89,8 +89,8 @@ _SIGNATURES = {
     "aon_mse": (c_int, [vp, vp, c_i64, c_float, vp, vp, vp]),
     "aon_colsum_workspace_bytes": (c_size, [c_i64, c_i64]),
     "aon_colsum": (c_int, [vp, c_i64, c_i64, c_i64, c_int, vp, vp, c_size, vp]),
-    "aon_adam_step": (c_int, [ctypes.POINTER(AonAdamTensor), c_int, c_float, c_float, c_float,
-                              c_float, c_i64, vp]),
+    "aon_adam_step": (c_int, [ctypes.POINTER(AonAdamTensor), c_int, ctypes.c_double,
+                              ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, vp]),
     "aon_pos_enc_bwd": (c_int, [vp, c_i64, vp, c_i64, c_i64, c_int, c_int, c_int, vp, c_i64, vp]),
     "aon_latent_reg": (c_int, [vp, c_i64, c_i64, c_float, c_int, vp, vp, vp]),
 }
@@ -110,7 +110,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.aon_abi_version() != 3:
+        if handle.aon_abi_version() != 4:
             raise ImportError("aonerf: ABI version mismatch")
         _lib = handle
     return _lib

@@ -369,3 +369,7 @@ class Adam:
             L.call("aon_adam_step", table, len(chunk), float(self.lr if lr is None else lr),
                    float(self.betas[0]), float(self.betas[1]), float(self.eps), self.step_count,
                    L.stream(self.params[0].device))
+        # the update is in place through raw pointers: bump each parameter's version counter so
+        # version-keyed caches (NeRFMLP.packed_weights) and autograd's saved-tensor checks see it
+        for p in self.params:
+            torch.autograd.graph.increment_version(p)

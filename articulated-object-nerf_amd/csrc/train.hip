@@ -204,8 +204,8 @@ struct AdamTable {
   int count;
 };
 
-__global__ void k_adam(AdamTable t, float step_size, float b1, float b2, float eps,
-                       float bc2_sqrt) {
+__global__ void k_adam(AdamTable t, float step_size, float one_minus_b1, float b2,
+                       float one_minus_b2, float eps, float bc2_sqrt) {
   const int64_t total = t.start[t.count];
   int k = 0;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
@@ -214,8 +214,8 @@ __global__ void k_adam(AdamTable t, float step_size, float b1, float b2, float e
     const int64_t i = e - t.start[k];
     const float g = t.g[k][i];
     float m = t.m[k][i], v = t.v[k][i];
-    m = __fadd_rn(m, __fmul_rn(__fsub_rn(1.0f, b1), __fsub_rn(g, m)));
-    v = __fadd_rn(__fmul_rn(v, b2), __fmul_rn(__fmul_rn(__fsub_rn(1.0f, b2), g), g));
+    m = __fadd_rn(m, __fmul_rn(one_minus_b1, __fsub_rn(g, m)));
+    v = __fadd_rn(__fmul_rn(v, b2), __fmul_rn(__fmul_rn(one_minus_b2, g), g));
     const float denom = __fadd_rn(__fdiv_rn(sqrtf(v), bc2_sqrt), eps);
     t.p[k][i] = __fsub_rn(t.p[k][i], __fmul_rn(step_size, __fdiv_rn(m, denom)));
     t.m[k][i] = m;
@@ -295,8 +295,8 @@ extern "C" int aon_colsum(const float* X, int64_t ldx, int64_t M, int64_t N, int
   return launch_status(__func__);
 }
 
-extern "C" int aon_adam_step(const aon_adam_tensor* tensors, int count, float lr, float beta1,
-                             float beta2, float eps, int64_t step, aon_stream_t stream) {
+extern "C" int aon_adam_step(const aon_adam_tensor* tensors, int count, double lr, double beta1,
+                             double beta2, double eps, int64_t step, aon_stream_t stream) {
   AON_REQUIRE(tensors && count >= 1 && count <= AON_ADAM_MAX_TENSORS, "bad tensor list");
   AON_REQUIRE(step >= 1, "step counts from 1");
   AdamTable t;
@@ -313,11 +313,13 @@ extern "C" int aon_adam_step(const aon_adam_tensor* tensors, int count, float lr
     t.start[i + 1] = t.start[i] + tensors[i].numel;
   }
   if (t.start[count] == 0) return 0;
-  // step size and bias corrections in double on the host, as torch computes them in Python
-  // floats before they meet the fp32 tensors
-  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  // Every scalar is formed in double from the Python-float hyperparameters, as torch.optim.Adam
+  // does (lerp weight 1 - beta1, addcmul value 1 - beta2, step size lr / bc1, sqrt(bc2)), and
+  // only then rounded to fp32 where it meets the fp32 tensors.
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
   hipLaunchKernelGGL(k_adam, grid_for(t.start[count], 256, 4096), 256, 0, (hipStream_t)stream, t,
-                     (float)((double)lr / bc1), beta1, beta2, eps, (float)std::sqrt(bc2));
+                     (float)(lr / bc1), (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
+                     (float)eps, (float)std::sqrt(bc2));
   return launch_status(__func__);
 }

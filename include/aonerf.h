@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 3
+#define AON_ABI_VERSION 4
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -330,7 +330,9 @@ int aon_colsum(const float* X, int64_t ldx, int64_t M, int64_t N, int accumulate
 
 /* torch.optim.Adam step (model.py:386-389; no weight decay / amsgrad) over up to
  * AON_ADAM_MAX_TENSORS parameter tensors; `step` counts from 1; lr from optimizer_step's
- * schedule (model.py:399-416). */
+ * schedule (model.py:399-416).  The hyperparameters are doubles (Python floats): 1 - beta1,
+ * 1 - beta2, lr / (1 - beta1^step) and sqrt(1 - beta2^step) are formed in double and rounded
+ * to fp32 once, as torch.optim.Adam forms them. */
 #define AON_ADAM_MAX_TENSORS 64
 typedef struct aon_adam_tensor {
   float* param;
@@ -339,8 +341,8 @@ typedef struct aon_adam_tensor {
   float* exp_avg_sq;
   int64_t numel;
 } aon_adam_tensor;
-int aon_adam_step(const aon_adam_tensor* tensors, int count, float lr, float beta1, float beta2,
-                  float eps, int64_t step, aon_stream_t stream);
+int aon_adam_step(const aon_adam_tensor* tensors, int count, double lr, double beta1,
+                  double beta2, double eps, int64_t step, aon_stream_t stream);
 
 /* ---------------------------------------------------------------- articulated training */
 /* Autograd of pos_enc (helper.py:136-140) on the deformed points of the articulated MLP
