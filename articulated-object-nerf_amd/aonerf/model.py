@@ -201,8 +201,9 @@ class NeRF(nn.Module):
         ``timers`` (dict) records hip events around each level's MLP / composite launches.
 
         With autograd enabled and trainable parameters, each level runs the training path
-        (train.RenderLevel: layer GEMMs keeping activations, HIP backward); otherwise the fused
-        inference kernels.
+        (train.RenderLevel: the fused training forward aon_mlp_fwd_train, which also stores the
+        activations and their ReLU' bits, then the HIP backward); otherwise the fused inference
+        kernels.
         """
         o, d, v = rays["rays_o"], rays["rays_d"], rays["viewdirs"]
         L.require_gpu(o, d, v)

@@ -26,7 +26,7 @@ import torch.nn.init as init
 
 from . import _lib as L
 from .linalg import ACT_SCALE, W_SCALE, gemm, linear_fwd
-from .model import level_t_vals
+from .model import _events, _record, level_t_vals
 
 class NeRFMLP(nn.Module):
     """reference model_autodecoder.py:60-166 (same nn.Linear layout and init)."""
@@ -285,13 +285,16 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
                                 embed_deg=embed_deg)
 
     def forward(self, rays, randomized, white_bkgd, near, far, latents, train=True, *,
-                u_coarse=None, u_fine=None, return_weights=False, return_intermediates=False):
+                u_coarse=None, u_fine=None, return_weights=False, return_intermediates=False,
+                timers=None):
         """reference model_autodecoder.py:278-337 -> [(comp_rgb, acc, depth)_coarse, (...)_fine]
-        (``u_coarse`` / ``u_fine`` inject randomized-mode uniforms; the extras as NeRF.forward).
+        (``u_coarse`` / ``u_fine`` inject randomized-mode uniforms; the extras as NeRF.forward;
+        ``timers`` (dict) records hip events around each level's MLP / composite launches).
 
         With autograd enabled and trainable parameters or latent codes, each level runs the
-        training path (train_art.ArtRenderLevel: layer GEMMs keeping activations, HIP backward
-        into the MLP parameters and the latent codes); otherwise the fused inference kernel."""
+        training path (train_art.ArtRenderLevel: the fused training forward
+        aon_mlp_art_fwd_train, which also stores the activations, then the HIP backward into the
+        MLP parameters and the latent codes); otherwise the fused inference kernel."""
         o, d, v = rays["rays_o"], rays["rays_d"], rays["viewdirs"]
         L.require_gpu(o, d, v)
         o, d, v = L.contig(o), L.contig(d), L.contig(v)
@@ -303,7 +306,8 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
                                        u_coarse, u_fine, return_weights, return_intermediates)
         with torch.no_grad():
             return self._forward_render(o, d, v, randomized, white_bkgd, near, far, latents,
-                                        u_coarse, u_fine, return_weights, return_intermediates)
+                                        u_coarse, u_fine, return_weights, return_intermediates,
+                                        timers)
 
     def _forward_train(self, o, d, v, randomized, white_bkgd, near, far, latents, u_coarse,
                        u_fine, return_weights, return_intermediates):
@@ -330,7 +334,7 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
         return ret
 
     def _forward_render(self, o, d, v, randomized, white_bkgd, near, far, latents, u_coarse,
-                        u_fine, return_weights, return_intermediates):
+                        u_fine, return_weights, return_intermediates, timers=None):
         B, dev = o.shape[0], o.device
         ret = []
         t_vals = weights = None
@@ -340,16 +344,20 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
                                   u_coarse, u_fine)
             mlp = self.coarse_mlp if level == 0 else self.fine_mlp
             S = t_vals.shape[1]
+            ev = _events(timers)
             raw = mlp.forward_rays(o, d, v, t_vals, latents)
+            _record(timers, ev, f"mlp{level}", B * S)
             if self.noise_std > 0 and randomized:  # model_autodecoder.py:318-319
                 raw[:, 3].copy_(raw[:, 3] + torch.rand_like(raw[:, 3]) * self.noise_std)
             comp = torch.empty((B, 3), device=dev)
             acc = torch.empty((B,), device=dev)
             weights = torch.empty((B, S), device=dev)
             depth = torch.empty((B,), device=dev)
+            ev = _events(timers)
             L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
                    B, S, int(bool(white_bkgd)), L.ACT_ARTIC, L.ptr(comp), L.ptr(acc),
                    L.ptr(weights), L.ptr(depth), L.stream(dev))
+            _record(timers, ev, f"comp{level}", B * S)
             out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
             if return_intermediates:
                 out = out + (dict(t_vals=t_vals, weights=weights, raw=raw),)

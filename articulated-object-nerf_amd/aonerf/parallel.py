@@ -48,13 +48,14 @@ def render_frame_sharded(model, c2w, H, W, focal, near=2.0, far=6.0, white_bkgd=
     """
     from .render import render_frame
 
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    ddp = dist.is_initialized()
+    world = dist.get_world_size(group) if ddp else 1
+    rank = dist.get_rank(group) if ddp else 0
     p0, n, n_max = band(H, W, rank, world)
     local = torch.zeros((n_max, 5), device=torch.device("cuda", torch.cuda.current_device()))
     if n > 0:
         local[:n] = render_frame(model, c2w, H, W, focal, near, far, white_bkgd, p0, n, timers=timers)
-    if world == 1 or not gather:
+    if not ddp or not gather:  # (a process group of one still runs the gather)
         return (local[:n] if world == 1 else None), local
     return gather_frame(local, H, W, dst, group), local
 
@@ -77,9 +78,9 @@ class GradAllReduce:
         self.flat = None
 
     def __call__(self):
-        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
-        if world == 1:
+        if not dist.is_initialized():  # (a process group of one still runs the all-reduce)
             return
+        world = dist.get_world_size(self.group)
         dev = self.params[0].device
         if self.flat is None or self.flat.device != dev:
             self.flat = torch.empty(sum(self.sizes), dtype=torch.float32, device=dev)

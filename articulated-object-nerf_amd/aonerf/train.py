@@ -3,13 +3,16 @@ optimizer_step, model.py:386-419) on the HIP kernels.
 
 One render level under autograd is ``RenderLevel`` (a torch.autograd.Function):
 
-  forward   pos_enc (aon_pos_enc) -> 11 layer GEMMs keeping every activation (aon_gemm: bias,
-            ReLU, the skip concat cat[h4, enc] and the view concat cat[bottleneck, enc_dir
-            tiled over samples] read in place) -> compositing (aon_composite_fwd, raw outputs +
-            sigmoid/relu as model.py:186-187)
-  backward  aon_composite_bwd (dL/draw) -> per layer, last to first: dW = dY^T X and
-            db = sum_rows dY from the same pass (split-K, deterministic), dX = (dY W) * relu'(X)
-            (aon_gemm mask)
+  forward   ONE fused kernel (aon_mlp_fwd_train: cast_rays, pos_enc, the whole NeRFMLP and the
+            sigmoid/relu of model.py:186-187 in registers) that also stores every hidden
+            activation and their ReLU' bits for the backward -> compositing (aon_composite_fwd)
+  backward  aon_composite_bwd (dL/draw) -> ONE fused kernel for the whole input-gradient chain
+            dX = (dY W) * relu'(X) (aon_mlp_bwd, masks from the stored bits) -> per layer
+            dW = dY^T X and db = sum_rows dY from the same pass (aon_gemm, split-K,
+            deterministic)
+
+(``FUSED_FORWARD`` / ``FUSED_BACKWARD`` = False select the layer-by-layer aon_gemm forward and
+backward that the fused kernels replaced; both are gated identically in tests/test_gpu_train.py.)
 
 Gradients land in each parameter's ``.grad`` through autograd, so the reference's own
 optimizer code runs unchanged; ``Adam`` below is the fused replacement (aon_adam_step) with
@@ -104,6 +107,24 @@ FUSED_FORWARD = True
 # backward of a level: input gradients in one fused kernel (aon_mlp_bwd) + weight-gradient GEMMs
 # when True, else every product as a GEMM (_backward_level)
 FUSED_BACKWARD = True
+# a dict -> hip events around each level's training kernels, keyed by name and sample count
+# (bench.py's train_step roofline): "fwd_train<S>", "bwd_chain<S>", "dweight<S>"
+TIMERS = None
+
+
+def _ev():
+    if TIMERS is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _rec(key, e0, rows):
+    if e0 is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        TIMERS.setdefault(key, []).append((e0, e1, rows))
 
 _packed = {}
 
@@ -173,8 +194,12 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
     dzb = torch.empty((R, 256), device=dev)
     dz = torch.empty((8, R, 256), device=dev)
     work = _buffer("work", 4, dev)
-    L.call("aon_mlp_bwd", L.ptr(_pack_bwd(P, dev)), L.ptr(draw), L.ptr(masks), R, L.ptr(dzv),
+    packed = _pack_bwd(P, dev)
+    e0 = _ev()
+    L.call("aon_mlp_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), R, L.ptr(dzv),
            L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
+    _rec(f"bwd_chain{S}", e0, R)
+    e0 = _ev()
     gs, acts = GRAD_SCALE, ACT_SCALE
 
     def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None):
@@ -194,6 +219,7 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
             dweight(G[0][0], dz[0], 256, 256, enc, 63, 63, db=G[0][1])
         else:
             dweight(G[i][0], dz[i], 256, 256, h[i - 1], 256, 256, db=G[i][1])
+    _rec(f"dweight{S}", e0, R)
 
 
 def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, masks=None):
@@ -236,9 +262,11 @@ class RenderLevel(torch.autograd.Function):
         if FUSED_FORWARD:
             noise = L.contig(noise) if noise is not None else None
             masks = torch.empty((9, R, 8), dtype=torch.int32, device=dev)
+            e0 = _ev()
             h, bot, hv = _forward_level_fused(P, L.contig(rays_o), L.contig(rays_d),
                                               L.contig(viewdirs), L.contig(t_vals), raw, noise,
                                               masks)
+            _rec(f"fwd_train{S}", e0, R)
         else:
             h, bot, hv = _forward_level(P, enc, venc, S, raw, noise)
         comp = torch.empty((B, 3), device=dev)

@@ -3,6 +3,15 @@
 samples (BASELINE.json configs[1]; configs[3] when launched on N GPUs: the frame is split into
 N row bands, one per rank, and gathered to rank 0 over RCCL).
 
+Sub-records in the same JSON line (after the headline, same timing protocol: warm-up, barrier +
+synchronize on both sides, max over ranks):
+  "articulated"     config C3 -- NeRF_AE_Art 320x240 frame render (N = 1 only)
+  "train_step"      config C5 -- LitNeRF.training_step on 4096 rays per rank + Adam (+ the DDP
+                    gradient all-reduce over RCCL on N > 1: weak scaling)
+  "train_step_art"  C5 on the articulated auto-decoder (LitNeRF_AutoDecoder.training_step)
+each with its own ms_per_step and roofline (MFMA fraction of the fine-level MLP kernels,
+HBM byte fractions of the training kernels counting the stored activations).
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
@@ -51,6 +60,9 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_TFLOPS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-chunks", type=int, default=2, help="3840-ray chunks in the CPU sample")
+    ap.add_argument("--no-extra", action="store_true", help="headline C2 render only")
+    ap.add_argument("--train-precision", default="f16x3", choices=("f16x3",),
+                    help="MFMA numerics of the C5 training step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,6 +113,12 @@ def main():
 
     mlp_ms, rows = avg_ms("mlp1")
     comp_ms, comp_rows = avg_ms("comp1")
+    extra = {}
+    if not args.no_extra:  # every rank takes part (the C5 step all-reduces over RCCL)
+        if world == 1:
+            extra["articulated"] = bench_articulated(args)
+        extra["train_step"] = bench_train(args, world, rank, local_rank)
+        extra["train_step_art"] = bench_train(args, world, rank, local_rank, art=True)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -159,11 +177,189 @@ def main():
                                      "frac": gbs / PEAK_HBM_GBS, "launch_ms": comp_ms,
                                      "algorithmic_bytes_per_launch": cb}
 
+    out.update(extra)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(frame, c2w, focal, args.cpu_chunks)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def timed(step, steps, warmup, world):
+    """W untimed steps, then K steps bracketed by barrier + synchronize; max over ranks (s)."""
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return el.item()
+
+
+def ev_ms(timers, key):
+    """(mean ms, rows) of the HIP-event pairs recorded under key."""
+    ev = timers.get(key, [])
+    if not ev:
+        return None, 0
+    return float(np.mean([a.elapsed_time(b) for a, b, _ in ev])), ev[0][2]
+
+
+def bench_articulated(args):
+    """C3: NeRF_AE_Art, 320x240 frame, 64c+128f, eval mode, white background, fixed latent
+    codes; MFMA roofline of the fine-level fused kernel in the reference's unfolded FLOP count
+    (2 x 794,880 per sample; the latent products are folded into per-call biases, so the issued
+    work is 714,880 MAC per sample)."""
+    from aonerf.model_autodecoder import NeRF_AE_Art
+    from aonerf.ray_utils import frame_rays
+    from aonerf.render import create_spheric_poses, sapien_focal
+    from aonerf.synthetic import art_latents, init_like_reference
+
+    h, w = 240, 320
+    net = init_like_reference(NeRF_AE_Art()).cuda()
+    lat = art_latents(0, device="cuda")
+    rays = frame_rays(torch.as_tensor(create_spheric_poses(4.0)[11]), h, w, sapien_focal(h))
+    timers = {}
+
+    @torch.no_grad()
+    def step(i):
+        return net(rays, False, True, 2.0, 6.0, lat, timers=timers if i >= args.warmup else None)
+
+    el = timed(step, args.steps, args.warmup, 1)
+    mlp_ms, rows = ev_ms(timers, "mlp1")
+    flop = 2.0 * 794_880 * rows
+    ach = flop / (mlp_ms * 1e-3) / 1e12
+    return {"metric": "articulated rays/sec at 320x240x(64c+128f) (NeRF_AE_Art, config C3)",
+            "value": h * w * args.steps / el, "unit": "rays/s", "steps": args.steps,
+            "ms_per_step": el / args.steps * 1e3,
+            "config": {"workload": "sapien_multi NeRF_AE_Art 320x240 frame render, 64c+128f, "
+                                   "randomized=False, white_bkgd, fixed latent codes",
+                       "rays_per_step": h * w},
+            "roofline": {"bound": "mfma", "kernel": "k_mlp_art_f16x3 (fine level)",
+                         "achieved": ach, "peak": PEAK_TFLOPS["f16x3"], "unit": "TFLOP/s",
+                         "frac": ach / PEAK_TFLOPS["f16x3"], "launch_ms": mlp_ms,
+                         "algorithmic_flop_per_launch": flop,
+                         "note": "unfolded reference count 2 x 794,880 FLOP/sample; issued "
+                                 "714,880 MAC/sample x 3 fp16 products"}}
+
+
+# bytes per sample of the training kernels (fp32 activations, SURVEY.md 8(d) extended to C5):
+# the fused forward writes raw (16) + 2,432 activations (8 x 256 + 256 + 128) + ReLU' bits
+# (9 x 32) and reads t (4); the backward chain reads d raw (16) + the bits and writes 2,432
+# input gradients; the weight-gradient GEMMs read each layer's dZ and its input X once.
+TRAIN_BYTES = {"fwd_train": 4 + 16 + 4 * 2432 + 288, "bwd_chain": 16 + 288 + 4 * 2432,
+               "dweight": 4 * (2432 + 2432 + 63 + 27)}
+# FLOP per sample: forward 2 x 593,408; input-gradient chain 2 x (593,408 - 256 x 63 - 128 x 27
+# (no gradient into the encodings)); weight gradients 2 x 593,408
+TRAIN_FLOP = {"fwd_train": 2 * MAC_PER_SAMPLE, "bwd_chain": 2 * (MAC_PER_SAMPLE - 256 * 63 - 128 * 27),
+              "dweight": 2 * MAC_PER_SAMPLE}
+
+
+def bench_train(args, world, rank, local_rank, art=False):
+    """C5: one LitNeRF.training_step (or LitNeRF_AutoDecoder.training_step) on 4096 rays per rank
+    drawn from 8 synthetic 640x480 views, randomized sampling, loss, HIP backward, gradient
+    all-reduce (RCCL, N > 1), fused Adam with the reference schedule."""
+    import types
+
+    from aonerf import train
+    from aonerf.model import NeRF
+    from aonerf.parallel import GradAllReduce
+    from aonerf.ray_utils import frame_rays
+    from aonerf.render import create_spheric_poses, sapien_focal
+    from aonerf.synthetic import init_like_reference
+
+    dev = torch.device("cuda", local_rank)
+    nrays = 4096
+    if art:
+        from aonerf import train_art
+        from aonerf.code_library import CodeLibraryArticulated
+        from aonerf.model_autodecoder import NeRF_AE_Art
+        from aonerf.synthetic import init_code_library
+
+        net = init_like_reference(NeRF_AE_Art()).to(dev)
+        lib = init_code_library(CodeLibraryArticulated(
+            types.SimpleNamespace(N_max_objs=151, N_obj_code_length=128))).to(dev)
+        ids = {"instance_id": torch.tensor([7], device=dev),
+               "articulation_id": torch.tensor([3], device=dev)}
+    else:
+        net = init_like_reference(NeRF()).to(dev)
+    poses = create_spheric_poses(4.0)
+    focal = sapien_focal(H)
+    views = [frame_rays(torch.as_tensor(poses[(5 * k) % len(poses)]), H, W, focal) for k in range(8)]
+    rays_all = {key: torch.cat([v[key] for v in views], 0) for key in ("rays_o", "rays_d", "viewdirs")}
+    rng = np.random.Generator(np.random.PCG64(3))
+    target_all = torch.from_numpy(rng.uniform(0, 1, size=(8 * H * W, 3)).astype(np.float32)).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    params = list(net.parameters()) + (list(lib.parameters()) if art else [])
+    opt = train.Adam(params)
+    sync = GradAllReduce(params)
+    timers = {}
+
+    def step(i):
+        train.TIMERS = timers if (i >= args.warmup and not art) else None
+        idx = torch.randint(0, 8 * H * W, (nrays,), device=dev, generator=gen)
+        batch = {k: v[idx] for k, v in rays_all.items()}
+        batch["target"] = target_all[idx]
+        opt.zero_grad()
+        if art:
+            batch.update(ids)
+            loss, _ = train_art.training_step(net, lib, batch, True, True, 2.0, 6.0)
+        else:
+            loss, _ = train.training_step(net, batch, True, True, 2.0, 6.0)
+        loss.backward()
+        sync()
+        opt.step(lr=train.learning_rate(i, 200000))
+
+    try:
+        el = timed(step, args.steps, args.warmup, world)
+    finally:
+        train.TIMERS = None
+    mac = 794_880 if art else MAC_PER_SAMPLE
+    samples = nrays * (NC + 1 + NC + 1 + NF)
+    ms = el / args.steps * 1e3
+    step_flop = 3 * 2.0 * mac * samples
+    ach = step_flop / (ms * 1e-3) / 1e12
+    rec = {"metric": ("training rays/sec, LitNeRF_AutoDecoder.training_step (NeRF_AE_Art), "
+                      "4096 rays/rank, 64c+128f, Adam (config C5)" if art else
+                      "training rays/sec, LitNeRF.training_step, 4096 rays/rank, 64c+128f, "
+                      "Adam (config C5)"),
+           "value": nrays * world * args.steps / el, "unit": "rays/s", "n_gpus": world,
+           "steps": args.steps, "ms_per_step": ms, "scaling": "weak",
+           "dtype": "f16x3 (fp16 hi/lo split MFMA, fp32 accumulate; fp32 activations)",
+           "config": {"workload": "C5 training step" + (" (articulated)" if art else ""),
+                      "rays_per_rank": nrays, "parallelism": f"ddp{world}" if world > 1 else "single GPU"},
+           "roofline": {"bound": "hbm+mfma", "kernel": "whole step (3 x forward FLOP)",
+                        "achieved": ach, "peak": PEAK_TFLOPS["f16x3"], "unit": "TFLOP/s",
+                        "frac": ach / PEAK_TFLOPS["f16x3"]}}
+    if not art:
+        kern = {}
+        hbm_bytes = 0.0
+        for name in ("fwd_train", "bwd_chain", "dweight"):
+            t_ms, rows = ev_ms(timers, f"{name}{NC + 1 + NF}")
+            if not t_ms:
+                continue
+            b = TRAIN_BYTES[name] * rows
+            f = TRAIN_FLOP[name] * rows
+            hbm_bytes += b
+            kern[name] = {"level": "fine", "ms": t_ms, "rows": rows,
+                          "algorithmic_bytes": b, "GB/s": b / (t_ms * 1e-3) / 1e9,
+                          "hbm_frac": b / (t_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                          "TFLOP/s": f / (t_ms * 1e-3) / 1e12,
+                          "mfma_frac": f / (t_ms * 1e-3) / 1e12 / PEAK_TFLOPS["f16x3"]}
+        rec["roofline"]["kernels"] = kern
+        if kern:
+            tot_ms = sum(k["ms"] for k in kern.values())
+            rec["roofline"]["fine_level_hbm_frac"] = hbm_bytes / (tot_ms * 1e-3) / 1e9 / PEAK_HBM_GBS
+            rec["roofline"]["fine_level_ms"] = tot_ms
+    return rec
 
 
 def cpu_baseline(frame, c2w, focal, nchunks):
@@ -172,7 +368,12 @@ def cpu_baseline(frame, c2w, focal, nchunks):
     from oracle import nerf_oracle as O
     from oracle import weights as Wt
 
-    threads = min(16, os.cpu_count() or 1)
+    # The host's CPU share of this one-GPU job: the pool gives a one-GPU box 16 CPUs
+    # (OMP_NUM_THREADS=16 there) of a host whose os.cpu_count() spans every GPU's share; the
+    # affinity mask / OMP_NUM_THREADS name that share, so that is what the baseline uses.
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(share, omp) if omp > 0 else share
     torch.set_num_threads(threads)
     params = O.split_state_dict(Wt.nerf_state_dict(0))
     dirs = O.get_ray_directions(H, W, focal)
@@ -201,6 +402,8 @@ def cpu_baseline(frame, c2w, focal, nchunks):
             "cpu_model": model, "host_cpu_count": os.cpu_count(),
             "sample": f"{nchunks} x 3840-ray chunks (pixels {p0}..{p0 + n}) of the same frame, "
                       f"oracle/nerf_oracle.py torch-CPU restatement, {threads} threads, {dt:.1f} s",
+            "threads_rationale": "the job's CPU share: min(affinity mask, OMP_NUM_THREADS); the "
+                                 "GPU box gives a one-GPU job 16 CPUs of the shared host",
             "max_abs_rgb_diff_vs_gpu": float((ref - gpu).abs().max()),
             "psnr_gpu_vs_reference_db": O.psnr_each([gpu], [ref]).item(),
             "psnr_delta_db": p_gpu - p_ref}

@@ -131,14 +131,9 @@ def fine_u(num_samples, batch_shape, randomized, u=None):
     return torch.broadcast_to(u, list(batch_shape) + [num_samples])
 
 
-def sorted_piecewise_constant_pdf(bins, weights, num_samples, randomized, u=None):
-    """reference helper.py:203-243, restated with a per-ray searchsorted.
-
-    The reference's mask form (mask = u >= cdf; bin0 = max over masked bins, bin1 = min over
-    unmasked, first/last fallbacks) equals ``idx = searchsorted(cdf, u, right=True)``,
-    ``i0 = clamp(idx-1, 0, n-1)``, ``i1 = clamp(idx, max=n-1)`` -- pinned bit-exactly by the
-    golden vectors (including zero-weight plateaus and u == cdf ties).
-    """
+def _pdf_bins(weights, num_samples, randomized, u=None):
+    """helper.py:207-229: eps padding, pdf, the 64-entry CDF [0, fmin(1, cumsum), 1], the u
+    schedule, and for every u the bin index searchsorted(cdf, u, right=True)."""
     eps = 1e-5
     weight_sum = weights.sum(dim=-1, keepdim=True)
     padding = torch.fmax(torch.zeros_like(weight_sum), eps - weight_sum)
@@ -150,8 +145,27 @@ def sorted_piecewise_constant_pdf(bins, weights, num_samples, randomized, u=None
     ones = torch.ones(list(cdf.shape[:-1]) + [1])
     cdf = torch.cat([zeros, cdf, ones], dim=-1)
     u = fine_u(num_samples, cdf.shape[:-1], randomized, u).contiguous()
-    n = cdf.shape[-1]
     idx = torch.searchsorted(cdf.contiguous(), u, right=True)
+    return cdf, u, idx
+
+
+def pdf_bin_index(weights, num_samples, randomized, u=None):
+    """The CDF bin every fine-sample u of helper.py:203-243 falls in, (..., num_samples) int64:
+    two weight vectors whose bin indices differ place some fine sample in a different bin
+    (test attribution of inverse-CDF flips)."""
+    return _pdf_bins(weights, num_samples, randomized, u)[2]
+
+
+def sorted_piecewise_constant_pdf(bins, weights, num_samples, randomized, u=None):
+    """reference helper.py:203-243, restated with a per-ray searchsorted.
+
+    The reference's mask form (mask = u >= cdf; bin0 = max over masked bins, bin1 = min over
+    unmasked, first/last fallbacks) equals ``idx = searchsorted(cdf, u, right=True)``,
+    ``i0 = clamp(idx-1, 0, n-1)``, ``i1 = clamp(idx, max=n-1)`` -- pinned bit-exactly by the
+    golden vectors (including zero-weight plateaus and u == cdf ties).
+    """
+    cdf, u, idx = _pdf_bins(weights, num_samples, randomized, u)
+    n = cdf.shape[-1]
     i0 = torch.clamp(idx - 1, 0, n - 1)
     i1 = torch.clamp(idx, max=n - 1)
     bin0, bin1 = torch.gather(bins, -1, i0), torch.gather(bins, -1, i1)

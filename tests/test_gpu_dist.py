@@ -3,7 +3,10 @@
 RCCL with the same code).  (1) The row-band frame render + gather (aonerf.parallel,
 BASELINE config C4) equals the single-process render bit for bit.  (2) A DDP training step
 (tools/bench_train.py): after GradAllReduce every rank holds the average of the two ranks'
-gradients, bit for bit as computed from each batch alone."""
+gradients, bit for bit as computed from each batch alone.  (3) The RCCL branch itself (backend
+"nccl", a process group of one on the box's GPU -- RCCL refuses two ranks on one device): the
+640x480 frame (config C4's size) gathered device-resident and the flat-bucket gradient
+all-reduce, both equal to the single-process results bit for bit."""
 import os
 import socket
 
@@ -101,3 +104,60 @@ def test_sharded_render_and_ddp_step_two_ranks():
     for r in range(world):
         for a, b, c in zip(got[r][1], g0, g1):
             np.testing.assert_array_equal(a, ((b + c) / 2).cpu().numpy())
+
+
+def _worker_rccl(port, q):
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        from aonerf import parallel
+        from aonerf.render import create_spheric_poses, sapien_focal
+
+        assert dist.get_backend() == "nccl"
+        staged = []
+        real_gather = dist.gather
+
+        def spy(t, *a, **k):  # the payload must reach RCCL in HBM, not staged through the host
+            staged.append(t.device.type)
+            return real_gather(t, *a, **k)
+
+        dist.gather = spy
+        try:
+            net = _net()
+            Hf, Wf = 480, 640
+            frame, _ = parallel.render_frame_sharded(net, create_spheric_poses(4.0)[7], Hf, Wf,
+                                                     sapien_focal(Hf))
+        finally:
+            dist.gather = real_gather
+        assert staged == ["cuda"] and frame.is_cuda
+        grads = _grads(net, 0)
+        parallel.GradAllReduce(net.parameters())()
+        torch.cuda.synchronize()
+        q.put((frame.cpu().numpy(), [g.cpu().numpy() for g in grads],
+               [p.grad.cpu().numpy() for p in net.parameters()]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_gather_and_allreduce_world1():
+    """C4's code path over RCCL: device-resident gather of a 640x480 frame and the DDP
+    all-reduce on an nccl process group (world 1), bit-identical to one process without one."""
+    from aonerf.render import create_spheric_poses, render_frame, sapien_focal
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl, args=(_free_port(), q))
+    p.start()
+    frame, g_before, g_after = q.get(timeout=240)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    net = _net()
+    ref = render_frame(net, create_spheric_poses(4.0)[7], 480, 640, sapien_focal(480)).cpu()
+    np.testing.assert_array_equal(frame, ref.numpy())
+    g_ref = _grads(net, 0)
+    for a, b, c in zip(g_after, g_before, g_ref):
+        np.testing.assert_array_equal(a, b)  # all-reduce over one rank / 1 is the identity
+        np.testing.assert_array_equal(b, c.cpu().numpy())

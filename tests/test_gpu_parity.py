@@ -10,13 +10,17 @@ weights; PSNR within 0.05 dB):
       (2) fine sample positions == the reference's sample_pdf applied to OUR coarse weights,
           bit for bit (the oracle's pdf is pinned bit-exactly to the reference);
       (3) fine level vs the reference evaluated on OUR fine sample positions: within 1e-4;
-    and against the reference's own end-to-end outputs: >= 98% of rays within 1e-4, PSNR
-    delta <= 0.05 dB.  The remaining rays are the reference's own discontinuity: where coarse
-    weights are exactly 0 (ReLU'd density) the CDF has plateaus, and a coarse-weight change of
-    ~1e-7 can move a u across a plateau edge, shifting a fine sample by a whole bin (observed:
-    one ray of 480 moves 0.0625 in t and 6e-4 in rgb from a 1.8e-7 coarse-weight difference).
-    Any fp32 implementation with a different summation order shows the same (the reference
-    with an fp64 or split-K GEMM moves 2.6e-2 on depth on a 64x64 frame: `env_*` arrays).
+    and against the reference's own end-to-end outputs: >= 99.5% of rays within 1e-4, PSNR
+    delta <= 0.05 dB, and EVERY ray outside 1e-4 attributed automatically (plateau_flips): its
+    coarse weights are within 1e-4 of the reference's, and the reference's own sample_pdf
+    places some fine-sample u in a different CDF bin under our coarse weights than under the
+    reference's.  That is the reference's own discontinuity: where coarse weights are exactly 0
+    (ReLU'd density) the CDF has plateaus, and a coarse-weight change of ~1e-7 can move a u
+    across a plateau edge, shifting a fine sample by a whole bin (observed: one ray of 480
+    moves 0.0625 in t and 6e-4 in rgb from a 1.8e-7 coarse-weight difference).  Any fp32
+    implementation with a different summation order shows the same (the reference with an fp64
+    or split-K GEMM moves 2.6e-2 on depth on a 64x64 frame: `env_*` arrays).  An outlier
+    without such a bin crossing fails the test.
 """
 import numpy as np
 import pytest
@@ -28,19 +32,46 @@ from oracle import weights as W
 pytestmark = pytest.mark.gpu
 
 E2E_ATOL = 1e-4
-E2E_MIN_FRAC = 0.98
+E2E_MIN_FRAC = 0.995
 ENV_FACTOR = 4.0
 
 
-def assert_e2e(name, err, env=None):
-    """Direct comparison with the reference's end-to-end output: >= 98% of entries within 1e-4
-    (the rest: CDF-plateau flips, see the module docstring; `env` reported for context)."""
-    frac = (err <= E2E_ATOL).mean()
-    if frac < 1 and env is not None:
-        bad = err > E2E_ATOL
-        print(f"  {name}: {bad.sum()} entries > 1e-4 (reference re-association envelope there: "
-              f"max {env[bad].max():.2e})")
-    assert frac >= E2E_MIN_FRAC, f"{name}: only {frac * 100:.2f}% within {E2E_ATOL}"
+def plateau_flips(w_ours, w_ref, num_fine, randomized=False, u=None):
+    """Per ray: True where the ray's inverse-CDF resampling (helper.py:203-243) flips between
+    our coarse weights and the reference's -- the reference's own pdf puts some fine-sample u in
+    a different CDF bin under the two weight vectors -- while every coarse weight of the ray is
+    within 1e-4 of the reference's.  w_* (B, S_c) coarse weights; u: the fine uniforms in
+    randomized mode."""
+    wo = torch.as_tensor(np.asarray(w_ours, np.float32))
+    wr = torch.as_tensor(np.asarray(w_ref, np.float32))
+    uu = None if u is None else torch.as_tensor(np.asarray(u, np.float32))
+    io = O.pdf_bin_index(wo[..., 1:-1], num_fine, randomized, uu)
+    ir = O.pdf_bin_index(wr[..., 1:-1], num_fine, randomized, uu)
+    crossed = (io != ir).any(-1).numpy()
+    close = (wo - wr).abs().amax(-1).numpy() <= E2E_ATOL
+    return crossed & close
+
+
+def assert_e2e(name, err, env=None, flips=None):
+    """Direct comparison with the reference's end-to-end output: >= 99.5% of rays within 1e-4,
+    and every ray outside it attributed by ``flips`` (plateau_flips: a CDF-bin crossing of the
+    fine samples under coarse weights within 1e-4; see the module docstring).  `env` (the
+    reference's own re-association envelope) is reported for context."""
+    err = np.asarray(err)
+    bad = (err > E2E_ATOL).reshape(len(err), -1).any(-1)
+    frac = 1.0 - bad.mean() if len(bad) else 1.0
+    if bad.any():
+        msg = f"  {name}: {bad.sum()} of {len(bad)} rays > 1e-4 (max {err.max():.2e})"
+        if env is not None:
+            msg += f"; reference re-association envelope there: max {np.asarray(env)[bad].max():.2e}"
+        if flips is not None:
+            msg += f"; attributed to CDF-bin flips: {(bad & flips).sum()}"
+        print(msg)
+    assert flips is not None or not bad.any(), f"{name}: outliers and no attribution given"
+    if flips is not None:
+        unexplained = np.nonzero(bad & ~flips)[0]
+        assert len(unexplained) == 0, f"{name}: rays {unexplained[:10]} off by > 1e-4 without a CDF-bin flip"
+    assert frac >= E2E_MIN_FRAC, f"{name}: only {frac * 100:.2f}% of rays within {E2E_ATOL}"
 
 
 def check_chain(net, rays, params, randomized=False, white=True, u_coarse=None, u_fine=None,
@@ -119,10 +150,12 @@ def test_ray_generation(golden):
         np.testing.assert_array_equal(npy(dirs), g[f"dirs{k}"])
         o, v, d, radii = ray_utils.get_rays(dirs, torch.from_numpy(g[f"c2w{k}"]), True, True)
         np.testing.assert_array_equal(npy(o), g[f"rays_o{k}"])
-        report("rays_d", npy(d), g[f"rays_d{k}"], 1e-7)
-        np.testing.assert_allclose(npy(d), g[f"rays_d{k}"], rtol=0, atol=1e-6)
-        np.testing.assert_allclose(npy(v), g[f"viewdirs{k}"], rtol=0, atol=1e-6)
-        np.testing.assert_allclose(npy(radii), g[f"radii{k}"], rtol=0, atol=1e-6)
+        # a1/a2 reproduce the reference's op order (forward fma chains of (n,3)@(3,3) and the
+        # row norm): bit-exact
+        report("radii", npy(radii), g[f"radii{k}"], 0)
+        np.testing.assert_array_equal(npy(d), g[f"rays_d{k}"])
+        np.testing.assert_array_equal(npy(v), g[f"viewdirs{k}"])
+        np.testing.assert_array_equal(npy(radii), g[f"radii{k}"])
         fr = ray_utils.frame_rays(torch.from_numpy(g[f"c2w{k}"]), H, Wd, float(f))
         np.testing.assert_array_equal(npy(fr["rays_d"]), npy(d))
         # a band of the frame equals the same rows of the full frame
@@ -385,14 +418,16 @@ def test_mlp_encoded_api(golden, nerf):
 
 
 # ----------------------------------------------------------------------------- end to end
-def check_levels(ret, g):
+def check_levels(ret, g, randomized=False):
+    flips = plateau_flips(npy(ret[0][3]), g["coarse_weights"], 128, randomized,
+                          g["u_fine"] if randomized else None)
     for lv, name in enumerate(("coarse", "fine")):
         for j, k in enumerate(("rgb", "acc", "depth", "weights")):
             err = report(f"e2e {name} {k}", npy(ret[lv][j]), g[f"{name}_{k}"], E2E_ATOL)
             if name == "coarse":  # no resampling upstream: every ray within 1e-4
                 assert err.max() <= E2E_ATOL, f"coarse {k}: {err.max():.3e}"
             else:
-                assert_e2e(f"fine {k}", err, g[f"env_fine_{k}"])
+                assert_e2e(f"fine {k}", err, g[f"env_fine_{k}"], flips)
 
 
 def golden_coarse(g):
@@ -411,7 +446,7 @@ def test_forward_randomized_end_to_end(golden, nerf):
     params = O.split_state_dict(W.nerf_state_dict(0))
     ret = check_chain(nerf, rays_of(g), params, randomized=True, white=False,
                       u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]), coarse_ref=golden_coarse(g))
-    check_levels(ret, g)
+    check_levels(ret, g, randomized=True)
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
@@ -427,11 +462,16 @@ def test_render_frame_chunks(golden, precision):
         net = make_nerf(precision, num_coarse_samples=nc)
         c2w = torch.from_numpy(g[f"{tag}_c2w"])
         rays = frame_rays(c2w, H, Wd, float(g[f"{tag}_focal"]))
-        check_chain(net, rays, params)
+        ret = check_chain(net, rays, params)
+        # the reference's coarse weights on these rays: the oracle's coarse level (pinned to the
+        # reference by test_oracle_golden.py) on the same coarse samples (bit-exact, a3)
+        rc = {k: v.cpu() for k, v in rays.items()}
+        w_ref = O.render_level(params, rc, ret[0][4]["t_vals"].cpu(), 0, True)[2]
+        flips = plateau_flips(npy(ret[0][3]), w_ref.numpy(), net.num_fine_samples)
         out = render_rays(net, rays, chunk, True, 2.0, 6.0)
         for k in ("comp_rgb", "acc", "depth"):
             err = report(f"frame {tag} {k}", npy(out[k]), g[f"{tag}_{k}"], E2E_ATOL)
-            assert_e2e(f"frame {tag} {k}", err, g[f"{tag}_env_{k}"])
+            assert_e2e(f"frame {tag} {k}", err, g[f"{tag}_env_{k}"], flips)
         full = render_frame(net, c2w, H, Wd, float(g[f"{tag}_focal"]))
         np.testing.assert_array_equal(npy(full[:, :3]), npy(out["comp_rgb"]))
 
@@ -450,6 +490,65 @@ def test_psnr_delta(golden, precision):
     p_ref = O.psnr_each([torch.from_numpy(g["c1_comp_rgb"])], [target]).item()
     print(f"PSNR gpu {p_gpu:.4f} ref {p_ref:.4f} delta {p_gpu - p_ref:+.2e} dB")
     assert abs(p_gpu - p_ref) <= 0.05
+
+
+# ----------------------------------------------------------------------------- option paths
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_lindisp(golden, precision):
+    """NeRF(lindisp=True) (helper.py:117-118): the coarse schedule linear in disparity equals the
+    reference's bit for bit, and the two-level chain holds every link at 1e-4."""
+    g = golden("forward_eval.npz")
+    params = O.split_state_dict(W.nerf_state_dict(0))
+    rays = rays_of(g)
+    net = make_nerf(precision, lindisp=True)
+    ret = check_chain(net, rays, params)
+    t_ref, _ = O.sample_along_rays(torch.from_numpy(g["rays_o"]), torch.from_numpy(g["rays_d"]),
+                                   64, 2.0, 6.0, False, True)
+    np.testing.assert_array_equal(npy(ret[0][4]["t_vals"]), t_ref.numpy())
+    assert not np.array_equal(t_ref.numpy(), g["coarse_t"])  # the option changed the schedule
+
+
+@pytest.mark.parametrize("path", ["render", "train"])
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_density_noise(golden, precision, path):
+    """noise_std > 0 in randomized mode (model.py:183-184): raw_sigma += U[0,1) * noise_std
+    before the ReLU, drawn from torch's CUDA generator in the reference's order (level 0's B*S
+    draws, then level 1's).  Both the fused inference path (noise added to the raw output, the
+    activations moved to the compositor) and the training path (noise added in the training
+    kernel's epilogue) against the oracle fed the same draws, every level within 1e-4."""
+    if path == "train" and precision == "fp32":
+        pytest.skip("the training kernels are f16x3")
+    g = golden("forward_random.npz")
+    params = O.split_state_dict(W.nerf_state_dict(0))
+    rays = rays_of(g)
+    B = rays["rays_o"].shape[0]
+    net = make_nerf(precision, noise_std=1.0)
+    kw = dict(u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]), return_weights=True,
+              return_intermediates=True)
+    if path == "train":
+        net.requires_grad_(True)
+    torch.manual_seed(1234)
+    with torch.set_grad_enabled(path == "train"):
+        ret = net(rays, True, False, 2.0, 6.0, **kw)
+    torch.manual_seed(1234)
+    draws = [torch.rand((B * 65,), device="cuda"), torch.rand((B * 193,), device="cuda")]
+    rc = {k: v.cpu() for k, v in rays.items()}
+    for level in range(2):
+        t = ret[level][4]["t_vals"].cpu()
+        S = t.shape[1]
+        samples = O.cast_rays(t, rc["rays_o"], rc["rays_d"])
+        raw_rgb, raw_sigma = O.mlp_forward(params[level], O.pos_enc(samples, 0, 10),
+                                           O.pos_enc(rc["viewdirs"], 0, 4))
+        raw_sigma = raw_sigma + draws[level].cpu().view(B, S, 1) * 1.0
+        comp, acc, w, depth = O.volumetric_rendering(torch.sigmoid(raw_rgb), torch.relu(raw_sigma),
+                                                     t, rc["rays_d"], False)
+        for j, (k, want) in enumerate((("rgb", comp), ("acc", acc), ("depth", depth), ("weights", w))):
+            err = report(f"noise {path} level {level} {k}", npy(ret[level][j]), want.numpy(), E2E_ATOL)
+            assert err.max() <= E2E_ATOL, (level, k)
+    quiet = make_nerf(precision)
+    with torch.no_grad():
+        ret0 = quiet(rays, True, False, 2.0, 6.0, u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]))
+    assert not torch.equal(ret0[0][0], ret[0][0].detach())  # the noise was applied
 
 
 # ----------------------------------------------------------------------------- full size
@@ -477,12 +576,9 @@ def test_full_frame_properties(nerf):
     ro, rv, rd = O.get_rays(dirs, c2w[:3, :4], True)
     params = O.split_state_dict(W.nerf_state_dict(0))
     sub = {"rays_o": ro[sel], "rays_d": rd[sel], "viewdirs": rv[sel]}
-    ref = O.nerf_forward(params, sub, False, True, 2.0, 6.0)[1]
+    ref_all, inter = O.nerf_forward(params, sub, False, True, 2.0, 6.0, return_intermediates=True)
+    ref = ref_all[1]
     env = oracle_envelope(params, sub)
-    for j, k in ((0, "rgb"), (2, "depth"), (1, "acc")):
-        got = o[sel][:, {0: slice(0, 3), 2: 3, 1: 4}[j]]
-        err = report(f"640x480 subset {k}", got, ref[j].numpy(), E2E_ATOL)
-        assert_e2e(f"640x480 subset {k}", err, env[j])
     # every link gated at 1e-4 on the same subset, through the GPU's own rays
     from aonerf.ray_utils import frame_rays
 
@@ -490,6 +586,11 @@ def test_full_frame_properties(nerf):
     sel_t = torch.from_numpy(sel).cuda()
     got_sub = check_chain(nerf, {k: v[sel_t].contiguous() for k, v in gr.items()}, params)
     np.testing.assert_array_equal(npy(got_sub[1][0]), o[sel][:, :3])
+    flips = plateau_flips(npy(got_sub[0][3]), inter[0]["weights"].numpy(), nerf.num_fine_samples)
+    for j, k in ((0, "rgb"), (2, "depth"), (1, "acc")):
+        got = o[sel][:, {0: slice(0, 3), 2: 3, 1: 4}[j]]
+        err = report(f"640x480 subset {k}", got, ref[j].numpy(), E2E_ATOL)
+        assert_e2e(f"640x480 subset {k}", err, env[j], flips)
 
 
 def oracle_envelope(params, rays):
