@@ -61,6 +61,7 @@ _SIGNATURES = {
     "aon_sample_pdf": (c_int, [vp, c_i64, vp, c_i64, c_i64, c_int, c_int, vp, c_i64, vp, c_int,
                                vp, vp, vp, vp, vp]),
     "aon_mlp_packed_bytes": (c_size, [c_int]),
+    "aon_mlp_read_status": (c_int, [vp, c_size, ctypes.POINTER(ctypes.c_uint32), vp]),
     "aon_mlp_pack": (c_int, [ctypes.POINTER(AonMlpParams), c_int, vp, vp]),
     "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
@@ -148,3 +149,24 @@ def require_gpu(*tensors):
 
 def contig(t):
     return t if t.is_contiguous() else t.contiguous()
+
+
+# ---------------------------------------------------------------------------- fp16x3 range guard
+# Every packed weight buffer ends in a 16-B status block (include/aonerf.h aon_mlp_read_status):
+# word 0 is set by a fp16x3 kernel that met a value its fp16 hi/lo split cannot hold.  Each
+# training pack registers here when it is (re)packed, so the next optimizer step can refuse
+# gradients computed from such values (and then forgets it).
+PENDING_PACKS = {}
+
+
+def status_word(buf):
+    """Device int32 0-dim view of a packed buffer's range-status word."""
+    return buf.view(torch.int32)[-4]
+
+
+def range_overflow(bufs):
+    """True if any of these packed buffers' kernels saw a fp16x3 range overflow (one sync)."""
+    bufs = [b for b in bufs if b is not None]
+    if not bufs:
+        return False
+    return bool(torch.stack([status_word(b) for b in bufs]).any().item())

@@ -12,6 +12,8 @@ loads unchanged.  The forward pass runs on the fused HIP kernels:
 Intermediates live in HBM (a 640x480 frame needs ~1.6 GB), so a whole frame is one launch
 per stage instead of the reference's 80 chunk iterations.
 """
+import warnings
+
 import torch
 import torch.nn as nn
 import torch.nn.init as init
@@ -125,6 +127,11 @@ class NeRFMLP(nn.Module):
                L.stream(x.device))
         raw = raw.view(B, S, 4)
         return raw[..., :3], raw[..., 3:]
+
+
+# render path: after a f16x3 render, read the packs' range-status words (one sync per forward;
+# skipped while a HIP graph is being captured) and fall back to the fp32 kernels on overflow
+RANGE_CHECK = True
 
 
 def _events(timers):
@@ -243,6 +250,20 @@ class NeRF(nn.Module):
             if not return_intermediates:
                 out = out[:4] if return_weights else out[:3]
             ret.append(out)
+        if (not training and RANGE_CHECK and self.coarse_mlp.precision == "f16x3"
+                and not torch.cuda.is_current_stream_capturing()
+                and L.range_overflow([self.coarse_mlp._packed, self.fine_mlp._packed])):
+            # an activation left the fp16x3 split's range (|x| > 8188): these outputs are
+            # invalid -- render again on the exact-fp32 MFMA kernels (no range limit)
+            warnings.warn("NeRF: an MLP activation exceeded the fp16x3 range; re-rendered with "
+                          "precision='fp32'", RuntimeWarning)
+            self.set_precision("fp32")
+            try:
+                return self.forward(rays, randomized, white_bkgd, near, far, u_coarse=u_coarse,
+                                    u_fine=u_fine, return_weights=return_weights,
+                                    return_intermediates=return_intermediates, timers=timers)
+            finally:
+                self.set_precision("f16x3")
         return ret
 
     def _level_t(self, level, o, d, t_prev, w_prev, randomized, near, far, u_coarse, u_fine):

@@ -20,12 +20,15 @@ per-call biases (b' = b + W[:, latent cols] . latent, one tiny GEMM each): the p
 see K = 3 (deformation input), 63 (trunk input), 256 + 63 (skip) and 256 + 27 (view input).
 Every product runs on the f16x3 MFMA GEMM (aon_gemm); no torch arithmetic on the path.
 """
+import warnings
+
 import torch
 import torch.nn as nn
 import torch.nn.init as init
 
 from . import _lib as L
 from .linalg import ACT_SCALE, W_SCALE, gemm, linear_fwd
+from . import model as _vanilla
 from .model import _events, _record, level_t_vals
 
 class NeRFMLP(nn.Module):
@@ -362,4 +365,22 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
             if return_intermediates:
                 out = out + (dict(t_vals=t_vals, weights=weights, raw=raw),)
             ret.append(out)
+        mlps = (self.coarse_mlp, self.fine_mlp)
+        if (_vanilla.RANGE_CHECK and all(m._fused_ok() for m in mlps)
+                and not torch.cuda.is_current_stream_capturing()
+                and L.range_overflow([getattr(m, "_art_packed", None) for m in mlps])):
+            # an activation left the fp16x3 split's range (|x| > 8188) in the fused kernel:
+            # render again layer by layer (aon_gemm operands carry 2^-8: range 1.6e7)
+            warnings.warn("NeRF_AE_Art: an MLP activation exceeded the fused fp16x3 range; "
+                          "re-rendered on the layer-by-layer path", RuntimeWarning)
+            fused = [m.fused for m in mlps]
+            for m in mlps:
+                m.fused = False
+            try:
+                return self._forward_render(o, d, v, randomized, white_bkgd, near, far, latents,
+                                            u_coarse, u_fine, return_weights,
+                                            return_intermediates, timers)
+            finally:
+                for m, f in zip(mlps, fused):
+                    m.fused = f
         return ret

@@ -139,27 +139,35 @@ def _params_struct(P):
     return prm
 
 
-def _buffer(key, nbytes, dev):
-    # one buffer per kind and device: a pack and the kernel reading it are stream-ordered
+def _buffer(key, nbytes, dev, guard=False):
+    # one buffer per kind and device: a pack and the kernel reading it are stream-ordered.
+    # guard: a packed weight stream whose range-status word the next Adam.step checks
     buf = _packed.get((key, str(dev)))
     if buf is None:
         buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
         _packed[(key, str(dev))] = buf
+    if guard:
+        L.PENDING_PACKS[("train", key, str(dev))] = buf
     return buf
 
 
-def _pack(P, dev):
+# Adam.step refuses a step whose kernels met a fp16x3 range overflow (one sync per step)
+RANGE_CHECK = True
+
+
+def _pack(P, dev, tag=""):
     """The f16x3 weight stream of one level's parameters, re-packed on every call (the
-    optimizer updates the parameters in place behind torch's version counters)."""
+    optimizer updates the parameters in place behind torch's version counters).  ``tag``: one
+    buffer per level (its range-status word must survive until the optimizer step)."""
     prec = L.PREC["f16x3"]
-    buf = _buffer("fwd", L.lib().aon_mlp_packed_bytes(prec), dev)
+    buf = _buffer(f"fwd{tag}", L.lib().aon_mlp_packed_bytes(prec), dev, guard=True)
     L.call("aon_mlp_pack", L.ctypes.byref(_params_struct(P)), prec, L.ptr(buf), L.stream(dev))
     return buf
 
 
-def _pack_bwd(P, dev):
+def _pack_bwd(P, dev, tag=""):
     """The transposed weight stream of the fused backward chain (aon_mlp_bwd_pack)."""
-    buf = _buffer("bwd", L.lib().aon_mlp_bwd_packed_bytes(), dev)
+    buf = _buffer(f"bwd{tag}", L.lib().aon_mlp_bwd_packed_bytes(), dev, guard=True)
     L.call("aon_mlp_bwd_pack", L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
     return buf
 
@@ -194,7 +202,7 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
     dzb = torch.empty((R, 256), device=dev)
     dz = torch.empty((8, R, 256), device=dev)
     work = _buffer("work", 4, dev)
-    packed = _pack_bwd(P, dev)
+    packed = _pack_bwd(P, dev, S)
     e0 = _ev()
     L.call("aon_mlp_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), R, L.ptr(dzv),
            L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
@@ -235,7 +243,7 @@ def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, m
     for w, b in P:
         if not (w.is_contiguous() and b.is_contiguous()):
             raise ValueError("MLP parameters must be contiguous")
-    packed = _pack(P, dev)
+    packed = _pack(P, dev, S)
     L.call("aon_mlp_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
            L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hbuf),
            L.ptr(bot), L.ptr(hv), L.ptr(raw), L.ptr(masks), L.stream(dev))
@@ -379,6 +387,17 @@ class Adam:
 
     @torch.no_grad()
     def step(self, lr=None):
+        if RANGE_CHECK:
+            dev = str(self.params[0].device)
+            keys = [k for k in L.PENDING_PACKS if k[2] == dev]
+            bufs = [L.PENDING_PACKS.pop(k) for k in keys]
+            if L.range_overflow(bufs):
+                raise FloatingPointError(
+                    "a fp16x3 training kernel met a value beyond its fp16 hi/lo range "
+                    "(|activation| > 8188 or an overflowing gradient): the gradients of this step "
+                    "are invalid and were not applied.  Train this model on the layer-by-layer "
+                    "GEMM path (train.FUSED_FORWARD = train.FUSED_BACKWARD = False; train_art "
+                    "likewise), whose operands carry a 2^-8 scale (range 1.6e7).")
         self.step_count += 1
         for p in self.params:
             if p.grad is None:

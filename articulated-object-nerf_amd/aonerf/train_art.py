@@ -157,16 +157,19 @@ def _params_struct(P, fb=None):
     return prm
 
 
-def _buffer(key, nbytes, dev):
-    # one buffer per kind and device: a pack and the kernel reading it are stream-ordered
+def _buffer(key, nbytes, dev, guard=False):
+    # one buffer per kind and device: a pack and the kernel reading it are stream-ordered.
+    # guard: a packed weight stream whose range-status word train.Adam.step checks
     buf = _packed.get((key, str(dev)))
     if buf is None:
         buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
         _packed[(key, str(dev))] = buf
+    if guard:
+        L.PENDING_PACKS[("train_art", key, str(dev))] = buf
     return buf
 
 
-def _pack(geo, P, lat):
+def _pack(geo, P, lat, tag=""):
     """The fused kernel's fp16x3 weight stream (aon_mlp_art_pack) of one level's parameters with
     this call's latent codes folded into the biases; re-packed on every call (the optimizer
     updates the parameters in place)."""
@@ -176,14 +179,14 @@ def _pack(geo, P, lat):
           PTS0: _fold(*P[PTS0], geo.ne, shape),
           PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
           VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
-    buf = _buffer("fwd", L.lib().aon_mlp_art_packed_bytes(), dev)
+    buf = _buffer(f"fwd{tag}", L.lib().aon_mlp_art_packed_bytes(), dev, guard=True)
     L.call("aon_mlp_art_pack", L.ctypes.byref(_params_struct(P, fb)), L.ptr(buf), L.stream(dev))
     return buf
 
 
-def _pack_bwd(P, dev):
+def _pack_bwd(P, dev, tag=""):
     """The transposed weight stream of the fused backward chain (aon_mlp_art_bwd_pack)."""
-    buf = _buffer("bwd", L.lib().aon_mlp_art_bwd_packed_bytes(), dev)
+    buf = _buffer(f"bwd{tag}", L.lib().aon_mlp_art_bwd_packed_bytes(), dev, guard=True)
     L.call("aon_mlp_art_bwd_pack", L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
     return buf
 
@@ -203,7 +206,7 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     hv = torch.empty((4, R, geo.wc), device=dev)
     enc = torch.empty((R, geo.ne), device=dev)
     xyz = torch.empty((R, 3), device=dev)
-    packed = _pack(geo, P, lat)
+    packed = _pack(geo, P, lat, S)
     L.call("aon_mlp_art_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
            L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h),
            L.ptr(bot), L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks), L.stream(dev))
@@ -329,7 +332,7 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     dxp = torch.empty((R, 3), device=dev)
     dzd = torch.empty((4, R, wd), device=dev)
     work = _buffer("work", 4, dev)
-    L.call("aon_mlp_art_bwd", L.ptr(_pack_bwd(P, dev)), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
+    L.call("aon_mlp_art_bwd", L.ptr(_pack_bwd(P, dev, S)), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
            L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
     gs, acts = GRAD_SCALE, ACT_SCALE
 

@@ -211,6 +211,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd_f32(
 // ---- packing: torch [out][in] fp32 -> stream blocks (+ padded biases)
 __global__ void k_pack_f32(PackArgs a, float* __restrict__ out) {
   const int64_t total = (int64_t)kStreamBlocks * 256 + kBiasFloats;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint32_t*>(out + total) = 0u;  // status
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     float v = 0.f;
@@ -254,6 +255,17 @@ extern "C" size_t aon_mlp_packed_bytes(int precision) {
   // both precisions use the same block grid: fp32 tiles, or hi+lo fp16 pairs of equal size
   if (precision == AON_PREC_FP32 || precision == AON_PREC_F16X3) return kPackedBytesF32;
   return 0;
+}
+
+extern "C" int aon_mlp_read_status(const void* packed, size_t packed_bytes, uint32_t* status,
+                                   aon_stream_t stream) {
+  AON_REQUIRE(packed && status, "null pointer");
+  AON_REQUIRE(packed_bytes >= kStatusBytes && packed_bytes % 16 == 0, "bad packed size");
+  const char* word = static_cast<const char*>(packed) + packed_bytes - kStatusBytes;
+  hipError_t e = hipMemcpyAsync(status, word, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  return static_cast<int>(e);
 }
 
 static int f16x3_ncol() {

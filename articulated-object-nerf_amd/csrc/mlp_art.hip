@@ -85,10 +85,10 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     float dv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? px[c][e < 3 ? e : 0] * kActS : 0.f;
-    split8(dv, din.hi[0][c], din.lo[0][c]);
+    split8(dv, din.hi[0][c], din.lo[0][c], din.ovf);
 #pragma unroll
     for (int e = 0; e < 8; ++e) vv[e] *= kActS;
-    split8(vv, venc.hi[0][c], venc.lo[0][c]);
+    split8(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
     stash[64 * (6 * c + 4)] = __builtin_bit_cast(f4, venc.hi[0][c]);
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      split8(ev[k], enc.hi[k][c], enc.lo[k][c]);
+      split8(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
       stash[64 * (6 * c + 2 * k)] = __builtin_bit_cast(f4, enc.hi[k][c]);
       stash[64 * (6 * c + 2 * k + 1)] = __builtin_bit_cast(f4, enc.lo[k][c]);
     }
@@ -179,6 +179,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       }
     }
   }
+  range_report(bias_g + Net::kBiasFloats, x.ovf | y.ovf | enc.ovf | venc.ovf | din.ovf);
 }
 
 }  // namespace mlp

@@ -124,8 +124,8 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
       dv[e] = (g == 0 && e < 3) ? d[e < 3 ? e : 0] * s : 0.f;
       sv[e] = (g == 0 && e == 0) ? d[3] * s : 0.f;
     }
-    split8(dv, drgb.hi[0][0], drgb.lo[0][0]);
-    split8(sv, dsig.hi[0][0], dsig.lo[0][0]);
+    split8(dv, drgb.hi[0][0], drgb.lo[0][0], drgb.ovf);
+    split8(sv, dsig.hi[0][0], dsig.lo[0][0], dsig.ovf);
     stash[0] = __builtin_bit_cast(f4, dsig.hi[0][0]);
     stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
   }
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
     float dv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? dx[e < 3 ? e : 0] * sd : 0.f;
-    split8(dv, ddx.hi[0][0], ddx.lo[0][0]);
+    split8(dv, ddx.hi[0][0], ddx.lo[0][0], ddx.ovf);
   }
   // deformation head and MLP: d hd3 = W_dl^T dL/dx', then deformations_linear.3 .. 1
   layer_h<Net, AB_DL, false>(fp, none, ddx, y, bias_l, g,
@@ -213,8 +213,12 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
                              mask_bits(a.masks + 2 * ms, a.dzd + 2 * ws, 128, rows, N, g, invd));
   layer_h<Net, AB_D2, false>(fp, x, none, y, bias_l, g,
                              mask_bits(a.masks + 1 * ms, a.dzd + 1 * ws, 128, rows, N, g, invd));
+  // (the last layer's outputs are only stored, the enc-column layers' fragments are consumed in
+  // their epilogues: neither fp16 split is used, so neither is range-checked)
+  const uint64_t used_ovf = x.ovf | y.ovf | drgb.ovf | dsig.ovf | ddx.ovf;
   layer_h<Net, AB_D1, false>(fp, y, none, x, bias_l, g,
                              mask_bits(a.masks + 0 * ms, a.dzd, 128, rows, N, g, invd));
+  range_report(bias_g + Net::kBiasFloats, used_ovf);
 }
 
 }  // namespace mlp

@@ -100,8 +100,8 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
       dv[e] = (g == 0 && e < 3) ? d[e < 3 ? e : 0] * s : 0.f;
       sv[e] = (g == 0 && e == 0) ? d[3] * s : 0.f;
     }
-    split8(dv, drgb.hi[0][0], drgb.lo[0][0]);
-    split8(sv, dsig.hi[0][0], dsig.lo[0][0]);
+    split8(dv, drgb.hi[0][0], drgb.lo[0][0], drgb.ovf);
+    split8(sv, dsig.hi[0][0], dsig.lo[0][0], dsig.ovf);
     stash[0] = __builtin_bit_cast(f4, dsig.hi[0][0]);
     stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
   }
@@ -141,8 +141,11 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
                            mask_bits(a.masks + 2 * ms, a.dz + 2 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_2, false>(fp, y, none, x, bias_l, g,
                            mask_bits(a.masks + 1 * ms, a.dz + 1 * hs, 256, rows, N, g, inv));
+  // (the last layer's outputs are only stored: its fp16 split is unused, so not range-checked)
+  const uint64_t used_ovf = x.ovf | y.ovf | drgb.ovf | dsig.ovf;
   layer_h<Net, B_1, false>(fp, x, none, y, bias_l, g,
                            mask_bits(a.masks + 0 * ms, a.dz, 256, rows, N, g, inv));
+  range_report(bias_g + Net::kBiasFloats, used_ovf);
 }
 
 }  // namespace mlp

@@ -95,11 +95,11 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     for (int k = 0; k < 2; ++k) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) ev[k][e] *= (AON_F16X3_V2 ? kActS : kActScale);
-      split8(ev[k], enc.hi[k][c], enc.lo[k][c]);
+      split8(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) vv[e] *= (AON_F16X3_V2 ? kActS : kActScale);
-    split8(vv, venc.hi[0][c], venc.lo[0][c]);
+    split8(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
   }
 
   // park the encodings in LDS until the skip / view layers need them (frees 24 VGPRs for the
@@ -169,6 +169,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       }
     }
   }
+  range_report(bias_g + kBiasFloats, x.ovf | y.ovf | enc.ovf | venc.ovf);
 }
 
 // ---- packing: torch [out][ldw] fp32 -> hi/lo fp16 blocks (+ biases at activation scale), for
@@ -230,6 +231,7 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
 #endif
     } else {
       const int i = static_cast<int>(e - nhalf);
+      if (i == 0) *reinterpret_cast<uint32_t*>(bias_out + a.bias_floats) = 0u;  // range status
       int li = 0;
       while (li + 1 < a.n_layers && a.layers[li + 1].bias0 <= i) ++li;
       const int o = i - a.layers[li].bias0;

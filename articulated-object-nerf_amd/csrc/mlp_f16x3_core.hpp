@@ -35,14 +35,31 @@ __device__ __forceinline__ _Float16 lo_of(float v, _Float16 h) {
 #endif
 }
 
-// 8 fp32 values (already at activation scale) -> (hi, lo) fp16 fragments
-__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
+// Range guard.  fp16 holds |x| <= 65504: at the 2^3 activation scale a hidden activation past
+// |x| = 8188 (gradients: past 65504 / their per-call scale) would become inf in the hi part --
+// and the NaN it makes in the next layer is squashed to 0 by fmax's ReLU: silent garbage.
+// Every value split into a hi/lo pair is range-tested (Frag::ovf: the wave's ballot of the
+// test, OR-ed in SGPRs -- one v_cmp + one s_or per value pair, no VGPR held; a running fmax or
+// a per-lane bool was a VGPR chain through every epilogue that made hipcc spill hundreds of
+// registers), and a wave that saw one past the limit sets
+// the status word behind its bias table (zeroed by the pack, read by aon_mlp_read_status): the
+// caller learns the result is invalid.
+constexpr float kF16Max = 65504.0f;
+__device__ __forceinline__ void range_report(const float* bias_end, uint64_t ovf) {
+  if (ovf && (threadIdx.x & 63) == 0) *reinterpret_cast<uint32_t*>(const_cast<float*>(bias_end)) = 1u;
+}
+
+// 8 fp32 values (already at activation scale) -> (hi, lo) fp16 fragments; ovf |= out of range
+__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, uint64_t& ovf) {
+  float m = 0.0f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const _Float16 h = static_cast<_Float16>(v[j]);
     hi[j] = h;
     lo[j] = lo_of(v[j], h);
+    m = fmaxf(m, fabsf(v[j]));
   }
+  ovf |= __builtin_amdgcn_ballot_w64(m > kF16Max);
 }
 
 // One-step-ahead fragment prefetch over the weight stream: blocks are consumed strictly in
@@ -96,6 +113,7 @@ struct FragPipe {
 template <int N, int NCOL>
 struct Frag {
   h8 hi[N][NCOL], lo[N][NCOL];
+  uint64_t ovf = 0;  // lanes that split a value out of fp16 range into this set (range guard)
 };
 
 // Epilogue policies of layer_h.  begin_pair(pr) runs at the start of output pair pr (before its
@@ -260,6 +278,7 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
       if (RELU) v = fmaxf(v, 0.0f);
       vv[e] = st.post(pr, uu, r0 + e, c, v);
     }
+    out.ovf |= __builtin_amdgcn_ballot_w64(fmaxf(fabsf(vv[0]), fabsf(vv[1])) > kF16Max);
     st.put(pr, uu, r0, c, vv[0], vv[1]);
 #if AON_F16X3_V2 && AON_FMA_MIX
     // hi pair by one v_cvt_pk_f16_f32; lo_e = v_e - hi_e by v_fma_mix_f32 reading the fp16 half

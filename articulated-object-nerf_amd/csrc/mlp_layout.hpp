@@ -81,7 +81,10 @@ constexpr int kStreamBlocks = (kBlocks + 63) / 64 * 64;          // 2368: whole 
 constexpr int kNumChunks = kStreamBlocks / kChunk;                // 148
 constexpr int kBiasFloats = 2464;
 constexpr size_t kStreamBytesF32 = (size_t)kStreamBlocks * 1024;
-constexpr size_t kPackedBytesF32 = kStreamBytesF32 + kBiasFloats * 4;
+// every packed buffer ends in a 16-B status block (word 0: the fp16x3 range guard,
+// mlp_f16x3_core.hpp range_report; zeroed by the pack, read by aon_mlp_status)
+constexpr size_t kStatusBytes = 16;
+constexpr size_t kPackedBytesF32 = kStreamBytesF32 + kBiasFloats * 4 + kStatusBytes;
 
 constexpr bool layout_ok() {
   int blk = 0, bias = 0;
@@ -203,7 +206,7 @@ struct NetH {
   static constexpr int kStreamBlocks = STREAM_BLOCKS;  // padded to whole LDS chunks
   static constexpr int kBiasFloats = BIAS_FLOATS;
   static constexpr size_t kStreamBytes = (size_t)STREAM_BLOCKS * 1024;
-  static constexpr size_t kPackedBytes = kStreamBytes + (size_t)BIAS_FLOATS * 4;
+  static constexpr size_t kPackedBytes = kStreamBytes + (size_t)BIAS_FLOATS * 4 + kStatusBytes;
   static constexpr LayerDesc layer(int i) { return TABLE[i]; }
   static constexpr bool ok() {
     int blk = 0, bias = 0;

@@ -126,6 +126,16 @@ size_t aon_mlp_packed_bytes(int precision);
 int aon_mlp_pack(const aon_mlp_params* params, int precision, void* packed,
                  aon_stream_t stream);
 
+/* fp16x3 range guard.  Every packed buffer (aon_mlp_pack, aon_mlp_art_pack, the backward-chain
+ * packs) ends in a 16-byte status block that the pack zeroes.  A fp16x3 kernel that met a value
+ * its fp16 hi/lo split cannot hold (|activation| > 8188, or a gradient past 65504 at its
+ * per-call scale) sets status word 0 to 1: the outputs of that launch are invalid.  The block
+ * stays set until the next pack (sticky across launches).  aon_mlp_read_status copies word 0
+ * to *status (host) and synchronises the stream; packed_bytes is the size the *_packed_bytes
+ * query returned.  (The fp32 MFMA path has no such limit and never sets it.) */
+int aon_mlp_read_status(const void* packed, size_t packed_bytes, uint32_t* status,
+                        aon_stream_t stream);
+
 /* NeRFMLP.forward (model.py:95-120) fused with cast_rays + pos_enc (model.py:175-181):
  * per sample row r = b*S + s: xyz = o[b] + t[r]*d[b], enc = pos_enc(xyz, 0, 10),
  * venc = pos_enc(viewdirs[b], 0, 4); out (B*S, 4) = [rgb(3), sigma].

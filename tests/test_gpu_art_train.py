@@ -340,8 +340,9 @@ def test_art_train_step_c5_4096_rays():
     """Config C5 on the articulated auto-decoder at its stated size: one training step on a
     4096-ray batch.  Loss against the oracle on our sample positions (rtol 1e-5) and end to end
     (rtol 1e-4), and every MLP parameter's and latent code's gradient teacher-forced against the
-    fp32 oracle within 1e-2 of the tensor's max (the deformation gradients see sin(2^9 x'):
-    the 64-ray test above measures the oracle's own fp32-vs-fp64 spread at ~1e-2 there)."""
+    fp32 oracle within max(2 x the oracle's own fp32-vs-fp64 distance, 1e-3) of the tensor's
+    max, as the 64-ray test above (the deformation gradients see sin(2^9 x'): there the fp32
+    oracle itself sits ~1e-2 from fp64)."""
     from aonerf import train_art
     from test_gpu_train import c5_batch
 
@@ -358,35 +359,46 @@ def test_art_train_step_c5_4096_rays():
         x.retain_grad()
     loss.backward()
     torch.cuda.synchronize()
-    rays = {k: batch[k].cpu() for k in ("rays_o", "rays_d", "viewdirs")}
-    tgt = target.cpu()
-    params = [{k: v.requires_grad_(True) for k, v in p.items()}
-              for p in O.split_state_dict(W.art_state_dict(0))]
-    lat = {k: v.detach().cpu().requires_grad_(True) for k, v in latents.items()}
+    lat_dev = {k: v.detach().cpu() for k, v in latents.items()}
     with torch.no_grad():
-        e2e = O.art_nerf_forward(params, rays, True, True, 2.0, 6.0, lat, u_coarse=u_c.cpu(),
+        rays = {k: batch[k].cpu() for k in ("rays_o", "rays_d", "viewdirs")}
+        params = O.split_state_dict(W.art_state_dict(0))
+        e2e = O.art_nerf_forward(params, rays, True, True, 2.0, 6.0, lat_dev, u_coarse=u_c.cpu(),
                                  u_fine=u_f.cpu())
-    ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
-    ref_loss = 0.0
-    for level in range(2):
-        t = ret[level][3]["t_vals"].cpu()
-        comp, acc, w, depth = O.art_render_level(params, rays, t, level, True, lat)
-        ref_loss = ref_loss + O.img2mse(comp, tgt)
-    ref_loss.backward()
-    print(f"C5 art loss gpu {loss.item():.8f}  oracle on our t {ref_loss.item():.8f}  "
+        tgt = target.cpu()
+        ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
+    ref, ref_loss = {}, None
+    for dtype in (torch.float32, torch.float64):
+        rays = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
+        params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
+                  for p in O.split_state_dict(W.art_state_dict(0))]
+        lat = {k: v.to(dtype).requires_grad_(True) for k, v in lat_dev.items()}
+        tgt = target.cpu().to(dtype)
+        lv_loss = 0.0
+        for level in range(2):
+            t = ret[level][3]["t_vals"].cpu().to(dtype)
+            comp, acc, w, depth = O.art_render_level(params, rays, t, level, True, lat)
+            lv_loss = lv_loss + O.img2mse(comp, tgt)
+        lv_loss.backward()
+        if dtype == torch.float32:
+            ref_loss = lv_loss.item()
+        ref[dtype] = {f"{pre}{n}": v.grad.double().numpy()
+                      for lv, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")) for n, v in params[lv].items()}
+        ref[dtype].update({f"latent {k}": v.grad.double().numpy() for k, v in lat.items()})
+        del params, lv_loss
+    print(f"C5 art loss gpu {loss.item():.8f}  oracle on our t {ref_loss:.8f}  "
           f"oracle end to end {ref_e2e:.8f}")
-    np.testing.assert_allclose(loss.item(), ref_loss.item(), rtol=1e-5)
+    np.testing.assert_allclose(loss.item(), ref_loss, rtol=1e-5)
     np.testing.assert_allclose(loss.item(), ref_e2e, rtol=1e-4)
     ours = {n: p.grad.cpu().numpy() for n, p in net.named_parameters()}
     ours.update({f"latent {k}": v.grad.cpu().numpy() for k, v in latents.items()})
-    want = {f"{pre}{n}": v.grad.numpy() for lv, pre in ((0, "coarse_mlp."), (1, "fine_mlp."))
-            for n, v in params[lv].items()}
-    want.update({f"latent {k}": v.grad.numpy() for k, v in lat.items()})
     worst = 0.0
-    for name, w_ in want.items():
-        e = rel_err(ours[name], w_)
+    for name, want in ref[torch.float32].items():
+        e = rel_err(ours[name], want)
+        env = rel_err(want, ref[torch.float64][name])
+        allow = max(2 * env, 1e-3)
         if e > 1e-4:
-            print(f"  {name:45s} {e:.2e}")
-        worst = max(worst, e)
-        assert e < 1e-2, (name, e)
-    print(f"C5 art teacher-forced grads (4096 rays): worst max-rel err {worst:.2e}")
+            print(f"  {name:45s} ours {e:.2e}  oracle fp32-vs-fp64 {env:.2e}")
+        worst = max(worst, e / allow)
+        assert e <= allow, (name, e, env)
+    print(f"C5 art teacher-forced grads (4096 rays): worst error / allowance {worst:.2f}")

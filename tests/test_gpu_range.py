@@ -1,0 +1,156 @@
+"""The fp16x3 range guard (include/aonerf.h aon_mlp_read_status).
+
+The fp16x3 kernels carry hidden activations at 2^3 in fp16 hi/lo pairs, so an activation past
+|x| = 8188 cannot be represented; the reference (fp32) has no such limit.  The kernels test
+every value they split and set the pack's status word; the render path then re-renders on the
+exact-fp32 MFMA kernels, the training optimizer refuses the step.
+
+Weights are the golden PCG64 weights with pts_linears.0 scaled by F (ReLU is positively
+homogeneous, so every hidden activation grows ~F-fold): F chosen from the oracle so the largest
+hidden activation is ~6e3 (inside the range: the f16x3 path must stay, within 1e-4 of the
+oracle on every gated link) or ~2e4 (outside: the guard must fire and the fp32 fallback must
+stay within 1e-4 of the oracle).  Parity of trained-magnitude activations is otherwise unpinned
+by the reference (it ships no checkpoints).
+"""
+import ctypes
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+from oracle import weights as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _max_hidden(p, enc, venc):
+    """Largest |activation| the fp16x3 kernels would split (every hidden layer, the bottleneck,
+    the view layer), by the oracle's arithmetic (model.py:95-120)."""
+    S, C = enc.shape[1:]
+    x = enc.reshape(-1, C)
+    inputs, m = x, 0.0
+    for i in range(8):
+        x = torch.relu(x @ p[f"pts_linears.{i}.weight"].T + p[f"pts_linears.{i}.bias"])
+        m = max(m, float(x.abs().max()))
+        if i == 4:
+            x = torch.cat([x, inputs], -1)
+    bot = x @ p["bottleneck_layer.weight"].T + p["bottleneck_layer.bias"]
+    m = max(m, float(bot.abs().max()))
+    cond = torch.tile(venc[:, None, :], (1, S, 1)).reshape(-1, venc.shape[-1])
+    hv = torch.relu(torch.cat([bot, cond], -1) @ p["views_linear.0.weight"].T + p["views_linear.0.bias"])
+    return max(m, float(hv.abs().max()))
+
+
+def _scaled(golden, target_max):
+    g = golden("forward_eval.npz")
+    sd = W.nerf_state_dict(0)
+    params = O.split_state_dict(sd)
+    rays = {k: torch.from_numpy(g[k]) for k in ("rays_o", "rays_d", "viewdirs")}
+    t, xyz = O.sample_along_rays(rays["rays_o"], rays["rays_d"], 64, 2.0, 6.0, False, False)
+    enc, venc = O.pos_enc(xyz, 0, 10), O.pos_enc(rays["viewdirs"], 0, 4)
+    m1 = _max_hidden(params[0], enc, venc)
+    # first guess by homogeneity, then one correction step (biases do not scale)
+    f = target_max / m1
+    for _ in range(3):
+        p = dict(params[0])
+        p["pts_linears.0.weight"] = p["pts_linears.0.weight"] * f
+        p["pts_linears.0.bias"] = p["pts_linears.0.bias"] * f
+        f *= target_max / _max_hidden(p, enc, venc)
+    sd = dict(sd)
+    for lv in ("coarse_mlp", "fine_mlp"):
+        for k in ("weight", "bias"):
+            sd[f"{lv}.pts_linears.0.{k}"] = (sd[f"{lv}.pts_linears.0.{k}"] * np.float32(f)).astype(np.float32)
+    params = O.split_state_dict(sd)
+    p = params[0]
+    return g, sd, params, _max_hidden(p, enc, venc)
+
+
+def _net(sd, precision="f16x3"):
+    from aonerf.model import NeRF
+
+    net = NeRF(precision=precision).cuda()
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return net.requires_grad_(False)
+
+
+def _coarse_vs_oracle(net, g, params):
+    rays = {k: torch.from_numpy(g[k]).cuda() for k in ("rays_o", "rays_d", "viewdirs")}
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        ret = net(rays, False, True, 2.0, 6.0, return_weights=True, return_intermediates=True)
+    rc = {k: v.cpu() for k, v in rays.items()}
+    ref = O.render_level(params, rc, ret[0][4]["t_vals"].cpu(), 0, True)
+    err = max(float((ret[0][0].cpu() - ref[0]).abs().max()), float((ret[0][1].cpu() - ref[1]).abs().max()),
+              float((ret[0][3].cpu() - ref[2]).abs().max()))
+    return err, [str(x.message) for x in w], net
+
+
+def test_inside_range_stays_f16x3(golden):
+    g, sd, params, m = _scaled(golden, 6.0e3)
+    print(f"largest hidden activation {m:.1f}")
+    assert 4e3 < m < 8e3
+    net = _net(sd)
+    err, warns, net = _coarse_vs_oracle(net, g, params)
+    from aonerf import _lib as L
+
+    print(f"f16x3 at |h| ~ {m:.0f}: coarse rgb/acc/weights max |gpu - oracle| {err:.2e}")
+    assert not warns and not L.range_overflow([net.coarse_mlp._packed])
+    assert err <= 1e-4
+
+
+def test_outside_range_detected_and_rendered_in_fp32(golden):
+    from aonerf import _lib as L
+
+    g, sd, params, m = _scaled(golden, 2.0e4)
+    print(f"largest hidden activation {m:.1f}")
+    assert m > 1.2e4
+    net = _net(sd)
+    # the raw kernel: the status word of the pack is set by the launch, cleared by a repack
+    rays = {k: torch.from_numpy(g[k]).cuda() for k in ("rays_o", "rays_d", "viewdirs")}
+    t = torch.from_numpy(np.ascontiguousarray(g["coarse_t"])).cuda()
+    net.coarse_mlp.forward_rays(rays["rays_o"], rays["rays_d"], rays["viewdirs"], t)
+    packed = net.coarse_mlp._packed
+    st = ctypes.c_uint32(7)
+    L.call("aon_mlp_read_status", L.ptr(packed), packed.numel() * 4, ctypes.byref(st),
+           L.stream(packed.device))
+    assert st.value == 1, "overflow not reported"
+    net.coarse_mlp._packed_key = None  # force a repack: the status word is cleared
+    net.coarse_mlp.packed_weights()
+    L.call("aon_mlp_read_status", L.ptr(net.coarse_mlp._packed), packed.numel() * 4,
+           ctypes.byref(st), L.stream(packed.device))
+    assert st.value == 0
+    # the render path: warns, re-renders on the fp32 kernels, matches the oracle
+    err, warns, net = _coarse_vs_oracle(net, g, params)
+    print(f"fallback render at |h| ~ {m:.0f}: max |gpu - oracle| {err:.2e}; warnings {warns}")
+    assert any("fp16x3 range" in w for w in warns)
+    assert net.coarse_mlp.precision == "f16x3"  # restored after the fallback
+    assert err <= 1e-4
+    # the fp32 path itself never reports
+    n32 = _net(sd, "fp32")
+    e32, w32, _ = _coarse_vs_oracle(n32, g, params)
+    assert not w32 and e32 <= 1e-4
+
+
+def test_training_step_refused_on_overflow(golden):
+    from aonerf import train
+
+    g, sd, params, m = _scaled(golden, 2.0e4)
+    net = _net(sd).requires_grad_(True)
+    rays = {k: torch.from_numpy(g[k]).cuda() for k in ("rays_o", "rays_d", "viewdirs")}
+    batch = dict(rays, target=torch.full((rays["rays_o"].shape[0], 3), 0.5, device="cuda"))
+    opt = train.Adam(net.parameters())
+    loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
+    loss.backward()
+    before = [p.detach().clone() for p in net.parameters()]
+    with pytest.raises(FloatingPointError):
+        opt.step()
+    assert all(torch.equal(a, p.detach()) for a, p in zip(before, net.parameters()))
+    # inside the range the same step goes through
+    g, sd, params, m = _scaled(golden, 6.0e3)
+    net = _net(sd).requires_grad_(True)
+    opt = train.Adam(net.parameters())
+    loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
+    loss.backward()
+    opt.step()

@@ -393,8 +393,8 @@ def test_train_step_c5_4096_rays():
     samples).  The loss against the oracle's end-to-end loss on the same rays and uniforms
     (rtol 1e-4: a CDF-bin flip of a few rays' fine samples moves the mean by ~1e-6), the loss of
     our sample positions to 1e-5, and every parameter's gradient teacher-forced against the fp32
-    oracle's autograd at our sample positions within 1e-3 of the tensor's max (the 64-ray test
-    above pins the oracle's own fp32-vs-fp64 spread; measured here: printed)."""
+    oracle's autograd at our sample positions within max(2 x the oracle's own fp32-vs-fp64
+    distance, 1e-3) of the tensor's max, as the 64-ray test above."""
     from aonerf import train
 
     net = _make_trainable(0)
@@ -405,28 +405,41 @@ def test_train_step_c5_4096_rays():
     loss = train.img2mse(ret[1][0], target) + train.img2mse(ret[0][0], target)
     loss.backward()
     torch.cuda.synchronize()
-    rays = {k: batch[k].cpu() for k in ("rays_o", "rays_d", "viewdirs")}
-    tgt = target.cpu()
     with torch.no_grad():
+        rays = {k: batch[k].cpu() for k in ("rays_o", "rays_d", "viewdirs")}
         e2e = O.nerf_forward(_oracle_params(0, False), rays, True, True, 2.0, 6.0,
                              u_coarse=u_c.cpu(), u_fine=u_f.cpu())
-    ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
-    params = _oracle_params(0)
-    ref_loss = 0.0
-    for level in range(2):
-        t = ret[level][4]["t_vals"].cpu()
-        comp, acc, w, depth = O.render_level(params, rays, t, level, True)
-        ref_loss = ref_loss + O.img2mse(comp, tgt)
-    ref_loss.backward()
-    print(f"C5 loss gpu {loss.item():.8f}  oracle on our t {ref_loss.item():.8f}  "
+        tgt = target.cpu()
+        ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
+    ref, ref_loss = {}, None
+    for dtype in (torch.float32, torch.float64):  # the oracle at our sample positions
+        rays = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
+        params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
+                  for p in O.split_state_dict(W.nerf_state_dict(0))]
+        tgt = target.cpu().to(dtype)
+        lv_loss = 0.0
+        for level in range(2):
+            t = ret[level][4]["t_vals"].cpu().to(dtype)
+            comp, acc, w, depth = O.render_level(params, rays, t, level, True)
+            lv_loss = lv_loss + O.img2mse(comp, tgt)
+        lv_loss.backward()
+        if dtype == torch.float32:
+            ref_loss = lv_loss.item()
+        ref[dtype] = {f"{pre}{n}": v.grad.double().numpy()
+                      for lv, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")) for n, v in params[lv].items()}
+        del params, lv_loss
+    print(f"C5 loss gpu {loss.item():.8f}  oracle on our t {ref_loss:.8f}  "
           f"oracle end to end {ref_e2e:.8f}")
-    np.testing.assert_allclose(loss.item(), ref_loss.item(), rtol=1e-5)
+    np.testing.assert_allclose(loss.item(), ref_loss, rtol=1e-5)
     np.testing.assert_allclose(loss.item(), ref_e2e, rtol=1e-4)
     named = dict(net.named_parameters())
     worst = 0.0
-    for lv, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")):
-        for n, v in params[lv].items():
-            e = rel_err(named[pre + n].grad.cpu().numpy(), v.grad.numpy())
-            worst = max(worst, e)
-            assert e < 1e-3, (pre + n, e)
-    print(f"C5 teacher-forced grads (4096 rays): worst max-rel err {worst:.2e} vs the fp32 oracle")
+    for name, want in ref[torch.float32].items():
+        e = rel_err(named[name].grad.cpu().numpy(), want)
+        env = rel_err(want, ref[torch.float64][name])
+        allow = max(2 * env, 1e-3)
+        if e > 1e-4:
+            print(f"  {name:40s} ours {e:.2e}  oracle fp32-vs-fp64 {env:.2e}")
+        worst = max(worst, e / allow)
+        assert e <= allow, (name, e, env)
+    print(f"C5 teacher-forced grads (4096 rays): worst error / allowance {worst:.2f}")
