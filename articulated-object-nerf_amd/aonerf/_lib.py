@@ -38,7 +38,7 @@ class AonGemmArgs(ctypes.Structure):
                 ("B", vp), ("ldb", c_i64), ("b_kc", c_int), ("b_rdiv", c_i64),
                 ("C", vp), ("ldc", c_i64), ("bias", vp), ("mask", vp), ("ldm", c_i64),
                 ("relu", c_int), ("accumulate", c_int), ("a_scale", c_float), ("b_scale", c_float),
-                ("k_splits", c_i64), ("rowsum", vp)]
+                ("k_splits", c_i64), ("rowsum", vp), ("a_amax", vp)]
 
 
 class AonAdamTensor(ctypes.Structure):
@@ -111,7 +111,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.aon_abi_version() != 4:
+        if handle.aon_abi_version() != 5:
             raise ImportError("aonerf: ABI version mismatch")
         _lib = handle
     return _lib

@@ -208,11 +208,13 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
            L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
     _rec(f"bwd_chain{S}", e0, R)
     e0 = _ev()
-    gs, acts = GRAD_SCALE, ACT_SCALE
+    acts = ACT_SCALE
 
     def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None):
+        # dY rides at the chain's own per-call scale from max |d raw| (the word in `work`)
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
-             b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=gs, b_scale=acts, rowsum=db)
+             b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=1.0, b_scale=acts, rowsum=db,
+             a_amax=work)
 
     dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1])               # rgb_layer
     dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0

@@ -336,11 +336,15 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
            L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
     gs, acts = GRAD_SCALE, ACT_SCALE
 
-    def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True):
+    def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True, chain_scale=True):
+        # chain_scale: dY is in the chain's d raw domain (draw, view/trunk outputs): A rides at
+        # the chain's own per-call scale from max |d raw| (the word it left in `work`); the
+        # deformation branch (dL/dx' carries pos_enc's 2^9, rescaled per sample) keeps 2^10
         dW = G[i][0]
         gemm(dW[:, col0:] if col0 else dW, dY, X, dW.shape[0], n_in, R, lda=ldy, a_kc=False,
-             ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0), a_scale=gs, b_scale=acts,
-             rowsum=G[i][1] if bias else None)
+             ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0), a_scale=1.0 if chain_scale else gs,
+             b_scale=acts, rowsum=G[i][1] if bias else None,
+             a_amax=work if chain_scale else None)
 
     def dlatent(i, col0, l, dl, accumulate):
         dW, db = G[i]
@@ -365,10 +369,10 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     dlatent(PTS0 + 5, nw + ne, shape, dshape, False)
     dweight(PTS0, dz[0], nw, enc, ne, ne)                                 # pts_linears.0
     dlatent(PTS0, ne, shape, dshape, True)
-    dweight(DL, dxp, 3, hd[3], wd, wd)                                    # deformation_layer
+    dweight(DL, dxp, 3, hd[3], wd, wd, chain_scale=False)                 # deformation_layer
     for i in range(3, 0, -1):                                             # deformations_linear.i
-        dweight(DEF0 + i, dzd[i], wd, hd[i - 1], wd, wd)
-    dweight(DEF0, dzd[0], wd, xyz, 3, 3)                                  # deformations_linear.0
+        dweight(DEF0 + i, dzd[i], wd, hd[i - 1], wd, wd, chain_scale=False)
+    dweight(DEF0, dzd[0], wd, xyz, 3, 3, chain_scale=False)               # deformations_linear.0
     dlatent(DEF0, 3, shape, dshape, True)
     dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
 

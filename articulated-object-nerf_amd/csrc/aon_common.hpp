@@ -117,4 +117,17 @@ __device__ __forceinline__ float pos_enc_feature(float x0, float x1, float x2, i
   return sinf(cosine ? __fadd_rn(xb, kHalfPi) : xb);
 }
 
+// Per-call power-of-two scale of a gradient operand from the bits of its max |x| (k_absmax):
+// |x * s| < 2^8 for the largest |x|: s = 2^(8 - e) with max = m 2^e, m in [0.5, 1).  The fp16
+// hi/lo splits of the backward chains and the weight-gradient GEMMs carry gradients at s, so
+// their hi parts stay normal however small the loss gradient gets (a mean over 4096 rays).
+__device__ __forceinline__ float grad_scale(uint32_t bits) {
+  const float m = __uint_as_float(bits);
+  if (!(m > 0.0f) || !isfinite(m)) return 1.0f;
+  int e;
+  (void)frexpf(m, &e);
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  return __builtin_ldexpf(1.0f, 8 - e);
+}
+
 }  // namespace aon

@@ -51,6 +51,7 @@ struct Params {
   int64_t ldm;
   int relu, accumulate;
   float sa, sb, inv_s;  // operand prescales (powers of two); result * inv_s
+  const uint32_t* sa_bits;  // optional: A's scale also times grad_scale(*sa_bits) (per call)
   int64_t kchunk;       // K rows per blockIdx.z (split-K); == K when not split
   float* part;          // split-K partials [z][M][N] (unscaled epilogue-free sums * inv_s)
   float* rowsum;        // !a_kc: rowsum[m] = sum_k A(m, k) (bias gradient of a dW product)
@@ -198,6 +199,13 @@ struct TileLoad {
 
 template <bool AKC, bool BKC, bool VA, bool VB>
 __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
+  // A's prescale: a constant, or per call from the gradient's max |x| (exact powers of two)
+  float sa = p.sa, inv_s = p.inv_s;
+  if (p.sa_bits) {
+    const float gs = grad_scale(*p.sa_bits);
+    sa = __fmul_rn(sa, gs);
+    inv_s = __fdiv_rn(inv_s, gs);
+  }
   __shared__ __align__(16) _Float16 smem[2 * STAGE];  // 2 stages x (A hi, A lo, B hi, B lo)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
     constexpr int S = decltype(set)::value;
     if (!AKC && want_rows) ta[S].add_rows(rs);
     _Float16* s = smem + stage * STAGE;
-    ta[S].store(s, s + PLANE, p.sa, tid);
+    ta[S].store(s, s + PLANE, sa, tid);
     tb[S].store(s + 2 * PLANE, s + 3 * PLANE, p.sb, tid);
   };
   using Set0 = std::integral_constant<int, 0>;
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
       for (int r = 0; r < 4; ++r) {
         const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
         if (m >= p.M) continue;
-        float v = __fmul_rn(__fadd_rn(acc_h[i][j][r], __fmul_rn(acc_x[i][j][r], kInvLo)), p.inv_s);
+        float v = __fmul_rn(__fadd_rn(acc_h[i][j][r], __fmul_rn(acc_x[i][j][r], kInvLo)), inv_s);
         if (split) {
           p.part[((int64_t)z * p.M + m) * p.N + n] = v;
           continue;
@@ -429,6 +437,7 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   p.bias = a->bias; p.mask = a->mask; p.ldm = a->ldm;
   p.relu = a->relu; p.accumulate = a->accumulate;
   p.sa = a->a_scale; p.sb = a->b_scale; p.inv_s = 1.0f / (a->a_scale * a->b_scale);
+  p.sa_bits = a->a_amax;
   const int64_t splits = gemm_splits(a);
   p.kchunk = splits > 1 ? ((a->K + splits - 1) / splits + BK - 1) / BK * BK : (a->K > 0 ? a->K : 1);
   const int64_t zs = a->K > 0 ? (a->K + p.kchunk - 1) / p.kchunk : 1;

@@ -295,6 +295,10 @@ extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* pack
     a.layers[i] = precision == AON_PREC_FP32 ? kLayers[i] : kLayersH[i];
   }
   if (precision == AON_PREC_F16X3) return pack_f16x3(a, packed, (hipStream_t)stream);
+  // the fp32 kernels never set the range-status word: cleared once here
+  const hipError_t e = hipMemsetAsync(static_cast<char*>(packed) + kPackedBytesF32 - kStatusBytes, 0,
+                                      kStatusBytes, (hipStream_t)stream);
+  if (e != hipSuccess) return static_cast<int>(e);
   const int64_t total = (int64_t)kStreamBlocks * 256 + kBiasFloats;
   hipLaunchKernelGGL(k_pack_f32, grid_for(total, 256, 4096), 256, 0, (hipStream_t)stream, a,
                      static_cast<float*>(packed));

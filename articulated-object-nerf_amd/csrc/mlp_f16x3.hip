@@ -225,13 +225,17 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
       w *= kWS;  // exact (power of two)
       const _Float16 h = static_cast<_Float16>(w);
       out[e] = lo_part ? static_cast<_Float16>(w - static_cast<float>(h)) : h;
+      // range guard (mlp_f16x3_core.hpp): a weight whose scaled hi part is not a finite fp16
+      // makes every kernel reading this stream invalid -- status 2 (the word was cleared by
+      // pack_h before this launch; many lanes may store the same value)
+      if (!lo_part && !(fabsf(w) <= kF16Max))
+        *reinterpret_cast<uint32_t*>(bias_out + a.bias_floats) = 2u;
 #else
       const _Float16 h = static_cast<_Float16>(w);
       out[e] = lo_part ? static_cast<_Float16>((w - static_cast<float>(h)) * kLoScale) : h;
 #endif
     } else {
       const int i = static_cast<int>(e - nhalf);
-      if (i == 0) *reinterpret_cast<uint32_t*>(bias_out + a.bias_floats) = 0u;  // range status
       int li = 0;
       while (li + 1 < a.n_layers && a.layers[li + 1].bias0 <= i) ++li;
       const int o = i - a.layers[li].bias0;
@@ -248,6 +252,12 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
 
 int pack_h(PackArgsH a, void* packed, hipStream_t stream) {
   const int64_t total = (int64_t)a.stream_blocks * 512 + a.bias_floats;
+  // the range-status word behind the bias table: cleared (stream-ordered) before the pack, which
+  // sets it for an unrepresentable weight; the kernels reading the stream set it on overflow
+  const hipError_t e = hipMemsetAsync(
+      static_cast<char*>(packed) + (size_t)a.stream_blocks * 1024 + (size_t)a.bias_floats * 4, 0,
+      kStatusBytes, stream);
+  if (e != hipSuccess) return static_cast<int>(e);
   hipLaunchKernelGGL(k_pack_h, grid_for(total, 256, 4096), 256, 0, stream, a,
                      static_cast<float*>(packed));
   return launch_status("aon_mlp_pack");

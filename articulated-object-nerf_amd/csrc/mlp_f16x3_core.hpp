@@ -243,16 +243,8 @@ struct StorePick<true, NCOL> {
   }
 };
 
-// ---- backward chains (mlp_bwd.hip, mlp_art_bwd.hip)
-// |x * s| < 2^8 for the largest |x|: s = 2^(8 - e) with max = m 2^e, m in [0.5, 1)
-__device__ __forceinline__ float grad_scale(uint32_t bits) {
-  const float m = __uint_as_float(bits);
-  if (!(m > 0.0f) || !isfinite(m)) return 1.0f;
-  int e;
-  (void)frexpf(m, &e);
-  e = e < -100 ? -100 : (e > 100 ? 100 : e);
-  return __builtin_ldexpf(1.0f, 8 - e);
-}
+// ---- backward chains (mlp_bwd.hip, mlp_art_bwd.hip): per-call gradient scale, grad_scale()
+// in aon_common.hpp
 
 
 // epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):

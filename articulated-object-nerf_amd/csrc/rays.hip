@@ -61,8 +61,8 @@ __global__ void k_get_rays(const float* __restrict__ dirs, int64_t n, Mat34 c2w,
   }
 }
 
-// radii (ray_utils.py:138-143): || rd[y] - rd[y+1] || * 2 / sqrt(12) on UNnormalised
-// world directions; the last row repeats row H-2.
+// radii (ray_utils.py:138-143): || rd[y] - rd[y+1] || * 2 / sqrt(12) on UNnormalised world
+// directions; the last row repeats dx[-2:-1], the SECOND-to-last of dx's H-1 rows (row H-3).
 __global__ void k_radii(const float* __restrict__ dirs, int H, int W, Mat34 c2w,
                         float* __restrict__ radii) {
   const int64_t n = static_cast<int64_t>(H) * W;
@@ -70,7 +70,7 @@ __global__ void k_radii(const float* __restrict__ dirs, int H, int W, Mat34 c2w,
        p += (int64_t)gridDim.x * blockDim.x) {
     int64_t row = p / W;
     const int64_t col = p - row * W;
-    if (row == H - 1) row = H - 2;
+    if (row == H - 1) row = H - 3;  // torch.cat([dx, dx[-2:-1, :]])
     const int64_t a = row * W + col, b = (row + 1) * W + col;
     float o0, o1, o2, ax, ay, az, bx, by, bz;
     rotate_normalize(dirs[3 * a], dirs[3 * a + 1], dirs[3 * a + 2], c2w, o0, o1, o2, ax, ay, az,
@@ -78,7 +78,7 @@ __global__ void k_radii(const float* __restrict__ dirs, int H, int W, Mat34 c2w,
     rotate_normalize(dirs[3 * b], dirs[3 * b + 1], dirs[3 * b + 2], c2w, o0, o1, o2, bx, by, bz,
                      false);
     const float dx = __fsub_rn(ax, bx), dy = __fsub_rn(ay, by), dz = __fsub_rn(az, bz);
-    // torch.sum over 3 squared terms (pairwise order of a 3-wide reduction: (x+y)+z)
+    // torch.sum over 3 squared terms (a 3-wide reduction adds (x+y)+z)
     const float s = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
     radii[p] = __fdiv_rn(__fmul_rn(sqrtf(s), 2.0f), 3.46410155f);
   }
@@ -233,7 +233,8 @@ extern "C" int aon_get_rays(const float* dirs, int64_t n, const float* c2w_host,
   hipLaunchKernelGGL(k_get_rays, grid_for(n, 256, 65536), 256, 0, (hipStream_t)stream, dirs, n, c,
                      rays_o, rays_d, viewdirs);
   if (radii) {
-    AON_REQUIRE(H >= 2 && (int64_t)H * W == n, "radii need a full (H>=2, W) direction grid");
+    // dx has H-1 rows and the reference appends dx[-2:-1]: H = 2 leaves it a row short
+    AON_REQUIRE(H >= 3 && (int64_t)H * W == n, "radii need a full (H>=3, W) direction grid");
     hipLaunchKernelGGL(k_radii, grid_for(n, 256, 65536), 256, 0, (hipStream_t)stream, dirs, H, W,
                        c, radii);
   }

