@@ -23,6 +23,72 @@ namespace mlp {
 #define AON_STASH_REGS 0  // 1: keep the encodings in VGPRs instead of parking them in LDS
 #endif
 
+#ifndef AON_STAGGER
+#define AON_STAGGER 0  // 1: waves 4-7 run their epilogues 4 k-steps later (A/B: no gain, profiles/r02/ab_stagger)
+#endif
+
+// The layer sequence of k_mlp_fwd_f16x3 (model.py:95-120), instantiated per FragPipe type: the
+// two halves of the workgroup differ in the k-step of their epilogues (FragPipe EOFF).
+template <int NCOL, bool STORE, typename FP>
+__device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<1, NCOL>& venc,
+                                               Frag<8, NCOL>& x, Frag<8, NCOL>& y, f4* stash,
+                                               float* bias_s, int g, int wave,
+                                               const int64_t (&rows)[NCOL], int64_t N, int act,
+                                               float* __restrict__ raw, const TrainStore& ts) {
+  fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
+#if AON_PRIO_HALF
+  if (wave >= GeomH<NCOL>::kWaves / 2) __builtin_amdgcn_s_setprio(AON_PRIO_HALF);
+#endif
+  lds_float* bias_l = opaque_lds(bias_s + 4 * g);  // this lane group's rows of the bias table
+
+  Frag<1, NCOL> none;
+  using SP = StorePick<STORE, NCOL>;
+  const int64_t hs = N * 256;  // one pts_linears output in ts.h
+  const int64_t ms = N * 4;    // one layer's ReLU' bits in ts.masks
+  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g, ts.masks));
+  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 1 * hs, 256, rows, N, g, ts.masks + 1 * ms));
+  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g, ts.masks + 2 * ms));
+  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g, ts.masks + 3 * ms));
+  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g, ts.masks + 4 * ms));
+#pragma unroll
+  for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
+      enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
+    }
+  // skip: cat[h, enc] (model.py:102-103)
+  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g, ts.masks + 5 * ms));
+  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g, ts.masks + 6 * ms));
+  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g, ts.masks + 7 * ms));
+  f4 dens[NCOL], rgb[NCOL];
+  head_h<NetVanillaH, LDEN>(fp, y, dens, bias_l, g);             // model.py:105-107
+  // bottleneck, no activation (model.py:109)
+  layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g, SP::make(ts.bot, 256, rows, N, g));
+#pragma unroll
+  for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c) {
+    venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
+    venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
+  }
+  // cat[bottleneck, enc_dir] + ReLU (:110-116)
+  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g, ts.masks + 8 * ms));
+  head_h<NetVanillaH, LRGB>(fp, y, rgb, bias_l, g);              // model.py:118
+
+  if (g == 0) {
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+      if (rows[c] < N) {
+        const float s = AON_F16X3_V2 ? 1.0f : 1.0f / kActScale;  // V2 heads are at true scale
+        float sig = dens[c][0] * s;
+        if (STORE && ts.noise) sig = __fadd_rn(sig, ts.noise[rows[c]]);  // raw_sigma + noise
+        const f4 o = {act_rgb(rgb[c][0] * s, act), act_rgb(rgb[c][1] * s, act),
+                      act_rgb(rgb[c][2] * s, act), act_sigma(sig, act)};
+        *reinterpret_cast<f4*>(raw + 4 * rows[c]) = o;
+      }
+    }
+  }
+}
+
 // MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: encoded x (N, 63), condition (B, 27)
 template <int MODE, int NCOL, bool STORE = false>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_fwd_f16x3(
@@ -115,59 +181,16 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
 
-  FragPipe<WeightPipe<NetVanillaH, G::kThreads>> fp(p);
-  fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
-#if AON_PRIO_HALF
-  if (wave >= G::kWaves / 2) __builtin_amdgcn_s_setprio(AON_PRIO_HALF);
-#endif
-  lds_float* bias_l = opaque_lds(bias_s + 4 * g);  // this lane group's rows of the bias table
-
   Frag<8, NCOL> x, y;
-  Frag<1, NCOL> none;
-  using SP = StorePick<STORE, NCOL>;
-  const int64_t hs = N * 256;  // one pts_linears output in ts.h
-  const int64_t ms = N * 4;    // one layer's ReLU' bits in ts.masks
-  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g, ts.masks));
-  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 1 * hs, 256, rows, N, g, ts.masks + 1 * ms));
-  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g, ts.masks + 2 * ms));
-  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g, ts.masks + 3 * ms));
-  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g, ts.masks + 4 * ms));
-#pragma unroll
-  for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
-      enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
-    }
-  // skip: cat[h, enc] (model.py:102-103)
-  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g, ts.masks + 5 * ms));
-  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g, ts.masks + 6 * ms));
-  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g, ts.masks + 7 * ms));
-  f4 dens[NCOL], rgb[NCOL];
-  head_h<NetVanillaH, LDEN>(fp, y, dens, bias_l, g);             // model.py:105-107
-  // bottleneck, no activation (model.py:109)
-  layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g, SP::make(ts.bot, 256, rows, N, g));
-#pragma unroll
-  for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c) {
-    venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
-    venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
-  }
-  // cat[bottleneck, enc_dir] + ReLU (:110-116)
-  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g, ts.masks + 8 * ms));
-  head_h<NetVanillaH, LRGB>(fp, y, rgb, bias_l, g);              // model.py:118
-
-  if (g == 0) {
-#pragma unroll
-    for (int c = 0; c < NCOL; ++c) {
-      if (rows[c] < N) {
-        const float s = AON_F16X3_V2 ? 1.0f : 1.0f / kActScale;  // V2 heads are at true scale
-        float sig = dens[c][0] * s;
-        if (STORE && ts.noise) sig = __fadd_rn(sig, ts.noise[rows[c]]);  // raw_sigma + noise
-        const f4 o = {act_rgb(rgb[c][0] * s, act), act_rgb(rgb[c][1] * s, act),
-                      act_rgb(rgb[c][2] * s, act), act_sigma(sig, act)};
-        *reinterpret_cast<f4*>(raw + 4 * rows[c]) = o;
-      }
-    }
+  using WP = WeightPipe<NetVanillaH, G::kThreads>;
+  // wave-uniform branch (readfirstlane): the running range masks stay in SGPRs across it
+  // (not the training forward: with its row stores the second copy spills)
+  if (AON_STAGGER && NCOL == 1 && !STORE && __builtin_amdgcn_readfirstlane(wave) >= G::kWaves / 2) {
+    FragPipe<WP, AON_PREFETCH, 4> fp(p);
+    vanilla_layers<NCOL, STORE>(fp, enc, venc, x, y, stash, bias_s, g, wave, rows, N, act, raw, ts);
+  } else {
+    FragPipe<WP, AON_PREFETCH, 0> fp(p);
+    vanilla_layers<NCOL, STORE>(fp, enc, venc, x, y, stash, bias_s, g, wave, rows, N, act, raw, ts);
   }
   range_report(bias_g + kBiasFloats, x.ovf | y.ovf | enc.ovf | venc.ovf);
 }

@@ -45,6 +45,24 @@ __device__ __forceinline__ _Float16 lo_of(float v, _Float16 h) {
 // the status word behind its bias table (zeroed by the pack, read by aon_mlp_read_status): the
 // caller learns the result is invalid.
 constexpr float kF16Max = 65504.0f;
+// ovf |= ballot(bad): the running OR is pinned to one SGPR pair per step (an empty asm on it);
+// left to itself hipcc keeps every ballot live until the final OR, and the hundreds of mask
+// pairs spill into VGPR lanes (1,072 v_writelane / v_readlane in the vanilla kernel, -5%)
+#ifndef AON_PIN_OVF
+#define AON_PIN_OVF(v) asm("" : "+s"(v))
+#endif
+#ifndef AON_RANGE_GUARD
+#define AON_RANGE_GUARD 1  // 0: timing-only A/B build without the range test
+#endif
+__device__ __forceinline__ void or_ballot(uint64_t& ovf, bool bad) {
+#if AON_RANGE_GUARD
+  ovf |= __builtin_amdgcn_ballot_w64(bad);
+  AON_PIN_OVF(ovf);
+#else
+  (void)ovf;
+  (void)bad;
+#endif
+}
 __device__ __forceinline__ void range_report(const float* bias_end, uint64_t ovf) {
   if (ovf && (threadIdx.x & 63) == 0) *reinterpret_cast<uint32_t*>(const_cast<float*>(bias_end)) = 1u;
 }
@@ -59,7 +77,7 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, uint
     lo[j] = lo_of(v[j], h);
     m = fmaxf(m, fabsf(v[j]));
   }
-  ovf |= __builtin_amdgcn_ballot_w64(m > kF16Max);
+  or_ballot(ovf, m > kF16Max);
 }
 
 // One-step-ahead fragment prefetch over the weight stream: blocks are consumed strictly in
@@ -74,8 +92,13 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, uint
 #define AON_PREFETCH 3
 #endif
 
-template <typename P, int D = AON_PREFETCH>
+// EOFF: the k-step at which a layer starts the pending pair's epilogue (layer_h).  Waves
+// w and w + 4 of an 8-wave workgroup share a SIMD; run in lockstep they reach the epilogue VALU
+// and the epilogue-free MFMA steps together, so neither wave's VALU rides beside the other's
+// MFMAs.  Waves 4-7 take EOFF = 4 (a stagger: MI355X_MICROARCH.md "Two waves per SIMD" item 9).
+template <typename P, int D = AON_PREFETCH, int EOFF = 0>
 struct FragPipe {
+  static constexpr int kEpiOff = EOFF;
   P& p;
   f4 nh[D], nl[D];  // fragments of the next D steps
   __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
@@ -270,7 +293,7 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
       if (RELU) v = fmaxf(v, 0.0f);
       vv[e] = st.post(pr, uu, r0 + e, c, v);
     }
-    out.ovf |= __builtin_amdgcn_ballot_w64(fmaxf(fabsf(vv[0]), fabsf(vv[1])) > kF16Max);
+    or_ballot(out.ovf, fmaxf(fabsf(vv[0]), fabsf(vv[1])) > kF16Max);
     st.put(pr, uu, r0, c, vv[0], vv[1]);
 #if AON_F16X3_V2 && AON_FMA_MIX
     // hi pair by one v_cvt_pk_f16_f32; lo_e = v_e - hi_e by v_fma_mix_f32 reading the fp16 half
@@ -306,6 +329,8 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
   constexpr LayerDesc d = Net::layer(LAYER);
   constexpr int K = d.ka + d.kb;
   constexpr int NP = d.u / 2;
+  constexpr int EO = P::kEpiOff;  // epilogue parts of pair p-1 at k-steps EO..EO+3 of pair p
+  constexpr int QIN = K - EO < 0 ? 0 : (K - EO > 4 ? 4 : K - EO);  // parts done inside the loop
   static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
   f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
   f4 pbias[2];                     // V2: that pair's biases, added in its epilogue
@@ -349,11 +374,11 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
 #endif
         }
       }
-      if (pr > 0 && k < 4) epi_part<RELU>(k, phh, pxx, pbias, out, pr - 1, st);
+      if (pr > 0 && k >= EO && k - EO < 4) epi_part<RELU>(k - EO, phh, pxx, pbias, out, pr - 1, st);
     }
     if (pr > 0) {
 #pragma unroll
-      for (int q = K; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, pr - 1, st);
+      for (int q = QIN; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, pr - 1, st);
     }
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {

@@ -10,7 +10,7 @@ FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fhip-fp32-c
 OTHERS=$(ls build/*.o | grep -v mlp_f16x3)
 while [ $# -ge 2 ]; do
   name=$1; extra=$2; shift 2
-  /opt/rocm/bin/hipcc $FLAGS $extra -c mlp_f16x3.hip -o build/variants/mlp_f16x3_$name.o
+  /opt/rocm/bin/hipcc $FLAGS -mllvm -amdgpu-sched-strategy=iterative-ilp $extra -c mlp_f16x3.hip -o build/variants/mlp_f16x3_$name.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/variants/libaonerf_$name.so $OTHERS build/variants/mlp_f16x3_$name.o
   echo "built $name ($extra)"
 done
