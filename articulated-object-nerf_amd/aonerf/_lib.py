@@ -60,6 +60,8 @@ _SIGNATURES = {
     "aon_cast_rays": (c_int, [vp, vp, vp, c_i64, c_int, vp, c_i64, vp, c_int, c_int, vp, vp]),
     "aon_sample_pdf": (c_int, [vp, c_i64, vp, c_i64, c_i64, c_int, c_int, vp, c_i64, vp, c_int,
                                vp, vp, vp, vp, vp]),
+    "aon_composite_march": (c_int, [vp, vp, vp, c_i64, c_int, c_int, c_int, vp, c_i64, c_int, vp,
+                                    vp, vp, vp, vp, vp]),
     "aon_mlp_packed_bytes": (c_size, [c_int]),
     "aon_mlp_read_status": (c_int, [vp, c_size, ctypes.POINTER(ctypes.c_uint32), vp]),
     "aon_mlp_pack": (c_int, [ctypes.POINTER(AonMlpParams), c_int, vp, vp]),

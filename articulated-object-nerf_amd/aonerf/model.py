@@ -149,6 +149,38 @@ def _record(timers, ev, key, rows):
         timers.setdefault(key, []).append((ev[0], ev[1], rows))
 
 
+def fine_uniforms(B, num_fine_samples, randomized, dev, u_fine=None):
+    """The u of the fine level's inverse-CDF sampling (helper.py:227-231) and its row stride:
+    per-ray draws in randomized mode (or the injected ``u_fine``), else one shared linspace."""
+    if randomized:
+        u = torch.rand((B, num_fine_samples), device=dev) if u_fine is None else L.contig(u_fine)
+        return u, num_fine_samples
+    return helper.eval_u(num_fine_samples, dev), 0
+
+
+def composite_march(raw, t_vals, d, white_bkgd, act, u, u_stride, num_fine_samples,
+                    keep_weights):
+    """Coarse compositing + the fine level's resampling in one kernel (aon_composite_march):
+    (comp, acc, depth, weights or None), t_fine (B, S + Nf) -- helper.py:157-252 and
+    model.py:163-172, the coarse weights kept on chip unless asked for."""
+    B, S = t_vals.shape
+    dev = t_vals.device
+    comp = torch.empty((B, 3), device=dev)
+    acc = torch.empty((B,), device=dev)
+    depth = torch.empty((B,), device=dev)
+    weights = torch.empty((B, S), device=dev) if keep_weights else None
+    t_fine = torch.empty((B, S + num_fine_samples), device=dev)
+    L.call("aon_composite_march", L.ptr(raw), L.ptr(t_vals), L.ptr(d), B, S, int(bool(white_bkgd)),
+           act, L.ptr(u), u_stride, num_fine_samples, L.ptr(comp), L.ptr(acc), L.ptr(weights),
+           L.ptr(depth), L.ptr(t_fine), L.stream(dev))
+    return (comp, acc, depth, weights), t_fine
+
+
+# render path: the coarse compositor and the fine level's resampling as one kernel
+# (aon_composite_march); False: aon_composite_fwd + aon_sample_pdf (bit-identical outputs)
+FUSED_MARCH = True
+
+
 def level_t_vals(level, o, d, t_prev, w_prev, randomized, near, far, num_coarse_samples,
                  num_fine_samples, lindisp, u_coarse=None, u_fine=None):
     """Sample positions of a level: stratified (helper.py:106-133) or inverse-CDF resampling
@@ -160,11 +192,7 @@ def level_t_vals(level, o, d, t_prev, w_prev, randomized, near, far, num_coarse_
                                              lindisp, u=u_coarse, want_coords=False)
         return t_vals
     Sc = t_prev.shape[1]
-    if randomized:
-        u = torch.rand((B, num_fine_samples), device=dev) if u_fine is None else L.contig(u_fine)
-        u_stride = num_fine_samples
-    else:
-        u, u_stride = helper.eval_u(num_fine_samples, dev), 0
+    u, u_stride = fine_uniforms(B, num_fine_samples, randomized, dev, u_fine)
     w_prev = L.contig(w_prev.detach())
     t_new = torch.empty((B, Sc + num_fine_samples), device=dev)
     # bins = mids of t (model.py:163), weights[..., 1:-1] as a strided view
@@ -219,11 +247,11 @@ class NeRF(nn.Module):
         B = o.shape[0]
         dev = o.device
         ret = []
-        t_vals = weights = None
+        t_vals = weights = t_next = None
         for level in range(2):
             with torch.no_grad():
-                t_vals = self._level_t(level, o, d, t_vals, weights, randomized, near, far,
-                                       u_coarse, u_fine)
+                t_vals = t_next if t_next is not None else self._level_t(
+                    level, o, d, t_vals, weights, randomized, near, far, u_coarse, u_fine)
             mlp = self.coarse_mlp if level == 0 else self.fine_mlp
             S = t_vals.shape[1]
             if training:
@@ -242,9 +270,15 @@ class NeRF(nn.Module):
             # the last level's weights are an output only when asked for: otherwise the
             # compositor skips writing them (4 B of its 24 B per sample)
             keep_w = level == 0 or return_weights or return_intermediates
+            march = FUSED_MARCH and level == 0
+            if march:  # the coarse weights are needed on chip only
+                keep_w = return_weights or return_intermediates
             with torch.no_grad():
-                out, weights = self._render_level_fused(mlp, o, d, v, t_vals, randomized,
-                                                        white_bkgd, level, timers, keep_w)
+                out, weights, t_next = self._render_level_fused(
+                    mlp, o, d, v, t_vals, randomized, white_bkgd, level, timers, keep_w,
+                    # drawn inside, after the level's density noise (the reference's RNG order)
+                    march_u=(lambda: fine_uniforms(B, self.num_fine_samples, randomized, dev,
+                                                   u_fine)) if march else None)
             if not return_weights:
                 out = out[:3] + out[4:]
             if not return_intermediates:
@@ -272,7 +306,10 @@ class NeRF(nn.Module):
                             u_coarse, u_fine)
 
     def _render_level_fused(self, mlp, o, d, v, t_vals, randomized, white_bkgd, level, timers,
-                            keep_weights=True):
+                            keep_weights=True, march_u=None):
+        """One inference level: fused MLP, then compositing -- with ``march_u`` (a callable
+        returning the fine level's (u, u_stride)) also the next level's resampling in the same
+        kernel (returned t_next, else None)."""
         B, S = t_vals.shape
         dev = o.device
         # the activations (model.py:186-187) run in the MLP epilogue, unless density noise
@@ -283,13 +320,21 @@ class NeRF(nn.Module):
         _record(timers, ev, f"mlp{level}", B * S)
         if noisy:
             raw[:, 3] += torch.rand_like(raw[:, 3]) * self.noise_std
-        comp = torch.empty((B, 3), device=dev)
-        acc = torch.empty((B,), device=dev)
-        weights = torch.empty((B, S), device=dev) if keep_weights else None
-        depth = torch.empty((B,), device=dev)
+        act = L.ACT_VANILLA if noisy else L.ACT_NONE
+        t_next = None
         ev = _events(timers)
-        L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
-               B, S, int(bool(white_bkgd)), L.ACT_VANILLA if noisy else L.ACT_NONE,
-               L.ptr(comp), L.ptr(acc), L.ptr(weights), L.ptr(depth), L.stream(dev))
-        _record(timers, ev, f"comp{level}", B * S)
-        return (comp, acc, depth, weights, dict(t_vals=t_vals, weights=weights, rgb_sigma=raw)), weights
+        if march_u is not None:
+            u, u_stride = march_u()
+            (comp, acc, depth, weights), t_next = composite_march(
+                raw, t_vals, d, white_bkgd, act, u, u_stride, self.num_fine_samples, keep_weights)
+            _record(timers, ev, f"march{level}", B * S)
+        else:
+            comp = torch.empty((B, 3), device=dev)
+            acc = torch.empty((B,), device=dev)
+            weights = torch.empty((B, S), device=dev) if keep_weights else None
+            depth = torch.empty((B,), device=dev)
+            L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
+                   B, S, int(bool(white_bkgd)), act, L.ptr(comp), L.ptr(acc), L.ptr(weights),
+                   L.ptr(depth), L.stream(dev))
+            _record(timers, ev, f"comp{level}", B * S)
+        return (comp, acc, depth, weights, dict(t_vals=t_vals, weights=weights, rgb_sigma=raw)), weights, t_next

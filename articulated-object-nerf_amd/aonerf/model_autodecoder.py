@@ -29,7 +29,7 @@ import torch.nn.init as init
 from . import _lib as L
 from .linalg import ACT_SCALE, W_SCALE, gemm, linear_fwd
 from . import model as _vanilla
-from .model import _events, _record, level_t_vals
+from .model import _events, _record, composite_march, fine_uniforms, level_t_vals
 
 class NeRFMLP(nn.Module):
     """reference model_autodecoder.py:60-166 (same nn.Linear layout and init)."""
@@ -340,11 +340,11 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
                         u_fine, return_weights, return_intermediates, timers=None):
         B, dev = o.shape[0], o.device
         ret = []
-        t_vals = weights = None
+        t_vals = weights = t_next = None
         for level in range(2):
-            t_vals = level_t_vals(level, o, d, t_vals, weights, randomized, near, far,
-                                  self.num_coarse_samples, self.num_fine_samples, self.lindisp,
-                                  u_coarse, u_fine)
+            t_vals = t_next if t_next is not None else level_t_vals(
+                level, o, d, t_vals, weights, randomized, near, far, self.num_coarse_samples,
+                self.num_fine_samples, self.lindisp, u_coarse, u_fine)
             mlp = self.coarse_mlp if level == 0 else self.fine_mlp
             S = t_vals.shape[1]
             ev = _events(timers)
@@ -352,15 +352,24 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
             _record(timers, ev, f"mlp{level}", B * S)
             if self.noise_std > 0 and randomized:  # model_autodecoder.py:318-319
                 raw[:, 3].copy_(raw[:, 3] + torch.rand_like(raw[:, 3]) * self.noise_std)
-            comp = torch.empty((B, 3), device=dev)
-            acc = torch.empty((B,), device=dev)
-            weights = torch.empty((B, S), device=dev)
-            depth = torch.empty((B,), device=dev)
             ev = _events(timers)
-            L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals), L.ptr(d),
-                   B, S, int(bool(white_bkgd)), L.ACT_ARTIC, L.ptr(comp), L.ptr(acc),
-                   L.ptr(weights), L.ptr(depth), L.stream(dev))
-            _record(timers, ev, f"comp{level}", B * S)
+            if level == 0 and _vanilla.FUSED_MARCH:
+                # coarse compositing + the fine level's resampling in one kernel; the coarse
+                # weights reach HBM only when asked for
+                u, u_stride = fine_uniforms(B, self.num_fine_samples, randomized, dev, u_fine)
+                (comp, acc, depth, weights), t_next = composite_march(
+                    raw, t_vals, d, white_bkgd, L.ACT_ARTIC, u, u_stride, self.num_fine_samples,
+                    return_weights or return_intermediates)
+                _record(timers, ev, f"march{level}", B * S)
+            else:
+                comp = torch.empty((B, 3), device=dev)
+                acc = torch.empty((B,), device=dev)
+                weights = torch.empty((B, S), device=dev)
+                depth = torch.empty((B,), device=dev)
+                L.call("aon_composite_fwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals),
+                       L.ptr(d), B, S, int(bool(white_bkgd)), L.ACT_ARTIC, L.ptr(comp), L.ptr(acc),
+                       L.ptr(weights), L.ptr(depth), L.stream(dev))
+                _record(timers, ev, f"comp{level}", B * S)
             out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
             if return_intermediates:
                 out = out + (dict(t_vals=t_vals, weights=weights, raw=raw),)

@@ -7,59 +7,9 @@
 // CPU's cumprod does (fp64 accumulator, measured), so T_i matches the reference bit-for-bit in
 // practice.  The per-ray sums (acc = sum w, depth = sum w*t, rgb = sum w*c) are staged in LDS
 // and evaluated in torch's CPU summation order by the whole wave (torch_sum.hpp).
-#include "aon_common.hpp"
-#include "torch_sum.hpp"
+#include "composite_core.hpp"
 
 namespace aon {
-
-#ifndef AON_COMP_OCC_FINE
-#define AON_COMP_OCC_FINE 6  // waves per SIMD the fine-level (S = 193) instantiation is built for (7: 72 VGPRs, 8: spills; both no faster)
-#endif
-
-constexpr int kCompWaves = 4;
-constexpr int kCompMaxS = 512;
-constexpr int kCompScratch = 256;  // wave_row_sums task partials (<= 236 at S = 512)
-
-// wave_row_sums task partials the compositor's sums need at S samples (3 rgb sums over S terms,
-// 16 vector-lane sums over S/8 terms; torch_sum.hpp)
-constexpr int comp_scratch(int S) {
-  return S < 8 ? 256
-               : 3 * 4 * ((S >> 2 >> 4) + 1) + 16 * 4 * (((S / 8) >> 2 >> 4) + 1);
-}
-
-__device__ __forceinline__ void wave_sync_c() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// ---- DPP lane moves (gfx9 controls).  Lanes whose source is outside the pattern keep `old`.
-template <int CTRL, int ROW_MASK = 0xF>
-__device__ __forceinline__ double dpp_f64(double src, double old) {
-  const long long s = __builtin_bit_cast(long long, src), o = __builtin_bit_cast(long long, old);
-  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)s, CTRL, ROW_MASK, 0xF, false);
-  const int hi =
-      __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(s >> 32), CTRL, ROW_MASK, 0xF, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-  const long long s = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_readlane((int)s, lane);
-  const int hi = __builtin_amdgcn_readlane((int)(s >> 32), lane);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-}
-
-// inclusive prefix product over the 64 lanes: row_shr 1/2/4/8 inside 16-lane rows, then
-// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- VALU lane moves, no LDS
-__device__ __forceinline__ double wave_incl_prod(double x) {
-  x *= dpp_f64<0x111>(x, 1.0);
-  x *= dpp_f64<0x112>(x, 1.0);
-  x *= dpp_f64<0x114>(x, 1.0);
-  x *= dpp_f64<0x118>(x, 1.0);
-  x *= dpp_f64<0x142, 0xA>(x, 1.0);
-  x *= dpp_f64<0x143, 0xC>(x, 1.0);
-  return x;
-}
 
 // One 64-lane wave per ray, NB = ceil(S/64) blocks of 64 samples (lane i owns samples i + 64b).
 // All of a ray's loads are issued up front (NB x {16-B raw, 4-B t} per lane), the
@@ -86,7 +36,6 @@ __global__ __launch_bounds__(64 * kCompWaves, SC > 0 ? (SC > 128 ? AON_COMP_OCC_
   float* sums = scratch + kScratch;
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * kCompWaves;
-  const bool inner8 = S >= 8;
   for (int64_t ray = (int64_t)blockIdx.x * kCompWaves + (threadIdx.x >> 6); ray < B;
        ray += nwaves) {
     const int64_t row0 = ray * S;
@@ -108,90 +57,8 @@ __global__ __launch_bounds__(64 * kCompWaves, SC > 0 ? (SC > 128 ? AON_COMP_OCC_
         }
       }
     }
-    const float dx = dirs[3 * ray], dy = dirs[3 * ray + 1], dz = dirs[3 * ray + 2];
-    const float dnorm = sqrtf(fmaf(dz, dz, fmaf(dy, dy, __fmul_rn(dx, dx))));
-    double carry = 1.0;  // prod_{j < block start} (1 - alpha_j + 1e-10)
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int i = 64 * b + lane;
-      const bool valid = i < S;
-      // t[i + 1]: lane i + 1 of this block, or lane 0 of the next (wave_shl:1)
-      const float tnext0 = b + 1 < NB ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(
-                                                                      __builtin_bit_cast(int, tt[b + 1]), 0))
-                                      : 0.f;
-      const float tn = __builtin_bit_cast(
-          float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, tnext0),
-                                             __builtin_bit_cast(int, tt[b]), 0x130, 0xF, 0xF, false));
-      const float ti = tt[b];
-      float alpha = 0.f;
-      double f = 1.0;
-      if (valid) {
-        const float dist = (i + 1 < S) ? __fsub_rn(tn, ti) : 1e10f;
-        const float sgm = act_sigma(raw[b].w, act);
-        alpha = __fsub_rn(1.0f, expf(__fmul_rn(-sgm, __fmul_rn(dist, dnorm))));
-        if (i + 1 < S) f = (double)__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f);
-      }
-      const double incl = wave_incl_prod(f);
-      const double excl = dpp_f64<0x138>(incl, 1.0);  // wave_shr:1, lane 0 -> 1
-      const float T = (float)(carry * excl);
-      if (b + 1 < NB) carry *= readlane_f64(incl, 63);
-      if (valid) {
-        const float w = __fmul_rn(alpha, T);
-        if (out_w) out_w[row0 + i] = w;
-        P[i] = w;
-        P[SM + i] = __fmul_rn(w, ti);
-        P[2 * SM + i] = __fmul_rn(w, act_rgb(raw[b].x, act));
-        P[3 * SM + i] = __fmul_rn(w, act_rgb(raw[b].y, act));
-        P[4 * SM + i] = __fmul_rn(w, act_rgb(raw[b].z, act));
-      }
-    }
-    wave_sync_c();
-    // torch-order sums (torch_sum.hpp): specs 0..2 = rgb over S terms (stride-3 outer sum);
-    // S >= 8: specs 3..18 = the 8 vector lanes of the inner sums of w (3..10) and w*t (11..18)
-    // over S/8 terms each; S < 8: specs 3, 4 = scalar sums of w, w*t.
-    wave_row_sums(
-        [&](int sp, const float*& base, int& str) {
-          if (sp < 3) {
-            base = P + (2 + sp) * SM;
-            str = 1;
-          } else if (inner8) {
-            base = P + ((sp - 3) >> 3) * SM + ((sp - 3) & 7);
-            str = 8;
-          } else {
-            base = P + (sp - 3) * SM;
-            str = 1;
-          }
-        },
-        3, S, inner8 ? 16 : 2, inner8 ? S / 8 : S, scratch, sums, lane, wave_sync_c);
-    if (lane < 2) {
-      // acc (lane 0) / depth (lane 1): tail x[8m..S) from 0, then + vector lanes 0..7
-      float s;
-      if (inner8) {
-        s = 0.f;
-        for (int e = (S / 8) * 8; e < S; ++e) s = __fadd_rn(s, P[lane * SM + e]);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) s = __fadd_rn(s, sums[3 + 8 * lane + c]);
-      } else {
-        s = sums[3 + lane];
-      }
-      if (lane == 0) {
-        float sr = sums[0], sg = sums[1], sb = sums[2];
-        if (white) {
-          const float bg = __fsub_rn(1.0f, s);
-          sr = __fadd_rn(sr, bg);
-          sg = __fadd_rn(sg, bg);
-          sb = __fadd_rn(sb, bg);
-        }
-        out_rgb[3 * ray] = sr;
-        out_rgb[3 * ray + 1] = sg;
-        out_rgb[3 * ray + 2] = sb;
-        out_acc[ray] = s;
-      } else {
-        // nan_to_num(depth, nan=inf) then clamp(depth, min, max) over the chunk, which is the
-        // identity on the resulting values (helper.py:182-183)
-        out_depth[ray] = nan_to_num(s, __builtin_inff());
-      }
-    }
+    composite_ray<NB, SC>(tt, raw, dirs, ray, S, lane, act, white, P, SM, scratch, sums, out_rgb,
+                          out_acc, out_w, out_depth);
     wave_sync_c();  // LDS reuse by this wave's next ray
   }
 }

@@ -10,55 +10,9 @@
 //   4. samples are bitonic-sorted in LDS (randomized u is unsorted) and merged with the sorted
 //      coarse t by rank (position = own index + rank in the other list) -- the values equal
 //      torch.sort(cat[t, samples]) exactly; xyz = o + t*d optionally.
-#include "aon_common.hpp"
-#include "torch_sum.hpp"
+#include "pdf_core.hpp"
 
 namespace aon {
-
-#ifndef AON_PDF_PIPE
-#define AON_PDF_PIPE 0  // 1: next ray's inputs loaded one ray ahead on a resident grid (7% slower)
-#endif
-
-constexpr int kPdfWaves = 4;
-constexpr int kMaxBins = 256;
-constexpr int kMaxNs = 512;
-constexpr int kMaxNt = 512;
-
-// order this wave's LDS writes before its later LDS reads (lanes exchange data through LDS)
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// number of entries of sorted a[0..n) that are <= x  (upper bound)
-__device__ __forceinline__ int count_le(const float* a, int n, float x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] <= x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// number of entries of sorted a[0..n) that are < x  (lower bound)
-__device__ __forceinline__ int count_lt(const float* a, int n, float x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// per-wave LDS, sized for rows of up to 64 * NBX entries (bins, weights, samples, t_merge)
-template <int NBX>
-struct PdfLds {
-  float bins[64 * NBX];
-  float cdf[64 * NBX];
-  float w[64 * NBX];
-  float samp[64 * NBX];
-  float tm[64 * NBX];
-};
 
 // A ray's inputs -- its t_merge row (or bins), weights and u, NBX 64-entry blocks of each -- are
 // read by coalesced wave-wide loads, all issued before any math, and staged in LDS (the weight
@@ -109,115 +63,7 @@ __global__ __launch_bounds__(64 * kPdfWaves) void k_sample_pdf(
     if (!bins_g) {  // bins = mids of t_merge (model.py:163)
       for (int k = lane; k < nb; k += 64) L.bins[k] = __fmul_rn(0.5f, __fadd_rn(L.tm[k + 1], L.tm[k]));
     }
-    // ---- weight sum (torch CPU order, torch_sum.hpp) + padding (helper.py:206-212)
-    const float* w = L.w;
-    float part = 0.f;
-    if (nw >= 8) {
-      if (lane < 8) part = inner_sum_lane([&](int e) { return w[e]; }, nw, lane);
-      else if (lane == 8) part = inner_sum_tail([&](int e) { return w[e]; }, nw);
-    } else if (lane == 0) {
-      part = row_sum_ilp4([&](int e) { return w[e]; }, nw);
-    }
-    float ws = __shfl(part, nw >= 8 ? 8 : 0);
-    if (nw >= 8) {
-#pragma unroll
-      for (int c = 0; c < 8; ++c) ws = __fadd_rn(ws, __shfl(part, c));
-    }
-    const float pad = fmaxf(0.0f, __fsub_rn(1e-5f, ws));
-    const float padw = __fdiv_rn(pad, static_cast<float>(nw));
-    const float wsum = __fadd_rn(ws, pad);
-    // ---- cdf (helper.py:213-223): fp64 scan of pdf[0 .. nw-2]
-    double carry = 0.0;
-    for (int base = 0; base < nw - 1; base += 64) {
-      const int k = base + lane;
-      double v = 0.0;
-      if (k < nw - 1) v = (double)__fdiv_rn(__fadd_rn(w[k], padw), wsum);
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double x = __shfl_up(v, o);
-        if (lane >= o) v += x;
-      }
-      if (k < nw - 1) L.cdf[k + 1] = fminf(1.0f, (float)(carry + v));
-      carry += __shfl(v, 63);
-    }
-    if (lane == 0) {
-      L.cdf[0] = 0.0f;
-      L.cdf[nb - 1] = 1.0f;
-    }
-    wave_sync();
-    // ---- inverse cdf (helper.py:232-241)
-#pragma unroll
-    for (int b = 0; b < NBX; ++b) {
-      const int j = 64 * b + lane;
-      if (j >= Ns_pow2) break;
-      float s = __builtin_inff();  // sort padding
-      if (j < Ns) {
-        const float uj = cu[b];
-        const int idx = count_le(L.cdf, nb, uj);
-        const int i0 = idx - 1 < 0 ? 0 : (idx - 1 > nb - 1 ? nb - 1 : idx - 1);
-        const int i1 = idx > nb - 1 ? nb - 1 : idx;
-        const float c0 = L.cdf[i0], c1 = L.cdf[i1];
-        const float b0 = L.bins[i0], b1 = L.bins[i1];
-        float q = nan_to_num(__fdiv_rn(__fsub_rn(uj, c0), __fsub_rn(c1, c0)), 0.0f);
-        q = fminf(fmaxf(q, 0.0f), 1.0f);
-        s = __fadd_rn(b0, __fmul_rn(q, __fsub_rn(b1, b0)));
-      }
-      L.samp[j] = s;
-    }
-    wave_sync();
-    // ---- bitonic sort of the samples (ascending), skipped when they already are (sorted u,
-    // e.g. the eval-mode linspace, maps to nondecreasing samples); a NaN compares unordered
-    // and keeps the sort on, as before
-    bool unsorted = false;
-    for (int j = lane; j + 1 < Ns; j += 64) unsorted |= !(L.samp[j] <= L.samp[j + 1]);
-    const bool need_sort = __any(unsorted);
-    for (int k = 2; need_sort && k <= Ns_pow2; k <<= 1) {
-      for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        for (int i = lane; i < Ns_pow2; i += 64) {
-          const int p = i ^ jj;
-          if (p > i) {
-            const float a = L.samp[i], b = L.samp[p];
-            const bool up = (i & k) == 0;
-            if ((a > b) == up) {
-              L.samp[i] = b;
-              L.samp[p] = a;
-            }
-          }
-        }
-        wave_sync();
-      }
-    }
-    // ---- write (merged) output
-    const int No = tm_g ? Nt + Ns : Ns;
-    float* o = out + ray * No;
-    float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
-    if (xyz) {
-      ox = ro[3 * ray]; oy = ro[3 * ray + 1]; oz = ro[3 * ray + 2];
-      dx = rd[3 * ray]; dy = rd[3 * ray + 1]; dz = rd[3 * ray + 2];
-    }
-    float* xo = xyz ? xyz + ray * No * 3 : nullptr;
-    for (int j = lane; j < Ns; j += 64) {
-      const float s = L.samp[j];
-      const int pos = tm_g ? j + count_le(L.tm, Nt, s) : j;
-      o[pos] = s;
-      if (xo) {
-        xo[3 * pos] = __fadd_rn(ox, __fmul_rn(s, dx));
-        xo[3 * pos + 1] = __fadd_rn(oy, __fmul_rn(s, dy));
-        xo[3 * pos + 2] = __fadd_rn(oz, __fmul_rn(s, dz));
-      }
-    }
-    if (tm_g) {
-      for (int i = lane; i < Nt; i += 64) {
-        const float tv = L.tm[i];
-        const int pos = i + count_lt(L.samp, Ns, tv);
-        o[pos] = tv;
-        if (xo) {
-          xo[3 * pos] = __fadd_rn(ox, __fmul_rn(tv, dx));
-          xo[3 * pos + 1] = __fadd_rn(oy, __fmul_rn(tv, dy));
-          xo[3 * pos + 2] = __fadd_rn(oz, __fmul_rn(tv, dz));
-        }
-      }
-    }
+    pdf_ray<NBX>(L, L.w, nb, Ns, Ns_pow2, cu, tm_g != nullptr, Nt, ray, lane, out, xyz, ro, rd);
     wave_sync();  // LDS reuse by the next ray of this wave
     if (AON_PDF_PIPE) {
 #pragma unroll

@@ -52,6 +52,13 @@ def composite_bytes(S, weights_out=True):
     return 16 * S + 4 * S + 12 + 20 + (4 * S if weights_out else 0)
 
 
+def march_bytes(S, Ns):
+    # fused coarse composite + resample (aon_composite_march) per ray: raw (S,4) + t (S) + dirs
+    # read; rgb + acc + depth and the merged fine t (S + Ns) written.  The coarse weights stay on
+    # chip (the eval-mode u is one shared 512-B row, L2-resident: not counted).
+    return 16 * S + 4 * S + 12 + 20 + 4 * (S + Ns)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -113,6 +120,7 @@ def main():
 
     mlp_ms, rows = avg_ms("mlp1")
     comp_ms, comp_rows = avg_ms("comp1")
+    march_ms, march_rows = avg_ms("march0")
     extra = {}
     if not args.no_extra:  # every rank takes part (the C5 step all-reduces over RCCL)
         if world == 1:
@@ -176,6 +184,13 @@ def main():
                                      "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "frac": gbs / PEAK_HBM_GBS, "launch_ms": comp_ms,
                                      "algorithmic_bytes_per_launch": cb}
+    if march_ms:
+        mb = march_bytes(NC + 1, NF) * (march_rows // (NC + 1))
+        gbs = mb / (march_ms * 1e-3) / 1e9
+        out["roofline_march"] = {"bound": "hbm", "kernel": "k_composite_march (coarse composite + "
+                                 "inverse-CDF resample + merge, fused)", "achieved": gbs,
+                                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                                 "launch_ms": march_ms, "algorithmic_bytes_per_launch": mb}
 
     out.update(extra)
     if world == 1 and not args.no_cpu_baseline:

@@ -104,6 +104,21 @@ int aon_sample_pdf(const float* bins, int64_t bins_stride, const float* weights,
                    int64_t u_stride, const float* t_merge, int Nt, const float* rays_o,
                    const float* rays_d, float* out, float* xyz, aon_stream_t stream);
 
+/* The coarse level's volumetric_rendering (helper.py:157-195) fused with the resampling that
+ * consumes its weights (model.py:163-172: sample_pdf on the mids of t and weights[..., 1:-1],
+ * merged with t; helper.py:203-252) -- one kernel, the coarse weights stay on chip.
+ *   raw:     (B*S, 4) [r, g, b, sigma], 16-byte aligned (aon_mlp_fwd's output), act as in
+ *            aon_composite_fwd; t: (B, S) sorted; dirs: (B, 3) rays_d;
+ *   u:       (B, Ns) with row stride u_stride (0 = one shared row, eval mode);
+ *   outputs: comp_rgb (B, 3), acc, depth (B), weights (B, S) or NULL, and
+ *            t_fine = sorted(cat[t, samples]) (B, S + Ns).
+ * Equal, bit for bit, to aon_composite_fwd followed by aon_sample_pdf(bins = NULL, weights + 1,
+ * t_merge = t).  Limits: 3 <= S <= 256, 1 <= Ns <= 256. */
+int aon_composite_march(const float* raw, const float* t, const float* dirs, int64_t B, int S,
+                        int white_bkgd, int act, const float* u, int64_t u_stride, int Ns,
+                        float* comp_rgb, float* acc, float* weights, float* depth, float* t_fine,
+                        aon_stream_t stream);
+
 /* ---------------------------------------------------------------- MLP */
 /* Device pointers to one NeRFMLP's nn.Linear parameters in torch layout ([out][in]),
  * models/vanilla_nerf/model.py:39-93 with the default geometry (min_deg_point 0,

@@ -485,6 +485,69 @@ def case_datasets():
     save("datasets.npz", **out)
 
 
+LIGHTNING_META = {"epoch": 7, "global_step": 1234, "pytorch-lightning_version": "1.5.10"}
+
+
+def lightning_checkpoints():
+    """The two Lightning checkpoint layouts the reference evaluates from (run.py:156-163):
+    LitNeRF (self.model = NeRF, model.py:218) and LitNeRF_AutoDecoder (self.model = NeRF_AE_Art,
+    self.code_library = CodeLibraryArticulated, model_autodecoder.py:356-357), with PCG64 weights
+    (oracle/weights.py) and the keys of the reference modules' own state_dict()."""
+    net, _ = make_nerf(0)
+    mad = _refimport.load_articulated()
+    art = mad.NeRF_AE_Art()
+    art.load_state_dict({k: torch.from_numpy(v) for k, v in W.art_state_dict(0).items()})
+    lib = {k: torch.from_numpy(v) for k, v in W.code_library_state_dict(0).items()}
+    van = {"model." + k: v for k, v in net.state_dict().items()}
+    artsd = {"model." + k: v for k, v in art.state_dict().items()}
+    artsd.update({"code_library." + k: v for k, v in lib.items()})
+    return {"vanilla": dict(LIGHTNING_META, state_dict=van, optimizer_states=[], lr_schedulers=[]),
+            "articulated": dict(LIGHTNING_META, state_dict=artsd, optimizer_states=[],
+                                lr_schedulers=[])}
+
+
+CKPT_CASES = (("vanilla", "model", []), ("vanilla", "model", ["coarse_mlp"]),
+              ("articulated", "model", []), ("articulated", "code_library", []),
+              ("articulated", "model", ["fine_mlp.views_linear"]))
+
+
+def case_checkpoint():
+    """The reference's own utils.extract_model_state_dict (utils/__init__.py:117-132) applied to
+    the checkpoints of lightning_checkpoints(): per case the extracted keys in order, their
+    shapes and the sha256 of every tensor's bytes -> checkpoint_manifest.json (the checkpoint
+    files themselves, ~10 MB, are regenerated by tests/test_checkpoint.py from the same PCG64
+    weights and compared against this manifest)."""
+    import hashlib
+    import tempfile
+
+    ref_utils = sys.modules["utils"]  # imported by the reference's model.py (utils.train_helper)
+    cks = lightning_checkpoints()
+    out = {"meta": LIGHTNING_META, "layouts": {}, "cases": []}
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, ck in cks.items():
+            path = os.path.join(tmp, f"{name}.ckpt")
+            torch.save(ck, path)
+            out["layouts"][name] = [[k, list(v.shape)] for k, v in ck["state_dict"].items()]
+        for name, model_name, ignore in CKPT_CASES:
+            ext = ref_utils.extract_model_state_dict(os.path.join(tmp, f"{name}.ckpt"), model_name,
+                                                     list(ignore))
+            out["cases"].append({
+                "checkpoint": name, "model_name": model_name, "prefixes_to_ignore": list(ignore),
+                "keys": list(ext), "shapes": [list(v.shape) for v in ext.values()],
+                "sha256": [hashlib.sha256(v.contiguous().numpy().tobytes()).hexdigest()
+                           for v in ext.values()]})
+        # load_ckpt into a fresh reference NeRF: its state_dict afterwards
+        fresh = model.NeRF()
+        ref_utils.load_ckpt(fresh, os.path.join(tmp, "vanilla.ckpt"))
+        out["load_ckpt_vanilla_sha256"] = {
+            k: hashlib.sha256(v.contiguous().numpy().tobytes()).hexdigest()
+            for k, v in fresh.state_dict().items()}
+    path = os.path.join(HERE, "checkpoint_manifest.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0)
+    print(f"checkpoint_manifest.json: {os.path.getsize(path) / 1e3:.1f} kB")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # e.g. `make_golden.py case_art_train_step`
         for name in sys.argv[1:]:
@@ -501,3 +564,4 @@ if __name__ == "__main__":
     case_articulated()
     case_datasets()
     case_art_train_step()
+    case_checkpoint()

@@ -657,3 +657,109 @@ def oracle_envelope(params, rays):
     finally:
         O.mlp_forward = orig
     return env
+
+
+# ----------------------------------------------------------------------------- fused march
+MARCH_CASES = [(65, 128), (33, 128), (65, 16), (100, 64), (129, 128), (200, 50), (3, 1)]
+
+
+@pytest.mark.parametrize("S,Ns", MARCH_CASES)
+def test_composite_march_equals_two_kernels(S, Ns):
+    """aon_composite_march (coarse compositing + sample_pdf on mids / weights[1:-1] + merge, one
+    kernel: helper.py:157-252, model.py:163-172) equals aon_composite_fwd followed by
+    aon_sample_pdf bit for bit -- every output, eval (one shared u row) and randomized (per-ray u,
+    unsorted), with and without the weights output, every activation mode, white on and off;
+    plus the fine t against the oracle's sample_pdf on the GPU's own weights."""
+    from aonerf import _lib as L
+    from aonerf import helper
+
+    g = torch.Generator().manual_seed(S * 1000 + Ns)
+    B = 700
+    t = torch.sort(2.0 + 4.0 * torch.rand((B, S), generator=g), -1).values
+    raw = torch.cat([torch.randn((B, S, 3), generator=g),
+                     3.0 * torch.randn((B, S, 1), generator=g)], -1).reshape(-1, 4)
+    raw[: 5 * S, 3] = -1.0  # rays of zero density: all-zero weights, the eps padding
+    dirs = torch.randn((B, 3), generator=g)
+    raw_d, t_d, dirs_d = cuda(raw), cuda(t), cuda(dirs)
+    for rnd in (False, True):
+        if rnd:
+            u, us = cuda(torch.rand((B, Ns), generator=g)), Ns
+        else:
+            u, us = helper.eval_u(Ns, "cuda"), 0
+        for act, white, keep_w in ((L.ACT_VANILLA, 1, True), (L.ACT_ARTIC, 0, False),
+                                   (L.ACT_VANILLA, 0, False)):
+            two = [torch.empty(s, device="cuda") for s in ((B, 3), (B,), (B, S), (B,))]
+            L.call("aon_composite_fwd", L.ptr(raw_d), 4, L.ptr(raw_d[:, 3:]), 4, L.ptr(t_d),
+                   L.ptr(dirs_d), B, S, white, act, *[L.ptr(o) for o in two], L.stream())
+            t2 = torch.empty((B, S + Ns), device="cuda")
+            L.call("aon_sample_pdf", None, 0, L.ptr(two[2][:, 1:]), S, B, S - 1, Ns, L.ptr(u), us,
+                   L.ptr(t_d), S, None, None, L.ptr(t2), None, L.stream())
+            one = [torch.empty(s, device="cuda") for s in ((B, 3), (B,), (B, S), (B,))]
+            t1 = torch.empty((B, S + Ns), device="cuda")
+            L.call("aon_composite_march", L.ptr(raw_d), L.ptr(t_d), L.ptr(dirs_d), B, S, white,
+                   act, L.ptr(u), us, Ns, L.ptr(one[0]), L.ptr(one[1]),
+                   L.ptr(one[2]) if keep_w else None, L.ptr(one[3]), L.ptr(t1), L.stream())
+            torch.cuda.synchronize()
+            for k, (a, b) in enumerate(zip(one, two)):
+                if k == 2 and not keep_w:
+                    continue
+                assert torch.equal(a, b), f"S={S} Ns={Ns} rnd={rnd} act={act} output {k}"
+            assert torch.equal(t1, t2), f"S={S} Ns={Ns} rnd={rnd} act={act} fine t"
+        w = two[2].cpu()
+        mids = 0.5 * (t[..., 1:] + t[..., :-1])
+        t_ref, _ = O.sample_pdf(mids[:64], w[:64, 1:-1], torch.zeros(64, 3), dirs[:64], t[:64], Ns,
+                                rnd, **({"u": u[:64].cpu()} if rnd else {}))
+        np.testing.assert_array_equal(npy(t1[:64]), t_ref.numpy())
+
+
+def test_composite_march_ray_loop():
+    """The fused kernel's grid caps at 65,536 workgroups and loops: a 270,000-ray launch equals
+    900-ray launches bit for bit."""
+    from aonerf import _lib as L
+    from aonerf import helper
+
+    g = torch.Generator().manual_seed(5)
+    B, S, Ns = 270000, 65, 128
+    t = cuda(torch.sort(2.0 + 4.0 * torch.rand((B, S), generator=g), -1).values)
+    raw = cuda(torch.cat([torch.rand((B, S, 3), generator=g), 3.0 * torch.rand((B, S, 1), generator=g)],
+                         -1).reshape(-1, 4))
+    dirs = cuda(torch.nn.functional.normalize(torch.randn((B, 3), generator=g), dim=-1))
+    u = helper.eval_u(Ns, "cuda")
+
+    def run(lo, hi):
+        n = hi - lo
+        outs = [torch.empty(s, device="cuda") for s in ((n, 3), (n,), (n,), (n, S + Ns))]
+        L.call("aon_composite_march", L.ptr(raw[lo * S:]), L.ptr(t[lo:]), L.ptr(dirs[lo:]), n, S, 1,
+               L.ACT_VANILLA, L.ptr(u), 0, Ns, L.ptr(outs[0]), L.ptr(outs[1]), None, L.ptr(outs[2]),
+               L.ptr(outs[3]), L.stream())
+        return outs
+
+    whole = run(0, B)
+    parts = [run(lo, min(lo + 900, B)) for lo in range(0, B, 900)]
+    torch.cuda.synchronize()
+    for k in range(4):
+        assert torch.equal(whole[k], torch.cat([p[k] for p in parts])), k
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_render_fused_march_equals_unfused(golden, precision):
+    """NeRF.forward with the fused coarse composite + resample (model.FUSED_MARCH) equals the
+    two-kernel path bit for bit, eval and randomized."""
+    from aonerf import model as M
+
+    g = golden("forward_random.npz")
+    net = make_nerf(precision)
+    rays = rays_of(g)
+    outs = {}
+    for fused in (True, False):
+        M.FUSED_MARCH = fused
+        try:
+            outs[fused] = [net(rays, False, True, 2.0, 6.0),
+                           net(rays, True, False, 2.0, 6.0, u_coarse=cuda(g["u_coarse"]),
+                               u_fine=cuda(g["u_fine"]))]
+        finally:
+            M.FUSED_MARCH = True
+    for a, b in zip(outs[True], outs[False]):
+        for la, lb in zip(a, b):
+            for x, y in zip(la, lb):
+                assert torch.equal(x, y)
