@@ -27,35 +27,6 @@ __device__ __forceinline__ void wave_sync_c() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// ---- DPP lane moves (gfx9 controls).  Lanes whose source is outside the pattern keep `old`.
-template <int CTRL, int ROW_MASK = 0xF>
-__device__ __forceinline__ double dpp_f64(double src, double old) {
-  const long long s = __builtin_bit_cast(long long, src), o = __builtin_bit_cast(long long, old);
-  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)s, CTRL, ROW_MASK, 0xF, false);
-  const int hi =
-      __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(s >> 32), CTRL, ROW_MASK, 0xF, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-  const long long s = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_readlane((int)s, lane);
-  const int hi = __builtin_amdgcn_readlane((int)(s >> 32), lane);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-}
-
-// inclusive prefix product over the 64 lanes: row_shr 1/2/4/8 inside 16-lane rows, then
-// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- VALU lane moves, no LDS
-__device__ __forceinline__ double wave_incl_prod(double x) {
-  x *= dpp_f64<0x111>(x, 1.0);
-  x *= dpp_f64<0x112>(x, 1.0);
-  x *= dpp_f64<0x114>(x, 1.0);
-  x *= dpp_f64<0x118>(x, 1.0);
-  x *= dpp_f64<0x142, 0xA>(x, 1.0);
-  x *= dpp_f64<0x143, 0xC>(x, 1.0);
-  return x;
-}
-
 // The compositor's math for one ray, its inputs in registers (lane i: sample 64 b + i's t and
 // raw [r, g, b, sigma]): alpha, the fp64 DPP transmittance scan, weights into the planar LDS
 // arrays P (and out_w when given), the torch-order sums and the ray's rgb / acc / depth.  Leaves

@@ -16,14 +16,19 @@
 namespace aon {
 
 // LDS of one wave: the compositor's planar rows + sum scratch, then the resampler's rows
-template <int SM, int SCR, int NBX>
+template <int SM, int SCR, int NBX, int NO>
 struct MarchLds {
   float P[5 * SM + SCR + 32];
   PdfLds<NBX> L;
+  float orow[NO];  // the merged fine t row, written out by coalesced stores
 };
 
+#ifndef AON_MARCH_OCC
+#define AON_MARCH_OCC 7  // waves per SIMD the S = 65 instantiation is built for (6 / 8 slower: profiles/r02/ab_march)
+#endif
+
 template <int NB, int SC, int NBX>
-__global__ __launch_bounds__(64 * kCompWaves) void k_composite_march(
+__global__ __launch_bounds__(64 * kCompWaves, SC > 0 ? AON_MARCH_OCC : 1) void k_composite_march(
     const float* __restrict__ raw4, const float* __restrict__ tv, const float* __restrict__ dirs,
     int64_t B, int S_rt, int white, int act, const float* __restrict__ u_g, int64_t u_stride,
     int Ns, int Ns_pow2, float* __restrict__ out_rgb, float* __restrict__ out_acc,
@@ -31,8 +36,8 @@ __global__ __launch_bounds__(64 * kCompWaves) void k_composite_march(
   constexpr int SM = SC > 0 ? SC : 64 * NB;
   constexpr int kScratch = SC > 0 ? comp_scratch(SC) : kCompScratch;
   const int S = SC > 0 ? SC : S_rt;
-  __shared__ MarchLds<SM, kScratch, NBX> lds_all[kCompWaves];
-  MarchLds<SM, kScratch, NBX>& M = lds_all[threadIdx.x >> 6];
+  __shared__ MarchLds<SM, kScratch, NBX, SM + 64 * NBX> lds_all[kCompWaves];
+  MarchLds<SM, kScratch, NBX, SM + 64 * NBX>& M = lds_all[threadIdx.x >> 6];
   float* P = M.P;
   float* scratch = P + 5 * SM;
   float* sums = scratch + kScratch;
@@ -73,8 +78,13 @@ __global__ __launch_bounds__(64 * kCompWaves) void k_composite_march(
     wave_sync();
     for (int k = lane; k < nb; k += 64) L.bins[k] = __fmul_rn(0.5f, __fadd_rn(L.tm[k + 1], L.tm[k]));
     // weights[..., 1:-1] straight from the compositor's LDS row (P[0 .. S) = w)
-    pdf_ray<NBX>(L, P + 1, nb, Ns, Ns_pow2, cu, true, S, ray, lane, t_out, nullptr, nullptr,
+    pdf_ray<NBX>(L, P + 1, nb, Ns, Ns_pow2, cu, true, S, ray, lane, M.orow, nullptr, nullptr,
                  nullptr);
+    wave_sync();
+    // the merged row leaves in wave-contiguous stores (the merge scatters within it)
+    const int No = S + Ns;
+    float* orow_g = t_out + ray * No;
+    for (int i = lane; i < No; i += 64) orow_g[i] = M.orow[i];
     wave_sync();  // LDS reuse by this wave's next ray
   }
 }

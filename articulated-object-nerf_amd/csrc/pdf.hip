@@ -63,7 +63,8 @@ __global__ __launch_bounds__(64 * kPdfWaves) void k_sample_pdf(
     if (!bins_g) {  // bins = mids of t_merge (model.py:163)
       for (int k = lane; k < nb; k += 64) L.bins[k] = __fmul_rn(0.5f, __fadd_rn(L.tm[k + 1], L.tm[k]));
     }
-    pdf_ray<NBX>(L, L.w, nb, Ns, Ns_pow2, cu, tm_g != nullptr, Nt, ray, lane, out, xyz, ro, rd);
+    pdf_ray<NBX>(L, L.w, nb, Ns, Ns_pow2, cu, tm_g != nullptr, Nt, ray, lane,
+                 out + ray * (tm_g ? Nt + Ns : Ns), xyz, ro, rd);
     wave_sync();  // LDS reuse by the next ray of this wave
     if (AON_PDF_PIPE) {
 #pragma unroll

@@ -22,8 +22,53 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Two-level counts in a sorted LDS row, 2 dependent LDS round trips instead of log2(n): the
+// every-8th "pivots" a[8m + 7] (the same address on every lane: broadcast reads) give the first
+// bucket q whose pivot is not counted; buckets before it count whole, bucket q entry by entry,
+// everything after it is past x (sorted).  Equal to the binary searches below for any x
+// (NaN x: 0; +inf entries sort last).
+template <bool LE>
+__device__ __forceinline__ int count_sorted(const float* a, int n, float x) {
+  const int nfull = n >> 3;
+  int q = 0;
+  for (int m = 0; m < nfull; ++m) {
+    const float p = a[8 * m + 7];
+    q += LE ? (p <= x) : (p < x);
+  }
+  int c = 8 * q;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int i = 8 * q + e;
+    if (i < n) {
+      const float v = a[i];
+      c += LE ? (v <= x) : (v < x);
+    }
+  }
+  return c;
+}
+
+// Branch-free binary lifting: the largest c with a[c-1] <= x (LE) / < x, one probe per power of
+// two below n -- a trip count uniform across the wave (no divergent loop exits).  Equal to the
+// while-loop searches below on sorted rows (NaN x: 0).
+template <bool LE>
+__device__ __forceinline__ int count_lift(const float* a, int n, float x) {
+  int c = 0;
+  if (n <= 0) return 0;
+  for (int step = 1 << (31 - __builtin_clz(n)); step > 0; step >>= 1) {
+    const int j = c + step;
+    const float v = a[(j < n ? j : n) - 1];
+    const bool ok = j <= n && (LE ? v <= x : v < x);
+    c = ok ? j : c;
+  }
+  return c;
+}
+
+#ifndef AON_PDF_SEARCH2
+#define AON_PDF_SEARCH2 2  // 2: count_lift (fused march 0.418 -> 0.394 ms); 1: two-level searches (more LDS reads: 5-15% slower); 0: while-loop binary searches (profiles/r02/ab_march)
+#endif
+
 // number of entries of sorted a[0..n) that are <= x  (upper bound)
-__device__ __forceinline__ int count_le(const float* a, int n, float x) {
+__device__ __forceinline__ int count_le_bin(const float* a, int n, float x) {
   int lo = 0, hi = n;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
@@ -33,7 +78,7 @@ __device__ __forceinline__ int count_le(const float* a, int n, float x) {
 }
 
 // number of entries of sorted a[0..n) that are < x  (lower bound)
-__device__ __forceinline__ int count_lt(const float* a, int n, float x) {
+__device__ __forceinline__ int count_lt_bin(const float* a, int n, float x) {
   int lo = 0, hi = n;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
@@ -41,6 +86,19 @@ __device__ __forceinline__ int count_lt(const float* a, int n, float x) {
   }
   return lo;
 }
+
+__device__ __forceinline__ int count_le(const float* a, int n, float x) {
+  return AON_PDF_SEARCH2 == 2 ? count_lift<true>(a, n, x)
+         : AON_PDF_SEARCH2 ? count_sorted<true>(a, n, x) : count_le_bin(a, n, x);
+}
+__device__ __forceinline__ int count_lt(const float* a, int n, float x) {
+  return AON_PDF_SEARCH2 == 2 ? count_lift<false>(a, n, x)
+         : AON_PDF_SEARCH2 ? count_sorted<false>(a, n, x) : count_lt_bin(a, n, x);
+}
+
+#ifndef AON_PDF_DPP_SCAN
+#define AON_PDF_DPP_SCAN 1  // 0: the shuffle (ds_bpermute) scan
+#endif
 
 // per-wave LDS, sized for rows of up to 64 * NBX entries (bins, weights, samples, t_merge)
 template <int NBX>
@@ -54,11 +112,12 @@ struct PdfLds {
 
 // The resampling of one ray once its LDS rows are staged (L.bins; L.tm when merging; the nb - 1
 // weights at w, any LDS row): torch-order weight sum + padding, fp64 CDF scan, inverse CDF per u
-// (cu[b] = u[64 b + lane]), the sort when needed, and the (merged) output row; xyz optional.
+// (cu[b] = u[64 b + lane]), the sort when needed, and the (merged) output row o (global, or an
+// LDS row the caller copies out); xyz optional.
 template <int NBX>
 __device__ __forceinline__ void pdf_ray(PdfLds<NBX>& L, const float* w, int nb, int Ns,
                                         int Ns_pow2, const float (&cu)[NBX], bool merge, int Nt,
-                                        int64_t ray, int lane, float* __restrict__ out,
+                                        int64_t ray, int lane, float* __restrict__ o,
                                         float* __restrict__ xyz, const float* __restrict__ ro,
                                         const float* __restrict__ rd) {
   const int nw = nb - 1;
@@ -70,10 +129,14 @@ __device__ __forceinline__ void pdf_ray(PdfLds<NBX>& L, const float* w, int nb, 
   } else if (lane == 0) {
     part = row_sum_ilp4([&](int e) { return w[e]; }, nw);
   }
-  float ws = __shfl(part, nw >= 8 ? 8 : 0);
+  // lane partials gathered by v_readlane (SGPR broadcasts; the lane index is uniform)
+  auto lane_val = [&](int c) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, part), c));
+  };
+  float ws = lane_val(nw >= 8 ? 8 : 0);
   if (nw >= 8) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) ws = __fadd_rn(ws, __shfl(part, c));
+    for (int c = 0; c < 8; ++c) ws = __fadd_rn(ws, lane_val(c));
   }
   const float pad = fmaxf(0.0f, __fsub_rn(1e-5f, ws));
   const float padw = __fdiv_rn(pad, static_cast<float>(nw));
@@ -84,13 +147,17 @@ __device__ __forceinline__ void pdf_ray(PdfLds<NBX>& L, const float* w, int nb, 
     const int k = base + lane;
     double v = 0.0;
     if (k < nw - 1) v = (double)__fdiv_rn(__fadd_rn(w[k], padw), wsum);
+#if AON_PDF_DPP_SCAN
+    v = wave_incl_sum(v);  // DPP lane moves, no LDS round trips
+#else
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const double x = __shfl_up(v, o);
       if (lane >= o) v += x;
     }
+#endif
     if (k < nw - 1) L.cdf[k + 1] = fminf(1.0f, (float)(carry + v));
-    carry += __shfl(v, 63);
+    carry += readlane_f64(v, 63);
   }
   if (lane == 0) {
     L.cdf[0] = 0.0f;
@@ -141,7 +208,6 @@ __device__ __forceinline__ void pdf_ray(PdfLds<NBX>& L, const float* w, int nb, 
   }
   // ---- write (merged) output
   const int No = merge ? Nt + Ns : Ns;
-  float* o = out + ray * No;
   float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
   if (xyz) {
     ox = ro[3 * ray]; oy = ro[3 * ray + 1]; oz = ro[3 * ray + 2];

@@ -71,6 +71,24 @@ def main():
     pb = 4 * (Sc + (Sc - 2) + Sc + Nf)
     gbs = pb * B / (ms * 1e-3) / 1e9
     res["sample_pdf"] = {"ms": ms, "GB/s": gbs, "frac_hbm": gbs / 8000.0, "bytes_per_ray": pb}
+    # the fused coarse composite + resample (aon_composite_march) on the coarse level's inputs
+    raw = torch.rand((B * Sc, 4), device=dev, generator=g)
+    dirs = torch.nn.functional.normalize(torch.randn((B, 3), device=dev, generator=g), dim=-1)
+    outs = [torch.empty(s, device=dev) for s in ((B, 3), (B,), (B,))]
+
+    def run_march():
+        L.call("aon_composite_march", L.ptr(raw), L.ptr(tc), L.ptr(dirs), B, Sc, 1, L.ACT_NONE,
+               L.ptr(u), 0, Nf, L.ptr(outs[0]), L.ptr(outs[1]), None, L.ptr(outs[2]), L.ptr(tn),
+               L.stream())
+
+    ms = timed(run_march, args.reps)
+    mb = 16 * Sc + 4 * Sc + 12 + 20 + 4 * (Sc + Nf)
+    gbs = mb * B / (ms * 1e-3) / 1e9
+    import hashlib
+
+    res["march"] = {"ms": ms, "GB/s": gbs, "frac_hbm": gbs / 8000.0, "bytes_per_ray": mb,
+                    "sha256_t_fine": hashlib.sha256(tn.cpu().numpy().tobytes()).hexdigest()[:16],
+                    "sha256_rgb": hashlib.sha256(outs[0].cpu().numpy().tobytes()).hexdigest()[:16]}
     print(json.dumps(res), flush=True)
 
 
