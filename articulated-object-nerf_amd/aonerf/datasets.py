@@ -106,9 +106,21 @@ class SapienDataset:
         return {"rays_o": ro, "rays_d": rd, "viewdirs": rd, "target": tgt}
 
     def random_batch(self, n, generator=None):
-        """A uniformly drawn training batch (the DataLoader's shuffled batches, drawn on device)."""
+        """A batch of n samples drawn uniformly WITH replacement (synthetic benches).  The
+        reference's training loader (DataLoader(shuffle=True), model.py:228-236) visits every
+        sample once per epoch: that is epoch_batches."""
         idx = torch.randint(0, len(self), (n,), device=self.device, generator=generator)
         return self.batch(idx)
+
+    def epoch_batches(self, n, generator=None, drop_last=False):
+        """One epoch of the reference's shuffled DataLoader (batch_size n, shuffle=True,
+        drop_last False): a device permutation of every sample index, cut into batches of n
+        (the last one ragged)."""
+        perm = torch.randperm(len(self), device=self.device, generator=generator)
+        for i in range(0, perm.numel(), n):
+            if drop_last and i + n > perm.numel():
+                break
+            yield self.batch(perm[i:i + n])
 
     def __getitem__(self, idx):
         if self.split == "train":

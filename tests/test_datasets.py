@@ -46,6 +46,14 @@ def test_train_batches_match_reference(golden):
     # a random batch is drawn from the same table
     rb = ds.random_batch(4096, torch.Generator(device="cuda").manual_seed(0))
     assert rb["target"].shape == (4096, 3) and torch.isfinite(rb["rays_d"]).all()
+    # one shuffled epoch (the reference's DataLoader(shuffle=True)) visits every sample once:
+    # the union of its batches (ragged last one included) is the whole table, each row once
+    full = ds.batch(torch.arange(len(ds), device="cuda"))
+    seen = torch.cat([torch.cat([b["rays_d"], b["target"]], -1)
+                      for b in ds.epoch_batches(1000, torch.Generator(device="cuda").manual_seed(1))])
+    assert seen.shape[0] == len(ds)
+    key = lambda x: x[torch.argsort(x[:, 0] * 1e4 + x[:, 1] * 1e2 + x[:, 2])]  # noqa: E731
+    assert torch.equal(key(seen[:, :3]), key(full["rays_d"]))
 
 
 @pytest.mark.gpu
