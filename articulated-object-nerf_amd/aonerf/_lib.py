@@ -14,7 +14,8 @@ LIB_PATH = os.environ.get("AONERF_LIB", os.path.join(os.path.dirname(_HERE), "li
 
 c_i64, c_int, c_float, c_size, vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 
-PREC = {"fp32": 0, "f16x3": 1}
+PREC = {"fp32": 0, "f16x3": 1}  # render precisions (aon_mlp_fwd)
+PREC_BF16 = 2  # the training step's bf16 mode (aon_mlp_fwd_train_bf16, aon_mlp_bwd_bf16)
 ACT_NONE, ACT_VANILLA, ACT_ARTIC = 0, 1, 2
 
 
@@ -38,7 +39,8 @@ class AonGemmArgs(ctypes.Structure):
                 ("B", vp), ("ldb", c_i64), ("b_kc", c_int), ("b_rdiv", c_i64),
                 ("C", vp), ("ldc", c_i64), ("bias", vp), ("mask", vp), ("ldm", c_i64),
                 ("relu", c_int), ("accumulate", c_int), ("a_scale", c_float), ("b_scale", c_float),
-                ("k_splits", c_i64), ("rowsum", vp), ("a_amax", vp)]
+                ("k_splits", c_i64), ("rowsum", vp), ("a_amax", vp), ("mma_bf16", c_int),
+                ("a_bf16", c_int), ("b_bf16", c_int)]
 
 
 class AonAdamTensor(ctypes.Structure):
@@ -68,6 +70,10 @@ _SIGNATURES = {
     "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp]),
+    "aon_mlp_fwd_train_bf16": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp,
+                                       vp]),
+    "aon_mlp_bwd_pack_bf16": (c_int, [ctypes.POINTER(AonMlpParams), vp, vp]),
+    "aon_mlp_bwd_bf16": (c_int, [vp, vp, vp, c_i64, vp, vp, vp, vp, vp]),
     "aon_relu_masks": (c_int, [vp, c_i64, c_int, vp, vp]),
     "aon_mlp_bwd_packed_bytes": (c_size, []),
     "aon_mlp_bwd_pack": (c_int, [ctypes.POINTER(AonMlpParams), vp, vp]),

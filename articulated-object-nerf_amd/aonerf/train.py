@@ -107,6 +107,11 @@ FUSED_FORWARD = True
 # backward of a level: input gradients in one fused kernel (aon_mlp_bwd) + weight-gradient GEMMs
 # when True, else every product as a GEMM (_backward_level)
 FUSED_BACKWARD = True
+# numerics of the fused training kernels: "f16x3" (fp32-class, the parity mode) or "bf16"
+# (BASELINE config C5's bf16 training step: one bf16 MFMA per product in the forward, the
+# backward chain and the weight-gradient GEMMs, activations and gradients kept as bf16; the
+# compositing, loss, its backward and Adam stay fp32 on fp32 master weights)
+PRECISION = "f16x3"
 # a dict -> hip events around each level's training kernels, keyed by name and sample count
 # (bench.py's train_step roofline): "fwd_train<S>", "bwd_chain<S>", "dweight<S>"
 TIMERS = None
@@ -155,20 +160,23 @@ def _buffer(key, nbytes, dev, guard=False):
 RANGE_CHECK = True
 
 
-def _pack(P, dev, tag=""):
-    """The f16x3 weight stream of one level's parameters, re-packed on every call (the
+def _pack(P, dev, tag="", bf16=False):
+    """The f16x3 (or bf16) weight stream of one level's parameters, re-packed on every call (the
     optimizer updates the parameters in place behind torch's version counters).  ``tag``: one
     buffer per level (its range-status word must survive until the optimizer step)."""
-    prec = L.PREC["f16x3"]
-    buf = _buffer(f"fwd{tag}", L.lib().aon_mlp_packed_bytes(prec), dev, guard=True)
+    prec = L.PREC_BF16 if bf16 else L.PREC["f16x3"]
+    buf = _buffer(f"fwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_packed_bytes(prec), dev,
+                  guard=not bf16)
     L.call("aon_mlp_pack", L.ctypes.byref(_params_struct(P)), prec, L.ptr(buf), L.stream(dev))
     return buf
 
 
-def _pack_bwd(P, dev, tag=""):
-    """The transposed weight stream of the fused backward chain (aon_mlp_bwd_pack)."""
-    buf = _buffer(f"bwd{tag}", L.lib().aon_mlp_bwd_packed_bytes(), dev, guard=True)
-    L.call("aon_mlp_bwd_pack", L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
+def _pack_bwd(P, dev, tag="", bf16=False):
+    """The transposed weight stream of the fused backward chain (aon_mlp_bwd_pack[_bf16])."""
+    buf = _buffer(f"bwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_bwd_packed_bytes(), dev,
+                  guard=not bf16)
+    L.call("aon_mlp_bwd_pack_bf16" if bf16 else "aon_mlp_bwd_pack",
+           L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
     return buf
 
 
@@ -196,25 +204,28 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
     the weight gradients dW = dZ^T X and db = sum_rows dZ stay split-K GEMMs.  ``masks``: the
     ReLU' bits of h0..h7, hv from the fused forward (built from the activations when None)."""
     R, dev = enc.shape[0], enc.device
+    bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
         masks = relu_masks(list(h) + [hv], R)
-    dzv = torch.empty((R, 128), device=dev)
-    dzb = torch.empty((R, 256), device=dev)
-    dz = torch.empty((8, R, 256), device=dev)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    dzv = torch.empty((R, 128), device=dev, dtype=dt)
+    dzb = torch.empty((R, 256), device=dev, dtype=dt)
+    dz = torch.empty((8, R, 256), device=dev, dtype=dt)
     work = _buffer("work", 4, dev)
-    packed = _pack_bwd(P, dev, S)
+    packed = _pack_bwd(P, dev, S, bf16)
     e0 = _ev()
-    L.call("aon_mlp_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), R, L.ptr(dzv),
-           L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
+    L.call("aon_mlp_bwd_bf16" if bf16 else "aon_mlp_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks),
+           R, L.ptr(dzv), L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
     _rec(f"bwd_chain{S}", e0, R)
     e0 = _ev()
     acts = ACT_SCALE
 
     def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None):
-        # dY rides at the chain's own per-call scale from max |d raw| (the word in `work`)
+        # f16x3: dY rides at the chain's own per-call scale from max |d raw| (the word in
+        # `work`); bf16: one bf16 MFMA per product, no scales needed
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
-             b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=1.0, b_scale=acts, rowsum=db,
-             a_amax=work)
+             b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=1.0, b_scale=1.0 if bf16 else acts,
+             rowsum=db, a_amax=None if bf16 else work, mma_bf16=bf16)
 
     dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1])               # rgb_layer
     dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0
@@ -232,21 +243,25 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
     _rec(f"dweight{S}", e0, R)
 
 
-def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, masks=None):
+def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, masks=None,
+                         bf16=False):
     """_forward_level on the fused kernel: raw (R x 4) and the kept activations; ``masks``
-    ((9, R, 8) int32) receives their ReLU' bits for the backward chain."""
+    ((9, R, 8) int32) receives their ReLU' bits for the backward chain.  bf16: the bf16
+    training mode (activations kept as torch.bfloat16)."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
     if masks is None:
         masks = torch.empty((9, R, 8), dtype=torch.int32, device=dev)
-    hbuf = torch.empty((8, R, 256), device=dev)
-    bot = torch.empty((R, 256), device=dev)
-    hv = torch.empty((R, 128), device=dev)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    hbuf = torch.empty((8, R, 256), device=dev, dtype=dt)
+    bot = torch.empty((R, 256), device=dev, dtype=dt)
+    hv = torch.empty((R, 128), device=dev, dtype=dt)
     for w, b in P:
         if not (w.is_contiguous() and b.is_contiguous()):
             raise ValueError("MLP parameters must be contiguous")
-    packed = _pack(P, dev, S)
-    L.call("aon_mlp_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
+    packed = _pack(P, dev, S, bf16)
+    L.call("aon_mlp_fwd_train_bf16" if bf16 else "aon_mlp_fwd_train", L.ptr(packed), L.ptr(rays_o),
+           L.ptr(rays_d), L.ptr(viewdirs),
            L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hbuf),
            L.ptr(bot), L.ptr(hv), L.ptr(raw), L.ptr(masks), L.stream(dev))
     return list(hbuf.unbind(0)), bot, hv
@@ -275,7 +290,7 @@ class RenderLevel(torch.autograd.Function):
             e0 = _ev()
             h, bot, hv = _forward_level_fused(P, L.contig(rays_o), L.contig(rays_d),
                                               L.contig(viewdirs), L.contig(t_vals), raw, noise,
-                                              masks)
+                                              masks, bf16=PRECISION == "bf16")
             _rec(f"fwd_train{S}", e0, R)
         else:
             h, bot, hv = _forward_level(P, enc, venc, S, raw, noise)

@@ -388,6 +388,243 @@ static void launch_v(const Params& p, bool va, bool vb, dim3 grid, hipStream_t s
   else launch<AKC, BKC, false, false>(p, grid, st);
 }
 
+
+// ---- bf16 mode (the C5 training step's bf16 precision): weight-gradient products
+// C (M x N) (+)= A^T B over K rows with both operands reduction-major (A = dY [K][M], B = X
+// [K][N], row k of B at (k / b_rdiv) * ldb), each element fp32 or bf16 (template), rounded to
+// bf16 while staging; ONE v_mfma_f32_16x16x32_bf16 per 16x16x32 step (fp32 accumulate) where
+// the f16x3 kernel issues three.  Same tile grid, XCD-aware order, split-K and deterministic
+// reduction as k_gemm_f16x3; rowsum = the fp32 sums of A's staged values (bias gradients).
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+constexpr int STAGE_BF = 2 * PLANE;  // A, B planes of bf16 (same [row][k] geometry)
+
+template <typename T>
+__device__ __forceinline__ float to_f32(T v) { return static_cast<float>(v); }
+
+// 128 rows x 32 k of a reduction-major operand: thread t -> rows rq..rq+3 (rq = 16 (t >> 5) +
+// 4 (t & 3)), k = kq..kq+3 (kq = 4 ((t >> 2) & 7)); one 4-element row run per k
+template <typename T, bool VEC>
+struct TileLoadKM {
+  float r[4][4];  // [k][row]
+  __device__ __forceinline__ void load(const T* p, int64_t ld, int64_t rdiv, int64_t row0,
+                                       int64_t R, int64_t k0, int64_t kend, int tid) {
+    const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t k = k0 + kq + i;
+      const int64_t row = row0 + rq;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[i][j] = 0.f;
+      if (k < kend) {
+        const T* src = p + (rdiv == 1 ? k : k / rdiv) * ld + row;
+        if (VEC && row + 3 < R) {
+          if (sizeof(T) == 4) {
+            const f4 v = *reinterpret_cast<const f4*>(src);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r[i][j] = v[j];
+          } else {
+            const bf4 v = *reinterpret_cast<const bf4*>(src);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r[i][j] = static_cast<float>(v[j]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (row + j < R) r[i][j] = to_f32(src[j]);
+        }
+      }
+    }
+  }
+  // rows' sums of this thread's 4 k values, in k order (of the bf16-rounded values)
+  __device__ __forceinline__ void add_rows(float (&rs)[4]) const {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = static_cast<float>(static_cast<__bf16>(r[i][j]));
+      rs[j] = __fadd_rn(rs[j], __fadd_rn(__fadd_rn(__fadd_rn(v[0], v[1]), v[2]), v[3]));
+    }
+  }
+  // transposed into the [row][k] bf16 plane: row rq + j gets k = kq .. kq + 3 (one 8-B store)
+  __device__ __forceinline__ void store(__bf16* plane, int tid) const {
+    const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bf4 v = {static_cast<__bf16>(r[0][j]), static_cast<__bf16>(r[1][j]),
+                     static_cast<__bf16>(r[2][j]), static_cast<__bf16>(r[3][j])};
+      *reinterpret_cast<bf4*>(plane + (rq + j) * ROWH + kq) = v;
+    }
+  }
+};
+
+// The same tile from a bf16 source, kept as raw 16-bit lanes (no fp32 round trip): 4 rows of
+// each k are one 8-B load, and the 4 x 4 transpose into [row][k] is 2 v_perm_b32 per row.
+template <bool VEC>
+struct TileLoadKMb {
+  uint2 r[4];  // r[i]: rows rq..rq+3 at k = kq + i (bf16 bits, two per dword)
+  __device__ __forceinline__ void load(const __bf16* p, int64_t ld, int64_t rdiv, int64_t row0,
+                                       int64_t R, int64_t k0, int64_t kend, int tid) {
+    const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
+    const uint16_t* q = reinterpret_cast<const uint16_t*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t k = k0 + kq + i;
+      const int64_t row = row0 + rq;
+      uint2 v = {0u, 0u};
+      if (k < kend) {
+        const uint16_t* src = q + (rdiv == 1 ? k : k / rdiv) * ld + row;
+        if (VEC && row + 3 < R) {
+          v = *reinterpret_cast<const uint2*>(src);
+        } else {
+          uint32_t e[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) e[j] = row + j < R ? src[j] : 0u;
+          v = uint2{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+        }
+      }
+      r[i] = v;
+    }
+  }
+  __device__ __forceinline__ static float elem(uint2 v, int j) {  // bf16 -> fp32: exact shift
+    const uint32_t w = (j >> 1) ? v.y : v.x;
+    return __uint_as_float((j & 1) ? (w & 0xffff0000u) : (w << 16));
+  }
+  __device__ __forceinline__ void add_rows(float (&rs)[4]) const {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      rs[j] = __fadd_rn(rs[j], __fadd_rn(__fadd_rn(__fadd_rn(elem(r[0], j), elem(r[1], j)),
+                                                   elem(r[2], j)), elem(r[3], j)));
+  }
+  __device__ __forceinline__ void store(__bf16* plane, int tid) const {
+    const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // half (j & 1) of dword (j >> 1) of each k: [k0 | k1 << 16], [k2 | k3 << 16]
+      const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
+      const uint32_t d0 = (j >> 1) ? r[0].y : r[0].x, d1 = (j >> 1) ? r[1].y : r[1].x;
+      const uint32_t d2 = (j >> 1) ? r[2].y : r[2].x, d3 = (j >> 1) ? r[3].y : r[3].x;
+      const uint2 o = {__builtin_amdgcn_perm(d1, d0, sel), __builtin_amdgcn_perm(d3, d2, sel)};
+      *reinterpret_cast<uint2*>(plane + (rq + j) * ROWH + kq) = o;
+    }
+  }
+};
+
+template <typename T, bool VEC>
+struct KMLoader {
+  using type = TileLoadKM<T, VEC>;
+};
+template <bool VEC>
+struct KMLoader<__bf16, VEC> {
+  using type = TileLoadKMb<VEC>;
+};
+
+template <typename TA, typename TB, bool VA, bool VB>
+__global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_km(Params p) {
+  __shared__ __align__(16) __bf16 smem[2 * STAGE_BF];  // 2 stages x (A, B)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn, tile, z;
+  if (!split_of(p, tile, z)) return;
+  if (!tile_of(p, tile, tm, tn)) return;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)z * p.kchunk;
+  const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
+  const TA* A = reinterpret_cast<const TA*>(p.A);
+  const TB* Bm = reinterpret_cast<const TB*>(p.B);
+  typename KMLoader<TA, VA>::type ta;
+  typename KMLoader<TB, VB>::type tb;
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const bool want_rows = p.rowsum && tn == 0;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load = [&](int kt) {
+    const int64_t k0 = kbeg + (int64_t)kt * BK;
+    ta.load(A, p.lda, 1, m0, p.M, k0, kend, tid);
+    tb.load(Bm, p.ldb, p.b_rdiv, n0, p.N, k0, kend, tid);
+  };
+  auto store = [&](int stage) {
+    if (want_rows) ta.add_rows(rs);
+    __bf16* s = smem + stage * STAGE_BF;
+    ta.store(s, tid);
+    tb.store(s + PLANE, tid);
+  };
+  if (nk > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int P = kt & 1;
+    if (kt + 1 < nk) load(kt + 1);  // global loads in flight under this step's MFMAs
+    const __bf16* s = smem + P * STAGE_BF;
+    bf8 b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      b[j] = *reinterpret_cast<const bf8*>(s + PLANE + (wn * 64 + 16 * j + r16) * ROWH + 8 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf8 a = *reinterpret_cast<const bf8*>(s + (wm * 64 + 16 * i + r16) * ROWH + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(1 - P);
+    __syncthreads();
+  }
+  const bool split = p.zsplit > 1;
+  if (want_rows) {
+    float* red = reinterpret_cast<float*>(smem);  // [8 k quads][128 rows]
+    const int kqi = (tid >> 2) & 7, rq = 16 * (tid >> 5) + 4 * (tid & 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[kqi * BM + rq + j] = rs[j];
+    __syncthreads();
+    if (tid < BM && m0 + tid < p.M) {
+      float v = red[tid];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v = __fadd_rn(v, red[q * BM + tid]);
+      if (split) p.rowsum_part[(int64_t)z * p.M + m0 + tid] = v;
+      else p.rowsum[m0 + tid] = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + 16 * j + r16;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+        if (m >= p.M) continue;
+        float v = acc[i][j][r];
+        if (split) {
+          p.part[((int64_t)z * p.M + m) * p.N + n] = v;
+          continue;
+        }
+        float* c = p.C + m * p.ldc + n;
+        if (p.accumulate) v = __fadd_rn(*c, v);
+        *c = v;
+      }
+    }
+}
+
+template <typename TA, typename TB>
+static void launch_bf(const Params& p, bool va, bool vb, dim3 grid, hipStream_t st) {
+#define AON_BF_L(VA_, VB_) \
+  hipLaunchKernelGGL((k_gemm_bf16_km<TA, TB, VA_, VB_>), grid, dim3(THREADS), 0, st, p)
+  if (va && vb) AON_BF_L(true, true);
+  else if (va) AON_BF_L(true, false);
+  else if (vb) AON_BF_L(false, true);
+  else AON_BF_L(false, false);
+#undef AON_BF_L
+}
+
 }  // namespace gemm
 }  // namespace aon
 
@@ -426,6 +663,12 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   AON_REQUIRE(!a->mask || a->ldm >= a->N, "bad mask leading dimension");
   AON_REQUIRE(a->b_kc || a->b_rdiv >= 1, "b_rdiv must be >= 1");
   AON_REQUIRE(a->a_scale > 0.f && a->b_scale > 0.f, "operand scales must be positive");
+  const bool bf = a->mma_bf16 != 0;
+  AON_REQUIRE(bf || (!a->a_bf16 && !a->b_bf16), "bf16 operands need mma_bf16");
+  AON_REQUIRE(!bf || (!a->a_kc && !a->b_kc && !a->A2 && !a->bias && !a->mask && !a->relu &&
+                      !a->a_amax),
+              "mma_bf16 computes reduction-major weight gradients only (a_kc = b_kc = 0, no A2 / "
+              "bias / mask / relu / a_amax)");
   if (a->M == 0 || a->N == 0) return 0;
   Params p;
   p.M = a->M; p.N = a->N; p.K = a->K;
@@ -468,7 +711,15 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   const bool va = aligned16(a->A) && a->lda % 4 == 0 && (!a->A2 || a->K1 % 4 == 0);
   const bool vb = aligned16(a->B) && a->ldb % 4 == 0;
   hipStream_t st = (hipStream_t)stream;
-  if (a->a_kc && a->b_kc) launch_v<true, true>(p, va, vb, grid, st);
+  if (bf) {
+    // element size of each operand: 8-B (bf16) or 16-B (fp32) runs of 4 rows
+    const bool va16 = a->a_bf16 ? (reinterpret_cast<uintptr_t>(a->A) & 7) == 0 && a->lda % 4 == 0 : va;
+    const bool vb16 = a->b_bf16 ? (reinterpret_cast<uintptr_t>(a->B) & 7) == 0 && a->ldb % 4 == 0 : vb;
+    if (a->a_bf16 && a->b_bf16) launch_bf<__bf16, __bf16>(p, va16, vb16, grid, st);
+    else if (a->a_bf16) launch_bf<__bf16, float>(p, va16, vb16, grid, st);
+    else if (a->b_bf16) launch_bf<float, __bf16>(p, va16, vb16, grid, st);
+    else launch_bf<float, float>(p, va16, vb16, grid, st);
+  } else if (a->a_kc && a->b_kc) launch_v<true, true>(p, va, vb, grid, st);
   else if (a->a_kc) launch_v<true, false>(p, va, vb, grid, st);
   else if (a->b_kc) launch_v<false, true>(p, va, vb, grid, st);
   else launch_v<false, false>(p, va, vb, grid, st);

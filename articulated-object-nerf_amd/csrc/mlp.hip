@@ -252,8 +252,10 @@ using namespace aon;
 using namespace aon::mlp;
 
 extern "C" size_t aon_mlp_packed_bytes(int precision) {
-  // both precisions use the same block grid: fp32 tiles, or hi+lo fp16 pairs of equal size
-  if (precision == AON_PREC_FP32 || precision == AON_PREC_F16X3) return kPackedBytesF32;
+  // every precision uses the same block grid: fp32 tiles, or hi+lo fp16 pairs of equal size
+  // (bf16: bf16 weights in the hi blocks)
+  if (precision == AON_PREC_FP32 || precision == AON_PREC_F16X3 || precision == AON_PREC_BF16)
+    return kPackedBytesF32;
   return 0;
 }
 
@@ -279,7 +281,9 @@ static int f16x3_ncol() {
 extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* packed,
                             aon_stream_t stream) {
   AON_REQUIRE(prm && packed, "null pointer");
-  AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3, "unsupported precision");
+  AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3 ||
+                  precision == AON_PREC_BF16,
+              "unsupported precision");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
   PackArgs a;
   for (int i = 0; i < 8; ++i) {
@@ -294,7 +298,8 @@ extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* pack
     AON_REQUIRE(a.w[i] && a.b[i], "null layer parameter");
     a.layers[i] = precision == AON_PREC_FP32 ? kLayers[i] : kLayersH[i];
   }
-  if (precision == AON_PREC_F16X3) return pack_f16x3(a, packed, (hipStream_t)stream);
+  if (precision != AON_PREC_FP32)
+    return pack_f16x3(a, packed, (hipStream_t)stream, precision == AON_PREC_BF16);
   // the fp32 kernels never set the range-status word: cleared once here
   const hipError_t e = hipMemsetAsync(static_cast<char*>(packed) + kPackedBytesF32 - kStatusBytes, 0,
                                       kStatusBytes, (hipStream_t)stream);
@@ -309,7 +314,8 @@ static int mlp_launch(int mode, const void* packed, int precision, const float* 
                       const float* a1, const float* a2, const float* a3, int64_t B, int S,
                       int act, float* raw, aon_stream_t stream) {
   AON_REQUIRE(packed && raw && a0 && a1, "null pointer");
-  AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3, "unsupported precision");
+  AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3,
+              "unsupported precision (AON_PREC_BF16 is the training forward's: aon_mlp_fwd_train_bf16)");
   AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
   AON_REQUIRE(act >= AON_ACT_NONE && act <= AON_ACT_ARTIC, "bad activation");
   AON_REQUIRE(aligned16(packed) && aligned16(raw), "packed / raw must be 16-byte aligned");
@@ -359,5 +365,25 @@ extern "C" int aon_mlp_fwd_train(const void* packed, const float* rays_o, const 
   AON_REQUIRE((N + 127) / 128 < (1ll << 31), "too many rows");
   const TrainStore ts{h, bot, hv, noise, reinterpret_cast<uint2*>(masks)};
   return launch_f16x3(2, 1, packed, rays_o, rays_d, viewdirs, t, B, S, AON_ACT_NONE, raw,
+                      (hipStream_t)stream, &ts);
+}
+
+extern "C" int aon_mlp_fwd_train_bf16(const void* packed, const float* rays_o,
+                                      const float* rays_d, const float* viewdirs, const float* t,
+                                      int64_t B, int S, const float* noise, uint16_t* h,
+                                      uint16_t* bot, uint16_t* hv, float* raw, uint32_t* masks,
+                                      aon_stream_t stream) {
+  AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && h && bot && hv && raw && masks,
+              "null pointer");
+  AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
+  AON_REQUIRE(aligned16(packed) && aligned16(raw) && aligned16(masks) && aligned16(h) &&
+                  aligned16(bot) && aligned16(hv),
+              "packed / output buffers must be 16-byte aligned");
+  const int64_t N = B * S;
+  if (N == 0) return 0;
+  AON_REQUIRE((N + 127) / 128 < (1ll << 31), "too many rows");
+  const TrainStore ts{reinterpret_cast<float*>(h), reinterpret_cast<float*>(bot),
+                      reinterpret_cast<float*>(hv), noise, reinterpret_cast<uint2*>(masks)};
+  return launch_f16x3(3, 1, packed, rays_o, rays_d, viewdirs, t, B, S, AON_ACT_NONE, raw,
                       (hipStream_t)stream, &ts);
 }

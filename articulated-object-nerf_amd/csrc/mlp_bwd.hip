@@ -59,9 +59,16 @@ int absmax(const float* x, int64_t n, uint32_t* out, hipStream_t stream) {
   return launch_status("absmax");
 }
 
+// BF: the bf16 training mode -- one bf16 MFMA per product, dZ stored as bf16 (BwdArgs' output
+// pointers then address bf16 arrays of the same shapes)
+template <bool BF = false>
 __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, BwdArgs a) {
   constexpr int NCOL = 1;
+  using T = typename std::conditional<BF, __bf16, float>::type;
+  T* const dzv = reinterpret_cast<T*>(a.dzv);
+  T* const dzb = reinterpret_cast<T*>(a.dzb);
+  T* const dz = reinterpret_cast<T*>(a.dz);
   using G = GeomH<NCOL>;
   using Net = NetBwdH;
   constexpr int kStash = G::kWaves * 64 * 2;  // f4: d raw_sigma fragment, hi & lo
@@ -100,13 +107,13 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
       dv[e] = (g == 0 && e < 3) ? d[e < 3 ? e : 0] * s : 0.f;
       sv[e] = (g == 0 && e == 0) ? d[3] * s : 0.f;
     }
-    split8(dv, drgb.hi[0][0], drgb.lo[0][0], drgb.ovf);
-    split8(sv, dsig.hi[0][0], dsig.lo[0][0], dsig.ovf);
+    split8<BF>(dv, drgb.hi[0][0], drgb.lo[0][0], drgb.ovf);
+    split8<BF>(sv, dsig.hi[0][0], dsig.lo[0][0], dsig.ovf);
     stash[0] = __builtin_bit_cast(f4, dsig.hi[0][0]);
     stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
   }
 
-  FragPipe<WeightPipe<Net, G::kThreads>> fp(p);
+  FragPipe<WeightPipe<Net, G::kThreads>, AON_PREFETCH, 0, BF> fp(p);
   fp.start();
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 
@@ -115,11 +122,11 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   Frag<1, NCOL> none;
   // d hv = W_rgb^T d rgb, * ReLU'(hv) -> dZ of views_linear.0
   layer_h<Net, B_RGB, false>(fp, none, drgb, x, bias_l, g,
-                             mask_bits(a.masks + 8 * ms, a.dzv, 128, rows, N, g, inv));
+                             mask_bits(a.masks + 8 * ms, dzv, 128, rows, N, g, inv));
   // d bottleneck = W_view[:, :256]^T dZ_view (linear layer: no mask)
   {
-    RowStore<NCOL> st;
-    st.rowp[0] = rows[0] < N ? a.dzb + rows[0] * 256 + 4 * g : nullptr;
+    RowStore<NCOL, T> st;
+    st.rowp[0] = rows[0] < N ? dzb + rows[0] * 256 + 4 * g : nullptr;
     st.s = inv;
     layer_h<Net, B_VIEW, false>(fp, x, none, y, bias_l, g, st);
   }
@@ -127,24 +134,24 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
   // d h7 = W_bot^T dZ_bot + W_den^T d sigma, * ReLU'(h7) -> dZ_7
   layer_h<Net, B_BOTDEN, false>(fp, y, dsig, x, bias_l, g,
-                                mask_bits(a.masks + 7 * ms, a.dz + 7 * hs, 256, rows, N, g, inv));
+                                mask_bits(a.masks + 7 * ms, dz + 7 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_7, false>(fp, x, none, y, bias_l, g,
-                           mask_bits(a.masks + 6 * ms, a.dz + 6 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 6 * ms, dz + 6 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_6, false>(fp, y, none, x, bias_l, g,
-                           mask_bits(a.masks + 5 * ms, a.dz + 5 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 5 * ms, dz + 5 * hs, 256, rows, N, g, inv));
   // the skip layer's enc columns carry no gradient (positions are not differentiated)
   layer_h<Net, B_5, false>(fp, x, none, y, bias_l, g,
-                           mask_bits(a.masks + 4 * ms, a.dz + 4 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 4 * ms, dz + 4 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_4, false>(fp, y, none, x, bias_l, g,
-                           mask_bits(a.masks + 3 * ms, a.dz + 3 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 3 * ms, dz + 3 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_3, false>(fp, x, none, y, bias_l, g,
-                           mask_bits(a.masks + 2 * ms, a.dz + 2 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 2 * ms, dz + 2 * hs, 256, rows, N, g, inv));
   layer_h<Net, B_2, false>(fp, y, none, x, bias_l, g,
-                           mask_bits(a.masks + 1 * ms, a.dz + 1 * hs, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 1 * ms, dz + 1 * hs, 256, rows, N, g, inv));
   // (the last layer's outputs are only stored: its fp16 split is unused, so not range-checked)
   const uint64_t used_ovf = x.ovf | y.ovf | drgb.ovf | dsig.ovf;
   layer_h<Net, B_1, false>(fp, x, none, y, bias_l, g,
-                           mask_bits(a.masks + 0 * ms, a.dz, 256, rows, N, g, inv));
+                           mask_bits(a.masks + 0 * ms, dz, 256, rows, N, g, inv));
   range_report(bias_g + Net::kBiasFloats, used_ovf);
 }
 
@@ -156,7 +163,7 @@ using namespace aon::mlp;
 
 extern "C" size_t aon_mlp_bwd_packed_bytes(void) { return NetBwdH::kPackedBytes; }
 
-extern "C" int aon_mlp_bwd_pack(const aon_mlp_params* prm, void* packed, aon_stream_t stream) {
+static int bwd_pack(const aon_mlp_params* prm, void* packed, aon_stream_t stream, bool bf16) {
   AON_REQUIRE(prm && packed, "null pointer");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
   PackArgsH a{};
@@ -179,12 +186,21 @@ extern "C" int aon_mlp_bwd_pack(const aon_mlp_params* prm, void* packed, aon_str
   a.n_layers = kNumLayersBwd;
   a.stream_blocks = NetBwdH::kStreamBlocks;
   a.bias_floats = NetBwdH::kBiasFloats;
+  a.bf16 = bf16 ? 1 : 0;
   return pack_h(a, packed, (hipStream_t)stream);
 }
 
-extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const uint32_t* masks,
-                           int64_t N, float* dzv, float* dzb, float* dz, void* work,
-                           aon_stream_t stream) {
+extern "C" int aon_mlp_bwd_pack(const aon_mlp_params* prm, void* packed, aon_stream_t stream) {
+  return bwd_pack(prm, packed, stream, false);
+}
+
+extern "C" int aon_mlp_bwd_pack_bf16(const aon_mlp_params* prm, void* packed,
+                                     aon_stream_t stream) {
+  return bwd_pack(prm, packed, stream, true);
+}
+
+static int bwd_launch(const void* packed, const float* draw, const uint32_t* masks, int64_t N,
+                      void* dzv, void* dzb, void* dz, void* work, aon_stream_t stream, bool bf16) {
   AON_REQUIRE(packed && draw && masks && dzv && dzb && dz && work, "null pointer");
   AON_REQUIRE(N >= 0, "bad shape");
   AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(masks) && aligned16(dzv) &&
@@ -198,12 +214,28 @@ extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const uint32_t
   uint32_t* amax = static_cast<uint32_t*>(work);
   const int rc = absmax(draw, 4 * N, amax, st);
   if (rc) return rc;
-  BwdArgs args{draw, reinterpret_cast<const uint2*>(masks), dzv, dzb, dz, amax, N};
+  BwdArgs args{draw, reinterpret_cast<const uint2*>(masks), static_cast<float*>(dzv),
+               static_cast<float*>(dzb), static_cast<float*>(dz), amax, N};
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetBwdH::kStreamBytes);
-  hipLaunchKernelGGL(k_mlp_bwd_f16x3, (unsigned)grid, G::kThreads, 0, st, ws, bias, args);
-  return launch_status(__func__);
+  if (bf16)
+    hipLaunchKernelGGL(k_mlp_bwd_f16x3<true>, (unsigned)grid, G::kThreads, 0, st, ws, bias, args);
+  else
+    hipLaunchKernelGGL(k_mlp_bwd_f16x3<false>, (unsigned)grid, G::kThreads, 0, st, ws, bias, args);
+  return launch_status(bf16 ? "aon_mlp_bwd_bf16" : "aon_mlp_bwd");
+}
+
+extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const uint32_t* masks,
+                           int64_t N, float* dzv, float* dzb, float* dz, void* work,
+                           aon_stream_t stream) {
+  return bwd_launch(packed, draw, masks, N, dzv, dzb, dz, work, stream, false);
+}
+
+extern "C" int aon_mlp_bwd_bf16(const void* packed, const float* draw, const uint32_t* masks,
+                                int64_t N, uint16_t* dzv, uint16_t* dzb, uint16_t* dz, void* work,
+                                aon_stream_t stream) {
+  return bwd_launch(packed, draw, masks, N, dzv, dzb, dz, work, stream, true);
 }
 
 // ReLU' bits of an activation tensor h (N x width, width = 32 x pairs <= 256) in the layout

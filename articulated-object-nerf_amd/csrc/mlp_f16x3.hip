@@ -29,7 +29,7 @@ namespace mlp {
 
 // The layer sequence of k_mlp_fwd_f16x3 (model.py:95-120), instantiated per FragPipe type: the
 // two halves of the workgroup differ in the k-step of their epilogues (FragPipe EOFF).
-template <int NCOL, bool STORE, typename FP>
+template <int NCOL, bool STORE, typename T, typename FP>
 __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<1, NCOL>& venc,
                                                Frag<8, NCOL>& x, Frag<8, NCOL>& y, f4* stash,
                                                float* bias_s, int g, int wave,
@@ -42,14 +42,18 @@ __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);  // this lane group's rows of the bias table
 
   Frag<1, NCOL> none;
-  using SP = StorePick<STORE, NCOL>;
+  using SP = StorePick<STORE, NCOL, T>;
+  // the kept activations (training forward): fp32, or bf16 in the bf16 training mode
+  T* const th = reinterpret_cast<T*>(ts.h);
+  T* const tbot = reinterpret_cast<T*>(ts.bot);
+  T* const thv = reinterpret_cast<T*>(ts.hv);
   const int64_t hs = N * 256;  // one pts_linears output in ts.h
   const int64_t ms = N * 4;    // one layer's ReLU' bits in ts.masks
-  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g, ts.masks));
-  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 1 * hs, 256, rows, N, g, ts.masks + 1 * ms));
-  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g, ts.masks + 2 * ms));
-  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g, ts.masks + 3 * ms));
-  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g, ts.masks + 4 * ms));
+  layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g, SP::make(th, 256, rows, N, g, ts.masks));
+  layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g, SP::make(th + 1 * hs, 256, rows, N, g, ts.masks + 1 * ms));
+  layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g, SP::make(th + 2 * hs, 256, rows, N, g, ts.masks + 2 * ms));
+  layer_h<NetVanillaH, L3, true>(fp, x, none, y, bias_l, g, SP::make(th + 3 * hs, 256, rows, N, g, ts.masks + 3 * ms));
+  layer_h<NetVanillaH, L4, true>(fp, y, none, x, bias_l, g, SP::make(th + 4 * hs, 256, rows, N, g, ts.masks + 4 * ms));
 #pragma unroll
   for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c)
 #pragma unroll
@@ -58,20 +62,20 @@ __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<
       enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
     }
   // skip: cat[h, enc] (model.py:102-103)
-  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g, ts.masks + 5 * ms));
-  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g, ts.masks + 6 * ms));
-  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g, ts.masks + 7 * ms));
+  layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g, SP::make(th + 5 * hs, 256, rows, N, g, ts.masks + 5 * ms));
+  layer_h<NetVanillaH, L6, true>(fp, y, none, x, bias_l, g, SP::make(th + 6 * hs, 256, rows, N, g, ts.masks + 6 * ms));
+  layer_h<NetVanillaH, L7, true>(fp, x, none, y, bias_l, g, SP::make(th + 7 * hs, 256, rows, N, g, ts.masks + 7 * ms));
   f4 dens[NCOL], rgb[NCOL];
   head_h<NetVanillaH, LDEN>(fp, y, dens, bias_l, g);             // model.py:105-107
   // bottleneck, no activation (model.py:109)
-  layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g, SP::make(ts.bot, 256, rows, N, g));
+  layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g, SP::make(tbot, 256, rows, N, g));
 #pragma unroll
   for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c) {
     venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
     venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
   }
   // cat[bottleneck, enc_dir] + ReLU (:110-116)
-  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g, ts.masks + 8 * ms));
+  layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g, SP::make(thv, 128, rows, N, g, ts.masks + 8 * ms));
   head_h<NetVanillaH, LRGB>(fp, y, rgb, bias_l, g);              // model.py:118
 
   if (g == 0) {
@@ -89,8 +93,10 @@ __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<
   }
 }
 
-// MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: encoded x (N, 63), condition (B, 27)
-template <int MODE, int NCOL, bool STORE = false>
+// MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: encoded x (N, 63), condition (B, 27).
+// BF: bf16 numerics (one bf16 MFMA per k-step; the kept activations stored as bf16) -- the
+// bf16 training mode; the stream then carries bf16 weights in its hi blocks (k_pack_h bf16).
+template <int MODE, int NCOL, bool STORE = false, bool BF = false>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_fwd_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
@@ -161,11 +167,11 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     for (int k = 0; k < 2; ++k) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) ev[k][e] *= (AON_F16X3_V2 ? kActS : kActScale);
-      split8(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
+      split8<BF>(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) vv[e] *= (AON_F16X3_V2 ? kActS : kActScale);
-    split8(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
+    split8<BF>(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
   }
 
   // park the encodings in LDS until the skip / view layers need them (frees 24 VGPRs for the
@@ -183,14 +189,15 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 
   Frag<8, NCOL> x, y;
   using WP = WeightPipe<NetVanillaH, G::kThreads>;
+  using T = typename std::conditional<BF, __bf16, float>::type;
   // wave-uniform branch (readfirstlane): the running range masks stay in SGPRs across it
   // (not the training forward: with its row stores the second copy spills)
   if (AON_STAGGER && NCOL == 1 && !STORE && __builtin_amdgcn_readfirstlane(wave) >= G::kWaves / 2) {
-    FragPipe<WP, AON_PREFETCH, 4> fp(p);
-    vanilla_layers<NCOL, STORE>(fp, enc, venc, x, y, stash, bias_s, g, wave, rows, N, act, raw, ts);
+    FragPipe<WP, AON_PREFETCH, 4, BF> fp(p);
+    vanilla_layers<NCOL, STORE, T>(fp, enc, venc, x, y, stash, bias_s, g, wave, rows, N, act, raw, ts);
   } else {
-    FragPipe<WP, AON_PREFETCH, 0> fp(p);
-    vanilla_layers<NCOL, STORE>(fp, enc, venc, x, y, stash, bias_s, g, wave, rows, N, act, raw, ts);
+    FragPipe<WP, AON_PREFETCH, 0, BF> fp(p);
+    vanilla_layers<NCOL, STORE, T>(fp, enc, venc, x, y, stash, bias_s, g, wave, rows, N, act, raw, ts);
   }
   range_report(bias_g + kBiasFloats, x.ovf | y.ovf | enc.ovf | venc.ovf);
 }
@@ -246,6 +253,10 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
       }
 #if AON_F16X3_V2
       w *= kWS;  // exact (power of two)
+      if (a.bf16) {  // bf16 mode: the hi block holds bf16(w), the lo block is never read
+        out[e] = lo_part ? static_cast<_Float16>(0.0f) : bf_bits(w);
+        continue;
+      }
       const _Float16 h = static_cast<_Float16>(w);
       out[e] = lo_part ? static_cast<_Float16>(w - static_cast<float>(h)) : h;
       // range guard (mlp_f16x3_core.hpp): a weight whose scaled hi part is not a finite fp16
@@ -286,8 +297,9 @@ int pack_h(PackArgsH a, void* packed, hipStream_t stream) {
   return launch_status("aon_mlp_pack");
 }
 
-int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream) {
+int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream, bool bf16) {
   PackArgsH h{};
+  h.bf16 = bf16 ? 1 : 0;
   for (int i = 0; i < kNumLayers; ++i) {
     h.w[i] = a.w[i];
     h.b[i] = a.b[i];
@@ -310,10 +322,14 @@ int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const 
   hipLaunchKernelGGL((k_mlp_fwd_f16x3<M, C>),                                                    \
                      static_cast<int>((N + GeomH<C>::kRowsPerBlock - 1) / GeomH<C>::kRowsPerBlock), \
                      GeomH<C>::kThreads, 0, stream, ws, bias, a0, a1, a2, a3, B, S, act, raw)
-  if (mode == 2) {  // training forward: MODE 0 inputs + activation stores
-    hipLaunchKernelGGL((k_mlp_fwd_f16x3<0, 1, true>),
-                       static_cast<int>((N + GeomH<1>::kRowsPerBlock - 1) / GeomH<1>::kRowsPerBlock),
-                       GeomH<1>::kThreads, 0, stream, ws, bias, a0, a1, a2, a3, B, S, act, raw, *ts);
+  if (mode == 2 || mode == 3) {  // training forward: MODE 0 inputs + activation stores
+    const int grid = static_cast<int>((N + GeomH<1>::kRowsPerBlock - 1) / GeomH<1>::kRowsPerBlock);
+    if (mode == 3)  // bf16 training mode
+      hipLaunchKernelGGL((k_mlp_fwd_f16x3<0, 1, true, true>), grid, GeomH<1>::kThreads, 0, stream,
+                         ws, bias, a0, a1, a2, a3, B, S, act, raw, *ts);
+    else
+      hipLaunchKernelGGL((k_mlp_fwd_f16x3<0, 1, true>), grid, GeomH<1>::kThreads, 0, stream, ws,
+                         bias, a0, a1, a2, a3, B, S, act, raw, *ts);
     return launch_status("aon_mlp_fwd_train");
   }
   if (mode == 0 && ncol == 1) AON_LAUNCH_H(0, 1);

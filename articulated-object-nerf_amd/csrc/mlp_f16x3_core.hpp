@@ -4,6 +4,8 @@
 // Numerics and tiling are described at the top of mlp_f16x3.hip.
 #pragma once
 
+#include <type_traits>
+
 #include "aon_common.hpp"
 #include "mlp_layout.hpp"
 #include "mlp_pipe.hpp"
@@ -22,6 +24,19 @@ __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
 }
 
 __device__ __forceinline__ h8 as_h8(f4 v) { return __builtin_bit_cast(h8, v); }
+
+// ---- bf16 numerics (the C5 training step's bf16 mode): one v_mfma_f32_16x16x32_bf16 per
+// k-step and tile instead of three fp16 products; operands are plain bf16 (fp32's exponent
+// range: no scaling limits, no range guard), carried in the same h8 registers as raw bits.
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f4 mfma_bf(h8 a, h8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
+                                                 __builtin_bit_cast(bf8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ _Float16 bf_bits(float v) {
+  return __builtin_bit_cast(_Float16, static_cast<__bf16>(v));  // round to nearest even
+}
 
 // fp32 value (already at activation scale) -> (hi, lo) fp16 pair: V2 lo = x - hi (exact in
 // fp32, normal in fp16 for |x| >= 2^-3 at scale); V1 lo = (x - hi) * 2^11
@@ -67,8 +82,15 @@ __device__ __forceinline__ void range_report(const float* bias_end, uint64_t ovf
   if (ovf && (threadIdx.x & 63) == 0) *reinterpret_cast<uint32_t*>(const_cast<float*>(bias_end)) = 1u;
 }
 
-// 8 fp32 values (already at activation scale) -> (hi, lo) fp16 fragments; ovf |= out of range
+// 8 fp32 values (already at activation scale) -> (hi, lo) fp16 fragments; ovf |= out of range.
+// BF: bf16 values in hi, no lo, no range test.
+template <bool BF = false>
 __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, uint64_t& ovf) {
+  if (BF) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hi[j] = bf_bits(v[j]);
+    return;
+  }
   float m = 0.0f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -96,9 +118,11 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, uint
 // w and w + 4 of an 8-wave workgroup share a SIMD; run in lockstep they reach the epilogue VALU
 // and the epilogue-free MFMA steps together, so neither wave's VALU rides beside the other's
 // MFMAs.  Waves 4-7 take EOFF = 4 (a stagger: MI355X_MICROARCH.md "Two waves per SIMD" item 9).
-template <typename P, int D = AON_PREFETCH, int EOFF = 0>
+// BF: bf16 numerics -- the stream's lo blocks are never read (and carry zeros).
+template <typename P, int D = AON_PREFETCH, int EOFF = 0, bool BF = false>
 struct FragPipe {
   static constexpr int kEpiOff = EOFF;
+  static constexpr bool kBF16 = BF;
   P& p;
   f4 nh[D], nl[D];  // fragments of the next D steps
   __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
@@ -112,7 +136,7 @@ struct FragPipe {
 #endif
     if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
     h = p.block(blk);
-    l = p.block(blk + 1);
+    if (!BF) l = p.block(blk + 1);
   }
   __device__ __forceinline__ void start() {
 #pragma unroll
@@ -153,15 +177,22 @@ struct NoStore {
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
 };
 
-template <int NCOL>
+// two consecutive outputs at true scale: one 8-B fp32 store, or (bf16 mode) one 4-B bf16 store
+__device__ __forceinline__ void store2(float* p, float v0, float v1) {
+  *reinterpret_cast<float2*>(p) = float2{v0, v1};
+}
+__device__ __forceinline__ void store2(__bf16* p, float v0, float v1) {
+  *reinterpret_cast<bf2*>(p) = bf2{static_cast<__bf16>(v0), static_cast<__bf16>(v1)};
+}
+
+template <int NCOL, typename T = float>
 struct RowStore {
-  float* rowp[NCOL];  // y + row * ld + 4 g of each column's sample, nullptr when row >= N
-  float s;            // to true scale (a power of two: exact)
+  T* rowp[NCOL];  // y + row * ld + 4 g of each column's sample, nullptr when row >= N
+  float s;        // to true scale (a power of two: exact)
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
-    if (rowp[c])
-      *reinterpret_cast<float2*>(rowp[c] + 16 * (2 * pr + uu) + r0) = float2{v0 * s, v1 * s};
+    if (rowp[c]) store2(rowp[c] + 16 * (2 * pr + uu) + r0, v0 * s, v1 * s);
   }
 };
 
@@ -170,13 +201,13 @@ struct RowStore {
 // layout [layer][N][4] of uint2), so the backward chains read 1/32 of the bytes of the fp32
 // activations for their masks.  Written a byte per output pair (the pair's 2 tiles x 4 rows),
 // so nothing is carried across pairs.
-template <int NCOL>
-struct RowStoreBits : RowStore<NCOL> {
+template <int NCOL, typename T = float>
+struct RowStoreBits : RowStore<NCOL, T> {
   uint8_t* mrow[NCOL];  // bytes of word (row, g), nullptr when row >= N
   bool narrow;          // 4-pair (128-wide) layer: bytes 4..7 of the word are written as 0
   mutable uint32_t b[NCOL];  // the current pair's 8 bits (byte pr of the word)
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
-    RowStore<NCOL>::put(pr, uu, r0, c, v0, v1);
+    RowStore<NCOL, T>::put(pr, uu, r0, c, v0, v1);
     const uint32_t m = (v0 > 0.0f ? 1u : 0u) | (v1 > 0.0f ? 2u : 0u);  // v: post-ReLU, s > 0
     const int bit = 4 * uu + r0;  // within the pair's byte (compile-time after unrolling)
     b[c] = bit == 0 ? m : (b[c] | (m << bit));
@@ -189,10 +220,10 @@ struct RowStoreBits : RowStore<NCOL> {
 
 // Backward-chain epilogue with ReLU' from those bits (no reads of the fp32
 // activations): the layer's word is loaded when its first pair starts.
-template <int NCOL>
+template <int NCOL, typename T = float>
 struct MaskBits {
   const uint2* mrow[NCOL];  // masks + row * 4 + g, nullptr when row >= N
-  float* rowp[NCOL];        // out + row * ld + 4 g, nullptr when row >= N
+  T* rowp[NCOL];            // out + row * ld + 4 g, nullptr when row >= N
   float s;
   mutable uint2 m[NCOL];
   __device__ __forceinline__ void begin_pair(int pr) const {
@@ -207,16 +238,15 @@ struct MaskBits {
     return (w >> (bit & 31)) & 1u ? v : 0.0f;
   }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
-    if (rowp[c])
-      *reinterpret_cast<float2*>(rowp[c] + 16 * (2 * pr + uu) + r0) = float2{v0 * s, v1 * s};
+    if (rowp[c]) store2(rowp[c] + 16 * (2 * pr + uu) + r0, v0 * s, v1 * s);
   }
 };
 
-template <int NCOL>
-__device__ __forceinline__ MaskBits<NCOL> mask_bits(const uint2* mbase, float* obase, int ld,
-                                                    const int64_t (&rows)[NCOL], int64_t N, int g,
-                                                    float s) {
-  MaskBits<NCOL> mb;
+template <int NCOL, typename T = float>
+__device__ __forceinline__ MaskBits<NCOL, T> mask_bits(const uint2* mbase, T* obase, int ld,
+                                                       const int64_t (&rows)[NCOL], int64_t N,
+                                                       int g, float s) {
+  MaskBits<NCOL, T> mb;
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
     const bool ok = rows[c] < N;
@@ -227,35 +257,35 @@ __device__ __forceinline__ MaskBits<NCOL> mask_bits(const uint2* mbase, float* o
   return mb;
 }
 
-// NoStore (STORE = false) or a RowStore at y + row * ld (true scale) for the training forward
-template <bool STORE, int NCOL>
+// NoStore (STORE = false) or a RowStore at y + row * ld (true scale) for the training forward;
+// T = the stored element type (fp32, or bf16 in the bf16 training mode)
+template <bool STORE, int NCOL, typename T = float>
 struct StorePick {
-  __device__ __forceinline__ static NoStore make(float*, int, const int64_t (&)[NCOL], int64_t,
-                                                 int) {
+  __device__ __forceinline__ static NoStore make(T*, int, const int64_t (&)[NCOL], int64_t, int) {
     return {};
   }
-  __device__ __forceinline__ static NoStore make(float*, int, const int64_t (&)[NCOL], int64_t,
-                                                 int, uint2*) {
+  __device__ __forceinline__ static NoStore make(T*, int, const int64_t (&)[NCOL], int64_t, int,
+                                                 uint2*) {
     return {};
   }
 };
-template <int NCOL>
-struct StorePick<true, NCOL> {
-  __device__ __forceinline__ static RowStore<NCOL> make(float* base, int ld,
-                                                        const int64_t (&rows)[NCOL], int64_t N,
-                                                        int g) {
-    RowStore<NCOL> r;
+template <int NCOL, typename T>
+struct StorePick<true, NCOL, T> {
+  __device__ __forceinline__ static RowStore<NCOL, T> make(T* base, int ld,
+                                                           const int64_t (&rows)[NCOL], int64_t N,
+                                                           int g) {
+    RowStore<NCOL, T> r;
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + rows[c] * ld + 4 * g : nullptr;
     r.s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;
     return r;
   }
   // a ReLU layer: also its ReLU' bits at mbase ([N][4] uint2); ld / 32 output pairs
-  __device__ __forceinline__ static RowStoreBits<NCOL> make(float* base, int ld,
-                                                            const int64_t (&rows)[NCOL], int64_t N,
-                                                            int g, uint2* mbase) {
-    RowStoreBits<NCOL> r;
-    static_cast<RowStore<NCOL>&>(r) = make(base, ld, rows, N, g);
+  __device__ __forceinline__ static RowStoreBits<NCOL, T> make(T* base, int ld,
+                                                               const int64_t (&rows)[NCOL],
+                                                               int64_t N, int g, uint2* mbase) {
+    RowStoreBits<NCOL, T> r;
+    static_cast<RowStore<NCOL, T>&>(r) = make(base, ld, rows, N, g);
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
       r.mrow[c] = rows[c] < N ? reinterpret_cast<uint8_t*>(mbase + rows[c] * 4 + g) : nullptr;
@@ -272,7 +302,7 @@ struct StorePick<true, NCOL> {
 
 // epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
 // part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
-template <bool RELU, int NCOL, int NO, typename Store = NoStore>
+template <bool RELU, bool BF, int NCOL, int NO, typename Store = NoStore>
 __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
                                          const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr,
                                          const Store& st = Store{}) {
@@ -292,6 +322,18 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
 #endif
       if (RELU) v = fmaxf(v, 0.0f);
       vv[e] = st.post(pr, uu, r0 + e, c, v);
+    }
+    if (BF) {  // bf16 mode: the pair as one v_cvt_pk_bf16_f32, no lo part, no range limit
+      st.put(pr, uu, r0, c, vv[0], vv[1]);
+      // the packed pair goes in as ONE dword of the fragment: ROCm 7.2's clang mis-lowers
+      // bit_cast<_Float16>(pair[1]) of a <2 x bfloat> (it yields element 0;
+      // tools/diag/bf16_pack_probe.hip), so no bf16 element is extracted
+      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+      const bf2 hb = {static_cast<__bf16>(vv[0]), static_cast<__bf16>(vv[1])};
+      u4 w = __builtin_bit_cast(u4, out.hi[pr][c]);
+      w[q] = __builtin_bit_cast(uint32_t, hb);
+      out.hi[pr][c] = __builtin_bit_cast(h8, w);
+      continue;
     }
     or_ballot(out.ovf, fmaxf(fabsf(vv[0]), fabsf(vv[1])) > kF16Max);
     st.put(pr, uu, r0, c, vv[0], vv[1]);
@@ -330,6 +372,7 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
   constexpr int K = d.ka + d.kb;
   constexpr int NP = d.u / 2;
   constexpr int EO = P::kEpiOff;  // epilogue parts of pair p-1 at k-steps EO..EO+3 of pair p
+  constexpr bool BF = P::kBF16;   // bf16 numerics: one MFMA per k-step and tile
   constexpr int QIN = K - EO < 0 ? 0 : (K - EO > 4 ? 4 : K - EO);  // parts done inside the loop
   static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
   f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
@@ -364,6 +407,12 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
           const h8 xh = k < d.ka ? a.hi[ia][c] : b.hi[ib][c];
           const h8 xl = k < d.ka ? a.lo[ia][c] : b.lo[ib][c];
 #if AON_F16X3_V2
+          if (BF) {
+            hh[uu][c] = mfma_bf(wh, xh, hh[uu][c]);
+            (void)xl;
+            (void)wl;
+            continue;
+          }
           hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
           hh[uu][c] = mfma16(wh, xl, hh[uu][c]);
           hh[uu][c] = mfma16(wl, xh, hh[uu][c]);
@@ -374,11 +423,11 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
 #endif
         }
       }
-      if (pr > 0 && k >= EO && k - EO < 4) epi_part<RELU>(k - EO, phh, pxx, pbias, out, pr - 1, st);
+      if (pr > 0 && k >= EO && k - EO < 4) epi_part<RELU, BF>(k - EO, phh, pxx, pbias, out, pr - 1, st);
     }
     if (pr > 0) {
 #pragma unroll
-      for (int q = QIN; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, pr - 1, st);
+      for (int q = QIN; q < 4; ++q) epi_part<RELU, BF>(q, phh, pxx, pbias, out, pr - 1, st);
     }
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
@@ -391,7 +440,7 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) epi_part<RELU>(q, phh, pxx, pbias, out, NP - 1, st);
+  for (int q = 0; q < 4; ++q) epi_part<RELU, BF>(q, phh, pxx, pbias, out, NP - 1, st);
 }
 
 // single-tile head (density / rgb): returns the 16-row tile at activation scale
@@ -399,6 +448,7 @@ template <typename Net, int LAYER, typename P, int NCOL, int NA>
 __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[NCOL],
                                        lds_float* bias_l, int g) {
   constexpr LayerDesc d = Net::layer(LAYER);
+  constexpr bool BF = P::kBF16;
   static_assert(d.u == 1 && d.kb == 0 && d.ka <= NA, "head shape");
   f4 hh[NCOL], xx[NCOL];
   const f4 bias = *reinterpret_cast<lds_f4*>(bias_l + d.bias0);
@@ -419,6 +469,10 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
 #if AON_F16X3_V2
+      if (BF) {
+        hh[c] = mfma_bf(wh, a.hi[k][c], hh[c]);
+        continue;
+      }
       hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
       hh[c] = mfma16(wh, a.lo[k][c], hh[c]);
       hh[c] = mfma16(wl, a.hi[k][c], hh[c]);

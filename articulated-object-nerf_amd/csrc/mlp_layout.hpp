@@ -253,6 +253,7 @@ struct PackArgsH {
   int tr[kMaxLayersH];
   LayerDesc layers[kMaxLayersH];
   int n_layers, stream_blocks, bias_floats;
+  int bf16;  // 1: bf16 weights in the hi blocks, zero lo blocks (the bf16 training mode)
 };
 
 // Training forward of the fused kernel (launch_f16x3 mode 2): every hidden activation goes to
@@ -280,7 +281,7 @@ struct TrainStoreArt {
 };
 
 // fp16x3 path (mlp_f16x3.hip)
-int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream);
+int pack_f16x3(const PackArgs& a, void* packed, hipStream_t stream, bool bf16 = false);
 int pack_h(PackArgsH a, void* packed, hipStream_t stream);
 // *out = bits of max |x| over n floats (memset + k_absmax, mlp_bwd.hip): the backward chains'
 // per-call gradient scale

@@ -7,7 +7,8 @@ Sub-records in the same JSON line (after the headline, same timing protocol: war
 synchronize on both sides, max over ranks):
   "articulated"     config C3 -- NeRF_AE_Art 320x240 frame render (N = 1 only)
   "train_step"      config C5 -- LitNeRF.training_step on 4096 rays per rank + Adam (+ the DDP
-                    gradient all-reduce over RCCL on N > 1: weak scaling)
+                    gradient all-reduce over RCCL on N > 1: weak scaling), f16x3 kernels
+  "train_step_bf16" the same step in C5's bf16 mode (train.PRECISION = "bf16")
   "train_step_art"  C5 on the articulated auto-decoder (LitNeRF_AutoDecoder.training_step)
 each with its own ms_per_step and roofline (MFMA fraction of the fine-level MLP kernels,
 HBM byte fractions of the training kernels counting the stored activations).
@@ -15,8 +16,8 @@ HBM byte fractions of the training kernels counting the stored activations).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-A step = generate the frame's rays, coarse sample, coarse MLP, composite, pdf resample, fine
-MLP, composite, gather.  value = 307,200 rays x steps / max-over-ranks wall time.  Rank 0 prints
+A step = generate the frame's rays, coarse sample, coarse MLP, the fused coarse composite +
+pdf resample (aon_composite_march), fine MLP, composite, gather.  value = 307,200 rays x steps / max-over-ranks wall time.  Rank 0 prints
 ONE JSON line.  Inputs: create_spheric_poses(4)[7] camera, fovy-35 focal, near 2 / far 6,
 random NeRF weights (aonerf.synthetic, PCG64 seed 0: the oracle's test weights bit for bit,
 tests/test_synthetic.py).  The CPU baseline is the torch restatement in oracle/ on a bounded
@@ -68,8 +69,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-chunks", type=int, default=2, help="3840-ray chunks in the CPU sample")
     ap.add_argument("--no-extra", action="store_true", help="headline C2 render only")
-    ap.add_argument("--train-precision", default="f16x3", choices=("f16x3",),
-                    help="MFMA numerics of the C5 training step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,6 +125,7 @@ def main():
         if world == 1:
             extra["articulated"] = bench_articulated(args)
         extra["train_step"] = bench_train(args, world, rank, local_rank)
+        extra["train_step_bf16"] = bench_train(args, world, rank, local_rank, precision="bf16")
         extra["train_step_art"] = bench_train(args, world, rank, local_rank, art=True)
     if rank != 0:
         if world > 1:
@@ -276,12 +276,19 @@ TRAIN_BYTES = {"fwd_train": 4 + 16 + 4 * 2432 + 288, "bwd_chain": 16 + 288 + 4 *
 # (no gradient into the encodings)); weight gradients 2 x 593,408
 TRAIN_FLOP = {"fwd_train": 2 * MAC_PER_SAMPLE, "bwd_chain": 2 * (MAC_PER_SAMPLE - 256 * 63 - 128 * 27),
               "dweight": 2 * MAC_PER_SAMPLE}
+# bf16 mode: the kept activations and gradients are 2 B (encodings, d raw and masks unchanged)
+TRAIN_BYTES_BF16 = {"fwd_train": 4 + 16 + 2 * 2432 + 288, "bwd_chain": 16 + 288 + 2 * 2432,
+                    "dweight": 2 * (2432 + 2432) + 4 * (63 + 27)}
+# dense MFMA peak in algorithmic FLOP/s per training precision: f16x3 issues 3 fp16 products
+# per fp32-class MAC, bf16 one bf16 product
+TRAIN_PEAK = {"f16x3": 2500.0 / 3, "bf16": 2500.0}
 
 
-def bench_train(args, world, rank, local_rank, art=False):
+def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
     """C5: one LitNeRF.training_step (or LitNeRF_AutoDecoder.training_step) on 4096 rays per rank
     drawn from 8 synthetic 640x480 views, randomized sampling, loss, HIP backward, gradient
-    all-reduce (RCCL, N > 1), fused Adam with the reference schedule."""
+    all-reduce (RCCL, N > 1), fused Adam with the reference schedule.  precision: the fused
+    kernels' numerics (train.PRECISION: "f16x3" fp32-class, or C5's "bf16")."""
     import types
 
     from aonerf import train
@@ -333,10 +340,13 @@ def bench_train(args, world, rank, local_rank, art=False):
         sync()
         opt.step(lr=train.learning_rate(i, 200000))
 
+    old_prec = train.PRECISION
+    train.PRECISION = precision
     try:
         el = timed(step, args.steps, args.warmup, world)
     finally:
         train.TIMERS = None
+        train.PRECISION = old_prec
     mac = 794_880 if art else MAC_PER_SAMPLE
     samples = nrays * (NC + 1 + NC + 1 + NF)
     ms = el / args.steps * 1e3
@@ -348,12 +358,14 @@ def bench_train(args, world, rank, local_rank, art=False):
                       "Adam (config C5)"),
            "value": nrays * world * args.steps / el, "unit": "rays/s", "n_gpus": world,
            "steps": args.steps, "ms_per_step": ms, "scaling": "weak",
-           "dtype": "f16x3 (fp16 hi/lo split MFMA, fp32 accumulate; fp32 activations)",
+           "dtype": ("bf16 (bf16 MFMA, fp32 accumulate; bf16 activations and gradients, fp32 "
+                     "compositing / loss / Adam master weights)" if precision == "bf16" else
+                     "f16x3 (fp16 hi/lo split MFMA, fp32 accumulate; fp32 activations)"),
            "config": {"workload": "C5 training step" + (" (articulated)" if art else ""),
                       "rays_per_rank": nrays, "parallelism": f"ddp{world}" if world > 1 else "single GPU"},
            "roofline": {"bound": "hbm+mfma", "kernel": "whole step (3 x forward FLOP)",
-                        "achieved": ach, "peak": PEAK_TFLOPS["f16x3"], "unit": "TFLOP/s",
-                        "frac": ach / PEAK_TFLOPS["f16x3"]}}
+                        "achieved": ach, "peak": TRAIN_PEAK[precision], "unit": "TFLOP/s",
+                        "frac": ach / TRAIN_PEAK[precision]}}
     if not art:
         kern = {}
         hbm_bytes = 0.0
@@ -361,14 +373,14 @@ def bench_train(args, world, rank, local_rank, art=False):
             t_ms, rows = ev_ms(timers, f"{name}{NC + 1 + NF}")
             if not t_ms:
                 continue
-            b = TRAIN_BYTES[name] * rows
+            b = (TRAIN_BYTES_BF16 if precision == "bf16" else TRAIN_BYTES)[name] * rows
             f = TRAIN_FLOP[name] * rows
             hbm_bytes += b
             kern[name] = {"level": "fine", "ms": t_ms, "rows": rows,
                           "algorithmic_bytes": b, "GB/s": b / (t_ms * 1e-3) / 1e9,
                           "hbm_frac": b / (t_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                           "TFLOP/s": f / (t_ms * 1e-3) / 1e12,
-                          "mfma_frac": f / (t_ms * 1e-3) / 1e12 / PEAK_TFLOPS["f16x3"]}
+                          "mfma_frac": f / (t_ms * 1e-3) / 1e12 / TRAIN_PEAK[precision]}
         rec["roofline"]["kernels"] = kern
         if kern:
             tot_ms = sum(k["ms"] for k in kern.values())

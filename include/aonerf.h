@@ -30,6 +30,9 @@ typedef void* aon_stream_t; /* hipStream_t */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
 #define AON_PREC_F16X3 1 /* fp16 hi/lo split, 3 products (hi*hi + hi*lo + lo*hi) per weight on
                             v_mfma_f32_16x16x32_f16, fp32 accumulate: ~22-bit operands */
+#define AON_PREC_BF16 2  /* bf16 operands, 1 product per weight (v_mfma_f32_16x16x32_bf16), fp32
+                         * accumulate: the training step's bf16 mode (BASELINE config C5) --
+                         * aon_mlp_fwd_train_bf16 / aon_mlp_bwd_bf16 / aon_gemm with bf16 operands */
 
 /* Output activation applied by the compositor (reference model.py:186-187,
  * model_autodecoder.py:321-323). */
@@ -181,6 +184,15 @@ int aon_mlp_fwd_train(const void* packed, const float* rays_o, const float* rays
                       float* h, float* bot, float* hv, float* raw, uint32_t* masks,
                       aon_stream_t stream);
 
+/* The same training forward in the bf16 mode: packed = an AON_PREC_BF16 stream; one bf16
+ * MFMA per weight product (fp32 accumulate, activations rounded to bf16 between layers) and
+ * the kept activations h / bot / hv stored as bf16 (raw bits, same shapes): half the bytes of
+ * the fp32 stores, and exactly the operands the next layer consumed. */
+int aon_mlp_fwd_train_bf16(const void* packed, const float* rays_o, const float* rays_d,
+                           const float* viewdirs, const float* t, int64_t B, int S,
+                           const float* noise, uint16_t* h, uint16_t* bot, uint16_t* hv,
+                           float* raw, uint32_t* masks, aon_stream_t stream);
+
 /* ReLU' bits of an activation tensor h (N x width, width a multiple of 32 up to 256) in the
  * layout of aon_mlp_fwd_train's masks (N, 4) pairs of uint32 -- for the fused backward chains
  * after a layer-by-layer forward (threshold_backward of model.py:95-120's ReLUs). */
@@ -198,6 +210,11 @@ int aon_relu_masks(const float* h, int64_t N, int width, uint32_t* masks, aon_st
  * of device scratch. */
 size_t aon_mlp_bwd_packed_bytes(void);
 int aon_mlp_bwd_pack(const aon_mlp_params* params, void* packed, aon_stream_t stream);
+/* bf16 training mode: the transposed stream with bf16 weights, and the chain on bf16 MFMAs
+ * writing dzv / dzb / dz as bf16 (raw bits, same shapes); draw and masks as aon_mlp_bwd. */
+int aon_mlp_bwd_pack_bf16(const aon_mlp_params* params, void* packed, aon_stream_t stream);
+int aon_mlp_bwd_bf16(const void* packed, const float* draw, const uint32_t* masks, int64_t N,
+                     uint16_t* dzv, uint16_t* dzb, uint16_t* dz, void* work, aon_stream_t stream);
 int aon_mlp_bwd(const void* packed, const float* draw, const uint32_t* masks, int64_t N,
                 float* dzv, float* dzb, float* dz, void* work, aon_stream_t stream);
 
@@ -335,6 +352,11 @@ typedef struct aon_gemm_args {
    * m in [0.5, 1) -- the backward chains' own per-call gradient scale, so small gradients keep
    * full fp16 hi/lo precision.  NULL: a_scale alone. */
   const uint32_t* a_amax;
+  /* bf16 mode (AON_PREC_BF16 training): mma_bf16 = 1 computes on one bf16 MFMA per product
+   * (operands rounded to bf16 while staged, fp32 accumulate) -- reduction-major operands only
+   * (a_kc = b_kc = 0: the weight gradients dW = dY^T X), no A2 / bias / mask / relu; a_bf16 /
+   * b_bf16 = 1: that operand's elements are bf16 (raw 16-bit), else fp32. */
+  int mma_bf16, a_bf16, b_bf16;
 } aon_gemm_args;
 
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);
