@@ -40,7 +40,7 @@ class AonGemmArgs(ctypes.Structure):
                 ("C", vp), ("ldc", c_i64), ("bias", vp), ("mask", vp), ("ldm", c_i64),
                 ("relu", c_int), ("accumulate", c_int), ("a_scale", c_float), ("b_scale", c_float),
                 ("k_splits", c_i64), ("rowsum", vp), ("a_amax", vp), ("mma_bf16", c_int),
-                ("a_bf16", c_int), ("b_bf16", c_int)]
+                ("a_bf16", c_int), ("b_bf16", c_int), ("a_tiled", c_int), ("b_tiled", c_int)]
 
 
 class AonAdamTensor(ctypes.Structure):
@@ -119,7 +119,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.aon_abi_version() != 5:
+        if handle.aon_abi_version() != 6:
             raise ImportError("aonerf: ABI version mismatch")
         _lib = handle
     return _lib

@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import tiles
 
 from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, colsum, gemm, linear_fwd  # noqa: F401
 
@@ -180,37 +181,33 @@ def _pack_bwd(P, dev, tag="", bf16=False):
     return buf
 
 
-def _stacked(h, R):
-    """The 8 kept activations as one (8, R, 256) buffer (a view when they already are one)."""
-    base = h[0].data_ptr()
-    if all(t.is_contiguous() and t.data_ptr() == base + i * R * 256 * 4 for i, t in enumerate(h)):
-        return h[0]
-    return torch.stack(h)
-
-
 def relu_masks(acts, R):
-    """ReLU' bits (len(acts), R, 4) x 64-bit words (aon_relu_masks) of stored activations, in the
-    layout the fused training forwards write: the masks of the fused backward chains after a
-    layer-by-layer forward."""
+    """ReLU' bits (len(acts), tiles.rows(R), 4) x 64-bit words (aon_relu_masks) of row-major
+    stored activations, in the (tiled) layout the fused training forwards write: the masks of
+    the fused backward chains after a layer-by-layer forward."""
     dev = acts[0].device
-    masks = torch.empty((len(acts), R, 8), dtype=torch.int32, device=dev)
+    masks = torch.empty((len(acts), tiles.rows(R), 8), dtype=torch.int32, device=dev)
     for i, a in enumerate(acts):
         L.call("aon_relu_masks", L.ptr(L.contig(a)), R, a.shape[-1], L.ptr(masks[i]), L.stream(dev))
     return masks
 
 
-def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
+def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_tiled=True):
     """_backward_level with every input-gradient product in one fused kernel (aon_mlp_bwd);
     the weight gradients dW = dZ^T X and db = sum_rows dZ stay split-K GEMMs.  ``masks``: the
-    ReLU' bits of h0..h7, hv from the fused forward (built from the activations when None)."""
+    ReLU' bits of h0..h7, hv from the fused forward (built from the activations when None).
+    h_tiled: h / bot / hv in the fused forward's tiled layout (tiles.py), else row-major (the
+    layer-by-layer forward).  The chain's dz / dzb / dzv are always tiled."""
     R, dev = enc.shape[0], enc.device
     bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
-        masks = relu_masks(list(h) + [hv], R)
+        acts = list(h) + [hv]
+        masks = relu_masks([tiles.untile(a, R) for a in acts] if h_tiled else acts, R)
     dt = torch.bfloat16 if bf16 else torch.float32
-    dzv = torch.empty((R, 128), device=dev, dtype=dt)
-    dzb = torch.empty((R, 256), device=dev, dtype=dt)
-    dz = torch.empty((8, R, 256), device=dev, dtype=dt)
+    NR = tiles.rows(R)
+    dzv = torch.empty((NR, 128), device=dev, dtype=dt)
+    dzb = torch.empty((NR, 256), device=dev, dtype=dt)
+    dz = torch.empty((8, NR, 256), device=dev, dtype=dt)
     work = _buffer("work", 4, dev)
     packed = _pack_bwd(P, dev, S, bf16)
     e0 = _ev()
@@ -220,18 +217,21 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
     e0 = _ev()
     acts = ACT_SCALE
 
-    def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None):
+    def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None, a_t=True):
         # f16x3: dY rides at the chain's own per-call scale from max |d raw| (the word in
-        # `work`); bf16: one bf16 MFMA per product, no scales needed
+        # `work`); bf16: one bf16 MFMA per product, no scales needed.  dY: the chain's tiled
+        # gradients (a_t) or row-major d raw; X: a kept activation (tiled when h_tiled) or the
+        # row-major encodings
+        b_t = h_tiled and X is not enc and X is not venc
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
              b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=1.0, b_scale=1.0 if bf16 else acts,
-             rowsum=db, a_amax=None if bf16 else work, mma_bf16=bf16)
+             rowsum=db, a_amax=None if bf16 else work, mma_bf16=bf16, a_tiled=a_t, b_tiled=b_t)
 
-    dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1])               # rgb_layer
+    dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1], a_t=False)    # rgb_layer
     dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0
     dweight(G[10][0], dzv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
     dweight(G[9][0], dzb, 256, 256, h[7], 256, 256, db=G[9][1])            # bottleneck
-    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256, db=G[8][1])        # density
+    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256, db=G[8][1], a_t=False)  # density
     for i in range(7, -1, -1):                                             # pts_linears.i
         if i == 5:
             dweight(G[5][0], dz[5], 256, 256, h[4], 256, 256, db=G[5][1])
@@ -245,17 +245,19 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None):
 
 def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, masks=None,
                          bf16=False):
-    """_forward_level on the fused kernel: raw (R x 4) and the kept activations; ``masks``
-    ((9, R, 8) int32) receives their ReLU' bits for the backward chain.  bf16: the bf16
+    """_forward_level on the fused kernel: raw (R x 4) and the kept activations (tiled,
+    tiles.rows(R) rows each); ``masks`` ((9, tiles.rows(R), 8) int32) receives their ReLU' bits
+    for the backward chain.  bf16: the bf16
     training mode (activations kept as torch.bfloat16)."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
+    NR = tiles.rows(R)  # kept tensors: the tiled layout (tiles.py)
     if masks is None:
-        masks = torch.empty((9, R, 8), dtype=torch.int32, device=dev)
+        masks = torch.empty((9, NR, 8), dtype=torch.int32, device=dev)
     dt = torch.bfloat16 if bf16 else torch.float32
-    hbuf = torch.empty((8, R, 256), device=dev, dtype=dt)
-    bot = torch.empty((R, 256), device=dev, dtype=dt)
-    hv = torch.empty((R, 128), device=dev, dtype=dt)
+    hbuf = torch.empty((8, NR, 256), device=dev, dtype=dt)
+    bot = torch.empty((NR, 256), device=dev, dtype=dt)
+    hv = torch.empty((NR, 128), device=dev, dtype=dt)
     for w, b in P:
         if not (w.is_contiguous() and b.is_contiguous()):
             raise ValueError("MLP parameters must be contiguous")
@@ -286,7 +288,7 @@ class RenderLevel(torch.autograd.Function):
         masks = None  # ReLU' bits for the fused backward chain (built there when None)
         if FUSED_FORWARD:
             noise = L.contig(noise) if noise is not None else None
-            masks = torch.empty((9, R, 8), dtype=torch.int32, device=dev)
+            masks = torch.empty((9, tiles.rows(R), 8), dtype=torch.int32, device=dev)
             e0 = _ev()
             h, bot, hv = _forward_level_fused(P, L.contig(rays_o), L.contig(rays_d),
                                               L.contig(viewdirs), L.contig(t_vals), raw, noise,
@@ -303,6 +305,7 @@ class RenderLevel(torch.autograd.Function):
                L.ptr(weights), L.ptr(depth), L.stream(dev))
         ctx.save_for_backward(rays_d, t_vals, enc, venc, raw, bot, hv, *h, *params)
         ctx.masks = masks
+        ctx.h_tiled = FUSED_FORWARD  # the fused forward keeps its tensors tiled
         ctx.meta = (B, S, bool(white_bkgd))
         ctx.mark_non_differentiable(weights)
         return comp, acc, depth, weights
@@ -326,8 +329,11 @@ class RenderLevel(torch.autograd.Function):
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
         if FUSED_BACKWARD:
-            _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, ctx.masks)
+            _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, ctx.masks, ctx.h_tiled)
         else:
+            if ctx.h_tiled:  # the all-GEMM backward reads row-major activations
+                h = [tiles.untile(x, R) for x in h]
+                bot, hv = tiles.untile(bot, R), tiles.untile(hv, R)
             _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
         return (None, None, None, None, None, None, *grads)

@@ -31,6 +31,7 @@ autograd and looks up / scatters the code-library rows (nn.Embedding).
 import torch
 
 from . import _lib as L
+from . import tiles
 from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, gemm
 from .train import Adam, img2mse, learning_rate, mse2psnr, relu_masks  # noqa: F401 (shared)
 
@@ -194,16 +195,18 @@ def _pack_bwd(P, dev, tag=""):
 def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None,
                          masks=None):
     """_forward_level on the fused kernel (aon_mlp_art_fwd_train): raw (R x 4) and the kept
-    activations, plus the sample points and pos_enc(x'); ``masks`` ((16, R, 8) int32) receives
-    the ReLU' bits of hd0..3, h0..7, hv0..3 for the backward chain."""
+    activations (tiled, tiles.rows(R) rows each), plus the sample points and pos_enc(x')
+    (row-major); ``masks`` ((16, tiles.rows(R), 8) int32) receives the ReLU' bits of hd0..3,
+    h0..7, hv0..3 for the backward chain."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
+    NR = tiles.rows(R)
     if masks is None:
-        masks = torch.empty((16, R, 8), dtype=torch.int32, device=dev)
-    hd = torch.empty((4, R, geo.wd), device=dev)
-    h = torch.empty((8, R, geo.nw), device=dev)
-    bot = torch.empty((R, geo.nw), device=dev)
-    hv = torch.empty((4, R, geo.wc), device=dev)
+        masks = torch.empty((16, NR, 8), dtype=torch.int32, device=dev)
+    hd = torch.empty((4, NR, geo.wd), device=dev)
+    h = torch.empty((8, NR, geo.nw), device=dev)
+    bot = torch.empty((NR, geo.nw), device=dev)
+    hv = torch.empty((4, NR, geo.wc), device=dev)
     enc = torch.empty((R, geo.ne), device=dev)
     xyz = torch.empty((R, 3), device=dev)
     packed = _pack(geo, P, lat, S)
@@ -315,36 +318,41 @@ def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, dra
 
 
 def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
-                          masks=None):
+                          masks=None, h_tiled=True):
     """_backward_level with every input-gradient product (and pos_enc's backward) in one fused
     kernel (aon_mlp_art_bwd); the weight gradients dW = dZ^T X, db = sum_rows dZ and the latent
     terms stay GEMMs.  ``masks``: the fused forward's ReLU' bits (built from the activations
-    when None)."""
+    when None); h_tiled: hd / h / bot / hv in the fused forward's tiled layout (else
+    row-major); the chain's dzv / dbot / dz / dzd are tiled."""
     R, dev = xyz.shape[0], xyz.device
     if masks is None:
-        masks = relu_masks(list(hd) + list(h) + list(hv), R)
+        acts = list(hd) + list(h) + list(hv)
+        masks = relu_masks([tiles.untile(a, R) for a in acts] if h_tiled else acts, R)
     wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
     shape, app, art = lat
     dshape, dapp, dart = dlat
-    dzv = torch.empty((4, R, wc), device=dev)
-    dbot = torch.empty((R, nw), device=dev)
-    dz = torch.empty((8, R, nw), device=dev)
+    NR = tiles.rows(R)
+    dzv = torch.empty((4, NR, wc), device=dev)
+    dbot = torch.empty((NR, nw), device=dev)
+    dz = torch.empty((8, NR, nw), device=dev)
     dxp = torch.empty((R, 3), device=dev)
-    dzd = torch.empty((4, R, wd), device=dev)
+    dzd = torch.empty((4, NR, wd), device=dev)
     work = _buffer("work", 4, dev)
     L.call("aon_mlp_art_bwd", L.ptr(_pack_bwd(P, dev, S)), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
            L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
     gs, acts = GRAD_SCALE, ACT_SCALE
 
-    def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True, chain_scale=True):
+    def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True, chain_scale=True, a_t=True):
         # chain_scale: dY is in the chain's d raw domain (draw, view/trunk outputs): A rides at
         # the chain's own per-call scale from max |d raw| (the word it left in `work`); the
-        # deformation branch (dL/dx' carries pos_enc's 2^9, rescaled per sample) keeps 2^10
+        # deformation branch (dL/dx' carries pos_enc's 2^9, rescaled per sample) keeps 2^10.
+        # a_t: dY is one of the chain's tiled gradients; X is tiled when it is a kept activation
         dW = G[i][0]
+        b_t = h_tiled and X is not enc and X is not venc and X is not xyz
         gemm(dW[:, col0:] if col0 else dW, dY, X, dW.shape[0], n_in, R, lda=ldy, a_kc=False,
              ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0), a_scale=1.0 if chain_scale else gs,
              b_scale=acts, rowsum=G[i][1] if bias else None,
-             a_amax=work if chain_scale else None)
+             a_amax=work if chain_scale else None, a_tiled=a_t, b_tiled=b_t)
 
     def dlatent(i, col0, l, dl, accumulate):
         dW, db = G[i]
@@ -355,21 +363,21 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
         gemm(dl, db, W[:, col0:], 1, n, n_out, lda=n_out, a_kc=True, ldb=W.stride(0), b_kc=False,
              ldc=n, accumulate=accumulate, a_scale=gs, b_scale=W_SCALE)
 
-    dweight(RGB, draw, 4, hv[3], wc, wc)                                  # rgb_layer
+    dweight(RGB, draw, 4, hv[3], wc, wc, a_t=False)                       # rgb_layer
     for i in range(3, 0, -1):                                             # views_linear.i
         dweight(VIEW0 + i, dzv[i], wc, hv[i - 1], wc, wc)
     dweight(VIEW0, dzv[0], wc, bot, nw, nw)                               # views_linear.0
     dweight(VIEW0, dzv[0], wc, venc, nv, nv, col0=nw, rdiv=S, bias=False)
     dlatent(VIEW0, nw + nv, app, dapp, False)
     dweight(BOT, dbot, nw, h[7], nw, nw)                                  # bottleneck
-    dweight(DENS, draw[:, 3:], 4, h[7], nw, nw)                           # density
+    dweight(DENS, draw[:, 3:], 4, h[7], nw, nw, a_t=False)                # density
     for i in range(7, 0, -1):                                             # pts_linears.i
         dweight(PTS0 + i, dz[i], nw, h[i - 1], nw, nw)
     dweight(PTS0 + 5, dz[5], nw, enc, ne, ne, col0=nw, bias=False)
     dlatent(PTS0 + 5, nw + ne, shape, dshape, False)
     dweight(PTS0, dz[0], nw, enc, ne, ne)                                 # pts_linears.0
     dlatent(PTS0, ne, shape, dshape, True)
-    dweight(DL, dxp, 3, hd[3], wd, wd, chain_scale=False)                 # deformation_layer
+    dweight(DL, dxp, 3, hd[3], wd, wd, chain_scale=False, a_t=False)      # deformation_layer
     for i in range(3, 0, -1):                                             # deformations_linear.i
         dweight(DEF0 + i, dzd[i], wd, hd[i - 1], wd, wd, chain_scale=False)
     dweight(DEF0, dzd[0], wd, xyz, 3, 3, chain_scale=False)               # deformations_linear.0
@@ -401,7 +409,7 @@ class ArtRenderLevel(torch.autograd.Function):
         noise = L.contig(noise) if noise is not None else None
         masks = None  # ReLU' bits for the fused backward chain (built there when None)
         if FUSED_FORWARD and _fused_ok(geo):
-            masks = torch.empty((16, R, 8), dtype=torch.int32, device=dev)
+            masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device=dev)
             xyz, hd, enc, h, bot, hv = _forward_level_fused(
                 geo, P, lat, L.contig(rays_o), L.contig(rays_d), L.contig(viewdirs),
                 L.contig(t_vals), raw, noise, masks)
@@ -419,6 +427,7 @@ class ArtRenderLevel(torch.autograd.Function):
                L.ptr(weights), L.ptr(depth), L.stream(dev))
         ctx.save_for_backward(rays_d, t_vals, xyz, enc, venc, raw, hd, h, bot, hv, *lat, *params)
         ctx.masks = masks
+        ctx.h_tiled = masks is not None  # the fused forward keeps its tensors tiled
         ctx.meta = (geo, B, S, bool(white_bkgd), tuple(x.shape for x in (shape, app, art)))
         ctx.mark_non_differentiable(weights)
         return comp, acc, depth, weights
@@ -443,8 +452,11 @@ class ArtRenderLevel(torch.autograd.Function):
         dlat = tuple(torch.empty_like(x) for x in lat)
         if FUSED_BACKWARD and _fused_ok(geo):
             _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
-                                  ctx.masks)
+                                  ctx.masks, ctx.h_tiled)
         else:
+            if ctx.h_tiled:  # the all-GEMM backward reads row-major activations
+                hd, h, hv = (torch.stack([tiles.untile(x, R) for x in t]) for t in (hd, h, hv))
+                bot = tiles.untile(bot, R)
             _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
         dlat = [d.reshape(s) for d, s in zip(dlat, lat_shapes)]

@@ -59,7 +59,17 @@ struct Params {
   int tiles_m, tiles_n, gm;  // XCD-aware tile order over a 1-D grid.x (see tile_of)
   int zsplit;                // split-K: number of K chunks (1 = not split), see split_of
   int tblocks;               // blocks of one K chunk's tile grid (tile_of's ids, with padding)
+  int a_tiled, b_tiled;      // reduction-major operand in the fused training kernels' 16-row
+                             // tiled layout (mlp_f16x3_core.hpp act_base; rdiv 1)
 };
+
+// start of the 4-element run (k, row .. row + 3) of a reduction-major operand (row % 4 == 0):
+// row-major storage row k / rdiv, or the 16-row tiled layout of the fused training kernels
+__device__ __forceinline__ int64_t km_off(int64_t k, int64_t row, int64_t ld, int64_t rdiv,
+                                          bool tiled) {
+  if (tiled) return (k & ~int64_t(15)) * ld + 256 * (row >> 4) + 16 * (k & 15) + (row & 15);
+  return (rdiv == 1 ? k : k / rdiv) * ld + row;
+}
 
 // Workgroups are dispatched round-robin over the 8 XCDs (block L -> XCD L mod 8), each with
 // its own L2.  The tiles (m, 0..tiles_n-1) that share one A row-block are given block ids
@@ -121,7 +131,7 @@ struct TileLoad {
   // KM: storage row k / rdiv.
   __device__ __forceinline__ void load(const float* p, int64_t ld, const float* p2, int64_t ld2,
                                        int64_t K1, int64_t rdiv, int64_t row0, int64_t R,
-                                       int64_t k0, int64_t kend, int tid) {
+                                       int64_t k0, int64_t kend, int tid, bool tiled = false) {
     if (KC) {
       const int kq = 4 * (tid & 7);
 #pragma unroll
@@ -150,7 +160,7 @@ struct TileLoad {
         const int64_t row = row0 + rq;
         f4 v = {0.f, 0.f, 0.f, 0.f};
         if (k < kend) {
-          const float* src = p + (rdiv == 1 ? k : k / rdiv) * ld + row;
+          const float* src = p + km_off(k, row, ld, rdiv, tiled);
           if (VEC && row + 3 < R) {
             v = *reinterpret_cast<const f4*>(src);
           } else {
@@ -233,8 +243,8 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
   auto load = [&](int kt, auto set) {
     constexpr int S = decltype(set)::value;
     const int64_t k0 = kbeg + (int64_t)kt * BK;
-    ta[S].load(p.A, p.lda, p.A2, p.lda2, p.K1, p.a2_rdiv, m0, p.M, k0, kend, tid);
-    tb[S].load(p.B, p.ldb, nullptr, 0, INT64_MAX, p.b_rdiv, n0, p.N, k0, kend, tid);
+    ta[S].load(p.A, p.lda, p.A2, p.lda2, p.K1, p.a2_rdiv, m0, p.M, k0, kend, tid, p.a_tiled);
+    tb[S].load(p.B, p.ldb, nullptr, 0, INT64_MAX, p.b_rdiv, n0, p.N, k0, kend, tid, p.b_tiled);
   };
   const bool want_rows = !AKC && p.rowsum && tn == 0;
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
@@ -408,7 +418,7 @@ template <typename T, bool VEC>
 struct TileLoadKM {
   float r[4][4];  // [k][row]
   __device__ __forceinline__ void load(const T* p, int64_t ld, int64_t rdiv, int64_t row0,
-                                       int64_t R, int64_t k0, int64_t kend, int tid) {
+                                       int64_t R, int64_t k0, int64_t kend, int tid, bool tiled) {
     const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -417,7 +427,7 @@ struct TileLoadKM {
 #pragma unroll
       for (int j = 0; j < 4; ++j) r[i][j] = 0.f;
       if (k < kend) {
-        const T* src = p + (rdiv == 1 ? k : k / rdiv) * ld + row;
+        const T* src = p + km_off(k, row, ld, rdiv, tiled);
         if (VEC && row + 3 < R) {
           if (sizeof(T) == 4) {
             const f4 v = *reinterpret_cast<const f4*>(src);
@@ -464,7 +474,7 @@ template <bool VEC>
 struct TileLoadKMb {
   uint2 r[4];  // r[i]: rows rq..rq+3 at k = kq + i (bf16 bits, two per dword)
   __device__ __forceinline__ void load(const __bf16* p, int64_t ld, int64_t rdiv, int64_t row0,
-                                       int64_t R, int64_t k0, int64_t kend, int tid) {
+                                       int64_t R, int64_t k0, int64_t kend, int tid, bool tiled) {
     const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
     const uint16_t* q = reinterpret_cast<const uint16_t*>(p);
 #pragma unroll
@@ -473,7 +483,7 @@ struct TileLoadKMb {
       const int64_t row = row0 + rq;
       uint2 v = {0u, 0u};
       if (k < kend) {
-        const uint16_t* src = q + (rdiv == 1 ? k : k / rdiv) * ld + row;
+        const uint16_t* src = q + km_off(k, row, ld, rdiv, tiled);
         if (VEC && row + 3 < R) {
           v = *reinterpret_cast<const uint2*>(src);
         } else {
@@ -544,8 +554,8 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_km(Params p) {
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
   auto load = [&](int kt) {
     const int64_t k0 = kbeg + (int64_t)kt * BK;
-    ta.load(A, p.lda, 1, m0, p.M, k0, kend, tid);
-    tb.load(Bm, p.ldb, p.b_rdiv, n0, p.N, k0, kend, tid);
+    ta.load(A, p.lda, 1, m0, p.M, k0, kend, tid, p.a_tiled);
+    tb.load(Bm, p.ldb, p.b_rdiv, n0, p.N, k0, kend, tid, p.b_tiled);
   };
   auto store = [&](int stage) {
     if (want_rows) ta.add_rows(rs);
@@ -669,8 +679,14 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
                       !a->a_amax),
               "mma_bf16 computes reduction-major weight gradients only (a_kc = b_kc = 0, no A2 / "
               "bias / mask / relu / a_amax)");
+  AON_REQUIRE(!a->a_tiled || (!a->a_kc && a->lda == a->M && a->M % 16 == 0),
+              "a_tiled: reduction-major A of width lda = M (a multiple of 16)");
+  AON_REQUIRE(!a->b_tiled || (!a->b_kc && a->b_rdiv == 1 && a->ldb == a->N && a->N % 16 == 0),
+              "b_tiled: reduction-major B of width ldb = N (a multiple of 16), b_rdiv = 1");
   if (a->M == 0 || a->N == 0) return 0;
   Params p;
+  p.a_tiled = a->a_tiled;
+  p.b_tiled = a->b_tiled;
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = a->A; p.lda = a->lda;
   p.A2 = a->A2; p.lda2 = a->A2 ? a->lda2 : 0; p.K1 = a->A2 ? a->K1 : INT64_MAX;

@@ -100,8 +100,8 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   Frag<8, NCOL> x, y;
   Frag<1, NCOL> none;
   using SP = StorePick<STORE, NCOL>;
-  const int64_t hds = N * 128, hs = N * 256;  // one deformation / pts_linears output
-  const int64_t ms = N * 4;  // one layer's ReLU' bits: hd0..3, h0..7, hv0..3 in ts.masks
+  const int64_t hds = act_rows(N) * 128, hs = act_rows(N) * 256;  // one deformation / pts_linears output
+  const int64_t ms = act_rows(N) * 4;  // one layer's ReLU' bits: hd0..3, h0..7, hv0..3 in ts.masks
   // deformation MLP (model_autodecoder.py:196-205)
   layer_h<Net, A_D0, true>(fp, none, din, x, bias_l, g, SP::make(ts.hd, 128, rows, N, g, ts.masks));
   layer_h<Net, A_D1, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + hds, 128, rows, N, g, ts.masks + 1 * ms));

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   fp.start();
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 
-  const int64_t hs = N * 256, ws = N * 128, ms = N * 4;  // ms: one layer's ReLU' bits
+  const int64_t hs = act_rows(N) * 256, ws = act_rows(N) * 128, ms = act_rows(N) * 4;  // ms: one layer's ReLU' bits
   Frag<8, NCOL> x, y;
   Frag<2, NCOL> junk;  // output fragments of the enc-column layers (consumed in the epilogue)
   Frag<1, NCOL> none;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   // d bottleneck = W_view0[:, :256]^T dZ_view0 (linear layer: no mask)
   {
     RowStore<NCOL> st;
-    st.rowp[0] = row < N ? a.dbot + row * 256 + 4 * g : nullptr;
+    st.rowp[0] = row < N ? a.dbot + act_base(row, 256, g) : nullptr;
     st.s = inv;
     layer_h<Net, AB_V0, false>(fp, y, none, x, bias_l, g, st);
   }

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   fp.start();
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 
-  const int64_t hs = N * 256, ms = N * 4;
+  const int64_t hs = act_rows(N) * 256, ms = act_rows(N) * 4;
   Frag<8, NCOL> x, y;
   Frag<1, NCOL> none;
   // d hv = W_rgb^T d rgb, * ReLU'(hv) -> dZ of views_linear.0
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   // d bottleneck = W_view[:, :256]^T dZ_view (linear layer: no mask)
   {
     RowStore<NCOL, T> st;
-    st.rowp[0] = rows[0] < N ? dzb + rows[0] * 256 + 4 * g : nullptr;
+    st.rowp[0] = rows[0] < N ? dzb + act_base(rows[0], 256, g) : nullptr;
     st.s = inv;
     layer_h<Net, B_VIEW, false>(fp, x, none, y, bias_l, g, st);
   }
@@ -238,9 +238,9 @@ extern "C" int aon_mlp_bwd_bf16(const void* packed, const float* draw, const uin
   return bwd_launch(packed, draw, masks, N, dzv, dzb, dz, work, stream, true);
 }
 
-// ReLU' bits of an activation tensor h (N x width, width = 32 x pairs <= 256) in the layout
-// RowStoreBits writes (the layer-by-layer forward's masks for the fused chains): word (row, g)
-// bit 4 t + r = h[row][16 t + 4 g + r] > 0.
+// ReLU' bits of a row-major activation tensor h (N x width, width = 32 x pairs <= 256) in the
+// (tiled) layout RowStoreBits writes (the layer-by-layer forward's masks for the fused chains):
+// word (row, g) bit 4 t + r = h[row][16 t + 4 g + r] > 0.
 __global__ void k_relu_masks(const float* __restrict__ h, int64_t N, int width,
                              uint2* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -251,7 +251,7 @@ __global__ void k_relu_masks(const float* __restrict__ h, int64_t N, int width,
     for (int t = 0; t < width / 16; ++t)
       for (int r = 0; r < 4; ++r)
         if (h[row * width + 16 * t + 4 * g + r] > 0.0f) b[t >> 3] |= 1u << ((4 * t + r) & 31);
-    out[i] = uint2{b[0], b[1]};
+    out[mask_index(row, g)] = uint2{b[0], b[1]};
   }
 }
 

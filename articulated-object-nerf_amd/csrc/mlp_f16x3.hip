@@ -47,8 +47,8 @@ __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<
   T* const th = reinterpret_cast<T*>(ts.h);
   T* const tbot = reinterpret_cast<T*>(ts.bot);
   T* const thv = reinterpret_cast<T*>(ts.hv);
-  const int64_t hs = N * 256;  // one pts_linears output in ts.h
-  const int64_t ms = N * 4;    // one layer's ReLU' bits in ts.masks
+  const int64_t hs = act_rows(N) * 256;  // one pts_linears output in ts.h
+  const int64_t ms = act_rows(N) * 4;    // one layer's ReLU' bits in ts.masks
   layer_h<NetVanillaH, L0, true>(fp, none, enc, x, bias_l, g, SP::make(th, 256, rows, N, g, ts.masks));
   layer_h<NetVanillaH, L1, true>(fp, x, none, y, bias_l, g, SP::make(th + 1 * hs, 256, rows, N, g, ts.masks + 1 * ms));
   layer_h<NetVanillaH, L2, true>(fp, y, none, x, bias_l, g, SP::make(th + 2 * hs, 256, rows, N, g, ts.masks + 2 * ms));

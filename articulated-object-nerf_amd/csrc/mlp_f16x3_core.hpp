@@ -185,14 +185,66 @@ __device__ __forceinline__ void store2(__bf16* p, float v0, float v1) {
   *reinterpret_cast<bf2*>(p) = bf2{static_cast<__bf16>(v0), static_cast<__bf16>(v1)};
 }
 
+// four consecutive outputs: one 16-B fp32 store, or one 8-B bf16 store
+__device__ __forceinline__ void store4(float* p, float v0, float v1, float v2, float v3) {
+  *reinterpret_cast<f4*>(p) = f4{v0, v1, v2, v3};
+}
+__device__ __forceinline__ void store4(__bf16* p, float v0, float v1, float v2, float v3) {
+  const bf2 a = {static_cast<__bf16>(v0), static_cast<__bf16>(v1)};
+  const bf2 b = {static_cast<__bf16>(v2), static_cast<__bf16>(v3)};
+  *reinterpret_cast<uint2*>(p) = uint2{__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b)};
+}
+
+#ifndef AON_TILED
+#define AON_TILED 1  // 0: row-major (A/B only: the training forward's stores 15-45% slower)
+#endif
+// Layout of the tensors the fused training kernels keep for the backward (activations, the
+// chains' pre-activation gradients, ReLU' bits): 16 x 16 tiles, each contiguous and row-major,
+// element (row, f) of a width-ld tensor at (row / 16) 16 ld + 256 (f / 16) + 16 (row % 16) +
+// f % 16.  A tile is one MFMA output fragment, so a wave's epilogue store (64 lanes x 2 or 4
+// consecutive values) covers one contiguous 1-KB / 512-B run instead of 16 rows' scattered
+// pieces (row-major stores held the bf16 training forward at 2.9 ms; tiled 1.5 ms,
+// profiles/r02/ab_tiled), and the weight-gradient GEMM still reads 64-B row runs.  Buffers
+// hold act_rows(N) = N rounded up to 16 rows.
+__host__ __device__ constexpr int64_t act_rows(int64_t N) { return AON_TILED ? (N + 15) & ~int64_t(15) : N; }
+__device__ __forceinline__ int64_t act_base(int64_t row, int ld, int g) {
+  return AON_TILED ? (row & ~int64_t(15)) * ld + 16 * (row & 15) + 4 * g : row * ld + 4 * g;
+}
+// uint2 index of the ReLU' word (row, g): [N][4], or tiled [N/16][64 lanes]
+__device__ __forceinline__ int64_t mask_index(int64_t row, int g) {
+  return AON_TILED ? (row & ~int64_t(15)) * 4 + 16 * g + (row & 15) : row * 4 + g;
+}
+constexpr int kTileStride = AON_TILED ? 256 : 16;  // elements between output tiles of one lane
+
+// pairs (r0 = 0, 2) of a tile meet in one 4-value store
+template <int NCOL, typename T>
+struct Store4 {
+  mutable float pend[NCOL][2];
+  __device__ __forceinline__ void emit(T* rowp, int pr, int uu, int r0, int c, float v0,
+                                       float v1) const {
+    // fp32: one 8-B store per part (a lane's 16-B pair store measured slower); bf16: the two
+    // parts of a tile row meet in one 8-B store (4-B stores: 1.73 -> 1.51 ms forward)
+    if (std::is_same<T, float>::value) {
+      if (rowp) store2(rowp + kTileStride * (2 * pr + uu) + r0, v0, v1);
+      return;
+    }
+    if (r0 == 0) {
+      pend[c][0] = v0;
+      pend[c][1] = v1;
+    } else if (rowp) {
+      store4(rowp + kTileStride * (2 * pr + uu), pend[c][0], pend[c][1], v0, v1);
+    }
+  }
+};
+
 template <int NCOL, typename T = float>
-struct RowStore {
-  T* rowp[NCOL];  // y + row * ld + 4 g of each column's sample, nullptr when row >= N
+struct RowStore : Store4<NCOL, T> {
+  T* rowp[NCOL];  // act_base(row) of each column's sample, nullptr when row >= N
   float s;        // to true scale (a power of two: exact)
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
-    if (rowp[c]) store2(rowp[c] + 16 * (2 * pr + uu) + r0, v0 * s, v1 * s);
+    this->emit(rowp[c], pr, uu, r0, c, v0 * s, v1 * s);
   }
 };
 
@@ -221,7 +273,7 @@ struct RowStoreBits : RowStore<NCOL, T> {
 // Backward-chain epilogue with ReLU' from those bits (no reads of the fp32
 // activations): the layer's word is loaded when its first pair starts.
 template <int NCOL, typename T = float>
-struct MaskBits {
+struct MaskBits : Store4<NCOL, T> {
   const uint2* mrow[NCOL];  // masks + row * 4 + g, nullptr when row >= N
   T* rowp[NCOL];            // out + row * ld + 4 g, nullptr when row >= N
   float s;
@@ -238,7 +290,7 @@ struct MaskBits {
     return (w >> (bit & 31)) & 1u ? v : 0.0f;
   }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
-    if (rowp[c]) store2(rowp[c] + 16 * (2 * pr + uu) + r0, v0 * s, v1 * s);
+    this->emit(rowp[c], pr, uu, r0, c, v0 * s, v1 * s);
   }
 };
 
@@ -250,8 +302,8 @@ __device__ __forceinline__ MaskBits<NCOL, T> mask_bits(const uint2* mbase, T* ob
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
     const bool ok = rows[c] < N;
-    mb.mrow[c] = ok ? mbase + rows[c] * 4 + g : nullptr;
-    mb.rowp[c] = ok ? obase + rows[c] * ld + 4 * g : nullptr;
+    mb.mrow[c] = ok ? mbase + mask_index(rows[c], g) : nullptr;
+    mb.rowp[c] = ok ? obase + act_base(rows[c], ld, g) : nullptr;
   }
   mb.s = s;
   return mb;
@@ -276,7 +328,7 @@ struct StorePick<true, NCOL, T> {
                                                            int g) {
     RowStore<NCOL, T> r;
 #pragma unroll
-    for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + rows[c] * ld + 4 * g : nullptr;
+    for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + act_base(rows[c], ld, g) : nullptr;
     r.s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;
     return r;
   }
@@ -288,7 +340,7 @@ struct StorePick<true, NCOL, T> {
     static_cast<RowStore<NCOL, T>&>(r) = make(base, ld, rows, N, g);
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
-      r.mrow[c] = rows[c] < N ? reinterpret_cast<uint8_t*>(mbase + rows[c] * 4 + g) : nullptr;
+      r.mrow[c] = rows[c] < N ? reinterpret_cast<uint8_t*>(mbase + mask_index(rows[c], g)) : nullptr;
       r.b[c] = 0u;
     }
     r.narrow = ld == 128;

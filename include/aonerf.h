@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 5
+#define AON_ABI_VERSION 6
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -172,11 +172,19 @@ int aon_mlp_fwd_encoded(const void* packed, int precision, const float* x,
                         const float* condition, int64_t B, int S, int act, float* out,
                         aon_stream_t stream);
 
-/* The training forward of one level (model.py:175-184 under autograd) on the fused fp16x3
+/* Kept tensors of the fused training kernels (activations, ReLU' bits, the backward chains'
+ * pre-activation gradients) are stored TILED, in contiguous row-major 16 x 16 tiles (one MFMA
+ * output fragment each): for N rows of width W (a multiple of 16), element (row, f) at
+ *     (row / 16) * 16 W + 256 (f / 16) + 16 (row % 16) + f % 16,
+ * and a layer's ReLU' word (row, g) (a pair of uint32) at (row / 16) * 64 + 16 g + row % 16.
+ * Every buffer holds NR = N rounded up to a multiple of 16 rows, and stacked tensors such as
+ * h (8, NR, 256) are NR rows apart.  aon_gemm reads them in place (a_tiled / b_tiled).
+ *
+ * The training forward of one level (model.py:175-184 under autograd) on the fused fp16x3
  * kernel: as aon_mlp_fwd with AON_ACT_NONE (packed = AON_PREC_F16X3 stream), plus every
- * hidden activation kept for the backward -- h (8, B*S, 256): post-ReLU pts_linears.0..7,
- * bot (B*S, 256): bottleneck_layer, hv (B*S, 128): post-ReLU views_linear.0 -- and
- * raw_sigma + noise[row] when noise (B*S) is not NULL.  masks (9, B*S, 4) pairs of uint32:
+ * hidden activation kept for the backward (tiled, NR = B*S rounded up to 16 rows) -- h (8, NR,
+ * 256): post-ReLU pts_linears.0..7, bot (NR, 256): bottleneck_layer, hv (NR, 128): post-ReLU
+ * views_linear.0 -- and raw_sigma + noise[row] when noise (B*S) is not NULL.  masks (9, NR, 4) pairs of uint32:
  * the ReLU' bits of h0..h7, hv for the backward chain (word (row, g), bit 4 t + r = output
  * feature 16 t + 4 g + r > 0; aon_relu_masks builds the same from stored activations). */
 int aon_mlp_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
@@ -193,8 +201,8 @@ int aon_mlp_fwd_train_bf16(const void* packed, const float* rays_o, const float*
                            const float* noise, uint16_t* h, uint16_t* bot, uint16_t* hv,
                            float* raw, uint32_t* masks, aon_stream_t stream);
 
-/* ReLU' bits of an activation tensor h (N x width, width a multiple of 32 up to 256) in the
- * layout of aon_mlp_fwd_train's masks (N, 4) pairs of uint32 -- for the fused backward chains
+/* ReLU' bits of a ROW-MAJOR activation tensor h (N x width, width a multiple of 32 up to 256)
+ * in the tiled layout of aon_mlp_fwd_train's masks (NR, 4) pairs of uint32 -- for the fused backward chains
  * after a layer-by-layer forward (threshold_backward of model.py:95-120's ReLUs). */
 int aon_relu_masks(const float* h, int64_t N, int width, uint32_t* masks, aon_stream_t stream);
 
@@ -202,9 +210,9 @@ int aon_relu_masks(const float* h, int64_t N, int width, uint32_t* masks, aon_st
  * autograd): from draw (B*S, 4) = dL/d[raw_rgb, raw_sigma] (aon_composite_bwd), all input-
  * gradient products dX = dZ W down to pts_linears.0 in one fused kernel, each masked by ReLU'
  * of the forward output it flows into (masks: the ReLU' bits of aon_mlp_fwd_train), writing
- *   dzv (B*S, 128): dL/d pre-activation of views_linear.0,
- *   dzb (B*S, 256): dL/d bottleneck_layer output,
- *   dz  (8, B*S, 256): dL/d pre-activation of pts_linears.i,
+ *   dzv (NR, 128): dL/d pre-activation of views_linear.0,
+ *   dzb (NR, 256): dL/d bottleneck_layer output,
+ *   dz  (8, NR, 256): dL/d pre-activation of pts_linears.i (all tiled, NR = N rounded up to 16),
  * the operands of the weight-gradient GEMMs dW = dZ^T X (aon_gemm).  packed: the transposed
  * weight stream of aon_mlp_bwd_pack (re-pack after every optimizer step); work: >= 4 bytes
  * of device scratch. */
@@ -258,9 +266,10 @@ int aon_mlp_art_fwd(const void* packed, const float* rays_o, const float* rays_d
                     aon_stream_t stream);
 /* Training forward of one articulated level (reference model_autodecoder.py:168-239 under
  * autograd): aon_mlp_art_fwd (MODE 0 inputs, raw outputs, no activation) that also keeps what
- * the backward needs -- hd (4, B*S, 128) deformation layers, h (8, B*S, 256) pts_linears, bot
- * (B*S, 256), hv (4, B*S, 128) views_linear, enc (B*S, 63) = pos_enc(x') and xyz (B*S, 3) the
- * sample points; raw_sigma += noise[r] when noise != NULL (:318-319); masks (16, B*S, 4) pairs
+ * the backward needs -- tiled (NR = B*S rounded up to 16): hd (4, NR, 128) deformation layers,
+ * h (8, NR, 256) pts_linears, bot (NR, 256), hv (4, NR, 128) views_linear; row-major: enc (B*S,
+ * 63) = pos_enc(x') and xyz (B*S, 3) the sample points; raw_sigma += noise[r] when noise !=
+ * NULL (:318-319); masks (16, NR, 4) pairs
  * of uint32: the ReLU' bits of hd0..3, h0..7, hv0..3 (layout of aon_mlp_fwd_train's).  Activation
  * buffers 8-byte aligned, raw and masks 16-byte aligned. */
 int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
@@ -272,9 +281,10 @@ int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* 
 /* Backward chain of one articulated level (autograd of model_autodecoder.py:168-239): from
  * dL/d raw (N, 4), the ReLU' bits (16, N, 4) of hd0..3, h0..7, hv0..3 and pos_enc(x') (enc) kept
  * by aon_mlp_art_fwd_train, to
- * every layer's dL/d pre-activation -- dzv (4, N, 128) views_linear.i, dbot (N, 256) the
- * bottleneck output, dz (8, N, 256) pts_linears.i, dxp (N, 3) = dL/dx' (the deformation head's
- * output, through pos_enc's backward), dzd (4, N, 128) deformations_linear.i -- the operands of
+ * every layer's dL/d pre-activation -- tiled (NR rows): dzv (4, NR, 128) views_linear.i, dbot
+ * (NR, 256) the bottleneck output, dz (8, NR, 256) pts_linears.i, dzd (4, NR, 128)
+ * deformations_linear.i; row-major dxp (N, 3) = dL/dx' (the deformation head's output, through
+ * pos_enc's backward) -- the operands of
  * the weight-gradient GEMMs.  packed: aon_mlp_art_bwd_pack of the forward weights (layout
  * kLayersArtBwd); work: >= 4 bytes.  Buffers 16-byte aligned (dxp: 4). */
 size_t aon_mlp_art_bwd_packed_bytes(void);
@@ -357,6 +367,10 @@ typedef struct aon_gemm_args {
    * (a_kc = b_kc = 0: the weight gradients dW = dY^T X), no A2 / bias / mask / relu; a_bf16 /
    * b_bf16 = 1: that operand's elements are bf16 (raw 16-bit), else fp32. */
   int mma_bf16, a_bf16, b_bf16;
+  /* a reduction-major operand stored in the fused training kernels' tiled layout (see
+   * aon_mlp_fwd_train): a_tiled needs lda == M, b_tiled ldb == N and b_rdiv 1, both widths
+   * multiples of 16 */
+  int a_tiled, b_tiled;
 } aon_gemm_args;
 
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);

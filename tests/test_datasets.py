@@ -86,3 +86,21 @@ def test_multi_masked_batch_matches_reference(golden):
     np.testing.assert_allclose(b["viewdirs"].cpu().numpy(), g["multi_viewdirs"], rtol=0, atol=1e-6)
     np.testing.assert_array_equal(b["target"].cpu().numpy(), g["multi_rgbs"])
     np.testing.assert_array_equal(b["mask"].cpu().numpy(), g["multi_mask"].reshape(-1))
+
+
+def test_tiled_layout_helpers():
+    """aonerf/tiles.py: element (row, f) of a tiled (rows(n), W) buffer sits at
+    (row // 16) 16 W + 256 (f // 16) + 16 (row % 16) + f % 16 (the layout
+    csrc/mlp_f16x3_core.hpp act_base writes), and untile inverts tile on ragged sizes."""
+    import torch
+    from aonerf import tiles
+
+    for n, W in ((37, 32), (16, 128), (2405, 256)):
+        x = torch.arange(n * W, dtype=torch.int64).reshape(n, W)
+        t = tiles.tile(x).reshape(-1)
+        assert t.numel() == tiles.rows(n) * W
+        for row in sorted(r for r in {0, 5, 15, 16, n - 1} if r < n):
+            for f in sorted({0, 3, 7, 17, W - 1}):
+                off = (row // 16) * 16 * W + 256 * (f // 16) + 16 * (row % 16) + f % 16
+                assert t[off] == x[row, f]
+        assert torch.equal(tiles.untile(t.reshape(-1, W), n), x)

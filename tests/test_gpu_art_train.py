@@ -89,7 +89,7 @@ def test_fused_art_train_forward_activations():
     layer-by-layer GEMM forward on a ragged batch: the points bit-exact, the deformation layers
     ~1e-6 of each tensor's range (both f16x3), pos_enc(x') and the layers after it within the
     sin(2^9 x') amplification of that (measured ~4e-5)."""
-    from aonerf import train_art
+    from aonerf import tiles, train_art
     from aonerf import _lib as L
 
     net, _ = _make(0)
@@ -104,11 +104,17 @@ def test_fused_art_train_forward_activations():
     lat = tuple(cuda(v) for v in W.art_latents(1).values())
     P = [(m.weight.detach(), m.bias.detach()) for m in train_art.art_layers(mlp)]
     raw_f = torch.empty((B * S, 4), device="cuda")
-    masks = torch.empty((16, B * S, 8), dtype=torch.int32, device="cuda")
-    xyz_f, hd_f, enc_f, h_f, bot_f, hv_f = train_art._forward_level_fused(geo, P, lat, o, d, d, t,
+    R = B * S
+    masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device="cuda")
+    xyz_f, hd_t, enc_f, h_t, bot_t, hv_t = train_art._forward_level_fused(geo, P, lat, o, d, d, t,
                                                                          raw_f, noise, masks)
+    # kept tensors are tiled (aonerf/tiles.py; 2,405 rows: a partial last block)
+    hd_f, h_f, hv_f = ([tiles.untile(x, R) for x in tt] for tt in (hd_t, h_t, hv_t))
+    bot_f = tiles.untile(bot_t, R)
     # the ReLU' bits written by the forward == those built from its stored activations
-    assert torch.equal(masks, train_art.relu_masks(list(hd_f) + list(h_f) + list(hv_f), B * S))
+    rebuilt = train_art.relu_masks(list(hd_f) + list(h_f) + list(hv_f), R)
+    for i in range(16):
+        assert torch.equal(tiles.untile_masks(masks[i], R), tiles.untile_masks(rebuilt[i], R)), i
     xyz = torch.empty((B * S, 3), device="cuda")
     L.call("aon_cast_rays", L.ptr(o), L.ptr(d), L.ptr(t), B, S, None, 0, L.ptr(xyz), 0, 0, None,
            L.stream())
@@ -132,8 +138,9 @@ def test_fused_art_train_forward_activations():
 def test_fused_art_backward_chain():
     """aon_mlp_art_bwd (+ the weight-gradient GEMMs) against the all-GEMM backward on the same
     kept activations and d raw (ragged batch): every parameter and latent gradient within
-    2e-5 of its tensor's max (two f16x3 evaluations of the same products)."""
-    from aonerf import train_art
+    2e-5 of its tensor's max (two f16x3 evaluations of the same products).  The fused chain
+    reads the forward's tiled tensors in place, the GEMM backward their row-major copies."""
+    from aonerf import tiles, train_art
 
     net, _ = _make(0)
     mlp = net.fine_mlp
@@ -153,10 +160,14 @@ def test_fused_art_backward_chain():
     L.call("aon_pos_enc", L.ptr(d), B, 0, 4, L.ptr(venc), L.stream())
     draw = (torch.randn(R, 4, generator=gen) * 1e-3).cuda()
     out = {}
+    rm = [torch.stack([tiles.untile(x, R) for x in tt]) for tt in (hd, h, hv)]
+    kept = {"fused": (hd, h, bot, hv),
+            "gemm": (rm[0], rm[1], tiles.untile(bot, R), rm[2])}
     for mode, fn in (("fused", train_art._backward_level_fused), ("gemm", train_art._backward_level)):
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
         dlat = tuple(torch.empty_like(x) for x in lat)
-        fn(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
+        khd, kh, kbot, khv = kept[mode]
+        fn(geo, P, G, lat, dlat, xyz, enc, venc, S, khd, kh, kbot, khv, draw)
         out[mode] = [g for pair in G for g in pair] + list(dlat)
     names = [f"{i}.{k}" for i in range(20) for k in ("w", "b")] + ["shape", "app", "art"]
     worst = 0.0

@@ -157,8 +157,9 @@ def fwd_mode(request):
 def test_fused_train_forward_activations():
     """aon_mlp_fwd_train's kept activations and raw outputs (with noise) against the
     layer-by-layer GEMM forward on a ragged batch: the two f16x3 evaluations agree to ~1e-6
-    relative of each tensor's range."""
-    from aonerf import train
+    relative of each tensor's range.  The kept tensors are tiled (aonerf/tiles.py; 2,405 rows:
+    a partial last 16-row block) and compared through tiles.untile."""
+    from aonerf import tiles, train
 
     net = _make_trainable(0)
     gen = torch.Generator().manual_seed(3)
@@ -169,10 +170,15 @@ def test_fused_train_forward_activations():
     noise = torch.rand(B * S, generator=gen).cuda()
     P = [(m.weight.detach(), m.bias.detach()) for m in net.fine_mlp._layers()]
     raw_f = torch.empty((B * S, 4), device="cuda")
-    masks = torch.empty((9, B * S, 8), dtype=torch.int32, device="cuda")
-    h_f, bot_f, hv_f = train._forward_level_fused(P, o, d, d, t, raw_f, noise, masks)
+    R = B * S
+    masks = torch.empty((9, tiles.rows(R), 8), dtype=torch.int32, device="cuda")
+    h_t, bot_t, hv_t = train._forward_level_fused(P, o, d, d, t, raw_f, noise, masks)
+    h_f = [tiles.untile(x, R) for x in h_t]
+    bot_f, hv_f = tiles.untile(bot_t, R), tiles.untile(hv_t, R)
     # the ReLU' bits written by the forward == those built from its stored activations
-    assert torch.equal(masks, train.relu_masks(list(h_f) + [hv_f], B * S))
+    rebuilt = train.relu_masks(list(h_f) + [hv_f], R)
+    for i in range(9):
+        assert torch.equal(tiles.untile_masks(masks[i], R), tiles.untile_masks(rebuilt[i], R)), i
     enc = torch.empty((B * S, 63), device="cuda")
     L = train.L
     L.call("aon_cast_rays", L.ptr(o), L.ptr(d), L.ptr(t), B, S, None, 0, None, 0, 10, L.ptr(enc),

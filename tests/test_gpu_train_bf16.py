@@ -166,3 +166,30 @@ def test_bf16_loss_trajectory():
     assert ref[-1] < 0.7 * ref[0], "the oracle run must actually train"
     np.testing.assert_allclose(f16, ref, rtol=1e-3)
     np.testing.assert_allclose(bf, ref, rtol=2e-2)
+
+
+@pytest.mark.parametrize("mma_bf16,dtype", [(False, torch.float32), (True, torch.float32),
+                                            (True, torch.bfloat16)])
+def test_weight_gradient_gemm_tiled_operands(mma_bf16, dtype):
+    """aon_gemm a_tiled / b_tiled: dW = dZ^T X read in place from the fused training kernels'
+    16-row tiled layout (aonerf/tiles.py; 70,003 rows: a partial last block, split-K) is
+    bit-identical to the same product on row-major copies -- the staged values and their
+    order are the same."""
+    from aonerf import tiles
+    from aonerf.linalg import gemm
+
+    g = torch.Generator(device="cuda").manual_seed(11)
+    K, M, N = 70003, 128, 256
+    A = (torch.randn((K, M), device="cuda", generator=g) * 1e-3).to(dtype)
+    B = torch.randn((K, N), device="cuda", generator=g).to(dtype)
+    At, Bt = tiles.tile(A), tiles.tile(B)
+    out = []
+    for a, b, tiled in ((A, B, False), (At, Bt, True)):
+        C = torch.zeros((M, N), device="cuda")
+        rs = torch.empty((M,), device="cuda")
+        gemm(C, a, b, M, N, K, lda=M, a_kc=False, ldb=N, b_kc=False, ldc=N, rowsum=rs,
+             a_scale=1.0 if mma_bf16 else 2.0 ** 10, b_scale=1.0 if mma_bf16 else 8.0,
+             mma_bf16=mma_bf16, a_tiled=tiled, b_tiled=tiled)
+        out.append((C, rs))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
