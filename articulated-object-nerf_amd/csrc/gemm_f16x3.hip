@@ -412,13 +412,34 @@ constexpr int STAGE_BF = 2 * PLANE;  // A, B planes of bf16 (same [row][k] geome
 template <typename T>
 __device__ __forceinline__ float to_f32(T v) { return static_cast<float>(v); }
 
+// Strength-reduced addressing of a thread's runs in full k-tiles of a reduction-major operand
+// (rdiv 1): the run of k-tile kt, k row i, starts at run + kt * tstep + i * istep elements
+// (row-major: istep = ld; tiled: 16), so a full tile costs no 64-bit index arithmetic (the
+// per-element km_off path left the bf16 kernel VALU-bound).  One per operand, shared by the
+// register sets.
+struct KmRun {
+  const void* run;
+  int64_t tstep, istep;
+  bool fast;
+  template <typename T>
+  __device__ __forceinline__ KmRun(const T* p, int64_t ld, int64_t rdiv, int64_t row0, int64_t R,
+                                   int64_t kbeg, int tid, bool tiled, bool vec) {
+    const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
+    fast = vec && rdiv == 1 && row0 + rq + 3 < R;
+    run = p + (fast ? km_off(kbeg + kq, row0 + rq, ld, 1, tiled) : 0);
+    tstep = BK * ld;
+    istep = tiled ? 16 : ld;
+  }
+};
+
 // 128 rows x 32 k of a reduction-major operand: thread t -> rows rq..rq+3 (rq = 16 (t >> 5) +
 // 4 (t & 3)), k = kq..kq+3 (kq = 4 ((t >> 2) & 7)); one 4-element row run per k
 template <typename T, bool VEC>
 struct TileLoadKM {
   float r[4][4];  // [k][row]
   __device__ __forceinline__ void load(const T* p, int64_t ld, int64_t rdiv, int64_t row0,
-                                       int64_t R, int64_t k0, int64_t kend, int tid, bool tiled) {
+                                       int64_t R, int64_t k0, int64_t kend, int tid, bool tiled,
+                                       const KmRun&, int) {
     const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -474,7 +495,15 @@ template <bool VEC>
 struct TileLoadKMb {
   uint2 r[4];  // r[i]: rows rq..rq+3 at k = kq + i (bf16 bits, two per dword)
   __device__ __forceinline__ void load(const __bf16* p, int64_t ld, int64_t rdiv, int64_t row0,
-                                       int64_t R, int64_t k0, int64_t kend, int tid, bool tiled) {
+                                       int64_t R, int64_t k0, int64_t kend, int tid, bool tiled,
+                                       const KmRun& a, int kt) {
+    if (a.fast && k0 + BK <= kend) {
+      const uint16_t* src = reinterpret_cast<const uint16_t*>(a.run) + kt * a.tstep;
+      const int64_t istep = a.istep;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = *reinterpret_cast<const uint2*>(src + i * istep);
+      return;
+    }
     const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
     const uint16_t* q = reinterpret_cast<const uint16_t*>(p);
 #pragma unroll
@@ -529,8 +558,26 @@ struct KMLoader<__bf16, VEC> {
   using type = TileLoadKMb<VEC>;
 };
 
+// f(integral_constant<I>) for I = B .. E-1 (compile-time register-set indices)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+#ifndef AON_GEMM_BF_PF
+#define AON_GEMM_BF_PF 2  // 1 / 2 / 3 / 4 measured equal (profiles/r02/ab_gemm)
+#endif
+constexpr int PFB = AON_GEMM_BF_PF;  // k-tiles in registers ahead of the one in LDS
+
+#ifndef AON_GEMM_BF_OCC
+#define AON_GEMM_BF_OCC 2  // waves per SIMD the bf16 kernel is built for
+#endif
+
 template <typename TA, typename TB, bool VA, bool VB>
-__global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_km(Params p) {
+__global__ __launch_bounds__(THREADS, AON_GEMM_BF_OCC) void k_gemm_bf16_km(Params p) {
   __shared__ __align__(16) __bf16 smem[2 * STAGE_BF];  // 2 stages x (A, B)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -543,8 +590,13 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_km(Params p) {
   const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
   const TA* A = reinterpret_cast<const TA*>(p.A);
   const TB* Bm = reinterpret_cast<const TB*>(p.B);
-  typename KMLoader<TA, VA>::type ta;
-  typename KMLoader<TB, VB>::type tb;
+  // PFB register sets: tile kt + 1 is published from its set at the end of step kt, and the
+  // set tile kt came from takes tile kt + PFB -- every load has PFB - 1 steps of MFMAs to land
+  // (one set left the kernel waiting on each tile's global load: 0.37 ms per fine-level dW)
+  typename KMLoader<TA, VA>::type ta[PFB];
+  typename KMLoader<TB, VB>::type tb[PFB];
+  const KmRun ra(A, p.lda, 1, m0, p.M, kbeg, tid, p.a_tiled, VA && sizeof(TA) == 2);
+  const KmRun rb(Bm, p.ldb, p.b_rdiv, n0, p.N, kbeg, tid, p.b_tiled, VB && sizeof(TB) == 2);
   f4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -552,27 +604,27 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_km(Params p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   const bool want_rows = p.rowsum && tn == 0;
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
-  auto load = [&](int kt) {
+  auto load = [&](int kt, auto set) {
+    constexpr int S = decltype(set)::value;
     const int64_t k0 = kbeg + (int64_t)kt * BK;
-    ta.load(A, p.lda, 1, m0, p.M, k0, kend, tid, p.a_tiled);
-    tb.load(Bm, p.ldb, p.b_rdiv, n0, p.N, k0, kend, tid, p.b_tiled);
+    ta[S].load(A, p.lda, 1, m0, p.M, k0, kend, tid, p.a_tiled, ra, kt);
+    tb[S].load(Bm, p.ldb, p.b_rdiv, n0, p.N, k0, kend, tid, p.b_tiled, rb, kt);
   };
-  auto store = [&](int stage) {
-    if (want_rows) ta.add_rows(rs);
+  auto store = [&](int stage, auto set) {
+    constexpr int S = decltype(set)::value;
+    if (want_rows) ta[S].add_rows(rs);
     __bf16* s = smem + stage * STAGE_BF;
-    ta.store(s, tid);
-    tb.store(s + PLANE, tid);
+    ta[S].store(s, tid);
+    tb[S].store(s + PLANE, tid);
   };
-  if (nk > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
   const int g = lane >> 4, r16 = lane & 15;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int P = kt & 1;
-    if (kt + 1 < nk) load(kt + 1);  // global loads in flight under this step's MFMAs
-    const __bf16* s = smem + P * STAGE_BF;
+  // step kt: tile kt in LDS stage kt & 1, set (kt % PFB) free for tile kt + PFB
+  auto step = [&](int kt, auto set) {
+    constexpr int S = decltype(set)::value;
+#ifndef AON_GEMM_ABL_NOLOAD  // timing-only ablations (wrong results)
+    if (kt + PFB < nk) load(kt + PFB, set);
+#endif
+    const __bf16* s = smem + (kt & 1) * STAGE_BF;
     bf8 b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -582,10 +634,29 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_km(Params p) {
       const bf8 a = *reinterpret_cast<const bf8*>(s + (wm * 64 + 16 * i + r16) * ROWH + 8 * g);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
+#ifndef AON_GEMM_ABL_NOMFMA
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+#else
+        acc[i][j][0] += static_cast<float>(a[0]) * static_cast<float>(b[j][0]);
+#endif
     }
-    if (kt + 1 < nk) store(1 - P);
+#ifndef AON_GEMM_ABL_NOSTORE
+    if (kt + 1 < nk) store(1 - (kt & 1), std::integral_constant<int, (S + 1) % PFB>{});
+#endif
+#ifndef AON_GEMM_ABL_NOSYNC
     __syncthreads();
+#endif
+  };
+  // prologue: tiles 0 .. PFB-1 in flight, tile 0 published
+  static_for<0, PFB>([&](auto set) {
+    if (decltype(set)::value < nk) load(decltype(set)::value, set);
+  });
+  if (nk > 0) store(0, std::integral_constant<int, 0>{});
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += PFB) {
+    static_for<0, PFB>([&](auto set) {
+      if (kt + decltype(set)::value < nk) step(kt + decltype(set)::value, set);
+    });
   }
   const bool split = p.zsplit > 1;
   if (want_rows) {
@@ -624,6 +695,380 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_km(Params p) {
     }
 }
 
+// ---- bf16 x bf16 weight gradients with both operands bf16 and reduction-major (the bf16
+// training mode's dW = dZ^T H on the fused kernels' tiled tensors, or row-major), M and N
+// multiples of 128.  The k-tile of each operand is copied, not transposed, while staging: a
+// thread loads two contiguous 16-B runs (8 columns of one k row; a wave reads 1 KB contiguous
+// in the tiled layout) and writes them as they are into a [k][128 columns] LDS image (XOR-
+// swizzled 16-B chunks, cdna_hip_programming.md T10 (b)); the MFMA fragments, 8 consecutive k
+// of one column, come out of ds_read_b64_tr_b16 (the hardware transpose read).  The
+// transposing loader of k_gemm_bf16_km (4 x 8-B loads scattered over 32-B pieces per thread)
+// held it at 0.34 ms per fine-level product: global loads, not MFMA or LDS, set its pace.
+typedef short tt_v4s __attribute__((ext_vector_type(4)));
+constexpr int TT_PLANE = BK * 256;  // bytes of one operand's [32 k][128 col] bf16 image
+
+__device__ __forceinline__ int tt_off(int row, int ch) {  // byte offset of 16-B chunk ch of row
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// a thread's two 16-B runs of every k-tile of one operand: run j = k row kl0 + 16 j, columns
+// cl .. cl + 7 of the workgroup tile; element offsets from the operand's base
+struct TTRun {
+  const uint16_t* base;  // run 0 of k-tile 0
+  int64_t jstep, tstep;  // run 1 - run 0, k-tile t+1 - k-tile t (elements)
+  int kl0, cl;
+  __device__ __forceinline__ TTRun(const __bf16* p, int64_t ld, int64_t col0, int64_t kbeg,
+                                   int tid, bool tiled) {
+    if (tiled) {  // memory order within a 16-row block's 4-KB column range: [tile][row][half]
+      const int T = tid >> 5, s = (tid >> 1) & 15, h = tid & 1;
+      kl0 = s;
+      cl = 16 * T + 8 * h;
+      base = reinterpret_cast<const uint16_t*>(p) + kbeg * ld + 256 * ((col0 >> 4) + T) + 16 * s + 8 * h;
+    } else {
+      kl0 = tid >> 4;
+      cl = 8 * (tid & 15);
+      base = reinterpret_cast<const uint16_t*>(p) + (kbeg + kl0) * ld + col0 + cl;
+    }
+    jstep = 16 * ld;
+    tstep = BK * ld;
+  }
+};
+
+struct TTSet {
+  uint4 v[2];
+  __device__ __forceinline__ void load(const TTRun& r, int kt, int64_t k0, int64_t kend) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      v[j] = uint4{0u, 0u, 0u, 0u};
+      if (k0 + r.kl0 + 16 * j < kend)
+        v[j] = *reinterpret_cast<const uint4*>(r.base + kt * r.tstep + j * r.jstep);
+    }
+  }
+  __device__ __forceinline__ void store(char* plane, const TTRun& r) const {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      *reinterpret_cast<uint4*>(plane + tt_off(r.kl0 + 16 * j, r.cl >> 3)) = v[j];
+  }
+  // column sums of the run values (bf16 -> fp32 exact), runs in k order
+  __device__ __forceinline__ void add_cols(float (&rs)[8]) const {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t d = w[e >> 1];
+        rs[e] = __fadd_rn(rs[e], __uint_as_float((e & 1) ? (d & 0xffff0000u) : (d << 16)));
+      }
+    }
+  }
+};
+
+// 8 consecutive k (rows 8 g .. 8 g + 7 of the image) of column c0 * 8 + (lane & 15): two
+// transposed reads of 4 rows x 16 columns each (lane 4 q + p addresses row q, columns 4 p..)
+__device__ __forceinline__ bf8 tt_frag(const char* plane, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  tt_v4s h[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const char* a = plane + tt_off(8 * g + 4 * hh + q, c0 + (p >> 1)) + 8 * (p & 1);
+    h[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        reinterpret_cast<__attribute__((address_space(3))) tt_v4s*>(
+            reinterpret_cast<uintptr_t>(a)));
+  }
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s w = {h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]};
+  return __builtin_bit_cast(bf8, w);
+}
+
+__global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_tt(Params p) {
+  __shared__ __align__(16) char smem[2 * 2 * TT_PLANE];  // 2 stages x (A, B) images
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn, tile, z;
+  if (!split_of(p, tile, z)) return;
+  if (!tile_of(p, tile, tm, tn)) return;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)z * p.kchunk;
+  const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
+  const TTRun ra(reinterpret_cast<const __bf16*>(p.A), p.lda, m0, kbeg, tid, p.a_tiled);
+  const TTRun rb(reinterpret_cast<const __bf16*>(p.B), p.ldb, n0, kbeg, tid, p.b_tiled);
+  TTSet ta[PFB], tb[PFB];
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const bool want_rows = p.rowsum && tn == 0;
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto load = [&](int kt, auto set) {
+    constexpr int S = decltype(set)::value;
+    const int64_t k0 = kbeg + (int64_t)kt * BK;
+    ta[S].load(ra, kt, k0, kend);
+    tb[S].load(rb, kt, k0, kend);
+  };
+  auto store = [&](int stage, auto set) {
+    constexpr int S = decltype(set)::value;
+    if (want_rows) ta[S].add_cols(rs);
+    char* s = smem + stage * 2 * TT_PLANE;
+    ta[S].store(s, ra);
+    tb[S].store(s + TT_PLANE, rb);
+  };
+  auto step = [&](int kt, auto set) {
+    constexpr int S = decltype(set)::value;
+    if (kt + PFB < nk) load(kt + PFB, set);
+    const char* s = smem + (kt & 1) * 2 * TT_PLANE;
+    bf8 b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = tt_frag(s + TT_PLANE, 8 * wn + 2 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf8 a = tt_frag(s, 8 * wm + 2 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(1 - (kt & 1), std::integral_constant<int, (S + 1) % PFB>{});
+    __syncthreads();
+  };
+  static_for<0, PFB>([&](auto set) {
+    if (decltype(set)::value < nk) load(decltype(set)::value, set);
+  });
+  if (nk > 0) store(0, std::integral_constant<int, 0>{});
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += PFB) {
+    static_for<0, PFB>([&](auto set) {
+      if (kt + decltype(set)::value < nk) step(kt + decltype(set)::value, set);
+    });
+  }
+  const bool split = p.zsplit > 1;
+  if (want_rows) {
+    // the 16 threads sharing a column range hold k rows kl0 (+ 16 j + 32 kt): summed in kl0 order
+    float* red = reinterpret_cast<float*>(smem);  // [16][128]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[ra.kl0 * BM + ra.cl + e] = rs[e];
+    __syncthreads();
+    if (tid < BM) {
+      float v = red[tid];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) v = __fadd_rn(v, red[q * BM + tid]);
+      if (split) p.rowsum_part[(int64_t)z * p.M + m0 + tid] = v;
+      else p.rowsum[m0 + tid] = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        float v = acc[i][j][r];
+        if (split) {
+          p.part[((int64_t)z * p.M + m) * p.N + n] = v;
+          continue;
+        }
+        float* c = p.C + m * p.ldc + n;
+        if (p.accumulate) v = __fadd_rn(*c, v);
+        *c = v;
+      }
+    }
+}
+
+
+// ---- the same product with the operand tiles copied HBM/L2 -> LDS by global_load_lds_dwordx4
+// (no register staging): a DNB-deep ring of [32 k][128 col] image pairs, DNB - 1 k-tiles in
+// flight ahead of the one in use.  The register-staged kernel above kept ~2 MB in flight
+// chip-wide (PMC: 1,363-cycle HBM queue latency, 3.2 TB/s); the ring keeps DNB - 1 tiles of
+// 16 KB per workgroup in flight.  The LDS image is lane-linear per copy (lane i of a wave's
+// copy lands at 16 i), so the XOR swizzle is applied on the global side: lane i fetches the
+// logical chunk that belongs at its physical slot.  A k-tile past the end of the reduction
+// (only the last one of the last chunk) goes through registers with zero fill.
+#ifndef AON_GEMM_BF_DMA
+#define AON_GEMM_BF_DMA 1  // 0: the register-staged copy kernel k_gemm_bf16_tt (A/B)
+#endif
+#ifndef AON_GEMM_DMA_NBUF
+#define AON_GEMM_DMA_NBUF 3  // 2 / 4: within 2-10%, 6: 50% slower (profiles/r02/ab_gemm)
+#endif
+constexpr int DNB = AON_GEMM_DMA_NBUF;
+
+// s_waitcnt vmcnt(n) (lgkmcnt, expcnt untouched); n a small constant after unrolling
+__device__ __forceinline__ void dma_wait_vm(int n) {
+#define AON_DW(n_) __builtin_amdgcn_s_waitcnt(((n_) & 0xF) | (((n_) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+  switch (n) {
+    case 0: AON_DW(0); break;
+    case 1: AON_DW(1); break;
+    case 2: AON_DW(2); break;
+    case 3: AON_DW(3); break;
+    case 4: AON_DW(4); break;
+    case 5: AON_DW(5); break;
+    case 6: AON_DW(6); break;
+    case 7: AON_DW(7); break;
+    case 8: AON_DW(8); break;
+    case 9: AON_DW(9); break;
+    case 10: AON_DW(10); break;
+    case 11: AON_DW(11); break;
+    default: AON_DW(12); break;
+  }
+#undef AON_DW
+}
+
+// one operand's copies: lane `lane` of wave w, copy c (0, 1) fills image row r = 8 w + 4 c +
+// lane / 16, physical chunk lane % 16 <- logical chunk (lane % 16) ^ swz(r)
+struct DmaOperand {
+  const char* gbase;  // byte address of k-tile 0's (row 0, column col0) origin, kbeg applied
+  int64_t tstep;      // bytes between k-tiles
+  uint32_t voff[2];   // per-lane byte offset of copy c within a k-tile
+  __device__ __forceinline__ DmaOperand(const __bf16* p, int64_t ld, int64_t col0, int64_t kbeg,
+                                        int wave, int lane, bool tiled) {
+    gbase = reinterpret_cast<const char*>(p) + 2 * (kbeg * ld + (tiled ? 16 * col0 : col0));
+    tstep = 2 * BK * ld;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int r = 8 * wave + 4 * c + (lane >> 4);
+      const int ch = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int64_t e = tiled ? (int64_t)(r & 16) * ld + 256 * (ch >> 1) + 16 * (r & 15) + 8 * (ch & 1)
+                              : (int64_t)r * ld + 8 * ch;
+      voff[c] = static_cast<uint32_t>(2 * e);
+    }
+  }
+  // copy k-tile kt into the image at LDS byte address `plane` (this wave's rows)
+  __device__ __forceinline__ void issue(uint32_t plane, int wave, int kt) const {
+    const char* g = gbase + kt * tstep;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane(plane + 256u * (8 * wave + 4 * c));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :
+                   : "s"(m0), "v"(voff[c]), "s"(g)
+                   : "memory", "m0");
+#pragma clang diagnostic pop
+    }
+  }
+  // the same copies through registers, rows at or past `rows_left` zero (the ragged last tile)
+  __device__ __forceinline__ void issue_ragged(char* plane, int wave, int lane, int kt,
+                                               int64_t rows_left) const {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int r = 8 * wave + 4 * c + (lane >> 4);
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (r < rows_left) v = *reinterpret_cast<const uint4*>(gbase + kt * tstep + voff[c]);
+      *reinterpret_cast<uint4*>(plane + 256 * (8 * wave + 4 * c) + 16 * lane) = v;
+    }
+    // s_barrier does not wait for LDS writes: land them before the tile's barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+};
+
+__global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_dma(Params p) {
+  __shared__ __align__(16) char smem[DNB * 2 * TT_PLANE];  // DNB stages x (A, B) images
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn, tile, z;
+  if (!split_of(p, tile, z)) return;
+  if (!tile_of(p, tile, tm, tn)) return;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)z * p.kchunk;
+  const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
+  const DmaOperand da(reinterpret_cast<const __bf16*>(p.A), p.lda, m0, kbeg, wave, lane, p.a_tiled);
+  const DmaOperand db(reinterpret_cast<const __bf16*>(p.B), p.ldb, n0, kbeg, wave, lane, p.b_tiled);
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
+  // copies of k-tile kt into stage kt % DNB (4 per wave: 2 per operand)
+  auto issue = [&](int kt) {
+    const int st = kt % DNB;
+    const int64_t left = kend - (kbeg + (int64_t)kt * BK);
+    if (left >= BK) {
+      da.issue(lds0 + st * 2 * TT_PLANE, wave, kt);
+      db.issue(lds0 + st * 2 * TT_PLANE + TT_PLANE, wave, kt);
+    } else {
+      dma_wait_vm(0);
+      da.issue_ragged(smem + st * 2 * TT_PLANE, wave, lane, kt, left);
+      db.issue_ragged(smem + st * 2 * TT_PLANE + TT_PLANE, wave, lane, kt, left);
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const bool want_rows = p.rowsum && tn == 0;
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // this thread's column-sum runs in the A image: rows kl0, kl0 + 16, columns cl .. cl + 7
+  const int kl0 = tid >> 4, cl = 8 * (tid & 15);
+  for (int kt = 0; kt < DNB - 1 && kt < nk; ++kt) issue(kt);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's copies of tile kt have landed once only the later tiles' may be pending
+    const int later = (kt + DNB - 2 < nk - 1 ? kt + DNB - 2 : nk - 1) - kt;
+    dma_wait_vm(4 * later);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // every wave is past tile kt - 1's reads: its stage takes tile kt + DNB - 1
+    if (kt + DNB - 1 < nk) issue(kt + DNB - 1);
+    const char* s = smem + (kt % DNB) * 2 * TT_PLANE;
+    if (want_rows) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint4 v = *reinterpret_cast<const uint4*>(s + tt_off(kl0 + 16 * j, cl >> 3));
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t d = w[e >> 1];
+          rs[e] = __fadd_rn(rs[e], __uint_as_float((e & 1) ? (d & 0xffff0000u) : (d << 16)));
+        }
+      }
+    }
+    bf8 b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = tt_frag(s + TT_PLANE, 8 * wn + 2 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf8 a = tt_frag(s, 8 * wm + 2 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  dma_wait_vm(0);
+  __syncthreads();  // LDS free for the row-sum reduction
+  const bool split = p.zsplit > 1;
+  if (want_rows) {
+    float* red = reinterpret_cast<float*>(smem);  // [16][128]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[kl0 * BM + cl + e] = rs[e];
+    __syncthreads();
+    if (tid < BM) {
+      float v = red[tid];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) v = __fadd_rn(v, red[q * BM + tid]);
+      if (split) p.rowsum_part[(int64_t)z * p.M + m0 + tid] = v;
+      else p.rowsum[m0 + tid] = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        float v = acc[i][j][r];
+        if (split) {
+          p.part[((int64_t)z * p.M + m) * p.N + n] = v;
+          continue;
+        }
+        float* c = p.C + m * p.ldc + n;
+        if (p.accumulate) v = __fadd_rn(*c, v);
+        *c = v;
+      }
+    }
+}
+
 template <typename TA, typename TB>
 static void launch_bf(const Params& p, bool va, bool vb, dim3 grid, hipStream_t st) {
 #define AON_BF_L(VA_, VB_) \
@@ -641,11 +1086,26 @@ static void launch_bf(const Params& p, bool va, bool vb, dim3 grid, hipStream_t 
 using namespace aon;
 using namespace aon::gemm;
 
+// both operands bf16 and reduction-major in whole 128 x 128 tiles with 16-B runs: the LDS-DMA
+// kernel (k_gemm_bf16_dma)
+static bool bf16_copy_path(const aon_gemm_args* a) {
+  const int64_t b_rdiv = a->b_kc ? 1 : a->b_rdiv;
+  return a->mma_bf16 && a->a_bf16 && a->b_bf16 && a->M % BM == 0 && a->N % BN == 0 &&
+         b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) && a->lda % 8 == 0 && a->ldb % 8 == 0;
+}
+
 static int64_t gemm_splits(const aon_gemm_args* a) {
   const int64_t tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
   // split the reduction only when the tile grid alone cannot fill the chip and K is long
   if (a->k_splits > 0) return a->k_splits;
   if (tiles >= 512 || a->K < 8 * 1024 || a->A2) return 1;
+  if (bf16_copy_path(a) && AON_GEMM_BF_DMA) {
+    // one round of 512 workgroups: 128 splits of a 2 x 2 tile grid measured 0.196 ms against
+    // 0.216 / 0.233 ms for 192 / 256 (profiles/r02/ab_gemm)
+    const int64_t cap = a->K / 2048 < 256 ? a->K / 2048 : 256;
+    const int64_t s = 512 / tiles < cap ? 512 / tiles : cap;
+    return s >= 8 ? s / 8 * 8 : (s < 1 ? 1 : s);
+  }
   // whole rounds of 512 workgroups (2 per CU): two rounds when K is long enough, else one --
   // a grid a few workgroups past a round runs its tail as a second, nearly empty round (a
   // 266k-row weight gradient on 544 workgroups took as long as one on 1024)
@@ -731,7 +1191,11 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     // element size of each operand: 8-B (bf16) or 16-B (fp32) runs of 4 rows
     const bool va16 = a->a_bf16 ? (reinterpret_cast<uintptr_t>(a->A) & 7) == 0 && a->lda % 4 == 0 : va;
     const bool vb16 = a->b_bf16 ? (reinterpret_cast<uintptr_t>(a->B) & 7) == 0 && a->ldb % 4 == 0 : vb;
-    if (a->a_bf16 && a->b_bf16) launch_bf<__bf16, __bf16>(p, va16, vb16, grid, st);
+    // both bf16, whole 128 x 128 tiles, 16-B runs: the copy-staged kernels
+    const bool tt = bf16_copy_path(a);
+    if (tt && AON_GEMM_BF_DMA) hipLaunchKernelGGL(k_gemm_bf16_dma, grid, dim3(THREADS), 0, st, p);
+    else if (tt) hipLaunchKernelGGL(k_gemm_bf16_tt, grid, dim3(THREADS), 0, st, p);
+    else if (a->a_bf16 && a->b_bf16) launch_bf<__bf16, __bf16>(p, va16, vb16, grid, st);
     else if (a->a_bf16) launch_bf<__bf16, float>(p, va16, vb16, grid, st);
     else if (a->b_bf16) launch_bf<float, __bf16>(p, va16, vb16, grid, st);
     else launch_bf<float, float>(p, va16, vb16, grid, st);
