@@ -75,6 +75,7 @@ _SIGNATURES = {
     "aon_mlp_bwd_pack_bf16": (c_int, [ctypes.POINTER(AonMlpParams), vp, vp]),
     "aon_mlp_bwd_bf16": (c_int, [vp, vp, vp, c_i64, vp, vp, vp, vp, vp]),
     "aon_relu_masks": (c_int, [vp, c_i64, c_int, vp, vp]),
+    "aon_absmax": (c_int, [vp, c_i64, vp, vp]),
     "aon_mlp_bwd_packed_bytes": (c_size, []),
     "aon_mlp_bwd_pack": (c_int, [ctypes.POINTER(AonMlpParams), vp, vp]),
     "aon_mlp_bwd": (c_int, [vp, vp, vp, c_i64, vp, vp, vp, vp, vp]),

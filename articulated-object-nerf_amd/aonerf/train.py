@@ -54,51 +54,66 @@ def _forward_level(P, enc, venc, S, raw, noise=None):
     return h, bot, hv
 
 
-def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
-    """Autograd of _forward_level: G[i] = (dW, db) of layer i, from dL/draw (R x 4)."""
-    R, dev = enc.shape[0], enc.device
-    gs, acts = GRAD_SCALE, ACT_SCALE
+def _amax_word(x, word):
+    """word (one int32 of a device tensor) = the bits of max |x| (aon_absmax): the per-call
+    scale of a gradient operand's fp16 hi/lo split (include/aonerf.h a_amax)."""
+    L.call("aon_absmax", L.ptr(x), x.numel(), L.ptr(word), L.stream(x.device))
+    return word
 
-    def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, ldw=None, db=None):
+
+def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
+    """Autograd of _forward_level: G[i] = (dW, db) of layer i, from dL/draw (R x 4).  Every
+    gradient operand dY enters the f16x3 split at its own per-call power-of-two scale from
+    max |dY| (aon_absmax -> aon_gemm a_amax), as the fused chain scales its d raw: a fixed
+    prescale would push the small dL/dz of a late-training step into fp16's subnormals."""
+    R, dev = enc.shape[0], enc.device
+    acts = ACT_SCALE
+    words = torch.zeros((8,), dtype=torch.int32, device=dev)
+
+    def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, ldw=None, db=None, amax=None):
         # dW[:, col0:col0+n_in] = dY^T X (K = rows, split over workgroups); db = sum_rows dY
         # from the same pass over dY
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
-             b_kc=False, b_rdiv=rdiv, ldc=ldw or dW.shape[1], a_scale=gs, b_scale=acts,
-             rowsum=db)
+             b_kc=False, b_rdiv=rdiv, ldc=ldw or dW.shape[1], a_scale=1.0, b_scale=acts,
+             rowsum=db, a_amax=amax)
 
-    def dinput(dX, dY, ldy, n_out, W, n_in, mask=None, accumulate=False):
+    def dinput(dX, dY, ldy, n_out, W, n_in, mask=None, accumulate=False, amax=None):
         # dX (R x n_in) = dY W[:, :n_in] (* relu mask)
         gemm(dX, dY, W, R, n_in, n_out, lda=ldy, a_kc=True, ldb=W.shape[1], b_kc=False,
              ldc=dX.shape[1], mask=mask, ldm=mask.shape[1] if mask is not None else 0,
-             accumulate=accumulate, a_scale=gs, b_scale=W_SCALE)
+             accumulate=accumulate, a_scale=1.0, b_scale=W_SCALE, a_amax=amax)
 
     # rgb head (N=3) and view layer
-    dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1])
+    wd = _amax_word(draw, words[0:1])  # d raw (its sigma column too: a max over both is safe)
+    dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1], amax=wd)
     dhv = torch.empty((R, 128), device=dev)
-    dinput(dhv, draw, 4, 3, P[11][0], 128, mask=hv)
-    dweight(G[10][0], dhv, 128, 128, bot, 256, 256, db=G[10][1])
-    dweight(G[10][0], dhv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
+    dinput(dhv, draw, 4, 3, P[11][0], 128, mask=hv, amax=wd)
+    wv = _amax_word(dhv, words[1:2])
+    dweight(G[10][0], dhv, 128, 128, bot, 256, 256, db=G[10][1], amax=wv)
+    dweight(G[10][0], dhv, 128, 128, venc, 27, 27, rdiv=S, col0=256, amax=wv)
     dbot = torch.empty((R, 256), device=dev)
-    dinput(dbot, dhv, 128, 128, P[10][0], 256)
+    dinput(dbot, dhv, 128, 128, P[10][0], 256, amax=wv)
     del dhv
     # bottleneck + density heads on h7
-    dweight(G[9][0], dbot, 256, 256, h[7], 256, 256, db=G[9][1])
-    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256, db=G[8][1])
+    wb = _amax_word(dbot, words[2:3])
+    dweight(G[9][0], dbot, 256, 256, h[7], 256, 256, db=G[9][1], amax=wb)
+    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256, db=G[8][1], amax=wd)
     dy = torch.empty((R, 256), device=dev)
-    dinput(dy, dbot, 256, 256, P[9][0], 256)
-    dinput(dy, draw[:, 3:], 4, 1, P[8][0], 256, mask=h[7], accumulate=True)
+    dinput(dy, dbot, 256, 256, P[9][0], 256, amax=wb)
+    dinput(dy, draw[:, 3:], 4, 1, P[8][0], 256, mask=h[7], accumulate=True, amax=wd)
     del dbot
     dx = torch.empty((R, 256), device=dev)
     for i in range(7, -1, -1):  # dy = dL/d(pre-activation of layer i)
+        wy = _amax_word(dy, words[3 + (i & 1):4 + (i & 1)])
         if i == 5:
-            dweight(G[5][0], dy, 256, 256, h[4], 256, 256, db=G[5][1])
-            dweight(G[5][0], dy, 256, 256, enc, 63, 63, col0=256)
+            dweight(G[5][0], dy, 256, 256, h[4], 256, 256, db=G[5][1], amax=wy)
+            dweight(G[5][0], dy, 256, 256, enc, 63, 63, col0=256, amax=wy)
         elif i == 0:
-            dweight(G[0][0], dy, 256, 256, enc, 63, 63, db=G[0][1])
+            dweight(G[0][0], dy, 256, 256, enc, 63, 63, db=G[0][1], amax=wy)
         else:
-            dweight(G[i][0], dy, 256, 256, h[i - 1], 256, 256, db=G[i][1])
+            dweight(G[i][0], dy, 256, 256, h[i - 1], 256, 256, db=G[i][1], amax=wy)
         if i > 0:
-            dinput(dx, dy, 256, 256, P[i][0], 256, mask=h[i - 1])
+            dinput(dx, dy, 256, 256, P[i][0], 256, mask=h[i - 1], amax=wy)
             dx, dy = dy, dx
 
 

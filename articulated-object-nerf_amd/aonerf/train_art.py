@@ -33,7 +33,7 @@ import torch
 from . import _lib as L
 from . import tiles
 from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, gemm
-from .train import Adam, img2mse, learning_rate, mse2psnr, relu_masks  # noqa: F401 (shared)
+from .train import Adam, _amax_word, img2mse, learning_rate, mse2psnr, relu_masks  # noqa: F401 (shared)
 
 # parameter layout of one articulated NeRFMLP in ArtRenderLevel: 20 layers x (weight, bias)
 DEF0, DL, PTS0, DENS, BOT, VIEW0, RGB = 0, 4, 5, 13, 14, 15, 19
@@ -224,28 +224,34 @@ def _fused_ok(geo):
 
 def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw):
     """Autograd of _forward_level from dL/draw (R x 4): G[i] = (dW, db) of layer i; dlat =
-    (dshape, dapp, dart) (1 x n each) receive the latent-code gradients."""
+    (dshape, dapp, dart) (1 x n each) receive the latent-code gradients.  Every dY enters the
+    f16x3 split at a per-call power-of-two scale from max |dY| (aon_absmax -> a_amax; for the
+    density column of d raw, from all of d raw), as the fused chain scales its gradients."""
     R, dev = xyz.shape[0], xyz.device
     wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
     shape, app, art = lat
     dshape, dapp, dart = dlat
     gs, acts = GRAD_SCALE, ACT_SCALE
+    word = torch.zeros((1,), dtype=torch.int32, device=dev)  # stream-ordered: reused per call
+
+    def amax(dY):
+        return _amax_word(draw if dY.data_ptr() == draw.data_ptr() + 12 else dY, word)
 
     def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True):
         # dW_i[:, col0:col0+n_in] = dY^T X (K = rows, split-K); db_i = sum_rows dY, same pass
         dW = G[i][0]
         n_out = dW.shape[0]
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
-             b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0), a_scale=gs, b_scale=acts,
-             rowsum=G[i][1] if bias else None)
+             b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0), a_scale=1.0, b_scale=acts,
+             rowsum=G[i][1] if bias else None, a_amax=amax(dY))
 
     def dinput(dX, dY, ldy, i, col0, n_in, mask=None, accumulate=False):
         # dX (R x n_in) (+)= dY W_i[:, col0:col0+n_in] (* relu'(mask))
         W = P[i][0]
         gemm(dX, dY, W[:, col0:] if col0 else W, R, n_in, W.shape[0], lda=ldy, a_kc=True,
              ldb=W.stride(0), b_kc=False, ldc=dX.stride(0), mask=mask,
-             ldm=mask.stride(0) if mask is not None else 0, accumulate=accumulate, a_scale=gs,
-             b_scale=W_SCALE)
+             ldm=mask.stride(0) if mask is not None else 0, accumulate=accumulate, a_scale=1.0,
+             b_scale=W_SCALE, a_amax=amax(dY))
 
     def dlatent(i, col0, l, dl, accumulate):
         # z = W [x; l] + b with l on every row: dW[:, col0:col0+n] = db l^T, dl (+)= db^T W_l

@@ -226,6 +226,11 @@ static int bwd_launch(const void* packed, const float* draw, const uint32_t* mas
   return launch_status(bf16 ? "aon_mlp_bwd_bf16" : "aon_mlp_bwd");
 }
 
+extern "C" int aon_absmax(const float* x, int64_t n, uint32_t* out, aon_stream_t stream) {
+  AON_REQUIRE(x && out && n >= 0, "bad arguments");
+  return absmax(x, n, out, (hipStream_t)stream);
+}
+
 extern "C" int aon_mlp_bwd(const void* packed, const float* draw, const uint32_t* masks,
                            int64_t N, float* dzv, float* dzb, float* dz, void* work,
                            aon_stream_t stream) {

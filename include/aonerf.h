@@ -206,6 +206,11 @@ int aon_mlp_fwd_train_bf16(const void* packed, const float* rays_o, const float*
  * after a layer-by-layer forward (threshold_backward of model.py:95-120's ReLUs). */
 int aon_relu_masks(const float* h, int64_t N, int width, uint32_t* masks, aon_stream_t stream);
 
+/* out = the bits of max |x| over n floats (one uint32 of device memory): the per-call gradient
+ * scale word aon_gemm's a_amax takes (the layer-by-layer backward scales each dY by it, as the
+ * fused chains scale theirs by max |d raw|). */
+int aon_absmax(const float* x, int64_t n, uint32_t* out, aon_stream_t stream);
+
 /* Backward chain of one level's NeRFMLP for the training step (model.py:95-120 under
  * autograd): from draw (B*S, 4) = dL/d[raw_rgb, raw_sigma] (aon_composite_bwd), all input-
  * gradient products dX = dZ W down to pts_linears.0 in one fused kernel, each masked by ReLU'

@@ -449,3 +449,45 @@ def test_train_step_c5_4096_rays():
         worst = max(worst, e / allow)
         assert e <= allow, (name, e, env)
     print(f"C5 teacher-forced grads (4096 rays): worst error / allowance {worst:.2f}")
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["gemm_backward", "fused_chain"])
+def test_backward_gradient_scale_invariance(fused):
+    """Late-training gradient magnitudes (a fixed 2^10 prescale of dY before the
+    fp16 hi/lo split would push small dL/dz into fp16's subnormals).  Both backward paths scale
+    every gradient operand per call by a power of two from its own max |dY| (aon_absmax /
+    k_absmax -> a_amax), so d raw x 2^-24 -- a loss ~1.7e7 times smaller than the 64-ray
+    golden's -- must give every weight and bias gradient x 2^-24 BIT FOR BIT; d raw x 2^20
+    likewise."""
+    from aonerf import train
+
+    net = _make_trainable(0)
+    gen = torch.Generator().manual_seed(5)
+    B, S = 61, 65
+    R = B * S
+    o = (torch.rand(B, 3, generator=gen) - 0.5).cuda()
+    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=gen), dim=-1).cuda()
+    t = (2.0 + 4.0 * torch.rand(B, S, generator=gen)).sort(-1).values.cuda()
+    P = [(m.weight.detach(), m.bias.detach()) for m in net.fine_mlp._layers()]
+    L = train.L
+    enc = torch.empty((R, 63), device="cuda")
+    L.call("aon_cast_rays", L.ptr(o), L.ptr(d), L.ptr(t), B, S, None, 0, None, 0, 10, L.ptr(enc),
+           L.stream(o.device))
+    venc = torch.empty((B, 27), device="cuda")
+    L.call("aon_pos_enc", L.ptr(d), B, 0, 4, L.ptr(venc), L.stream(o.device))
+    raw = torch.empty((R, 4), device="cuda")
+    h, bot, hv = train._forward_level(P, enc, venc, S, raw)
+    draw = (torch.randn(R, 4, generator=gen) * 1e-4).cuda()
+    out = {}
+    for k in (0, -24, 20):
+        G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
+        dr = draw * 2.0 ** k
+        if fused:
+            train._backward_level_fused(P, G, enc, venc, S, h, bot, hv, dr, h_tiled=False)
+        else:
+            train._backward_level(P, G, enc, venc, S, h, bot, hv, dr)
+        out[k] = [g for pair in G for g in pair]
+    torch.cuda.synchronize()
+    for k in (-24, 20):
+        for i, (a, b) in enumerate(zip(out[k], out[0])):
+            assert torch.equal(a * 2.0 ** -k, b), (k, i, float((a * 2.0 ** -k - b).abs().max()))
