@@ -1,13 +1,18 @@
 // Fused NeRFMLP forward on fp16 MFMA with a 3-product hi/lo split ("fp16x3").
 //
-// Every operand x is carried as x_hi = fp16(x) and x_lo = fp16((x - x_hi) * 2^11): together
-// ~22 significant bits.  A weight-activation product is w_hi*x_hi + 2^-11 (w_hi*x_lo + w_lo*x_hi)
-// (the dropped w_lo*x_lo term is 2^-22 relative), each on v_mfma_f32_16x16x32_f16 with fp32
-// accumulation into two accumulators (hi*hi, and the 2^11-scaled cross terms).  That is 3 fp16
-// MFMAs per 32-deep k-step where the fp32 path needs 8 v_mfma_f32_16x16x4_f32 of twice the
-// cycles: 16/3 = 5.3x the arithmetic rate at fp32-class accuracy (measured against the
-// reference in tests/test_gpu_parity.py).  Activations and biases are carried at 2^-8 scale so
-// fp16 cannot overflow below |x| = 1.6e7; the scaling is exact (powers of two).
+// Every operand x is carried as x_hi = fp16(x) and x_lo = fp16(x - x_hi) (x - x_hi is exact in
+// fp32): together ~22 significant bits.  A weight-activation product is
+// w_hi*x_hi + w_hi*x_lo + w_lo*x_hi (the dropped w_lo*x_lo term is 2^-22 relative), three
+// v_mfma_f32_16x16x32_f16 into ONE fp32 accumulator.  That is 3 fp16 MFMAs per 32-deep k-step
+// where the fp32 path needs 8 v_mfma_f32_16x16x4_f32 of twice the cycles: 16/3 = 5.3x the
+// arithmetic rate at fp32-class accuracy (measured against the reference in
+// tests/test_gpu_parity.py).  Scales (exact powers of two, mlp_layout.hpp AON_F16X3_V2):
+// activations ride at 2^3 (kActS) and weights at 2^6 (kWS), so the unscaled lo parts stay
+// normal in fp16 for |activation| >= 2^-6 and the products share the accumulator at 2^9; the
+// epilogue folds 2^-6 and the bias into one fma.  fp16 then bounds a hidden activation at
+// |x| < 65504 / 2^3 ~ 8188: every split value is range-tested and a wave that meets one sets
+// the pack's status word (range guard, mlp_f16x3_core.hpp or_ballot; aon_mlp_read_status),
+// and the callers fall back to the fp32 path or refuse the training step.
 //
 // Structure (mlp_layout.hpp kLayersH): feature-major tiles as in mlp.hip; a wave owns 16*NCOL
 // samples; output tiles are produced in pairs (u, u+1) whose accumulators, converted in the

@@ -63,13 +63,14 @@ constexpr LayerDesc kLayersH[kNumLayers] = {
     {4, 0, 1, 128, 0, 3, 2336, 2448},
 };
 
-// activations and biases of the fp16x3 path are carried at 2^-8 scale (overflow only past
-// |x| = 65504 * 256); the lo halves are carried at 2^11 scale
+// V1 numerics (AON_F16X3_V2 = 0, kept for A/B only): activations and biases carried at 2^-8,
+// lo halves at 2^11, two accumulators
 constexpr float kActScale = 1.0f / 256.0f;
 constexpr float kLoScale = 2048.0f;
-// V2 numerics (AON_F16X3_V2): activations carried at 2^3, weights at 2^6, so the lo parts
-// (x - fp16(x)) stay in fp16's normal range unscaled and hi*hi, hi*lo, lo*hi share ONE fp32
-// accumulator at scale 2^9; the epilogue folds the 2^-6 and the bias into one fma.
+// V2 numerics (AON_F16X3_V2, the default): activations carried at 2^3, weights at 2^6, so the
+// lo parts (x - fp16(x)) stay in fp16's normal range unscaled and hi*hi, hi*lo, lo*hi share ONE
+// fp32 accumulator at scale 2^9; the epilogue folds the 2^-6 and the bias into one fma.  A
+// hidden activation past 65504 / 2^3 overflows the hi part: the range guard reports it.
 #ifndef AON_F16X3_V2
 #define AON_F16X3_V2 1
 #endif
