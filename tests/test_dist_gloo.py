@@ -35,7 +35,9 @@ def _worker(rank, world, port, H, W, q):
     try:
         frame = gather_frame(fake_payload(H, W, rank, world), H, W, dst=0)
         if rank == 0:
-            q.put(frame)
+            # numpy: pickled by value (a torch CPU tensor crosses the queue as a shared-memory
+            # handle that dies with this process if the parent has not mapped it yet)
+            q.put(frame.numpy())
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -68,7 +70,7 @@ def test_gather_frame_gloo_world2(H, W):
     procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, q)) for r in range(world)]
     for p in procs:
         p.start()
-    frame = q.get(timeout=120)
+    frame = torch.from_numpy(q.get(timeout=120))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -90,7 +92,7 @@ def _ddp_worker(rank, world, port, q):
         for i, p in enumerate(ps):
             p.grad = torch.full(p.shape, float(rank + 1) * (i + 1))
         GradAllReduce(ps)()
-        q.put((rank, [p.grad.clone() for p in ps]))
+        q.put((rank, [p.grad.numpy().copy() for p in ps]))  # by value (see _worker)
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -111,4 +113,5 @@ def test_grad_allreduce_gloo_world2():
         assert p.exitcode == 0
     for _, grads in got:
         for i, gr in enumerate(grads):
+            gr = torch.from_numpy(gr)
             assert torch.equal(gr, torch.full(gr.shape, 1.5 * (i + 1)))
