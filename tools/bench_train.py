@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--max-steps", type=int, default=200000, help="schedule length (run_max_steps)")
+    ap.add_argument("--precision", choices=("f16x3", "bf16"), default="f16x3",
+                    help="train.PRECISION of the vanilla step (bf16: C5's bf16 mode)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -50,6 +52,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     from aonerf import train
     from aonerf.model import NeRF
+
+    train.PRECISION = args.precision
     from aonerf.parallel import GradAllReduce
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, sapien_focal
@@ -127,7 +131,8 @@ def main():
                        "training rays/sec (LitNeRF.training_step, 64c+128f, randomized, Adam)"),
             "value": rays / dt, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1000 * dt / args.steps,
-            "higher_is_better": True, "scaling": "weak", "dtype": "f16x3 (fp16 hi/lo split MFMA)",
+            "higher_is_better": True, "scaling": "weak",
+            "dtype": "bf16 (bf16 MFMA)" if args.precision == "bf16" and not art else "f16x3 (fp16 hi/lo split MFMA)",
             "data": "synthetic", "config": {"workload": "C5 training step" + (" (articulated)" if art else ""),
                                              "rays_per_rank": args.rays,
                                              "parallelism": f"ddp{world}"},
