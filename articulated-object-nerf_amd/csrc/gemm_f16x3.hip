@@ -364,18 +364,40 @@ __device__ __forceinline__ float sum_z(const float* src, int64_t stride, int spl
   return v;
 }
 
+// Four lanes per output: lane q sums the partials of the q-th quarter of the chunks in z order,
+// then the quarters combine as (q0 + q1) + (q2 + q3) -- a fixed order (deterministic), a quarter
+// of the dependent load rounds per thread and 4x the threads of a one-lane-per-output reduce
+// (whose 256 workgroups of sequential partial loads took ~11 us per weight gradient).
+__device__ __forceinline__ float sum_z4(const float* src, int64_t stride, int splits, int q) {
+  const int zq = (splits + 3) / 4;
+  const int z0 = q * zq, z1 = z0 + zq < splits ? z0 + zq : splits;
+  float v = 0.f;
+  if (z0 < z1) v = sum_z(src + (int64_t)z0 * stride, stride, z1 - z0);
+  const float w = __shfl_xor(v, 1, 64);  // lanes 4e + q: q0 + q1 and q2 + q3
+  const float pair = (q & 1) ? __fadd_rn(w, v) : __fadd_rn(v, w);
+  const float other = __shfl_xor(pair, 2, 64);
+  return (q & 2) ? __fadd_rn(other, pair) : __fadd_rn(pair, other);
+}
+
 __global__ void k_gemm_reduce(Params p, int splits) {
   const int64_t total = p.M * p.N;
   const int64_t extra = p.rowsum ? p.M : 0;  // rowsum entries ride along as e >= total
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total + extra;
-       e += (int64_t)gridDim.x * blockDim.x) {
+  const int q = threadIdx.x & 3;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  // every lane of a wave takes part in the shuffles: the loop bound is per group of 4 lanes and
+  // the grid stride a multiple of 4, so a group's lanes run the same iterations
+  for (int64_t e4 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (e4 >> 2) < total + extra;
+       e4 += nthreads) {
+    const int64_t e = e4 >> 2;
     if (e >= total) {
       const int64_t m = e - total;
-      p.rowsum[m] = sum_z(p.rowsum_part + m, p.M, splits);
+      const float v = sum_z4(p.rowsum_part + m, p.M, splits, q);
+      if (q == 0) p.rowsum[m] = v;
       continue;
     }
     const int64_t m = e / p.N, n = e - m * p.N;
-    float v = sum_z(p.part + e, total, splits);
+    float v = sum_z4(p.part + e, total, splits, q);
+    if (q != 0) continue;
     float* c = p.C + m * p.ldc + n;
     if (p.accumulate) v = __fadd_rn(*c, v);
     if (p.bias) v = __fadd_rn(v, p.bias[n]);
@@ -1206,7 +1228,7 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   if (zs > 1) {
     const int rc = launch_status(__func__);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_gemm_reduce, grid_for(a->M * a->N + a->M, 256, 4096), 256, 0, st, p, (int)zs);
+    hipLaunchKernelGGL(k_gemm_reduce, grid_for(4 * (a->M * a->N + a->M), 256, 16384), 256, 0, st, p, (int)zs);
   }
   return launch_status(__func__);
 }
