@@ -68,7 +68,9 @@ struct Params {
 __device__ __forceinline__ int64_t km_off(int64_t k, int64_t row, int64_t ld, int64_t rdiv,
                                           bool tiled) {
   if (tiled) return (k & ~int64_t(15)) * ld + 256 * (row >> 4) + 16 * (k & 15) + (row & 15);
-  return (rdiv == 1 ? k : k / rdiv) * ld + row;
+  // 32-bit division (aon_gemm checks K < 2^32): a 64-bit one is a ~40-instruction sequence
+  const int64_t kr = rdiv == 1 ? k : (int64_t)((uint32_t)k / (uint32_t)rdiv);
+  return kr * ld + row;
 }
 
 // Workgroups are dispatched round-robin over the 8 XCDs (block L -> XCD L mod 8), each with
@@ -1154,6 +1156,8 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
               "A2 needs a_kc, 0 <= K1 <= K, lda2 >= 1, a2_rdiv >= 1");
   AON_REQUIRE(!a->mask || a->ldm >= a->N, "bad mask leading dimension");
   AON_REQUIRE(a->b_kc || a->b_rdiv >= 1, "b_rdiv must be >= 1");
+  AON_REQUIRE(a->K < (int64_t(1) << 32) && (a->b_kc || a->b_rdiv < (int64_t(1) << 32)),
+              "K and b_rdiv must be below 2^32");
   AON_REQUIRE(a->a_scale > 0.f && a->b_scale > 0.f, "operand scales must be positive");
   const bool bf = a->mma_bf16 != 0;
   AON_REQUIRE(bf || (!a->a_bf16 && !a->b_bf16), "bf16 operands need mma_bf16");
