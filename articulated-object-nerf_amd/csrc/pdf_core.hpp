@@ -96,6 +96,10 @@ __device__ __forceinline__ int count_lt(const float* a, int n, float x) {
          : AON_PDF_SEARCH2 ? count_sorted<false>(a, n, x) : count_lt_bin(a, n, x);
 }
 
+#ifndef AON_PDF_HINT_MERGE
+#define AON_PDF_HINT_MERGE 1  // 0: merge by binary searches on both sides
+#endif
+
 #ifndef AON_PDF_DPP_SCAN
 #define AON_PDF_DPP_SCAN 1  // 0: the shuffle (ds_bpermute) scan
 #endif
@@ -165,15 +169,18 @@ __device__ __forceinline__ void pdf_ray(PdfLds<NBX>& L, const float* w, int nb, 
   }
   wave_sync();
   // ---- inverse cdf (helper.py:232-241)
+  int hint[NBX];  // sample j's lower bin i0: t_merge[0 .. i0] <= sample (the merge's start)
 #pragma unroll
   for (int b = 0; b < NBX; ++b) {
     const int j = 64 * b + lane;
+    hint[b] = 0;
     if (j >= Ns_pow2) break;
     float s = __builtin_inff();  // sort padding
     if (j < Ns) {
       const float uj = cu[b];
       const int idx = count_le(L.cdf, nb, uj);
       const int i0 = idx - 1 < 0 ? 0 : (idx - 1 > nb - 1 ? nb - 1 : idx - 1);
+      hint[b] = i0;
       const int i1 = idx > nb - 1 ? nb - 1 : idx;
       const float c0 = L.cdf[i0], c1 = L.cdf[i1];
       const float b0 = L.bins[i0], b1 = L.bins[i1];
@@ -214,6 +221,60 @@ __device__ __forceinline__ void pdf_ray(PdfLds<NBX>& L, const float* w, int nb, 
     dx = rd[3 * ray]; dy = rd[3 * ray + 1]; dz = rd[3 * ray + 2];
   }
   float* xo = xyz ? xyz + ray * No * 3 : nullptr;
+#if AON_PDF_HINT_MERGE
+  if (merge && !need_sort) {
+    // Samples in u order are ascending: sample j's bin i0 bounds its rank in t_merge from below
+    // (t_merge[i0] <= bins[i0] <= sample, bins = mids of t_merge), and it lies below
+    // t_merge[i0 + 2] but for ties, so a short walk replaces the binary search.  The merged
+    // row's remaining slots then take t_merge in order: slot p's rank among the empty slots
+    // comes from a ballot + mbcnt per 64 slots (no search over the samples).  Same positions as
+    // the searches below (ties: count_le / count_lt put samples after equal t, t before).
+    uint8_t* filled = reinterpret_cast<uint8_t*>(L.cdf);  // free after the inverse cdf
+    for (int p = lane; p < No; p += 64) filled[p] = 0;
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < NBX; ++b) {
+      const int j = 64 * b + lane;
+      if (j < Ns) {
+        const float s = L.samp[j];
+        int c = hint[b] + 1;
+        if (c > Nt || L.tm[c - 1] > s) {
+          c = count_le(L.tm, Nt, s);  // bins that are not t_merge's mids: no bound, search
+        } else {
+          while (c < Nt && L.tm[c] <= s) ++c;
+        }
+        const int pos = j + c;
+        filled[pos] = 1;
+        o[pos] = s;
+        if (xo) {
+          xo[3 * pos] = __fadd_rn(ox, __fmul_rn(s, dx));
+          xo[3 * pos + 1] = __fadd_rn(oy, __fmul_rn(s, dy));
+          xo[3 * pos + 2] = __fadd_rn(oz, __fmul_rn(s, dz));
+        }
+      }
+    }
+    wave_sync();
+    int carry = 0;  // empty slots before this 64-slot block
+    for (int p0 = 0; p0 < No; p0 += 64) {
+      const int p = p0 + lane;
+      const bool empty = p < No && filled[p] == 0;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(empty);
+      if (empty) {
+        const int rank = carry + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0));
+        const float tv = L.tm[rank];
+        o[p] = tv;
+        if (xo) {
+          xo[3 * p] = __fadd_rn(ox, __fmul_rn(tv, dx));
+          xo[3 * p + 1] = __fadd_rn(oy, __fmul_rn(tv, dy));
+          xo[3 * p + 2] = __fadd_rn(oz, __fmul_rn(tv, dz));
+        }
+      }
+      carry += __builtin_popcountll(m);
+    }
+    return;
+  }
+#endif
   for (int j = lane; j < Ns; j += 64) {
     const float s = L.samp[j];
     const int pos = merge ? j + count_le(L.tm, Nt, s) : j;
