@@ -67,6 +67,13 @@ __global__ __launch_bounds__(64 * kCompWaves, SC > 0 ? AON_MARCH_OCC : 1) void k
       const int i = 64 * b + lane;
       cu[b] = i < Ns ? u_g[ray * u_stride + i] : 0.f;
     }
+#ifdef AON_MARCH_ABL_NOCOMP  // timing-only ablation: weights = raw sigma, no compositing
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (64 * b + lane < S) P[64 * b + lane] = raw[b].w;
+    wave_sync();
+    if (false)
+#endif
     composite_ray<NB, SC>(tt, raw, dirs, ray, S, lane, act, white, P, SM, scratch, sums, out_rgb,
                           out_acc, out_w, out_depth);
     // the resampler's rows: t_merge = this ray's t (already in registers), bins = its mids
@@ -78,8 +85,10 @@ __global__ __launch_bounds__(64 * kCompWaves, SC > 0 ? AON_MARCH_OCC : 1) void k
     wave_sync();
     for (int k = lane; k < nb; k += 64) L.bins[k] = __fmul_rn(0.5f, __fadd_rn(L.tm[k + 1], L.tm[k]));
     // weights[..., 1:-1] straight from the compositor's LDS row (P[0 .. S) = w)
+#ifndef AON_MARCH_ABL_NOPDF  // timing-only ablation (wrong t_fine)
     pdf_ray<NBX>(L, P + 1, nb, Ns, Ns_pow2, cu, true, S, ray, lane, M.orow, nullptr, nullptr,
                  nullptr);
+#endif
     wave_sync();
     // the merged row leaves in wave-contiguous stores (the merge scatters within it)
     const int No = S + Ns;
