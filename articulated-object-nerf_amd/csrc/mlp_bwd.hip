@@ -81,7 +81,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   const int g = lane >> 4, j = lane & 15;
   const int64_t N = a.N;
 
-  WeightPipe<Net, G::kThreads> p;
+  WeightPipeP<Net, G::kThreads, BF> p;
   p.wbuf = smem;
   p.src = wstream;
   p.tid = tid;
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
     stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
   }
 
-  FragPipe<WeightPipe<Net, G::kThreads>, AON_PREFETCH, 0, BF> fp(p);
+  FragPipe<WeightPipeP<Net, G::kThreads, BF>, AON_PREFETCH, 0, BF> fp(p);
   fp.start();
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   const int g = lane >> 4, j = lane & 15;
   const int64_t N = B * S;
 
-  WeightPipe<NetVanillaH, G::kThreads> p;
+  WeightPipeP<NetVanillaH, G::kThreads, BF> p;
   p.wbuf = smem;
   p.src = wstream;
   p.tid = tid;
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   }
 
   Frag<8, NCOL> x, y;
-  using WP = WeightPipe<NetVanillaH, G::kThreads>;
+  using WP = WeightPipeP<NetVanillaH, G::kThreads, BF>;
   using T = typename std::conditional<BF, __bf16, float>::type;
   // wave-uniform branch (readfirstlane): the running range masks stay in SGPRs across it
   // (not the training forward: with its row stores the second copy spills)
@@ -219,7 +219,13 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e < nhalf) {
-      const int blk = static_cast<int>(e >> 9);
+      // bf16: compact stream -- element e of block c is element e of the fp16x3 hi block 2c;
+      // the second half of the stream region is unused (zero)
+      if (a.bf16 && e >= nhalf / 2) {
+        out[e] = static_cast<_Float16>(0.0f);
+        continue;
+      }
+      const int blk = static_cast<int>(a.bf16 ? 2 * (e >> 9) : (e >> 9));
       const int l = static_cast<int>((e >> 3) & 63), jj = static_cast<int>(e & 7);
       float w = 0.f;
       bool lo_part = false;
@@ -258,8 +264,8 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
       }
 #if AON_F16X3_V2
       w *= kWS;  // exact (power of two)
-      if (a.bf16) {  // bf16 mode: the hi block holds bf16(w), the lo block is never read
-        out[e] = lo_part ? static_cast<_Float16>(0.0f) : bf_bits(w);
+      if (a.bf16) {  // bf16 mode: bf16(w) in the compact (hi-only) stream
+        out[e] = bf_bits(w);
         continue;
       }
       const _Float16 h = static_cast<_Float16>(w);

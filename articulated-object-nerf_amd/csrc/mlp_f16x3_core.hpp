@@ -126,7 +126,9 @@ struct FragPipe {
   P& p;
   f4 nh[D], nl[D];  // fragments of the next D steps
   __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
-  __device__ __forceinline__ void fetch_into(int blk, f4& h, f4& l) {
+  __device__ __forceinline__ void fetch_into(int blk_in, f4& h, f4& l) {
+    // BF: the compact stream (WeightPipeP): fp16x3 block 2c (a hi block) is block c
+    const int blk = BF ? blk_in >> 1 : blk_in;
     if (blk >= P::kUsedBlocks) return;
 #ifdef AON_ABLATE_LDS  // timing-only build: reuse the first fragments (no LDS reads, wrong results)
     if (blk >= 2 * D) {
@@ -561,6 +563,13 @@ constexpr int kRingLead = AON_RING_LEAD;  // chunks in flight ahead of the one i
 // Weight pipeline: the LDS-DMA ring over the network's stream
 template <typename Net, int THREADS>
 using WeightPipe = DmaPipe<THREADS, kRing, kChunkH, Net::kStreamBlocks, Net::kBlocks, kRingLead>;
+// The bf16 mode's stream is compact: only the hi blocks (block 2c of the fp16x3 stream is block
+// c), in the first half of the stream region -- the ring moves half the bytes (the zero lo
+// blocks of the fp16x3 layout were ~9% of the bf16 forward and chain, profiles/r02/ab_ring)
+template <typename Net, int THREADS, bool BF>
+using WeightPipeP = typename std::conditional<
+    BF, DmaPipe<THREADS, kRing, kChunkH, Net::kStreamBlocks / 2, Net::kBlocks / 2, kRingLead>,
+    WeightPipe<Net, THREADS>>::type;
 constexpr int kLdsWeights = kRing * kChunkH * 64;  // f4
 
 #ifndef AON_WAVES_H
