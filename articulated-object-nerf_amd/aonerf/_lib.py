@@ -163,14 +163,31 @@ def contig(t):
 # ---------------------------------------------------------------------------- fp16x3 range guard
 # Every packed weight buffer ends in a 16-B status block (include/aonerf.h aon_mlp_read_status):
 # word 0 is set by a fp16x3 kernel that met a value its fp16 hi/lo split cannot hold.  Each
-# training pack registers here when it is (re)packed, so the next optimizer step can refuse
-# gradients computed from such values (and then forgets it).
+# training pack registers here when it is (re)packed (register_pack), so the next optimizer step
+# -- aonerf's Adam, or ANY torch optimizer through the global step pre-hook aonerf.train
+# installs -- can refuse gradients computed from such values (check_pending).  A buffer re-packed
+# before a step looked at it (gradient accumulation, two forwards of one level) first ORs its
+# status word into its device's sticky word, so the re-pack cannot erase an overflow.
 PENDING_PACKS = {}
+_STICKY = {}
 
 
 def status_word(buf):
     """Device int32 0-dim view of a packed buffer's range-status word."""
     return buf.view(torch.int32)[-4]
+
+
+def register_pack(key, buf):
+    """Call BEFORE (re)packing ``buf`` on the current stream: keep the status a pending pack
+    still holds (stream-ordered device OR, no sync), then mark ``buf`` pending."""
+    dev = str(buf.device)
+    k = (key[0], key[1], dev)
+    if k in PENDING_PACKS:
+        w = _STICKY.get(dev)
+        if w is None:
+            w = _STICKY[dev] = torch.zeros((), dtype=torch.int32, device=buf.device)
+        w.bitwise_or_(status_word(PENDING_PACKS[k]))
+    PENDING_PACKS[k] = buf
 
 
 def range_overflow(bufs):
@@ -179,3 +196,16 @@ def range_overflow(bufs):
     if not bufs:
         return False
     return bool(torch.stack([status_word(b) for b in bufs]).any().item())
+
+
+def check_pending(devices=None):
+    """Consume the pending training packs (and sticky words) of ``devices`` (str, None = all):
+    True if any saw an overflow since the last check (one sync; False without a sync when
+    nothing is pending)."""
+    keys = [k for k in PENDING_PACKS if devices is None or k[2] in devices]
+    words = [status_word(PENDING_PACKS.pop(k)) for k in keys]
+    for dev in [d for d in _STICKY if devices is None or d in devices]:
+        words.append(_STICKY.pop(dev))
+    if not words:
+        return False
+    return bool(torch.stack(words).any().item())

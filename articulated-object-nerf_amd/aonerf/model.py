@@ -5,9 +5,10 @@ names, so a reference Lightning checkpoint (``model.coarse_mlp.pts_linears.0.wei
 loads unchanged.  The forward pass runs on the fused HIP kernels:
 
     level 0: aon_sample_along_rays (t only) -> aon_mlp_fwd (xyz + pos_enc + MLP + sigmoid/relu
-             fused) -> aon_composite_fwd (alpha compositing, weights kept)
-    level 1: aon_sample_pdf (mids, pdf/cdf, inverse CDF, sort/merge) -> aon_mlp_fwd
-             -> aon_composite_fwd
+             fused) -> aon_composite_march (alpha compositing fused with the fine level's
+             sample_pdf: the coarse weights stay on chip; FUSED_MARCH / march_ok)
+    level 1: aon_mlp_fwd on the merged t -> aon_composite_fwd
+    (FUSED_MARCH = False, or N_importance > 256: aon_composite_fwd + aon_sample_pdf, bit-identical)
 
 Intermediates live in HBM (a 640x480 frame needs ~1.6 GB), so a whole frame is one launch
 per stage instead of the reference's 80 chunk iterations.
@@ -181,6 +182,12 @@ def composite_march(raw, t_vals, d, white_bkgd, act, u, u_stride, num_fine_sampl
 FUSED_MARCH = True
 
 
+def march_ok(S, num_fine_samples):
+    """The fused march kernel's limits (include/aonerf.h: 3 <= S <= 256, 1 <= Ns <= 256); larger
+    N_importance (up to aon_sample_pdf's 512) takes the two-kernel path."""
+    return FUSED_MARCH and 3 <= S <= 256 and 1 <= num_fine_samples <= 256
+
+
 def level_t_vals(level, o, d, t_prev, w_prev, randomized, near, far, num_coarse_samples,
                  num_fine_samples, lindisp, u_coarse=None, u_fine=None):
     """Sample positions of a level: stratified (helper.py:106-133) or inverse-CDF resampling
@@ -246,6 +253,9 @@ class NeRF(nn.Module):
         training = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         B = o.shape[0]
         dev = o.device
+        # the fp16x3 overflow fallback below re-renders with the same random draws (density
+        # noise, stratified t, fine u) and leaves the generator where one forward leaves it
+        rng = torch.cuda.get_rng_state(dev) if randomized and not training else None
         ret = []
         t_vals = weights = t_next = None
         for level in range(2):
@@ -270,7 +280,7 @@ class NeRF(nn.Module):
             # the last level's weights are an output only when asked for: otherwise the
             # compositor skips writing them (4 B of its 24 B per sample)
             keep_w = level == 0 or return_weights or return_intermediates
-            march = FUSED_MARCH and level == 0
+            march = level == 0 and march_ok(S, self.num_fine_samples)
             if march:  # the coarse weights are needed on chip only
                 keep_w = return_weights or return_intermediates
             with torch.no_grad():
@@ -292,6 +302,8 @@ class NeRF(nn.Module):
             warnings.warn("NeRF: an MLP activation exceeded the fp16x3 range; re-rendered with "
                           "precision='fp32'", RuntimeWarning)
             self.set_precision("fp32")
+            if rng is not None:
+                torch.cuda.set_rng_state(rng, dev)
             try:
                 return self.forward(rays, randomized, white_bkgd, near, far, u_coarse=u_coarse,
                                     u_fine=u_fine, return_weights=return_weights,

@@ -2,23 +2,25 @@
 (models/vanilla_nerf/model_autodecoder.py:60-337; config C3).
 
 Identical constructor keywords, forward signatures and parameter (state_dict) names.  One
-level runs:
+inference level runs ONE fused kernel (aon_mlp_art_fwd, k_mlp_art_f16x3; NeRFMLP.fused, the
+default):
 
-    cast_rays (aon_cast_rays: xyz)                                         helper.py:25-26
-    deformation MLP on cat[xyz, shape, articulation]: 4 x (GEMM + ReLU),   model_autodecoder.py:
-      deformation_layer (GEMM)                                             196-205
-    x' = deformation + xyz, pos_enc(x')   (aon_cast_rays offset + enc)     :205-212
+    cast_rays                                                              helper.py:25-26
+    deformation MLP on cat[xyz, shape, articulation]: 4 x (MFMA + ReLU),   model_autodecoder.py:
+      deformation_layer                                                    196-205
+    x' = deformation + xyz, pos_enc(x') in registers                       :205-212
     trunk on cat[pos_enc(x'), shape] with the skip concat, density,        :214-223
       bottleneck
-    view branch on cat[bottleneck, enc_dir, appearance]: 4 x (GEMM + ReLU) :224-235
-    rgb head; padded sigmoid / softplus(raw - 1) + compositing             :321-333
-      (aon_composite_fwd, AON_ACT_ARTIC)
+    view branch on cat[bottleneck, enc_dir, appearance]: 4 x (MFMA + ReLU) :224-235
+    rgb head; padded sigmoid / softplus(raw - 1) in the epilogue           :321-323
 
-The latent codes are the same for every sample (the reference repeats (1, C) rows over all
-B*S rows, :186-194), so their products with the weight columns they meet are folded into
-per-call biases (b' = b + W[:, latent cols] . latent, one tiny GEMM each): the per-sample GEMMs
-see K = 3 (deformation input), 63 (trunk input), 256 + 63 (skip) and 256 + 27 (view input).
-Every product runs on the f16x3 MFMA GEMM (aon_gemm); no torch arithmetic on the path.
+then the coarse compositor fused with the fine level's resampling (aon_composite_march) or, for
+the fine level, aon_composite_fwd (AON_ACT_ARTIC; :324-333).  The latent codes are the same for
+every sample (the reference repeats (1, C) rows over all B*S rows, :186-194), so their products
+with the weight columns they meet are folded into per-call biases (b' = b + W[:, latent cols] .
+latent, one tiny GEMM each).  ``NeRFMLP.fused = False`` selects the layer-by-layer path, every
+product on the f16x3 MFMA GEMM (aon_gemm), which is also the fallback when an activation leaves
+the fused kernel's fp16x3 range.  No torch arithmetic on the path.
 """
 import warnings
 
@@ -29,7 +31,7 @@ import torch.nn.init as init
 from . import _lib as L
 from .linalg import ACT_SCALE, W_SCALE, gemm, linear_fwd
 from . import model as _vanilla
-from .model import _events, _record, composite_march, fine_uniforms, level_t_vals
+from .model import _events, _record, composite_march, fine_uniforms, level_t_vals, march_ok
 
 class NeRFMLP(nn.Module):
     """reference model_autodecoder.py:60-166 (same nn.Linear layout and init)."""
@@ -339,6 +341,8 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
     def _forward_render(self, o, d, v, randomized, white_bkgd, near, far, latents, u_coarse,
                         u_fine, return_weights, return_intermediates, timers=None):
         B, dev = o.shape[0], o.device
+        # the overflow fallback below re-renders with the same random draws
+        rng = torch.cuda.get_rng_state(dev) if randomized else None
         ret = []
         t_vals = weights = t_next = None
         for level in range(2):
@@ -353,7 +357,7 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
             if self.noise_std > 0 and randomized:  # model_autodecoder.py:318-319
                 raw[:, 3].copy_(raw[:, 3] + torch.rand_like(raw[:, 3]) * self.noise_std)
             ev = _events(timers)
-            if level == 0 and _vanilla.FUSED_MARCH:
+            if level == 0 and march_ok(S, self.num_fine_samples):
                 # coarse compositing + the fine level's resampling in one kernel; the coarse
                 # weights reach HBM only when asked for
                 u, u_stride = fine_uniforms(B, self.num_fine_samples, randomized, dev, u_fine)
@@ -385,6 +389,8 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
             fused = [m.fused for m in mlps]
             for m in mlps:
                 m.fused = False
+            if rng is not None:
+                torch.cuda.set_rng_state(rng, dev)
             try:
                 return self._forward_render(o, d, v, randomized, white_bkgd, near, far, latents,
                                             u_coarse, u_fine, return_weights,

@@ -65,17 +65,28 @@ class GradAllReduce:
     """Data-parallel gradient averaging for the training step (run.py:109/151 trains with
     Lightning DDP: every rank draws its own ray batch, gradients are averaged).
 
-    The gradients of all parameters are packed into ONE flat fp32 bucket (vanilla NeRF:
-    1,191,688 values = 4.77 MB) and averaged with a single all-reduce (RCCL over xGMI; one
-    bucket amortises the per-collective latency, and at this size the ring is latency-, not
+    The gradients of all parameters are packed into ONE flat bucket (vanilla NeRF: 1,191,688
+    values = 4.77 MB in fp32) and averaged with a single all-reduce (RCCL over xGMI; one bucket
+    amortises the per-collective latency, and at this size the ring is latency-, not
     link-bound), then unpacked into each ``.grad``.
+
+    ``dtype=torch.bfloat16`` (for C5's bf16 mode) halves the bucket (2.38 MB):
+    each rank's gradients are rounded to bf16, summed by the collective in bf16 (RCCL's ring
+    rounds every partial sum to bf16: world - 1 roundings), then widened to fp32 and divided by
+    the world size.  Relative error per value <= ~world x 2^-8 of the largest magnitude summed
+    into it; the fp32 master weights and Adam state are unchanged.  On a gloo group (CPU
+    transport) a device bucket is staged through the host.
     """
 
-    def __init__(self, params, group=None):
+    def __init__(self, params, group=None, dtype=torch.float32):
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("GradAllReduce: dtype must be torch.float32 or torch.bfloat16")
         self.params = [p for p in params if p.requires_grad]
         self.group = group
+        self.dtype = dtype
         self.sizes = [p.numel() for p in self.params]
         self.flat = None
+        self.flat32 = None
 
     def __call__(self):
         if not dist.is_initialized():  # (a process group of one still runs the all-reduce)
@@ -83,16 +94,25 @@ class GradAllReduce:
         world = dist.get_world_size(self.group)
         dev = self.params[0].device
         if self.flat is None or self.flat.device != dev:
-            self.flat = torch.empty(sum(self.sizes), dtype=torch.float32, device=dev)
+            n = sum(self.sizes)
+            self.flat = torch.empty(n, dtype=self.dtype, device=dev)
+            self.flat32 = self.flat if self.dtype == torch.float32 else torch.empty(n, device=dev)
         off = 0
         for p, n in zip(self.params, self.sizes):
             if p.grad is None:
                 raise RuntimeError("GradAllReduce: a parameter has no gradient")
-            self.flat[off:off + n].copy_(p.grad.reshape(-1))
+            self.flat[off:off + n].copy_(p.grad.reshape(-1))  # (rounds to bf16 in that mode)
             off += n
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-        self.flat.div_(world)
+        if self.flat.is_cuda and dist.get_backend(self.group) == "gloo":
+            host = self.flat.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+            self.flat.copy_(host)
+        else:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        if self.flat32 is not self.flat:
+            self.flat32.copy_(self.flat)
+        self.flat32.div_(world)
         off = 0
         for p, n in zip(self.params, self.sizes):
-            p.grad.copy_(self.flat[off:off + n].view_as(p.grad))
+            p.grad.copy_(self.flat32[off:off + n].view_as(p.grad))
             off += n

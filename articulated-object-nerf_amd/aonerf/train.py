@@ -15,12 +15,14 @@ One render level under autograd is ``RenderLevel`` (a torch.autograd.Function):
 backward that the fused kernels replaced; both are gated identically in tests/test_gpu_train.py.)
 
 Gradients land in each parameter's ``.grad`` through autograd, so the reference's own
-optimizer code runs unchanged; ``Adam`` below is the fused replacement (aon_adam_step) with
-the reference's learning-rate schedule.  All arithmetic is in the HIP kernels; torch only
+optimizer code runs unchanged (the fp16x3 range guard reaches it through a global
+torch.optim step pre-hook); ``Adam`` below is the fused replacement (aon_adam_step) with the
+reference's learning-rate schedule.  All arithmetic is in the HIP kernels; torch only
 allocates buffers and routes autograd.
 """
 import numpy as np
 import torch
+import torch.optim.optimizer as _torch_optim
 
 from . import _lib as L
 from . import tiles
@@ -168,12 +170,38 @@ def _buffer(key, nbytes, dev, guard=False):
         buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
         _packed[(key, str(dev))] = buf
     if guard:
-        L.PENDING_PACKS[("train", key, str(dev))] = buf
+        L.register_pack(("train", key), buf)
     return buf
 
 
-# Adam.step refuses a step whose kernels met a fp16x3 range overflow (one sync per step)
+# an optimizer step refuses gradients whose kernels met a fp16x3 range overflow (one sync per
+# step): aonerf's Adam.step, and every other torch.optim optimizer through a global step pre-hook
 RANGE_CHECK = True
+
+_RANGE_MSG = ("a fp16x3 training kernel met a value beyond its fp16 hi/lo range (|activation| > "
+              "8188 or an overflowing gradient): the gradients of this step are invalid and were "
+              "not applied.  Train this model on the layer-by-layer GEMM path "
+              "(train.FUSED_FORWARD = train.FUSED_BACKWARD = False; train_art likewise), whose "
+              "operands carry a 2^-8 scale (range 1.6e7), or in train.PRECISION = 'bf16'.")
+
+
+def check_range(devices=None):
+    """Raise FloatingPointError if a fused fp16x3 training kernel on ``devices`` overflowed since
+    the last check (consumes the pending packs)."""
+    if RANGE_CHECK and L.check_pending(devices):
+        raise FloatingPointError(_RANGE_MSG)
+
+
+def _optimizer_step_pre_hook(optimizer, args, kwargs):
+    # the reference trains through Lightning with torch.optim.Adam (configure_optimizers,
+    # model.py:386-389): the guard must hold for any optimizer, not only aonerf's Adam
+    if not L.PENDING_PACKS and not L._STICKY:
+        return
+    devs = {str(p.device) for g in optimizer.param_groups for p in g["params"]}
+    check_range(devs)
+
+
+_HOOK = _torch_optim.register_optimizer_step_pre_hook(_optimizer_step_pre_hook)
 
 
 def _pack(P, dev, tag="", bf16=False):
@@ -425,17 +453,7 @@ class Adam:
 
     @torch.no_grad()
     def step(self, lr=None):
-        if RANGE_CHECK:
-            dev = str(self.params[0].device)
-            keys = [k for k in L.PENDING_PACKS if k[2] == dev]
-            bufs = [L.PENDING_PACKS.pop(k) for k in keys]
-            if L.range_overflow(bufs):
-                raise FloatingPointError(
-                    "a fp16x3 training kernel met a value beyond its fp16 hi/lo range "
-                    "(|activation| > 8188 or an overflowing gradient): the gradients of this step "
-                    "are invalid and were not applied.  Train this model on the layer-by-layer "
-                    "GEMM path (train.FUSED_FORWARD = train.FUSED_BACKWARD = False; train_art "
-                    "likewise), whose operands carry a 2^-8 scale (range 1.6e7).")
+        check_range({str(p.device) for p in self.params})
         self.step_count += 1
         for p in self.params:
             if p.grad is None:

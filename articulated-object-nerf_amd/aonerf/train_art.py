@@ -32,6 +32,7 @@ import torch
 
 from . import _lib as L
 from . import tiles
+from . import train as _train
 from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, gemm
 from .train import Adam, _amax_word, img2mse, learning_rate, mse2psnr, relu_masks  # noqa: F401 (shared)
 
@@ -166,7 +167,7 @@ def _buffer(key, nbytes, dev, guard=False):
         buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
         _packed[(key, str(dev))] = buf
     if guard:
-        L.PENDING_PACKS[("train_art", key, str(dev))] = buf
+        L.register_pack(("train_art", key), buf)
     return buf
 
 
@@ -210,9 +211,11 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     enc = torch.empty((R, geo.ne), device=dev)
     xyz = torch.empty((R, 3), device=dev)
     packed = _pack(geo, P, lat, S)
+    e0 = _train._ev()
     L.call("aon_mlp_art_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
            L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h),
            L.ptr(bot), L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks), L.stream(dev))
+    _train._rec(f"art_fwd_train{S}", e0, R)
     return xyz, hd, enc, h, bot, hv
 
 
@@ -344,8 +347,12 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     dxp = torch.empty((R, 3), device=dev)
     dzd = torch.empty((4, NR, wd), device=dev)
     work = _buffer("work", 4, dev)
-    L.call("aon_mlp_art_bwd", L.ptr(_pack_bwd(P, dev, S)), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
+    packed = _pack_bwd(P, dev, S)
+    e0 = _train._ev()
+    L.call("aon_mlp_art_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
            L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
+    _train._rec(f"art_bwd_chain{S}", e0, R)
+    e0 = _train._ev()
     gs, acts = GRAD_SCALE, ACT_SCALE
 
     def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True, chain_scale=True, a_t=True):
@@ -389,6 +396,7 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     dweight(DEF0, dzd[0], wd, xyz, 3, 3, chain_scale=False)               # deformations_linear.0
     dlatent(DEF0, 3, shape, dshape, True)
     dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
+    _train._rec(f"art_dweight{S}", e0, R)
 
 
 class ArtRenderLevel(torch.autograd.Function):

@@ -5,6 +5,8 @@ N row bands, one per rank, and gathered to rank 0 over RCCL).
 
 Sub-records in the same JSON line (after the headline, same timing protocol: warm-up, barrier +
 synchronize on both sides, max over ranks):
+  "render_fp32"     the same C2 frame on the exact-fp32 MFMA MLP (NeRF(precision="fp32"); N = 1
+                    only; min(K, 5) timed steps after 1 warm-up: 0.7 s per frame)
   "articulated"     config C3 -- NeRF_AE_Art 320x240 frame render (N = 1 only)
   "train_step"      config C5 -- LitNeRF.training_step on 4096 rays per rank + Adam (+ the DDP
                     gradient all-reduce over RCCL on N > 1: weak scaling), f16x3 kernels
@@ -67,7 +69,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_TFLOPS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-chunks", type=int, default=2, help="3840-ray chunks in the CPU sample")
+    ap.add_argument("--cpu-chunks", type=int, default=4, help="3840-ray chunks in the CPU sample")
     ap.add_argument("--no-extra", action="store_true", help="headline C2 render only")
     args = ap.parse_args()
 
@@ -123,6 +125,8 @@ def main():
     extra = {}
     if not args.no_extra:  # every rank takes part (the C5 step all-reduces over RCCL)
         if world == 1:
+            if args.precision != "fp32":
+                extra["render_fp32"] = bench_render_fp32(args, c2w, focal)
             extra["articulated"] = bench_articulated(args)
         extra["train_step"] = bench_train(args, world, rank, local_rank)
         extra["train_step_bf16"] = bench_train(args, world, rank, local_rank, precision="bf16")
@@ -228,11 +232,43 @@ def ev_ms(timers, key):
     return float(np.mean([a.elapsed_time(b) for a, b, _ in ev])), ev[0][2]
 
 
+def bench_render_fp32(args, c2w, focal):
+    """The C2 frame on the exact-fp32 MFMA path (v_mfma_f32_16x16x4_f32, no hi/lo emulation):
+    the non-emulated reference-precision render, measured by the same protocol on fewer steps."""
+    from aonerf.model import NeRF
+    from aonerf.parallel import render_frame_sharded
+    from aonerf.synthetic import init_like_reference
+
+    net = init_like_reference(NeRF(precision="fp32")).cuda()
+    timers = {}
+    steps, warmup = min(args.steps, 5), 1
+
+    def step(i):
+        render_frame_sharded(net, c2w, H, W, focal, 2.0, 6.0, True,
+                             timers=timers if i >= warmup else None)
+
+    el = timed(step, steps, warmup, 1)
+    mlp_ms, rows = ev_ms(timers, "mlp1")
+    flop = 2.0 * MAC_PER_SAMPLE * rows
+    ach = flop / (mlp_ms * 1e-3) / 1e12
+    return {"metric": "rays/sec at 640x480x(64c+128f), exact-fp32 MLP (NeRF(precision='fp32'))",
+            "value": H * W * steps / el, "unit": "rays/s", "steps": steps, "warmup": warmup,
+            "ms_per_step": el / steps * 1e3, "dtype": "fp32 (v_mfma_f32_16x16x4_f32)",
+            "roofline": {"bound": "mfma", "kernel": "k_mlp_fwd_f32 (fine level)", "achieved": ach,
+                         "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+                         "frac": ach / PEAK_TFLOPS["fp32"], "launch_ms": mlp_ms,
+                         "algorithmic_flop_per_launch": flop}}
+
+
+ART_MAC_ISSUED = 714_880    # NeRF_AE_Art MAC per sample the fused kernel issues (latents folded)
+ART_MAC_UNFOLDED = 794_880  # the reference's count with the latent columns as GEMM inputs
+
+
 def bench_articulated(args):
     """C3: NeRF_AE_Art, 320x240 frame, 64c+128f, eval mode, white background, fixed latent
-    codes; MFMA roofline of the fine-level fused kernel in the reference's unfolded FLOP count
-    (2 x 794,880 per sample; the latent products are folded into per-call biases, so the issued
-    work is 714,880 MAC per sample)."""
+    codes; MFMA roofline of the fine-level fused kernel on the 714,880 MAC per sample it issues
+    (the latent products are folded into per-call biases; the reference's unfolded count,
+    794,880, is reported as a note only)."""
     from aonerf.model_autodecoder import NeRF_AE_Art
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, sapien_focal
@@ -250,7 +286,7 @@ def bench_articulated(args):
 
     el = timed(step, args.steps, args.warmup, 1)
     mlp_ms, rows = ev_ms(timers, "mlp1")
-    flop = 2.0 * 794_880 * rows
+    flop = 2.0 * ART_MAC_ISSUED * rows
     ach = flop / (mlp_ms * 1e-3) / 1e12
     return {"metric": "articulated rays/sec at 320x240x(64c+128f) (NeRF_AE_Art, config C3)",
             "value": h * w * args.steps / el, "unit": "rays/s", "steps": args.steps,
@@ -262,8 +298,10 @@ def bench_articulated(args):
                          "achieved": ach, "peak": PEAK_TFLOPS["f16x3"], "unit": "TFLOP/s",
                          "frac": ach / PEAK_TFLOPS["f16x3"], "launch_ms": mlp_ms,
                          "algorithmic_flop_per_launch": flop,
-                         "note": "unfolded reference count 2 x 794,880 FLOP/sample; issued "
-                                 "714,880 MAC/sample x 3 fp16 products"}}
+                         "note": "achieved counts the 714,880 MAC/sample the kernel issues (x 3 "
+                                 "fp16 products); in the reference's unfolded count (794,880 "
+                                 "MAC/sample, latent columns as GEMM inputs) the same launch is "
+                                 f"{ach * ART_MAC_UNFOLDED / ART_MAC_ISSUED:.1f} TFLOP/s"}}
 
 
 # bytes per sample of the training kernels (fp32 activations, SURVEY.md 8(d) extended to C5):
@@ -279,6 +317,16 @@ TRAIN_FLOP = {"fwd_train": 2 * MAC_PER_SAMPLE, "bwd_chain": 2 * (MAC_PER_SAMPLE 
 # bf16 mode: the kept activations and gradients are 2 B (encodings, d raw and masks unchanged)
 TRAIN_BYTES_BF16 = {"fwd_train": 4 + 16 + 2 * 2432 + 288, "bwd_chain": 16 + 288 + 2 * 2432,
                     "dweight": 2 * (2432 + 2432) + 4 * (63 + 27)}
+# articulated level (NeRF_AE_Art, model_autodecoder.py:168-239), bytes per sample: the fused
+# forward writes raw (16) + 3,328 activations (hd 4x128, h 8x256, bot 256, hv 4x128) + pos_enc(x')
+# (63) + the points (3) + ReLU' bits (16 x 32) and reads t; the chain reads d raw + bits + enc and
+# writes 3,328 gradients + dL/dx' (3); the weight GEMMs read every dZ (3,335) and every layer
+# input once (3,484: activations, enc twice, points, view encodings)
+ART_TRAIN_BYTES = {"art_fwd_train": 4 + 16 + 4 * (3328 + 63 + 3) + 512,
+                   "art_bwd_chain": 16 + 512 + 4 * 63 + 4 * (3328 + 3),
+                   "art_dweight": 4 * (3335 + 3484)}
+ART_TRAIN_FLOP = {"art_fwd_train": 2 * 714_880, "art_bwd_chain": 2 * (714_880 - 3 * 128 - 128 * 27),
+                  "art_dweight": 2 * 714_880}
 # dense MFMA peak in algorithmic FLOP/s per training precision: f16x3 issues 3 fp16 products
 # per fp32-class MAC, bf16 one bf16 product
 TRAIN_PEAK = {"f16x3": 2500.0 / 3, "bf16": 2500.0}
@@ -322,11 +370,12 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     params = list(net.parameters()) + (list(lib.parameters()) if art else [])
     opt = train.Adam(params)
-    sync = GradAllReduce(params)
+    # C5's bf16 mode averages its gradients in a bf16 bucket (half the bytes on xGMI)
+    sync = GradAllReduce(params, dtype=torch.bfloat16 if precision == "bf16" else torch.float32)
     timers = {}
 
     def step(i):
-        train.TIMERS = timers if (i >= args.warmup and not art) else None
+        train.TIMERS = timers if i >= args.warmup else None
         idx = torch.randint(0, 8 * H * W, (nrays,), device=dev, generator=gen)
         batch = {k: v[idx] for k, v in rays_all.items()}
         batch["target"] = target_all[idx]
@@ -347,7 +396,7 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
     finally:
         train.TIMERS = None
         train.PRECISION = old_prec
-    mac = 794_880 if art else MAC_PER_SAMPLE
+    mac = ART_MAC_ISSUED if art else MAC_PER_SAMPLE
     samples = nrays * (NC + 1 + NC + 1 + NF)
     ms = el / args.steps * 1e3
     step_flop = 3 * 2.0 * mac * samples
@@ -362,30 +411,32 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
                      "compositing / loss / Adam master weights)" if precision == "bf16" else
                      "f16x3 (fp16 hi/lo split MFMA, fp32 accumulate; fp32 activations)"),
            "config": {"workload": "C5 training step" + (" (articulated)" if art else ""),
-                      "rays_per_rank": nrays, "parallelism": f"ddp{world}" if world > 1 else "single GPU"},
+                      "rays_per_rank": nrays, "parallelism": f"ddp{world}" if world > 1 else "single GPU",
+                      "grad_allreduce_dtype": "bf16" if precision == "bf16" else "fp32"},
            "roofline": {"bound": "hbm+mfma", "kernel": "whole step (3 x forward FLOP)",
                         "achieved": ach, "peak": TRAIN_PEAK[precision], "unit": "TFLOP/s",
                         "frac": ach / TRAIN_PEAK[precision]}}
-    if not art:
-        kern = {}
-        hbm_bytes = 0.0
-        for name in ("fwd_train", "bwd_chain", "dweight"):
-            t_ms, rows = ev_ms(timers, f"{name}{NC + 1 + NF}")
-            if not t_ms:
-                continue
-            b = (TRAIN_BYTES_BF16 if precision == "bf16" else TRAIN_BYTES)[name] * rows
-            f = TRAIN_FLOP[name] * rows
-            hbm_bytes += b
-            kern[name] = {"level": "fine", "ms": t_ms, "rows": rows,
-                          "algorithmic_bytes": b, "GB/s": b / (t_ms * 1e-3) / 1e9,
-                          "hbm_frac": b / (t_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                          "TFLOP/s": f / (t_ms * 1e-3) / 1e12,
-                          "mfma_frac": f / (t_ms * 1e-3) / 1e12 / TRAIN_PEAK[precision]}
-        rec["roofline"]["kernels"] = kern
-        if kern:
-            tot_ms = sum(k["ms"] for k in kern.values())
-            rec["roofline"]["fine_level_hbm_frac"] = hbm_bytes / (tot_ms * 1e-3) / 1e9 / PEAK_HBM_GBS
-            rec["roofline"]["fine_level_ms"] = tot_ms
+    kern = {}
+    hbm_bytes = 0.0
+    names = ("art_fwd_train", "art_bwd_chain", "art_dweight") if art else ("fwd_train", "bwd_chain", "dweight")
+    nbytes = ART_TRAIN_BYTES if art else TRAIN_BYTES_BF16 if precision == "bf16" else TRAIN_BYTES
+    nflop = ART_TRAIN_FLOP if art else TRAIN_FLOP
+    for name in names:
+        t_ms, rows = ev_ms(timers, f"{name}{NC + 1 + NF}")
+        if not t_ms:
+            continue
+        b, f = nbytes[name] * rows, nflop[name] * rows
+        hbm_bytes += b
+        kern[name] = {"level": "fine", "ms": t_ms, "rows": rows,
+                      "algorithmic_bytes": b, "GB/s": b / (t_ms * 1e-3) / 1e9,
+                      "hbm_frac": b / (t_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                      "TFLOP/s": f / (t_ms * 1e-3) / 1e12,
+                      "mfma_frac": f / (t_ms * 1e-3) / 1e12 / TRAIN_PEAK[precision]}
+    rec["roofline"]["kernels"] = kern
+    if kern:
+        tot_ms = sum(k["ms"] for k in kern.values())
+        rec["roofline"]["fine_level_hbm_frac"] = hbm_bytes / (tot_ms * 1e-3) / 1e9 / PEAK_HBM_GBS
+        rec["roofline"]["fine_level_ms"] = tot_ms
     return rec
 
 

@@ -297,39 +297,125 @@ def _lin(p, name, x):
     return torch.nn.functional.linear(x, p[f"{name}.weight"], p[f"{name}.bias"])
 
 
+def _pos_enc_args_fp32(x, min_deg, max_deg):
+    """The fp32 arguments of pos_enc's sin (helper.py:136-140) at fp32 points x (R, 3):
+    x 2^d (exact) and x 2^d + 0.5 pi (one fp32 add of 1.5707964f, as the reference's fp32
+    tensor arithmetic rounds it) -> (R, 6 (max_deg - min_deg)) fp32."""
+    x = x.float()
+    scales = torch.tensor([2 ** i for i in range(min_deg, max_deg)], dtype=torch.float32)
+    xb = torch.reshape(x[..., None, :] * scales[:, None], list(x.shape[:-1]) + [-1])
+    return torch.cat([xb, xb + 0.5 * np.pi], dim=-1)
+
+
+def pos_enc_at(x_value, x_graph, min_deg, max_deg):
+    """pos_enc (helper.py:136-140) whose VALUE is evaluated at the fp32 points x_value (the
+    sin arguments rounded exactly as the reference's fp32 arithmetic rounds them, the sin itself
+    in x_graph's dtype) and whose GRADIENT flows into x_graph: d/dx sin(a) = cos(a) 2^d at those
+    same arguments.  x_graph's value is not used (straight-through: teacher forcing at a given
+    x' while autograd still reaches the parameters that produced x_graph)."""
+    dt = x_graph.dtype
+    args = _pos_enc_args_fp32(x_value, min_deg, max_deg).to(dt)
+    delta = x_graph - x_graph.detach()  # zero, carries the gradient
+    scales = torch.tensor([2 ** i for i in range(min_deg, max_deg)], dtype=dt)
+    db = torch.reshape(delta[..., None, :] * scales[:, None], list(delta.shape[:-1]) + [-1])
+    return torch.cat([x_value.to(dt) + delta, torch.sin(args + torch.cat([db, db], dim=-1))], dim=-1)
+
+
 def art_mlp_forward(p, pos, condition, latents, netdepth=8, skip_layer=4, netdepth_deformation=4,
-                    netdepth_condition=4, min_deg_point=0, max_deg_point=10):
+                    netdepth_condition=4, min_deg_point=0, max_deg_point=10, xp_fixed=None,
+                    return_xp=False, record=None):
     """reference models/vanilla_nerf/model_autodecoder.py:168-239 (deformation_mlp=True,
     enc_after=True, embed_deg=False).
 
     pos: (B, S, 3) sample positions; condition: (B, 27) encoded view directions;
     latents: {density (1,128), color (1,128), articulation (1,32)} repeated over all rows
     (model_autodecoder.py:186-194).  Returns raw_rgb (B, S, 3), raw_density (B, S, 1).
+
+    Test hooks (not the reference's arithmetic): ``xp_fixed`` (B*S, 3) fp32 teacher-forces the
+    deformed points x' (pos_enc evaluated at those fp32 points, gradients straight through to
+    the deformation MLP, :func:`pos_enc_at`); ``return_xp`` also returns this call's x';
+    ``record`` (a dict) receives the intermediates in :func:`art_mlp_forward_kept`'s layout.
     """
+    rec = record if record is not None else {}
     S = pos.shape[1]
     pos = pos.reshape(-1, 3)
     BN = pos.shape[0]
     shape = latents["density"].repeat(BN, 1)
     app = latents["color"].repeat(BN, 1)
     art = latents["articulation"].repeat(BN, 1)
+    rec.update(xyz=pos, hd=[], h=[], hv=[])
     x = torch.cat([pos, shape, art], -1)
     for idx in range(netdepth_deformation):  # model_autodecoder.py:200-203
         x = torch.relu(_lin(p, f"deformations_linear.{idx}", x))
+        rec["hd"].append(x)
     x = _lin(p, "deformation_layer", x) + pos  # :205
-    x = pos_enc(x, min_deg_point, max_deg_point)  # :207-212 (enc_after)
+    xp = rec["xp"] = x
+    if xp_fixed is None:
+        x = pos_enc(x, min_deg_point, max_deg_point)  # :207-212 (enc_after)
+    else:
+        x = pos_enc_at(xp_fixed, x, min_deg_point, max_deg_point)
+    rec["enc"] = x
     x = torch.cat([x, shape], -1)
     inputs = x
     for idx in range(netdepth):  # :216-220
         x = torch.relu(_lin(p, f"pts_linears.{idx}", x))
+        rec["h"].append(x)
         if idx % skip_layer == 0 and idx > 0:
             x = torch.cat([x, inputs], dim=-1)
     raw_density = _lin(p, "density_layer", x).reshape(-1, S, 1)
-    bottleneck = _lin(p, "bottleneck_layer", x)
+    bottleneck = rec["bot"] = _lin(p, "bottleneck_layer", x)
     cond = torch.tile(condition[:, None, :], (1, S, 1)).reshape(-1, condition.shape[-1])
     x = torch.cat([bottleneck, cond, app], dim=-1)  # :229-231
     for idx in range(netdepth_condition):
         x = torch.relu(_lin(p, f"views_linear.{idx}", x))
+        rec["hv"].append(x)
     raw_rgb = _lin(p, "rgb_layer", x).reshape(-1, S, 3)
+    if return_xp:
+        return raw_rgb, raw_density, xp
+    return raw_rgb, raw_density
+
+
+def art_mlp_forward_kept(p, kept, condition, latents, S, min_deg_point=0, max_deg_point=10):
+    """Stage isolation of the articulated MLP's BACKWARD (model_autodecoder.py:168-239): the
+    forward of :func:`art_mlp_forward` whose every intermediate VALUE is the one a GPU forward
+    kept -- ``kept`` = {xyz (R,3), hd (4,R,wd), xp (R,3) = x', enc (R,63) = pos_enc(x'),
+    h (8,R,256), bot (R,256), hv (4,R,wc)}, ReLU' taken from the sign of the kept activation --
+    while autograd runs through this function's own linear maps in the parameters' dtype.  Its
+    backward from a given d raw is therefore the exact (e.g. fp64) backward at the GPU's own
+    forward values: nothing the forward computed differently (x', hence sin(2^9 x')) can be
+    amplified.  pos_enc's derivative is cos at the fp32 arguments of x' (:func:`pos_enc_at`).
+    condition: (B, 27) encoded view directions.  Returns raw_rgb (R, 3), raw_density (R, 1)."""
+    dt = p["rgb_layer.weight"].dtype
+    K = {k: (v.to(dt) if torch.is_tensor(v) else [x.to(dt) for x in v]) for k, v in kept.items()}
+    R = K["xyz"].shape[0]
+
+    def forced(value, z):
+        return value + (z - z.detach())
+
+    def relu_kept(value, z):
+        return forced(value, z * (value > 0).to(dt))
+
+    shape = latents["density"].repeat(R, 1)
+    app = latents["color"].repeat(R, 1)
+    art = latents["articulation"].repeat(R, 1)
+    x = torch.cat([K["xyz"], shape, art], -1)
+    for idx in range(len(K["hd"])):
+        x = relu_kept(K["hd"][idx], _lin(p, f"deformations_linear.{idx}", x))
+    xp = forced(K["xp"], _lin(p, "deformation_layer", x) + K["xyz"])
+    enc = forced(K["enc"], pos_enc_at(kept["xp"], xp, min_deg_point, max_deg_point))
+    x = torch.cat([enc, shape], -1)
+    inputs = x
+    for idx in range(len(K["h"])):
+        x = relu_kept(K["h"][idx], _lin(p, f"pts_linears.{idx}", x))
+        if idx % 4 == 0 and idx > 0:
+            x = torch.cat([x, inputs], dim=-1)
+    raw_density = _lin(p, "density_layer", x)
+    bot = forced(K["bot"], _lin(p, "bottleneck_layer", x))
+    cond = torch.tile(condition.to(dt)[:, None, :], (1, S, 1)).reshape(-1, condition.shape[-1])
+    x = torch.cat([bot, cond, app], dim=-1)
+    for idx in range(len(K["hv"])):
+        x = relu_kept(K["hv"][idx], _lin(p, f"views_linear.{idx}", x))
+    raw_rgb = _lin(p, "rgb_layer", x)
     return raw_rgb, raw_density
 
 
@@ -365,13 +451,16 @@ def art_nerf_forward(params, rays, randomized, white_bkgd, near, far, latents,
     return (ret, inter) if return_intermediates else ret
 
 
-def art_render_level(params, rays, t_vals, level, white_bkgd, latents, deg_view=4):
-    """One NeRF_AE_Art level on GIVEN sample positions (teacher forcing)."""
+def art_render_level(params, rays, t_vals, level, white_bkgd, latents, deg_view=4, xp_fixed=None,
+                     return_xp=False):
+    """One NeRF_AE_Art level on GIVEN sample positions (teacher forcing); ``xp_fixed`` /
+    ``return_xp`` as in :func:`art_mlp_forward` (x' appended to the returned tuple)."""
     samples = cast_rays(t_vals, rays["rays_o"], rays["rays_d"])
-    raw_rgb, raw_sigma = art_mlp_forward(params[level], samples,
-                                         pos_enc(rays["viewdirs"], 0, deg_view), latents)
-    rgb, sigma = art_activations(raw_rgb, raw_sigma)
-    return volumetric_rendering(rgb, sigma, t_vals, rays["rays_d"], white_bkgd)
+    out = art_mlp_forward(params[level], samples, pos_enc(rays["viewdirs"], 0, deg_view), latents,
+                          xp_fixed=xp_fixed, return_xp=return_xp)
+    rgb, sigma = art_activations(out[0], out[1])
+    res = volumetric_rendering(rgb, sigma, t_vals, rays["rays_d"], white_bkgd)
+    return res + (out[2],) if return_xp else res
 
 
 def code_library_latents(tables, instance_id, articulation_id):

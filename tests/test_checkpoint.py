@@ -118,3 +118,64 @@ def test_render_from_checkpoint(ckpt_dir):
         fb = render_frame(b, c2w, 24, 32, sapien_focal(24))
     assert torch.equal(fa, fb)
     assert np.isfinite(fa.cpu().numpy()).all()
+
+
+def _pl152_checkpoint(state_dict):
+    """A checkpoint with every top-level entry pytorch-lightning 1.5.2 (the reference's pin,
+    requirements.txt) writes from run.py's Trainer: CheckpointConnector.dump_checkpoint adds
+    epoch / global_step / version / state_dict / loops / callbacks (keyed by the callback's
+    state_key string) / optimizer_states / lr_schedulers / hyper_parameters (dict(model.hparams):
+    LitNeRF.__init__ updates it with vars(argparse hparams), model.py:216).  The structure is
+    restated from PL 1.5.2's published format (the library is absent here): parity unpinned
+    beyond the types it uses."""
+    params = list(state_dict.values())
+    adam = {"state": {i: {"step": 1200, "exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.ones_like(p)}
+                      for i, p in enumerate(params[:3])},
+            "param_groups": [{"lr": 4.9e-4, "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 0,
+                              "amsgrad": False, "params": list(range(len(params)))}]}
+    ckpt_key = ("ModelCheckpoint{'monitor': 'val/psnr', 'mode': 'max', 'every_n_train_steps': 0, "
+                "'every_n_epochs': 10, 'train_time_interval': None, 'save_on_train_epoch_end': True}")
+    return {
+        "epoch": 9, "global_step": 1200, "pytorch-lightning_version": "1.5.2",
+        "state_dict": state_dict,
+        "loops": {"fit_loop": {"state_dict": {}, "epoch_loop.state_dict": {"_batches_that_stepped": 1200},
+                               "epoch_progress": {"total": {"ready": 10, "started": 10,
+                                                            "processed": 10, "completed": 9},
+                                                  "current": {"ready": 10, "started": 10,
+                                                              "processed": 10, "completed": 9}}},
+                  "validate_loop": {"state_dict": {}}, "test_loop": {"state_dict": {}},
+                  "predict_loop": {"state_dict": {}}},
+        "callbacks": {ckpt_key: {"monitor": "val/psnr", "best_model_score": torch.tensor(27.5),
+                                 "best_model_path": "/results/exp/epoch=9.ckpt",
+                                 "current_score": torch.tensor(27.5), "dirpath": "/results/exp",
+                                 "best_k_models": {"/results/exp/epoch=9.ckpt": torch.tensor(27.5)},
+                                 "kth_best_model_path": "/results/exp/epoch=9.ckpt",
+                                 "kth_value": torch.tensor(27.5),
+                                 "last_model_path": "/results/exp/last.ckpt"}},
+        "optimizer_states": [adam], "lr_schedulers": [],
+        "hyper_parameters": {"root_dir": "data/laptop", "dataset_name": "sapien", "exp_name": "exp",
+                             "img_wh": [640, 480], "white_back": True, "chunk": 3840,
+                             "batch_size": 4096, "num_epochs": 100, "num_gpus": 8, "run_eval": True,
+                             "render_name": None, "is_optimize": None, "finetune_lpips": False,
+                             "lr_init": 5e-4, "lr_final": 5e-6, "lr_delay_steps": 2500,
+                             "lr_delay_mult": 0.01, "randomized": True},
+    }
+
+
+def test_full_pl152_checkpoint_loads_weights_only(tmp_path):
+    """a checkpoint with PL 1.5.2's whole key set (hyper_parameters, callbacks,
+    loops, Adam optimizer_states) is accepted by the weights-only loader, and yields the same
+    model weights as the minimal one."""
+    from aonerf.checkpoint import extract_model_state_dict, load_ckpt
+    from aonerf.model import NeRF
+
+    ck = our_checkpoints()["vanilla"]
+    p = tmp_path / "last.ckpt"
+    torch.save(_pl152_checkpoint(ck["state_dict"]), p)
+    full = torch.load(p, map_location="cpu", weights_only=True)  # nothing refused
+    assert full["hyper_parameters"]["img_wh"] == [640, 480]
+    ext = extract_model_state_dict(str(p))
+    assert [sha(v) for v in ext.values()] == [sha(v) for v in ck["state_dict"].values()]
+    net = NeRF()
+    load_ckpt(net, str(p))
+    assert {k: sha(v) for k, v in net.state_dict().items()} == MANIFEST["load_ckpt_vanilla_sha256"]

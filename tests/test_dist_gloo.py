@@ -115,3 +115,45 @@ def test_grad_allreduce_gloo_world2():
         for i, gr in enumerate(grads):
             gr = torch.from_numpy(gr)
             assert torch.equal(gr, torch.full(gr.shape, 1.5 * (i + 1)))
+
+
+def _ddp_bf16_worker(rank, world, port, q):
+    from aonerf.parallel import GradAllReduce
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(rank)
+        ps = [torch.zeros(s, requires_grad=True) for s in ((64, 3), (257,), (1,))]
+        for p in ps:
+            p.grad = torch.randn(p.shape, generator=g) * 10.0 ** torch.randint(-6, 2, p.shape, generator=g)
+        sent = [p.grad.clone() for p in ps]
+        GradAllReduce(ps, dtype=torch.bfloat16)()
+        q.put((rank, [x.numpy() for x in sent], [p.grad.numpy().copy() for p in ps]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_bf16_gloo_world2():
+    """The bf16 bucket (half the bytes): every rank holds (bf16(g0) + bf16(g1))
+    rounded to bf16, / 2, exactly -- i.e. within the bf16 rounding bound (3 roundings of 2^-9
+    relative to the summed magnitudes) of the fp32 average."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_bf16_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {r: (s, a) for r, s, a in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for i in range(3):
+        g0, g1 = (torch.from_numpy(got[r][0][i]) for r in range(world))
+        want = (g0.bfloat16().float() + g1.bfloat16().float()).bfloat16().float() / 2
+        mag = (g0.abs() + g1.abs()) / 2
+        for r in range(world):
+            avg = torch.from_numpy(got[r][1][i])
+            assert torch.equal(avg, want), i
+            assert torch.all((avg - (g0 + g1) / 2).abs() <= 3 * 2.0 ** -9 * mag + 1e-30)

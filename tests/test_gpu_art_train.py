@@ -6,10 +6,17 @@ vectors, teacher-forced per-level gradients, and an Adam step over all 83 parame
 
 Tolerances: pos_enc backward 1e-5 of each tensor's gradient scale (fp32 sin' = cos at the same
 fp32 arguments, ulp-level differences of cosf at |arg| <= 5120); regulariser 1e-6 relative;
-loss rtol 1e-5; gradients vs the reference within max(4 x the reference's own fp32-vs-fp64
-spread, 1e-4) of each tensor's max (as tests/test_gpu_train.py); teacher-forced gradients vs
-the fp32 oracle within max(2 x its distance from the fp64 oracle, 1e-3) (measured values
-printed).
+loss rtol 1e-5.  Gradients:
+  * stage-isolated (test_art_backward_stage_isolated): the backward kernels on the GPU
+    forward's own kept tensors vs the fp64 oracle backward at those same values, every tensor
+    within 1e-4 of its max -- the gate that sees a kernel error well below the reference's own
+    fp32 noise;
+  * x'-forced at C5's size: the fp64 oracle at our deformed points, 1e-4 of each tensor's max;
+  * free-running (the deformation gradients pass through sin(2^9 x'), so the reference's own
+    fp32 evaluation sits up to ~1e-2 from fp64): vs the reference's golden gradients within
+    max(4 x its fp32-vs-fp64 spread, 1e-4); teacher-forced vs the fp32 oracle within
+    max(2 x that tensor's own spread, 1e-3), at C5's size scaled by the measured ratio of our
+    x' rounding to the fp32 oracle's (measured values printed).
 """
 import numpy as np
 import pytest
@@ -176,6 +183,87 @@ def test_fused_art_backward_chain():
         worst = max(worst, e)
         assert e < 2e-5, (name, e)
     print(f"fused vs GEMM articulated backward: worst max-rel err {worst:.2e}")
+
+
+_ART_NAMES = ([f"deformations_linear.{i}" for i in range(4)] + ["deformation_layer"]
+              + [f"pts_linears.{i}" for i in range(8)] + ["density_layer", "bottleneck_layer"]
+              + [f"views_linear.{i}" for i in range(4)] + ["rgb_layer"])  # train_art.art_layers order
+
+
+@pytest.mark.parametrize("B,S,level,scale", [(29, 65, 1, 1e-3), (128, 193, 1, 1e-4),
+                                             (4096, 65, 0, 1e-4)],
+                         ids=["ragged", "fine193", "c5_coarse_4096"])
+@pytest.mark.parametrize("bwd", ["fused", "gemm"])
+def test_art_backward_stage_isolated(B, S, level, scale, bwd):
+    """Stage isolation of the articulated backward (model_autodecoder.py:168-239): the GPU
+    forward's own kept tensors -- the points, the deformation activations, x', pos_enc(x'), the
+    trunk / bottleneck / view activations and their ReLU' bits -- and a fixed d raw go through
+    (a) aon_mlp_art_bwd + the weight-gradient aon_gemm's (``fused``) or the all-GEMM backward
+    + aon_pos_enc_bwd (``gemm``), and (b) the oracle's fp64 autograd evaluated at exactly those
+    forward values (oracle.art_mlp_forward_kept; pos_enc's derivative cos at the fp32
+    arguments of the GPU's x').  Nothing the forward computed differently is amplified, so every
+    weight, bias and latent-code gradient must agree within 1e-4 of its tensor's max (f16x3
+    operands carry ~22 bits; measured values printed).  The last case is config C5's coarse
+    level at its size (4,096 rays)."""
+    from aonerf import tiles, train_art
+
+    net, _ = _make(0)
+    mlp = net.fine_mlp if level else net.coarse_mlp
+    geo = train_art._Geo(mlp)
+    gen = torch.Generator().manual_seed(B + S)
+    R = B * S
+    o = (torch.rand(B, 3, generator=gen) - 0.5).cuda()
+    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=gen), dim=-1).cuda()
+    t = (2.0 + 4.0 * torch.rand(B, S, generator=gen)).sort(-1).values.cuda()
+    lat = tuple(cuda(v) for v in W.art_latents(2).values())
+    layers = train_art.art_layers(mlp)
+    P = [(m.weight.detach(), m.bias.detach()) for m in layers]
+    raw = torch.empty((R, 4), device="cuda")
+    masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device="cuda")
+    xyz, hd, enc, h, bot, hv = train_art._forward_level_fused(geo, P, lat, o, d, d, t, raw, None,
+                                                              masks)
+    L = train_art.L
+    venc = torch.empty((B, 27), device="cuda")
+    L.call("aon_pos_enc", L.ptr(d), B, 0, 4, L.ptr(venc), L.stream())
+    draw = (torch.randn(R, 4, generator=gen) * scale).cuda()
+    G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
+    dlat = tuple(torch.empty_like(x) for x in lat)
+    rm = [torch.stack([tiles.untile(x, R) for x in tt]) for tt in (hd, h, hv)]
+    bot_rm = tiles.untile(bot, R)
+    if bwd == "fused":
+        train_art._backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv,
+                                        draw, masks, True)
+    else:
+        train_art._backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, rm[0], rm[1], bot_rm,
+                                  rm[2], draw)
+    torch.cuda.synchronize()
+    # fp64 oracle backward at the GPU's own forward values
+    sd = W.art_state_dict(0)
+    pre = "fine_mlp." if level else "coarse_mlp."
+    p64 = {k[len(pre):]: torch.from_numpy(v).double().requires_grad_(True)
+           for k, v in sd.items() if k.startswith(pre)}
+    names = ("density", "color", "articulation")
+    l64 = {k: x.cpu().double().requires_grad_(True) for k, x in zip(names, lat)}
+    enc_c = enc.cpu()
+    kept = {"xyz": xyz.cpu(), "hd": list(rm[0].cpu()), "xp": enc_c[:, :3].clone(), "enc": enc_c,
+            "h": list(rm[1].cpu()), "bot": bot_rm.cpu(), "hv": list(rm[2].cpu())}
+    r_rgb, r_sig = O.art_mlp_forward_kept(p64, kept, venc.cpu(), l64, S)
+    d64 = draw.cpu().double()
+    torch.autograd.backward([r_rgb, r_sig], [d64[:, :3], d64[:, 3:]])
+    worst, worst_name = 0.0, ""
+    for (dw, db), name in zip(G, _ART_NAMES):
+        for got, key in ((dw, f"{name}.weight"), (db, f"{name}.bias")):
+            e = rel_err(got.cpu().numpy(), p64[key].grad.numpy())
+            if e > worst:
+                worst, worst_name = e, key
+            assert e <= 1e-4, (key, e)
+    for got, k in zip(dlat, names):
+        e = rel_err(got.cpu().numpy(), l64[k].grad.numpy().reshape(got.shape))
+        if e > worst:
+            worst, worst_name = e, f"latent {k}"
+        assert e <= 1e-4, (k, e)
+    print(f"articulated backward ({bwd}, B={B}, S={S}) vs fp64 at the GPU's forward values: "
+          f"worst {worst:.2e} ({worst_name})")
 
 
 def _make(seed=0):
@@ -350,10 +438,20 @@ def test_art_adam_all_tensors(golden):
 def test_art_train_step_c5_4096_rays():
     """Config C5 on the articulated auto-decoder at its stated size: one training step on a
     4096-ray batch.  Loss against the oracle on our sample positions (rtol 1e-5) and end to end
-    (rtol 1e-4), and every MLP parameter's and latent code's gradient teacher-forced against the
-    fp32 oracle within max(2 x the oracle's own fp32-vs-fp64 distance, the largest such distance
-    over the level's tensors, 1e-3) of the tensor's max (the gradients see sin(2^9 x'): there
-    the fp32 oracle itself sits ~1e-2 from fp64)."""
+    (rtol 1e-4), and every MLP parameter's and latent code's gradient against the oracle on our
+    sample positions, twice:
+
+    (A) x'-forced: the fp64 oracle with pos_enc evaluated at OUR deformed points x' (gradients
+        straight through to its own deformation MLP, oracle.pos_enc_at): nothing is amplified,
+        so every tensor must agree within 1e-4 of its max -- the whole level (forward kernel,
+        compositing backward, backward chain, weight GEMMs) checked at C5's size;
+    (B) free-running against the fp32 oracle (the reference's arithmetic), per tensor within
+        max(2 r env, 1e-3) of the tensor's max, env = the oracle's own fp32-vs-fp64 distance on
+        that tensor.  The gradients see sin(2^9 x') (model_autodecoder.py:205-212), so they move
+        linearly with the rounding of x'; r = (rms of OUR x' error) / (rms of the fp32 oracle's
+        x' error), both against the fp64 x', measured on the level (f16x3 operands carry ~22
+        bits, fp32 24; r is printed).  That (A) holds at 1e-4 and test_art_backward_stage_
+        isolated at ~1e-6 is what shows the remaining distance is x' rounding, not a kernel."""
     from aonerf import train_art
     from test_gpu_train import c5_batch
 
@@ -371,15 +469,26 @@ def test_art_train_step_c5_4096_rays():
     loss.backward()
     torch.cuda.synchronize()
     lat_dev = {k: v.detach().cpu() for k, v in latents.items()}
+    # our x' per level: the fused forward at the level's t (deterministic: the values the
+    # autograd forward saw)
+    xp_ours = []
     with torch.no_grad():
+        lat_t = tuple(L_contig(latents[k]) for k in ("density", "color", "articulation"))
+        for level, mlp in enumerate((net.coarse_mlp, net.fine_mlp)):
+            t = ret[level][3]["t_vals"].contiguous()
+            P = [(m.weight.detach(), m.bias.detach()) for m in train_art.art_layers(mlp)]
+            raw = torch.empty((t.numel(), 4), device="cuda")
+            enc = train_art._forward_level_fused(train_art._Geo(mlp), P, lat_t, batch["rays_o"],
+                                                 batch["rays_d"], batch["viewdirs"], t, raw)[2]
+            xp_ours.append(enc[:, :3].cpu())
         rays = {k: batch[k].cpu() for k in ("rays_o", "rays_d", "viewdirs")}
         params = O.split_state_dict(W.art_state_dict(0))
         e2e = O.art_nerf_forward(params, rays, True, True, 2.0, 6.0, lat_dev, u_coarse=u_c.cpu(),
                                  u_fine=u_f.cpu())
         tgt = target.cpu()
         ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
-    ref, ref_loss = {}, None
-    for dtype in (torch.float32, torch.float64):
+    ref, ref_loss, xps = {}, None, {}
+    for mode, dtype in (("fp32", torch.float32), ("fp64", torch.float64), ("forced", torch.float64)):
         rays = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
         params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
                   for p in O.split_state_dict(W.art_state_dict(0))]
@@ -388,14 +497,16 @@ def test_art_train_step_c5_4096_rays():
         lv_loss = 0.0
         for level in range(2):
             t = ret[level][3]["t_vals"].cpu().to(dtype)
-            comp, acc, w, depth = O.art_render_level(params, rays, t, level, True, lat)
-            lv_loss = lv_loss + O.img2mse(comp, tgt)
+            out = O.art_render_level(params, rays, t, level, True, lat, return_xp=True,
+                                     xp_fixed=xp_ours[level] if mode == "forced" else None)
+            xps[(mode, level)] = out[4].detach().double()
+            lv_loss = lv_loss + O.img2mse(out[0], tgt)
         lv_loss.backward()
-        if dtype == torch.float32:
+        if mode == "fp32":
             ref_loss = lv_loss.item()
-        ref[dtype] = {f"{pre}{n}": v.grad.double().numpy()
-                      for lv, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")) for n, v in params[lv].items()}
-        ref[dtype].update({f"latent {k}": v.grad.double().numpy() for k, v in lat.items()})
+        ref[mode] = {f"{pre}{n}": v.grad.double().numpy()
+                     for lv, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")) for n, v in params[lv].items()}
+        ref[mode].update({f"latent {k}": v.grad.double().numpy() for k, v in lat.items()})
         del params, lv_loss
     print(f"C5 art loss gpu {loss.item():.8f}  oracle on our t {ref_loss:.8f}  "
           f"oracle end to end {ref_e2e:.8f}")
@@ -403,20 +514,34 @@ def test_art_train_step_c5_4096_rays():
     np.testing.assert_allclose(loss.item(), ref_e2e, rtol=1e-4)
     ours = {n: p.grad.cpu().numpy() for n, p in net.named_parameters()}
     ours.update({f"latent {k}": v.grad.cpu().numpy() for k, v in latents.items()})
-    # the level's noise floor: the oracle's own largest fp32-vs-fp64 distance over the level's
-    # tensors (on a randomized coarse level with acc ~ 1 the fp32 evaluation itself sits ~1e-2
-    # from fp64 on most tensors; one tensor's own distance can be 5x below its neighbours')
-    envs = {n: rel_err(w, ref[torch.float64][n]) for n, w in ref[torch.float32].items()}
-    level_env = {pre: max(e for n, e in envs.items() if n.startswith(pre))
-                 for pre in ("coarse_mlp.", "fine_mlp.", "latent")}
-    worst = 0.0
-    for name, want in ref[torch.float32].items():
+    # x' rounding: ours and the fp32 oracle's, against the fp64 oracle's, per level
+    rms = lambda a: float(a.pow(2).mean().sqrt())  # noqa: E731
+    ratio = {}
+    for level, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")):
+        x64 = xps[("fp64", level)]
+        e_ours = rms(xp_ours[level].double() - x64)
+        e_32 = rms(xps[("fp32", level)] - x64)
+        ratio[pre] = max(1.0, e_ours / e_32)
+        print(f"  level {level}: x' rms error vs fp64  ours {e_ours:.2e}  fp32 oracle {e_32:.2e}  "
+              f"r = {e_ours / e_32:.2f}")
+    ratio["latent"] = max(ratio.values())
+    worst_a = worst_b = 0.0
+    for name, want in ref["fp32"].items():
+        ea = rel_err(ours[name], ref["forced"][name])
+        worst_a = max(worst_a, ea)
+        env = rel_err(want, ref["fp64"][name])
+        r = next(v for pre, v in ratio.items() if name.startswith(pre))
         e = rel_err(ours[name], want)
-        env = envs[name]
-        lvl = next(v for pre, v in level_env.items() if name.startswith(pre))
-        allow = max(2 * env, lvl, 1e-3)
-        if e > 1e-4:
-            print(f"  {name:45s} ours {e:.2e}  oracle fp32-vs-fp64 {env:.2e} (level max {lvl:.2e})")
-        worst = max(worst, e / allow)
-        assert e <= allow, (name, e, env, lvl)
-    print(f"C5 art teacher-forced grads (4096 rays): worst error / allowance {worst:.2f}")
+        allow = max(2 * r * env, 1e-3)
+        if e > 1e-4 or ea > 1e-5:
+            print(f"  {name:45s} (A) x'-forced {ea:.2e}  (B) ours {e:.2e}  oracle fp32-vs-fp64 "
+                  f"{env:.2e}  allowance {allow:.2e}")
+        worst_b = max(worst_b, e / allow)
+        assert ea <= 1e-4, (name, "x'-forced", ea)
+        assert e <= allow, (name, e, env, r)
+    print(f"C5 art grads (4096 rays): (A) x'-forced worst {worst_a:.2e}; (B) free-running worst "
+          f"error / allowance {worst_b:.2f}")
+
+
+def L_contig(x):
+    return x.detach().reshape(1, -1).contiguous()

@@ -6,7 +6,10 @@ BASELINE config C4) equals the single-process render bit for bit.  (2) A DDP tra
 gradients, bit for bit as computed from each batch alone.  (3) The RCCL branch itself (backend
 "nccl", a process group of one on the box's GPU -- RCCL refuses two ranks on one device): the
 640x480 frame (config C4's size) gathered device-resident and the flat-bucket gradient
-all-reduce, both equal to the single-process results bit for bit."""
+all-reduce, both equal to the single-process results bit for bit.  (4) Config C4's own partition:
+8 ranks (gloo, all on the box's one GPU) each render their 60-row band of the 640x480 frame
+with the HIP kernels and gather_frame assembles it on rank 0, bit-equal to a single-process
+render_frame.  (5) interface.test_epoch at world 2 returns the single-rank stats exactly."""
 import os
 import socket
 
@@ -161,3 +164,106 @@ def test_rccl_gather_and_allreduce_world1():
     for a, b, c in zip(g_after, g_before, g_ref):
         np.testing.assert_array_equal(a, b)  # all-reduce over one rank / 1 is the identity
         np.testing.assert_array_equal(b, c.cpu().numpy())
+
+
+def _worker_c4(rank, world, port, q):
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from aonerf import parallel
+        from aonerf.render import create_spheric_poses, sapien_focal
+
+        net = _net()
+        p0, n, n_max = parallel.band(480, 640, rank, world)
+        frame, local = parallel.render_frame_sharded(net, create_spheric_poses(4.0)[7], 480, 640,
+                                                     sapien_focal(480))
+        q.put((rank, p0, n, n_max, local.shape[0],
+               frame.cpu().numpy() if frame is not None else None))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world, extra=()):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + tuple(extra)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = [q.get(timeout=300) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    for p in procs:
+        assert p.exitcode == 0
+    return got
+
+
+def test_c4_eight_row_bands_full_frame():
+    """BASELINE config C4's partition at its size: 8 ranks x 60 rows of the 640x480 frame
+    (38,400 rays each), rendered with the HIP kernels and gathered to rank 0 (interface.py:31-51 /
+    run.py:109-111 shard the test set across DDP ranks; here the frame's rows are the shards)."""
+    from aonerf.render import create_spheric_poses, render_frame, sapien_focal
+
+    world = 8
+    got = {r[0]: r[1:] for r in _spawn(_worker_c4, world)}
+    for rank in range(world):
+        p0, n, n_max, n_local, frame = got[rank]
+        assert (p0, n, n_max, n_local) == (rank * 60 * 640, 60 * 640, 60 * 640, 60 * 640)
+        assert (frame is None) == (rank != 0)
+    net = _net()
+    ref = render_frame(net, create_spheric_poses(4.0)[7], 480, 640, sapien_focal(480)).cpu().numpy()
+    assert got[0][4].shape == ref.shape == (480 * 640, 5)
+    np.testing.assert_array_equal(got[0][4], ref)
+
+
+def _mini_dataset():
+    from aonerf.datasets import SapienDataset
+
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "data", "sapien_mini")
+    split = "test" if os.path.isdir(os.path.join(root, "test")) else "val"
+    return SapienDataset(root, split, img_wh=(32, 24), white_back=True)
+
+
+def _epoch_net():
+    from aonerf.model import NeRF
+    from oracle import weights as W
+
+    net = NeRF().cuda().requires_grad_(False)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.nerf_state_dict(0).items()})
+    return net
+
+
+def _worker_epoch(rank, world, port, q, out_dir):
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from aonerf.interface import test_epoch
+
+        stats = test_epoch(_epoch_net(), _mini_dataset(), out_dir=out_dir if rank == 0 else None)
+        q.put((rank, stats))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_epoch_world2_equals_single_rank(tmp_path):
+    """interface.test_epoch (LitNeRF test loop + test_epoch_end, model.py:459-507,
+    interface.py:31-51) with its images rendered in row bands by 2 ranks and gathered: rank 0
+    returns exactly the single-rank PSNR / object-PSNR stats and writes the same images."""
+    from aonerf.interface import test_epoch
+
+    got = dict(_spawn(_worker_epoch, 2, (str(tmp_path / "w2"),)))
+    assert got[1] is None
+    single = test_epoch(_epoch_net(), _mini_dataset(), out_dir=str(tmp_path / "w1"))
+    assert got[0] == single, (got[0], single)
+    names = sorted(os.listdir(tmp_path / "w1"))
+    assert names == sorted(os.listdir(tmp_path / "w2")) and "results.json" in names
+    for nm in names:
+        assert open(tmp_path / "w1" / nm, "rb").read() == open(tmp_path / "w2" / nm, "rb").read(), nm

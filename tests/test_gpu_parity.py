@@ -554,6 +554,27 @@ def test_lindisp(golden, precision):
     assert not np.array_equal(t_ref.numpy(), g["coarse_t"])  # the option changed the schedule
 
 
+@pytest.mark.parametrize("nf", [300, 447])
+def test_large_num_fine_samples(golden, nf):
+    """N_importance beyond the fused march kernel's 256 (up to 447: the fine level's 65 + N samples within aon_composite_fwd's 512): the render
+    takes aon_composite_fwd + aon_sample_pdf (model.march_ok) for both NeRF and NeRF_AE_Art,
+    and the vanilla two-level chain holds every link at 1e-4 (fine t bit-exact)."""
+    from aonerf import model as M
+
+    assert not M.march_ok(65, nf) and M.march_ok(65, 256)
+    g = golden("forward_eval.npz")
+    params = O.split_state_dict(W.nerf_state_dict(0))
+    rays = rays_of(g)
+    ret = check_chain(make_nerf("f16x3", num_fine_samples=nf), rays, params)
+    assert ret[1][4]["t_vals"].shape[1] == 65 + nf
+    from aonerf.model_autodecoder import NeRF_AE_Art
+    from aonerf.synthetic import art_latents, init_like_reference
+
+    art = init_like_reference(NeRF_AE_Art(num_fine_samples=nf)).cuda().requires_grad_(False)
+    out = art(rays, False, True, 2.0, 6.0, art_latents(0, device="cuda"), return_intermediates=True)
+    assert out[1][3]["t_vals"].shape[1] == 65 + nf and torch.isfinite(out[1][0]).all()
+
+
 @pytest.mark.parametrize("path", ["render", "train"])
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_density_noise(golden, precision, path):

@@ -159,3 +159,52 @@ def test_training_step_refused_on_overflow(golden):
     loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
     loss.backward()
     opt.step()
+
+
+def test_torch_adam_refuses_overflow(golden):
+    """the reference trains through Lightning with torch.optim.Adam
+    (configure_optimizers, model.py:386-389).  The global optimizer step pre-hook aonerf.train
+    installs refuses that optimizer's step too, and leaves the parameters untouched."""
+    from aonerf import train
+
+    g, sd, params, m = _scaled(golden, 1.2e4)
+    net = _net(sd).requires_grad_(True)
+    rays = {k: torch.from_numpy(g[k]).cuda() for k in ("rays_o", "rays_d", "viewdirs")}
+    batch = dict(rays, target=torch.full((rays["rays_o"].shape[0], 3), 0.5, device="cuda"))
+    opt = torch.optim.Adam(net.parameters(), lr=5e-4)
+    loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
+    loss.backward()
+    before = [p.detach().clone() for p in net.parameters()]
+    with pytest.raises(FloatingPointError):
+        opt.step()
+    assert all(torch.equal(a, p.detach()) for a, p in zip(before, net.parameters()))
+    # the pending state was consumed: a clean step afterwards goes through
+    g, sd, params, m = _scaled(golden, 6.0e3)
+    net = _net(sd).requires_grad_(True)
+    opt = torch.optim.Adam(net.parameters(), lr=5e-4)
+    loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
+    loss.backward()
+    opt.step()
+
+
+def test_overflow_survives_repack_before_step(golden):
+    """a level re-packed before the optimizer step (gradient accumulation: two
+    forwards with the same sample count) must not erase the first forward's overflow -- the
+    status is kept in a sticky word, and the step is refused."""
+    from aonerf import train
+
+    g, sd_hot, _, _ = _scaled(golden, 1.2e4)
+    _, sd_ok, _, _ = _scaled(golden, 6.0e3)
+    net = _net(sd_hot).requires_grad_(True)
+    rays = {k: torch.from_numpy(g[k]).cuda() for k in ("rays_o", "rays_d", "viewdirs")}
+    batch = dict(rays, target=torch.full((rays["rays_o"].shape[0], 3), 0.5, device="cuda"))
+    opt = train.Adam(net.parameters())
+    loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
+    loss.backward()  # overflows
+    with torch.no_grad():  # second micro-batch on in-range weights, same sample counts
+        for k, p in net.named_parameters():
+            p.copy_(torch.from_numpy(sd_ok[k]))
+    loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
+    loss.backward()
+    with pytest.raises(FloatingPointError):
+        opt.step()

@@ -1,0 +1,62 @@
+"""Host logic of the fp16x3 range guard's bookkeeping (aonerf._lib register_pack /
+check_pending, aonerf.train's global optimizer step pre-hook), on CPU stand-in buffers whose
+last 16 bytes play the packed stream's status block (include/aonerf.h aon_mlp_read_status).
+No kernel runs: the status words are set by hand."""
+import pytest
+import torch
+
+
+def _buf(status=0):
+    b = torch.zeros(64, dtype=torch.float32)
+    b.view(torch.int32)[-4] = status
+    return b
+
+
+@pytest.fixture
+def L():
+    from aonerf import _lib
+
+    _lib.PENDING_PACKS.clear()
+    _lib._STICKY.clear()
+    yield _lib
+    _lib.PENDING_PACKS.clear()
+    _lib._STICKY.clear()
+
+
+def test_pending_consumed_once(L):
+    L.register_pack(("train", "fwd65"), _buf(1))
+    assert L.check_pending({"cpu"}) is True
+    assert L.check_pending({"cpu"}) is False  # consumed
+    L.register_pack(("train", "fwd65"), _buf(0))
+    assert L.check_pending(None) is False
+
+
+def test_repack_keeps_status_sticky(L):
+    b = _buf(1)
+    L.register_pack(("train", "fwd65"), b)
+    L.register_pack(("train", "fwd65"), b)  # called before the re-pack: the 1 is kept
+    b.view(torch.int32)[-4] = 0          # what the re-pack then does to the status word
+    assert "cpu" in L._STICKY
+    assert L.check_pending({"cpu"}) is True
+    assert not L._STICKY and not L.PENDING_PACKS
+
+
+def test_other_device_untouched(L):
+    L.register_pack(("train", "fwd65"), _buf(1))
+    assert L.check_pending({"cuda:0"}) is False
+    assert L.PENDING_PACKS  # still pending for its own device
+
+
+def test_torch_optimizer_hook_refuses(L):
+    from aonerf import train
+
+    p = torch.nn.Parameter(torch.ones(3))
+    p.grad = torch.ones(3)
+    opt = torch.optim.SGD([p], lr=0.1)
+    L.register_pack(("train", "fwd65"), _buf(1))
+    with pytest.raises(FloatingPointError):
+        opt.step()
+    assert torch.equal(p.detach(), torch.ones(3))
+    opt.step()  # consumed: the next step goes through
+    assert torch.allclose(p.detach(), torch.full((3,), 0.9))
+    assert train.RANGE_CHECK
