@@ -695,7 +695,7 @@ def test_composite_march_equals_two_kernels(S, Ns):
     from aonerf import helper
 
     g = torch.Generator().manual_seed(S * 1000 + Ns)
-    B = 700
+    B = 701  # ragged for the four-rays-per-wave kernel (S = 65, Ns = 128)
     t = torch.sort(2.0 + 4.0 * torch.rand((B, S), generator=g), -1).values
     raw = torch.cat([torch.randn((B, S, 3), generator=g),
                      3.0 * torch.randn((B, S, 1), generator=g)], -1).reshape(-1, 4)
@@ -704,7 +704,11 @@ def test_composite_march_equals_two_kernels(S, Ns):
     raw_d, t_d, dirs_d = cuda(raw), cuda(t), cuda(dirs)
     for rnd in (False, True):
         if rnd:
-            u, us = cuda(torch.rand((B, Ns), generator=g)), Ns
+            # per-ray u; every third row sorted, so waves mix rays that need the sort and rays
+            # that do not
+            ur = torch.rand((B, Ns), generator=g)
+            ur[::3] = ur[::3].sort(-1).values
+            u, us = cuda(ur), Ns
         else:
             u, us = helper.eval_u(Ns, "cuda"), 0
         for act, white, keep_w in ((L.ACT_VANILLA, 1, True), (L.ACT_ARTIC, 0, False),
