@@ -175,8 +175,11 @@ __device__ __forceinline__ double row_incl_sum(double x) {
 #ifndef AON_MARCH_DIRECT
 #define AON_MARCH_DIRECT 1  // 0: merged rows staged in LDS and copied out (more LDS per wave)
 #endif
+#ifndef AON_MARCH_PIPE
+#define AON_MARCH_PIPE 0  // 1: the next group's inputs loaded during this group's resampling (resident grid): 7% slower (profiles/r03/ab_march)
+#endif
 #ifndef AON_MARCH_ROWS_OCC
-#define AON_MARCH_ROWS_OCC 5  // waves per SIMD the register budget is built for (87 VGPRs; 6: 80 + spills)
+#define AON_MARCH_ROWS_OCC 5  // waves per SIMD the register budget is built for (92 VGPRs, no spills; 6 and 7 spill and run slower: profiles/r03/ab_march)
 #endif
 
 struct RayLds {
@@ -194,42 +197,70 @@ struct WaveLds {
 #endif
 };
 
+// sorted a[0 .. 64) (a[63] = 1 for a CDF): entries <= x, count_lift<true>(a, 64, x) exactly --
+// the top probe decides 64 / below, the six lower probes do not depend on it
+__device__ __forceinline__ int count_le64(const float* a, float x) {
+  const bool all = a[63] <= x;
+  int c = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1) c = a[c + step - 1] <= x ? c + step : c;
+  return all ? 64 : c;
+}
+
+template <int ACT>
 __global__ __launch_bounds__(64 * kWaves, AON_MARCH_ROWS_OCC) void k_march_rows(
     const float* __restrict__ raw4, const float* __restrict__ tv, const float* __restrict__ dirs,
-    int64_t B, int white, int act, const float* __restrict__ u_g, int64_t u_stride,
+    int64_t B, int white, const float* __restrict__ u_g, int64_t u_stride,
     float* __restrict__ out_rgb, float* __restrict__ out_acc, float* __restrict__ out_w,
     float* __restrict__ out_depth, float* __restrict__ t_out) {
+  constexpr int act = ACT;
   __shared__ WaveLds lds_all[kWaves];
   WaveLds& WL = lds_all[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63, row = lane >> 4, q = lane & 15;
   RayLds& L = WL.r[row];
   const int64_t ngroups = (B + 3) >> 2;
-  for (int64_t grp = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); grp < ngroups;
-       grp += (int64_t)gridDim.x * kWaves) {
-    const int64_t ray = 4 * grp + row;
-    const bool valid = ray < B;
-    const int64_t r0 = valid ? ray * kS : 0;
-    // ---- loads: t and raw of samples q + 16 m (m = 4: sample 64, lane 0), the fine u
-    float tt[5];
-    f4 rw[5];
+  const int64_t gstride = (int64_t)gridDim.x * kWaves;
+  // a group's per-ray inputs: t and raw of samples q + 16 m and sample 64 ("m = 4", every lane;
+  // lane 0's copy is the one used), rays_d.  The last group's rows past B read the last ray (no
+  // branches around the loads) and store nothing; 32-bit offsets (the host checks B * (S + Ns)
+  // < 2^31).  AON_MARCH_PIPE: the next group's inputs are loaded while this group resamples
+  // (its t / raw registers are dead by then), so a wave streaming several groups does not wait
+  // on HBM at the top of each.
+  auto load_group = [&](int64_t g, float (&t5)[5], f4 (&r5)[5], float (&d3)[3]) {
+    const int64_t ry = 4 * g + row;
+    const uint32_t rr = static_cast<uint32_t>(ry < B ? ry : B - 1);
 #pragma unroll
     for (int m = 0; m < 5; ++m) {
-      tt[m] = 0.f;
-      rw[m] = f4{0.f, 0.f, 0.f, 0.f};
-      if (valid && (m < 4 || q == 0)) {
-        tt[m] = tv[r0 + 16 * m + q];
-        rw[m] = *reinterpret_cast<const f4*>(raw4 + (r0 + 16 * m + q) * 4);
-      }
+      const uint32_t i = rr * kS + (m < 4 ? 16 * m + q : 64);
+      t5[m] = tv[i];
+      r5[m] = *reinterpret_cast<const f4*>(raw4 + 4 * i);
     }
-    float uu[8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) uu[n] = valid ? u_g[ray * u_stride + 16 * n + q] : 0.f;
-    float dx = 0.f, dy = 0.f, dz = 0.f;
-    if (valid) {
-      dx = dirs[3 * ray];
-      dy = dirs[3 * ray + 1];
-      dz = dirs[3 * ray + 2];
+    for (int c = 0; c < 3; ++c) d3[c] = dirs[3 * rr + c];
+  };
+  int64_t grp = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  float ntt[5], nd[3];
+  f4 nrw[5];
+  if (AON_MARCH_PIPE && grp < ngroups) load_group(grp, ntt, nrw, nd);
+  for (; grp < ngroups; grp += gstride) {
+    const int64_t ray = 4 * grp + row;
+    const bool valid = ray < B;
+    const uint32_t rc = static_cast<uint32_t>(valid ? ray : B - 1);
+    const uint32_t r0 = rc * kS;
+    float tt[5], d3[3];
+    f4 rw[5];
+    if (AON_MARCH_PIPE) {
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        tt[m] = ntt[m];
+        rw[m] = nrw[m];
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) d3[c] = nd[c];
+    } else {
+      load_group(grp, tt, rw, d3);
     }
+    const float dx = d3[0], dy = d3[1], dz = d3[2];
     const float dnorm = sqrtf(fmaf(dz, dz, fmaf(dy, dy, __fmul_rn(dx, dx))));
     // ---- t[i + 1] of sample i = q + 16 m: lane q + 1, or lane 0's block m + 1 (row_ror:15)
     float tn[4];
@@ -269,7 +300,7 @@ __global__ __launch_bounds__(64 * kWaves, AON_MARCH_ROWS_OCC) void k_march_rows(
     if (out_w && valid) {
 #pragma unroll
       for (int m = 0; m < 5; ++m)
-        if (m < 4 || q == 0) out_w[r0 + 16 * m + q] = w[m];
+        if (m < 4 || q == 0) out_w[r0 + (m < 4 ? 16 * m + q : 64)] = w[m];
     }
     // ---- rgb: row_sum_ilp4 over 65 terms x_i = w_i rgb_i: folds C_k = x[k] + x[4+k] + ...
     // + x[60+k] as row_ror:4 chains (term s of fold k sits at lane 4 (s % 4) + k, block s / 4),
@@ -344,6 +375,7 @@ __global__ __launch_bounds__(64 * kWaves, AON_MARCH_ROWS_OCC) void k_march_rows(
       L.bins[16 * m + q] = __fmul_rn(0.5f, __fadd_rn(tn[m], tt[m]));
     }
     if (q == 0) L.tm[64] = tt[4];
+    if (AON_MARCH_PIPE && grp + gstride < ngroups) load_group(grp + gstride, ntt, nrw, nd);
     // wn[m] at lane q = w[q + 16 m + 1] = the pdf's weight w'[q + 16 m]
     float wn[4];
 #pragma unroll
@@ -415,21 +447,53 @@ __global__ __launch_bounds__(64 * kWaves, AON_MARCH_ROWS_OCC) void k_march_rows(
       for (int k = q; k < 62; k += 16) out_w[r0 + 3 + k] = L.cdf[k + 1];
     }
 #endif
-    // inverse CDF (helper.py:232-241) for u_j, j = 16 n + q
+    // inverse CDF (helper.py:232-241) for u_j, j = 16 n + q (u loaded here, not with the
+    // compositor's inputs: 8 fewer registers live across the compositor; eval mode reads one
+    // shared L2-resident row).  The eight searches run level by level (count_le64's probes, all
+    // eight samples' LDS reads of a level issued together): sample by sample, each probe waited
+    // for its own read and the chain of dependent LDS round trips set the kernel's pace.
+    float uu[8];
+    const uint32_t u0 = rc * static_cast<uint32_t>(u_stride);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) uu[n] = u_g[u0 + 16 * n + q];
     float smp[8];
     int hint[8];
+    {
+      const float top = L.cdf[63];
+      int c[8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      const float uj = uu[n];
-      const int idx = count_lift<true>(L.cdf, 64, uj);
-      const int i0 = idx - 1 < 0 ? 0 : (idx - 1 > 63 ? 63 : idx - 1);
-      const int i1 = idx > 63 ? 63 : idx;
-      hint[n] = i0;
-      const float c0 = L.cdf[i0], c1 = L.cdf[i1];
-      const float b0 = L.bins[i0], b1 = L.bins[i1];
-      float qq = nan_to_num(__fdiv_rn(__fsub_rn(uj, c0), __fsub_rn(c1, c0)), 0.0f);
-      qq = fminf(fmaxf(qq, 0.0f), 1.0f);
-      smp[n] = __fadd_rn(b0, __fmul_rn(qq, __fsub_rn(b1, b0)));
+      for (int n = 0; n < 8; ++n) c[n] = 0;
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1) {
+        float v[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) v[n] = L.cdf[c[n] + step - 1];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) c[n] = v[n] <= uu[n] ? c[n] + step : c[n];
+      }
+      // the interpolation in two halves of four samples (register budget)
+#pragma unroll
+      for (int h = 0; h < 8; h += 4) {
+        float c0[4], c1[4], b0[4], b1[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = h + e;
+          const int idx = top <= uu[n] ? 64 : c[n];  // = count_le(cdf, 64, u)
+          const int i0 = idx - 1 < 0 ? 0 : (idx - 1 > 63 ? 63 : idx - 1);
+          const int i1 = idx > 63 ? 63 : idx;
+          hint[n] = i0;
+          c0[e] = L.cdf[i0];
+          c1[e] = L.cdf[i1];
+          b0[e] = L.bins[i0];
+          b1[e] = L.bins[i1];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float qq = nan_to_num(__fdiv_rn(__fsub_rn(uu[h + e], c0[e]), __fsub_rn(c1[e], c0[e])), 0.0f);
+          qq = fminf(fmaxf(qq, 0.0f), 1.0f);
+          smp[h + e] = __fadd_rn(b0[e], __fmul_rn(qq, __fsub_rn(b1[e], b0[e])));
+        }
+      }
     }
     // sorted already (u ascending: always in eval mode)?  NaN compares unordered -> sort
     bool unsorted = false;
@@ -442,7 +506,7 @@ __global__ __launch_bounds__(64 * kWaves, AON_MARCH_ROWS_OCC) void k_march_rows(
 #if AON_MARCH_DIRECT
     // the merged row goes straight to t_fine: a row's stores land in one ~772-B window, nearly
     // consecutive per instruction (slot j + rank of sample j)
-    float* orow = t_out + (valid ? ray : 0) * kNo;
+    float* orow = t_out + rc * kNo;
     float* samp = L.cdf;  // cdf + bins, dead after the inverse CDF
 #else
     float* orow = WL.orow + row * kNo;
@@ -455,28 +519,73 @@ __global__ __launch_bounds__(64 * kWaves, AON_MARCH_ROWS_OCC) void k_march_rows(
       uint8_t* filled = reinterpret_cast<uint8_t*>(L.cdf);
       for (int p = q; p < kNo; p += 16) filled[p] = 0;
       wave_sync();
+      // t[i0] <= bins[i0] <= s <= bins[i0 + 1] <= t[i0 + 2]: the rank is i0 + 1 .. i0 + 3 --
+      // t[c - 1 .. c + 2] read at once, the two steps as selects; pdf_ray's fallback rule (t[c - 1]
+      // > s, which a NaN sample never meets) or a third step still possible takes the search
+      int pos[8];
+      bool slow = false;
+#pragma unroll
+      for (int h = 0; h < 8; h += 4) {
+        float ta[4], tb[4], tc[4], td[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = hint[h + e] + 1;  // 1 .. 64
+          ta[e] = L.tm[c - 1];
+          tb[e] = L.tm[c];
+          tc[e] = L.tm[c + 1 < kS ? c + 1 : kS - 1];
+          td[e] = L.tm[c + 2 < kS ? c + 2 : kS - 1];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = h + e;
+          const float sv = smp[n];
+          const int c = hint[n] + 1;
+          const bool s1 = c < kS && tb[e] <= sv;
+          const bool s2 = s1 && c + 1 < kS && tc[e] <= sv;
+          const bool s3 = s2 && c + 2 < kS && td[e] <= sv;
+          const bool bad = ta[e] > sv || s3;
+          pos[n] = 16 * n + q + c + (s1 ? 1 : 0) + (s2 ? 1 : 0);
+          if (bad) pos[n] = -1;
+          slow |= bad;
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(slow)) {  // (never on rows whose bins are t's mids)
+#pragma unroll
+        for (int n = 0; n < 8; ++n)
+          if (pos[n] < 0) pos[n] = 16 * n + q + count_le(L.tm, kS, smp[n]);
+      }
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
-        const float s = smp[n];
-        int c = hint[n] + 1;
-        if (c > kS || L.tm[c - 1] > s) {
-          c = count_le(L.tm, kS, s);
-        } else {
-          while (c < kS && L.tm[c] <= s) ++c;
-        }
-        const int pos = 16 * n + q + c;
-        filled[pos] = 1;
-        if (!AON_MARCH_DIRECT || valid) orow[pos] = s;
+        filled[pos[n]] = 1;
+        if (!AON_MARCH_DIRECT || valid) orow[pos[n]] = smp[n];
       }
       wave_sync();
+      // the remaining slots take t in order: slot p's rank among the row's empty slots from a
+      // per-row ballot + popcount, all 13 blocks of 16 slots' flags read at once
+      constexpr int kBlk = (kNo + 15) / 16;
       int carry = 0;
       const uint32_t below = (1u << q) - 1u;
-      for (int p0 = 0; p0 < kNo; p0 += 16) {
-        const int p = p0 + q;
-        const bool empty = p < kNo && filled[p] == 0;
-        const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_ballot_w64(empty) >> (16 * row)) & 0xFFFFu;
-        if (empty && (!AON_MARCH_DIRECT || valid)) orow[p] = L.tm[carry + __builtin_popcount(m & below)];
-        carry += __builtin_popcount(m);
+#pragma unroll
+      for (int i0 = 0; i0 < kBlk; i0 += 7) {  // two passes of <= 7 blocks (register budget)
+        uint32_t fl[7];
+        int rank[7];
+        float tvv[7];
+#pragma unroll
+        for (int e = 0; e < 7; ++e) {
+          const int i = i0 + e;
+          fl[e] = (i < kBlk && 16 * i + q < kNo) ? filled[16 * i + q] : 1u;
+        }
+#pragma unroll
+        for (int e = 0; e < 7; ++e) {
+          const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_ballot_w64(fl[e] == 0) >> (16 * row)) & 0xFFFFu;
+          rank[e] = fl[e] == 0 ? carry + __builtin_popcount(m & below) : -1;
+          carry += __builtin_popcount(m);
+        }
+#pragma unroll
+        for (int e = 0; e < 7; ++e) tvv[e] = L.tm[rank[e] < 0 ? 0 : rank[e]];
+#pragma unroll
+        for (int e = 0; e < 7; ++e)
+          if (rank[e] >= 0 && (!AON_MARCH_DIRECT || valid)) orow[16 * (i0 + e) + q] = tvv[e];
       }
     } else {
       // some ray of the wave needs the sort: bitonic sort of every row's 128 samples (a sorted
@@ -560,12 +669,21 @@ extern "C" int aon_composite_march(const float* raw, const float* t, const float
 #define AON_MARCH(NB_, SC_, NBX_)                                                                 \
   launch_march<NB_, SC_, NBX_>(st, raw, t, dirs, B, S, white_bkgd, act, u, u_stride, Ns, p2,      \
                                comp_rgb, acc, weights, depth, t_fine)
-  if (AON_MARCH_ROWS && S == rowm::kS && Ns == rowm::kNs) {
+  if (AON_MARCH_ROWS && S == rowm::kS && Ns == rowm::kNs && B * rowm::kNo < (int64_t(1) << 31) &&
+      (u_stride == 0 || B * u_stride < (int64_t(1) << 31))) {
     // the render's coarse level (64 + 1 samples, 128 fine): four rays per wave
     const int64_t groups = (B + 3) / 4;
-    hipLaunchKernelGGL(rowm::k_march_rows, grid_for(groups, rowm::kWaves, 1 << 16),
-                       64 * rowm::kWaves, 0, st, raw, t, dirs, B, white_bkgd, act, u, u_stride,
-                       comp_rgb, acc, weights, depth, t_fine);
+#define AON_ROWS(A_)                                                                              \
+  hipLaunchKernelGGL(rowm::k_march_rows<A_>,                                                      \
+                     AON_MARCH_PIPE ? resident_grid(rowm::k_march_rows<A_>, 64 * rowm::kWaves,     \
+                                                    (groups + rowm::kWaves - 1) / rowm::kWaves)    \
+                                    : grid_for(groups, rowm::kWaves, 1 << 16),                     \
+                     64 * rowm::kWaves, 0, st, raw, t, dirs, B, white_bkgd, u, u_stride, comp_rgb, \
+                     acc, weights, depth, t_fine)
+    if (act == AON_ACT_NONE) AON_ROWS(AON_ACT_NONE);
+    else if (act == AON_ACT_VANILLA) AON_ROWS(AON_ACT_VANILLA);
+    else AON_ROWS(AON_ACT_ARTIC);
+#undef AON_ROWS
   } else if (S == 65 && nbx == 2) {
     AON_MARCH(2, 65, 2);  // S = 65 with other fine counts: 64 + 1 samples
   } else {

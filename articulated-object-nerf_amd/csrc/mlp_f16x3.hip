@@ -92,6 +92,9 @@ __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<
         if (STORE && ts.noise) sig = __fadd_rn(sig, ts.noise[rows[c]]);  // raw_sigma + noise
         const f4 o = {act_rgb(rgb[c][0] * s, act), act_rgb(rgb[c][1] * s, act),
                       act_rgb(rgb[c][2] * s, act), act_sigma(sig, act)};
+#ifdef AON_ABL_NO_RAW_STORE  // timing-only A/B build (fused-pipeline question): no raw store
+        if (__builtin_isnan(o[0] + o[1] + o[2] + o[3]))
+#endif
         *reinterpret_cast<f4*>(raw + 4 * rows[c]) = o;
       }
     }
