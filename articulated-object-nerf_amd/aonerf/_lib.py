@@ -86,8 +86,13 @@ _SIGNATURES = {
     "aon_mlp_art_bwd_packed_bytes": (c_size, []),
     "aon_mlp_art_bwd_pack": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
     "aon_mlp_art_bwd": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp, vp, vp]),
+    "aon_mlp_art_pack_bf16": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
+    "aon_mlp_art_bwd_pack_bf16": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
+    "aon_mlp_art_bwd_bf16": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp, vp, vp]),
     "aon_mlp_art_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp,
                                       vp, vp, vp]),
+    "aon_mlp_art_fwd_train_bf16": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp,
+                                           vp, vp, vp, vp, c_int, vp]),
     "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,
                                   vp, vp, vp, vp]),
     "aon_image_mse": (c_int, [vp, vp, c_i64, c_i64, vp, c_int, vp, vp, vp]),

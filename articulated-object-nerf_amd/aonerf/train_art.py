@@ -136,6 +136,20 @@ FUSED_FORWARD = True
 # backward of a level: every input gradient in one fused kernel (aon_mlp_art_bwd) + the
 # weight-gradient GEMMs when True, else every product as a GEMM (_backward_level)
 FUSED_BACKWARD = True
+# numerics of the fused training kernels: "f16x3" (fp32-class, the parity mode) or "bf16"
+# (BASELINE config C5's bf16 on the articulated model): the whole backward chain and the
+# weight-gradient GEMMs bf16 (aon_mlp_art_bwd_bf16, aon_gemm mma_bf16), kept activations and
+# gradients bf16 (aon_mlp_art_fwd_train_bf16); compositing, the loss, their backward, the latent
+# terms and Adam stay fp32 on fp32 master weights (tests/test_gpu_art_train_bf16.py).
+PRECISION = "f16x3"
+# bf16 mode, forward numerics.  False (default): fp16x3 throughout, only the stores bf16.  True:
+# the trunk, heads and view branch one bf16 MFMA per product on the mixed stream of
+# aon_mlp_art_pack_bf16 (the deformation MLP stays fp16x3: x' = delta + xyz feeds pos_enc's
+# sin(2^9 x'), where bf16's 8 bits would move the top degree's phase by radians) -- 13% faster
+# per step, but the articulated gradients are ill-conditioned in the forward values and its
+# 2^-9 forward rounding alone leaves the deformation gradients at cosine 0.987 to the fp32
+# oracle (the bf16 backward itself, stage-isolated, is at >= 0.9999)
+BF16_TRUNK = False
 
 _packed = {}
 
@@ -171,50 +185,62 @@ def _buffer(key, nbytes, dev, guard=False):
     return buf
 
 
-def _pack(geo, P, lat, tag=""):
+def _pack(geo, P, lat, tag="", bf16=False):
     """The fused kernel's fp16x3 weight stream (aon_mlp_art_pack) of one level's parameters with
     this call's latent codes folded into the biases; re-packed on every call (the optimizer
-    updates the parameters in place)."""
+    updates the parameters in place).  bf16: the bf16 mode's mixed stream (aon_mlp_art_pack_bf16,
+    range-guarded: its deformation part is fp16x3)."""
     shape, app, art = lat
     dev = shape.device
     fb = {DEF0: _fold(*P[DEF0], 3, torch.cat([shape, art], -1)),
           PTS0: _fold(*P[PTS0], geo.ne, shape),
           PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
           VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
-    buf = _buffer(f"fwd{tag}", L.lib().aon_mlp_art_packed_bytes(), dev, guard=True)
-    L.call("aon_mlp_art_pack", L.ctypes.byref(_params_struct(P, fb)), L.ptr(buf), L.stream(dev))
+    buf = _buffer(f"fwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_art_packed_bytes(), dev,
+                  guard=True)
+    L.call("aon_mlp_art_pack_bf16" if bf16 else "aon_mlp_art_pack",
+           L.ctypes.byref(_params_struct(P, fb)), L.ptr(buf), L.stream(dev))
     return buf
 
 
-def _pack_bwd(P, dev, tag=""):
-    """The transposed weight stream of the fused backward chain (aon_mlp_art_bwd_pack)."""
-    buf = _buffer(f"bwd{tag}", L.lib().aon_mlp_art_bwd_packed_bytes(), dev, guard=True)
-    L.call("aon_mlp_art_bwd_pack", L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
+def _pack_bwd(P, dev, tag="", bf16=False):
+    """The transposed weight stream of the fused backward chain (aon_mlp_art_bwd_pack[_bf16])."""
+    buf = _buffer(f"bwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_art_bwd_packed_bytes(), dev,
+                  guard=not bf16)
+    L.call("aon_mlp_art_bwd_pack_bf16" if bf16 else "aon_mlp_art_bwd_pack",
+           L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
     return buf
 
 
 def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None,
-                         masks=None):
+                         masks=None, bf16=False):
     """_forward_level on the fused kernel (aon_mlp_art_fwd_train): raw (R x 4) and the kept
     activations (tiled, tiles.rows(R) rows each), plus the sample points and pos_enc(x')
     (row-major); ``masks`` ((16, tiles.rows(R), 8) int32) receives the ReLU' bits of hd0..3,
-    h0..7, hv0..3 for the backward chain."""
+    h0..7, hv0..3 for the backward chain.  bf16: the bf16 mode (aon_mlp_art_fwd_train_bf16;
+    hd / h / bot / hv kept as torch.bfloat16)."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
     NR = tiles.rows(R)
     if masks is None:
         masks = torch.empty((16, NR, 8), dtype=torch.int32, device=dev)
-    hd = torch.empty((4, NR, geo.wd), device=dev)
-    h = torch.empty((8, NR, geo.nw), device=dev)
-    bot = torch.empty((NR, geo.nw), device=dev)
-    hv = torch.empty((4, NR, geo.wc), device=dev)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    hd = torch.empty((4, NR, geo.wd), device=dev, dtype=dt)
+    h = torch.empty((8, NR, geo.nw), device=dev, dtype=dt)
+    bot = torch.empty((NR, geo.nw), device=dev, dtype=dt)
+    hv = torch.empty((4, NR, geo.wc), device=dev, dtype=dt)
     enc = torch.empty((R, geo.ne), device=dev)
     xyz = torch.empty((R, 3), device=dev)
-    packed = _pack(geo, P, lat, S)
+    mixed = bf16 and BF16_TRUNK
+    packed = _pack(geo, P, lat, S, mixed)
     e0 = _train._ev()
-    L.call("aon_mlp_art_fwd_train", L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs),
-           L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h),
-           L.ptr(bot), L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks), L.stream(dev))
+    args = (L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs), L.ptr(t_vals), B, S,
+            L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h), L.ptr(bot),
+            L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks))
+    if bf16:
+        L.call("aon_mlp_art_fwd_train_bf16", *args, int(mixed), L.stream(dev))
+    else:
+        L.call("aon_mlp_art_fwd_train", *args, L.stream(dev))
     _train._rec(f"art_fwd_train{S}", e0, R)
     return xyz, hd, enc, h, bot, hv
 
@@ -334,22 +360,24 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     when None); h_tiled: hd / h / bot / hv in the fused forward's tiled layout (else
     row-major); the chain's dzv / dbot / dz / dzd are tiled."""
     R, dev = xyz.shape[0], xyz.device
+    bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
         acts = list(hd) + list(h) + list(hv)
-        masks = relu_masks([tiles.untile(a, R) for a in acts] if h_tiled else acts, R)
+        masks = relu_masks([tiles.untile(a, R).float() for a in acts] if h_tiled else acts, R)
     wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
     shape, app, art = lat
     dshape, dapp, dart = dlat
     NR = tiles.rows(R)
-    dzv = torch.empty((4, NR, wc), device=dev)
-    dbot = torch.empty((NR, nw), device=dev)
-    dz = torch.empty((8, NR, nw), device=dev)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    dzv = torch.empty((4, NR, wc), device=dev, dtype=dt)
+    dbot = torch.empty((NR, nw), device=dev, dtype=dt)
+    dz = torch.empty((8, NR, nw), device=dev, dtype=dt)
     dxp = torch.empty((R, 3), device=dev)
-    dzd = torch.empty((4, NR, wd), device=dev)
+    dzd = torch.empty((4, NR, wd), device=dev, dtype=dt)
     work = _buffer("work", 4, dev)
-    packed = _pack_bwd(P, dev, S)
+    packed = _pack_bwd(P, dev, S, bf16)
     e0 = _train._ev()
-    L.call("aon_mlp_art_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
+    L.call("aon_mlp_art_bwd_bf16" if bf16 else "aon_mlp_art_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
            L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
     _train._rec(f"art_bwd_chain{S}", e0, R)
     e0 = _train._ev()
@@ -359,13 +387,16 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
         # chain_scale: dY is in the chain's d raw domain (draw, view/trunk outputs): A rides at
         # the chain's own per-call scale from max |d raw| (the word it left in `work`); the
         # deformation branch (dL/dx' carries pos_enc's 2^9, rescaled per sample) keeps 2^10.
-        # a_t: dY is one of the chain's tiled gradients; X is tiled when it is a kept activation
+        # a_t: dY is one of the chain's tiled gradients; X is tiled when it is a kept activation.
+        # bf16: one bf16 MFMA per product, no scales (bf16 has fp32's exponent range)
         dW = G[i][0]
         b_t = h_tiled and X is not enc and X is not venc and X is not xyz
         gemm(dW[:, col0:] if col0 else dW, dY, X, dW.shape[0], n_in, R, lda=ldy, a_kc=False,
-             ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0), a_scale=1.0 if chain_scale else gs,
-             b_scale=acts, rowsum=G[i][1] if bias else None,
-             a_amax=work if chain_scale else None, a_tiled=a_t, b_tiled=b_t)
+             ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0),
+             a_scale=1.0 if (chain_scale or bf16) else gs, b_scale=1.0 if bf16 else acts,
+             rowsum=G[i][1] if bias else None,
+             a_amax=work if (chain_scale and not bf16) else None, mma_bf16=bf16, a_tiled=a_t,
+             b_tiled=b_t)
 
     def dlatent(i, col0, l, dl, accumulate):
         dW, db = G[i]
@@ -426,7 +457,7 @@ class ArtRenderLevel(torch.autograd.Function):
             masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device=dev)
             xyz, hd, enc, h, bot, hv = _forward_level_fused(
                 geo, P, lat, L.contig(rays_o), L.contig(rays_d), L.contig(viewdirs),
-                L.contig(t_vals), raw, noise, masks)
+                L.contig(t_vals), raw, noise, masks, bf16=PRECISION == "bf16")
         else:
             xyz = torch.empty((R, 3), device=dev)
             L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
@@ -468,9 +499,9 @@ class ArtRenderLevel(torch.autograd.Function):
             _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
                                   ctx.masks, ctx.h_tiled)
         else:
-            if ctx.h_tiled:  # the all-GEMM backward reads row-major activations
-                hd, h, hv = (torch.stack([tiles.untile(x, R) for x in t]) for t in (hd, h, hv))
-                bot = tiles.untile(bot, R)
+            if ctx.h_tiled:  # the all-GEMM backward reads row-major fp32 activations
+                hd, h, hv = (torch.stack([tiles.untile(x, R).float() for x in t]) for t in (hd, h, hv))
+                bot = tiles.untile(bot, R).float()
             _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
         dlat = [d.reshape(s) for d, s in zip(dlat, lat_shapes)]

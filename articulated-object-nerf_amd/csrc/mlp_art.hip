@@ -22,13 +22,19 @@ namespace mlp {
 // MODE 0: (rays_o, rays_d, viewdirs, t) inputs; MODE 1: points (N, 3), condition (B, 27).
 // STORE: the training forward -- every layer's activations, the encodings of x' and the
 // sample points are kept for the backward (TrainStoreArt), raw_sigma gets the noise.
-template <int MODE, int NCOL, bool STORE = false>
+// PREC (the training forward's numerics): 0 fp16x3, kept activations fp32; the bf16 training
+// mode keeps hd / h / bot / hv as bf16 (TrainStoreArt's pointers then address bf16 arrays;
+// pos_enc(x') and the points stay fp32) and computes 1: fp16x3 throughout, or 2: mixed (the
+// kArtMix stream, mlp_layout.hpp) -- the deformation MLP fp16x3 (x' = delta + xyz feeds
+// sin(2^9 x')), the trunk, heads and view branch one bf16 MFMA per product.
+template <int MODE, int NCOL, bool STORE = false, int PREC = 0>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_art_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
     int64_t B, int S, int act, float* __restrict__ raw, TrainStoreArt ts = {}) {
   using G = GeomH<NCOL>;
   using Net = NetArtH;
+  constexpr bool BFM = PREC == 2;
   constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
   __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + kStash];
   float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
@@ -39,7 +45,11 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   const int g = lane >> 4, j = lane & 15;
   const int64_t N = B * S;
 
-  WeightPipe<Net, G::kThreads> p;
+  using WP = typename std::conditional<
+      BFM, DmaPipe<G::kThreads, kRing, kChunkH, kArtMixStream, kArtMixUsed, kRingLead>,
+      WeightPipe<Net, G::kThreads>>::type;
+  using T = typename std::conditional<PREC != 0, __bf16, float>::type;
+  WP p;
   p.wbuf = smem;
   p.src = wstream;
   p.tid = tid;
@@ -88,25 +98,28 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     split8(dv, din.hi[0][c], din.lo[0][c], din.ovf);
 #pragma unroll
     for (int e = 0; e < 8; ++e) vv[e] *= kActS;
-    split8(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
+    split8<BFM>(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
     stash[64 * (6 * c + 4)] = __builtin_bit_cast(f4, venc.hi[0][c]);
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
 
-  FragPipe<WeightPipe<Net, G::kThreads>> fp(p);
+  FragPipe<WP, AON_PREFETCH, 0, false, kArtMix.lo, BFM ? kArtMix.hi : 0> fp(p);
   fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 
   Frag<8, NCOL> x, y;
   Frag<1, NCOL> none;
-  using SP = StorePick<STORE, NCOL>;
+  using SP = StorePick<STORE, NCOL, T>;
+  T* const hd_s = reinterpret_cast<T*>(ts.hd);
+  T* const h_s = reinterpret_cast<T*>(ts.h);
+  T* const hv_s = reinterpret_cast<T*>(ts.hv);
   const int64_t hds = act_rows(N) * 128, hs = act_rows(N) * 256;  // one deformation / pts_linears output
   const int64_t ms = act_rows(N) * 4;  // one layer's ReLU' bits: hd0..3, h0..7, hv0..3 in ts.masks
   // deformation MLP (model_autodecoder.py:196-205)
-  layer_h<Net, A_D0, true>(fp, none, din, x, bias_l, g, SP::make(ts.hd, 128, rows, N, g, ts.masks));
-  layer_h<Net, A_D1, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + hds, 128, rows, N, g, ts.masks + 1 * ms));
-  layer_h<Net, A_D2, true>(fp, y, none, x, bias_l, g, SP::make(ts.hd + 2 * hds, 128, rows, N, g, ts.masks + 2 * ms));
-  layer_h<Net, A_D3, true>(fp, x, none, y, bias_l, g, SP::make(ts.hd + 3 * hds, 128, rows, N, g, ts.masks + 3 * ms));
+  layer_h<Net, A_D0, true>(fp, none, din, x, bias_l, g, SP::make(hd_s, 128, rows, N, g, ts.masks));
+  layer_h<Net, A_D1, true>(fp, x, none, y, bias_l, g, SP::make(hd_s + hds, 128, rows, N, g, ts.masks + 1 * ms));
+  layer_h<Net, A_D2, true>(fp, y, none, x, bias_l, g, SP::make(hd_s + 2 * hds, 128, rows, N, g, ts.masks + 2 * ms));
+  layer_h<Net, A_D3, true>(fp, x, none, y, bias_l, g, SP::make(hd_s + 3 * hds, 128, rows, N, g, ts.masks + 3 * ms));
   f4 dlt[NCOL];
   head_h<Net, A_DOUT>(fp, y, dlt, bias_l, g);
 
@@ -128,18 +141,18 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      split8(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
+      split8<BFM>(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
       stash[64 * (6 * c + 2 * k)] = __builtin_bit_cast(f4, enc.hi[k][c]);
       stash[64 * (6 * c + 2 * k + 1)] = __builtin_bit_cast(f4, enc.lo[k][c]);
     }
   }
 
   // trunk on cat[enc, shape] (:214-220), shape folded into the pts_linears.0 / .5 biases
-  layer_h<Net, A_P0, true>(fp, none, enc, x, bias_l, g, SP::make(ts.h, 256, rows, N, g, ts.masks + 4 * ms));
-  layer_h<Net, A_P1, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + hs, 256, rows, N, g, ts.masks + 5 * ms));
-  layer_h<Net, A_P2, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 2 * hs, 256, rows, N, g, ts.masks + 6 * ms));
-  layer_h<Net, A_P3, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 3 * hs, 256, rows, N, g, ts.masks + 7 * ms));
-  layer_h<Net, A_P4, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 4 * hs, 256, rows, N, g, ts.masks + 8 * ms));
+  layer_h<Net, A_P0, true>(fp, none, enc, x, bias_l, g, SP::make(h_s, 256, rows, N, g, ts.masks + 4 * ms));
+  layer_h<Net, A_P1, true>(fp, x, none, y, bias_l, g, SP::make(h_s + hs, 256, rows, N, g, ts.masks + 5 * ms));
+  layer_h<Net, A_P2, true>(fp, y, none, x, bias_l, g, SP::make(h_s + 2 * hs, 256, rows, N, g, ts.masks + 6 * ms));
+  layer_h<Net, A_P3, true>(fp, x, none, y, bias_l, g, SP::make(h_s + 3 * hs, 256, rows, N, g, ts.masks + 7 * ms));
+  layer_h<Net, A_P4, true>(fp, y, none, x, bias_l, g, SP::make(h_s + 4 * hs, 256, rows, N, g, ts.masks + 8 * ms));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c)
 #pragma unroll
@@ -148,23 +161,23 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
     }
   // skip: cat[h, enc, shape]
-  layer_h<Net, A_P5, true>(fp, x, enc, y, bias_l, g, SP::make(ts.h + 5 * hs, 256, rows, N, g, ts.masks + 9 * ms));
-  layer_h<Net, A_P6, true>(fp, y, none, x, bias_l, g, SP::make(ts.h + 6 * hs, 256, rows, N, g, ts.masks + 10 * ms));
-  layer_h<Net, A_P7, true>(fp, x, none, y, bias_l, g, SP::make(ts.h + 7 * hs, 256, rows, N, g, ts.masks + 11 * ms));
+  layer_h<Net, A_P5, true>(fp, x, enc, y, bias_l, g, SP::make(h_s + 5 * hs, 256, rows, N, g, ts.masks + 9 * ms));
+  layer_h<Net, A_P6, true>(fp, y, none, x, bias_l, g, SP::make(h_s + 6 * hs, 256, rows, N, g, ts.masks + 10 * ms));
+  layer_h<Net, A_P7, true>(fp, x, none, y, bias_l, g, SP::make(h_s + 7 * hs, 256, rows, N, g, ts.masks + 11 * ms));
   f4 dens[NCOL], rgb[NCOL];
   head_h<Net, A_DEN>(fp, y, dens, bias_l, g);  // :221-223
   // bottleneck, no activation (:225)
-  layer_h<Net, A_BOT, false>(fp, y, none, x, bias_l, g, SP::make(ts.bot, 256, rows, N, g));
+  layer_h<Net, A_BOT, false>(fp, y, none, x, bias_l, g, SP::make(reinterpret_cast<T*>(ts.bot), 256, rows, N, g));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
     venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
     venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
   }
   // view branch on cat[bottleneck, enc_dir, appearance] (:226-235)
-  layer_h<Net, A_V0, true>(fp, x, venc, y, bias_l, g, SP::make(ts.hv, 128, rows, N, g, ts.masks + 12 * ms));
-  layer_h<Net, A_V1, true>(fp, y, none, x, bias_l, g, SP::make(ts.hv + hds, 128, rows, N, g, ts.masks + 13 * ms));
-  layer_h<Net, A_V2, true>(fp, x, none, y, bias_l, g, SP::make(ts.hv + 2 * hds, 128, rows, N, g, ts.masks + 14 * ms));
-  layer_h<Net, A_V3, true>(fp, y, none, x, bias_l, g, SP::make(ts.hv + 3 * hds, 128, rows, N, g, ts.masks + 15 * ms));
+  layer_h<Net, A_V0, true>(fp, x, venc, y, bias_l, g, SP::make(hv_s, 128, rows, N, g, ts.masks + 12 * ms));
+  layer_h<Net, A_V1, true>(fp, y, none, x, bias_l, g, SP::make(hv_s + hds, 128, rows, N, g, ts.masks + 13 * ms));
+  layer_h<Net, A_V2, true>(fp, x, none, y, bias_l, g, SP::make(hv_s + 2 * hds, 128, rows, N, g, ts.masks + 14 * ms));
+  layer_h<Net, A_V3, true>(fp, y, none, x, bias_l, g, SP::make(hv_s + 3 * hds, 128, rows, N, g, ts.masks + 15 * ms));
   head_h<Net, A_RGB>(fp, x, rgb, bias_l, g);  // :237
 
   if (g == 0) {
@@ -190,7 +203,7 @@ using namespace aon::mlp;
 
 extern "C" size_t aon_mlp_art_packed_bytes(void) { return NetArtH::kPackedBytes; }
 
-extern "C" int aon_mlp_art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream) {
+static int art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream, bool mixed) {
   AON_REQUIRE(prm && packed, "null pointer");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
   PackArgsH a{};
@@ -223,7 +236,22 @@ extern "C" int aon_mlp_art_pack(const aon_mlp_art_params* prm, void* packed, aon
   a.n_layers = kNumLayersArt;
   a.stream_blocks = NetArtH::kStreamBlocks;
   a.bias_floats = NetArtH::kBiasFloats;
+  if (mixed) {
+    a.bf16 = kArtMix.mode;
+    a.mx_lo = kArtMix.lo;
+    a.mx_hi = kArtMix.hi;
+  }
   return pack_h(a, packed, (hipStream_t)stream);
+}
+
+extern "C" int aon_mlp_art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream) {
+  return art_pack(prm, packed, stream, false);
+}
+
+// the bf16 training mode's mixed stream (kArtMix): same buffer size and bias table
+extern "C" int aon_mlp_art_pack_bf16(const aon_mlp_art_params* prm, void* packed,
+                                     aon_stream_t stream) {
+  return art_pack(prm, packed, stream, true);
 }
 
 static int art_launch(int mode, const void* packed, const float* a0, const float* a1,
@@ -257,11 +285,11 @@ extern "C" int aon_mlp_art_fwd(const void* packed, const float* rays_o, const fl
   return art_launch(0, packed, rays_o, rays_d, viewdirs, t, B, S, act, out, stream);
 }
 
-extern "C" int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
-                                     const float* viewdirs, const float* t, int64_t B, int S,
-                                     const float* noise, float* hd, float* h, float* bot,
-                                     float* hv, float* enc, float* xyz, float* raw,
-                                     uint32_t* masks, aon_stream_t stream) {
+static int art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
+                         const float* viewdirs, const float* t, int64_t B, int S,
+                         const float* noise, float* hd, float* h, float* bot, float* hv,
+                         float* enc, float* xyz, float* raw, uint32_t* masks, aon_stream_t stream,
+                         int prec) {
   AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && raw, "null pointer");
   AON_REQUIRE(hd && h && bot && hv && enc && xyz && masks, "null activation buffer");
   AON_REQUIRE(aligned16(masks), "masks must be 16-byte aligned");
@@ -279,10 +307,39 @@ extern "C" int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, co
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
   const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise, reinterpret_cast<uint2*>(masks)};
-  hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true>), (unsigned)grid, G::kThreads, 0,
-                     (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
-                     (int)AON_ACT_NONE, raw, ts);
-  return launch_status(__func__);
+  if (prec == 2)
+    hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 2>), (unsigned)grid, G::kThreads, 0,
+                       (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
+                       (int)AON_ACT_NONE, raw, ts);
+  else if (prec == 1)
+    hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 1>), (unsigned)grid, G::kThreads, 0,
+                       (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
+                       (int)AON_ACT_NONE, raw, ts);
+  else
+    hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true>), (unsigned)grid, G::kThreads, 0,
+                       (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
+                       (int)AON_ACT_NONE, raw, ts);
+  return launch_status(prec ? "aon_mlp_art_fwd_train_bf16" : "aon_mlp_art_fwd_train");
+}
+
+extern "C" int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
+                                     const float* viewdirs, const float* t, int64_t B, int S,
+                                     const float* noise, float* hd, float* h, float* bot,
+                                     float* hv, float* enc, float* xyz, float* raw,
+                                     uint32_t* masks, aon_stream_t stream) {
+  return art_fwd_train(packed, rays_o, rays_d, viewdirs, t, B, S, noise, hd, h, bot, hv, enc, xyz,
+                       raw, masks, stream, 0);
+}
+
+extern "C" int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_o,
+                                          const float* rays_d, const float* viewdirs,
+                                          const float* t, int64_t B, int S, const float* noise,
+                                          void* hd, void* h, void* bot, void* hv, float* enc,
+                                          float* xyz, float* raw, uint32_t* masks, int mixed,
+                                          aon_stream_t stream) {
+  return art_fwd_train(packed, rays_o, rays_d, viewdirs, t, B, S, noise, static_cast<float*>(hd),
+                       static_cast<float*>(h), static_cast<float*>(bot), static_cast<float*>(hv),
+                       enc, xyz, raw, masks, stream, mixed ? 2 : 1);
 }
 
 extern "C" int aon_mlp_art_fwd_points(const void* packed, const float* pos,

@@ -84,11 +84,19 @@ struct EncBwd {
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
 };
 
+// BF: the bf16 training mode -- the whole chain one bf16 MFMA per product on the compact stream
+// (the deformation branch too: only its forward needs fp16x3, for x'), every dZ stored as bf16
+// (ArtBwdArgs' dzv / dbot / dz / dzd then address bf16 arrays); dL/dx' stays fp32.
+template <bool BF = false>
 __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, ArtBwdArgs a) {
   constexpr int NCOL = 1;
   using G = GeomH<NCOL>;
   using Net = NetArtBwdH;
+  using T = typename std::conditional<BF, __bf16, float>::type;
+  T* const dzv = reinterpret_cast<T*>(a.dzv);
+  T* const dz = reinterpret_cast<T*>(a.dz);
+  T* const dzd = reinterpret_cast<T*>(a.dzd);
   // per lane: d raw_sigma fragment (hi, lo) + 4 f4 of parked skip-enc gradients
   constexpr int kSlots = 6;
   __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + G::kWaves * 64 * kSlots];
@@ -100,7 +108,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   const int g = lane >> 4, j = lane & 15;
   const int64_t N = a.N;
 
-  WeightPipe<Net, G::kThreads> p;
+  WeightPipeP<Net, G::kThreads, BF> p;
   p.wbuf = smem;
   p.src = wstream;
   p.tid = tid;
@@ -124,13 +132,13 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
       dv[e] = (g == 0 && e < 3) ? d[e < 3 ? e : 0] * s : 0.f;
       sv[e] = (g == 0 && e == 0) ? d[3] * s : 0.f;
     }
-    split8(dv, drgb.hi[0][0], drgb.lo[0][0], drgb.ovf);
-    split8(sv, dsig.hi[0][0], dsig.lo[0][0], dsig.ovf);
+    split8<BF>(dv, drgb.hi[0][0], drgb.lo[0][0], drgb.ovf);
+    split8<BF>(sv, dsig.hi[0][0], dsig.lo[0][0], dsig.ovf);
     stash[0] = __builtin_bit_cast(f4, dsig.hi[0][0]);
     stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
   }
 
-  FragPipe<WeightPipe<Net, G::kThreads>> fp(p);
+  FragPipe<WeightPipeP<Net, G::kThreads, BF>, AON_PREFETCH, 0, BF> fp(p);
   fp.start();
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 
@@ -140,17 +148,17 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   Frag<1, NCOL> none;
   // view branch: d hv3 = W_rgb^T d rgb, then views_linear.3 .. 1, each * ReLU'
   layer_h<Net, AB_RGB, false>(fp, none, drgb, x, bias_l, g,
-                              mask_bits(a.masks + 15 * ms, a.dzv + 3 * ws, 128, rows, N, g, inv));
+                              mask_bits(a.masks + 15 * ms, dzv + 3 * ws, 128, rows, N, g, inv));
   layer_h<Net, AB_V3, false>(fp, x, none, y, bias_l, g,
-                             mask_bits(a.masks + 14 * ms, a.dzv + 2 * ws, 128, rows, N, g, inv));
+                             mask_bits(a.masks + 14 * ms, dzv + 2 * ws, 128, rows, N, g, inv));
   layer_h<Net, AB_V2, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 13 * ms, a.dzv + 1 * ws, 128, rows, N, g, inv));
+                             mask_bits(a.masks + 13 * ms, dzv + 1 * ws, 128, rows, N, g, inv));
   layer_h<Net, AB_V1, false>(fp, x, none, y, bias_l, g,
-                             mask_bits(a.masks + 12 * ms, a.dzv, 128, rows, N, g, inv));
+                             mask_bits(a.masks + 12 * ms, dzv, 128, rows, N, g, inv));
   // d bottleneck = W_view0[:, :256]^T dZ_view0 (linear layer: no mask)
   {
-    RowStore<NCOL> st;
-    st.rowp[0] = row < N ? a.dbot + act_base(row, 256, g) : nullptr;
+    RowStore<NCOL, T> st;
+    st.rowp[0] = row < N ? reinterpret_cast<T*>(a.dbot) + act_base(row, 256, g) : nullptr;
     st.s = inv;
     layer_h<Net, AB_V0, false>(fp, y, none, x, bias_l, g, st);
   }
@@ -158,25 +166,25 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
   // d h7 = W_bot^T d bottleneck + W_den^T d sigma, * ReLU'(h7) -> dZ_7
   layer_h<Net, AB_BOTDEN, false>(fp, x, dsig, y, bias_l, g,
-                                 mask_bits(a.masks + 11 * ms, a.dz + 7 * hs, 256, rows, N, g, inv));
+                                 mask_bits(a.masks + 11 * ms, dz + 7 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P7, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 10 * ms, a.dz + 6 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 10 * ms, dz + 6 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P6, false>(fp, x, none, y, bias_l, g,
-                             mask_bits(a.masks + 9 * ms, a.dz + 5 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 9 * ms, dz + 5 * hs, 256, rows, N, g, inv));
   // skip layer: its h4 columns continue the chain, its enc columns are parked for the encoding's
   // gradient (y = dZ_5 feeds both)
   layer_h<Net, AB_P5, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 8 * ms, a.dz + 4 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 8 * ms, dz + 4 * hs, 256, rows, N, g, inv));
   float* slot = reinterpret_cast<float*>(stash + 2 * 64);
   layer_h<Net, AB_P5E, false>(fp, y, none, junk, bias_l, g, EncStash{slot});
   layer_h<Net, AB_P4, false>(fp, x, none, y, bias_l, g,
-                             mask_bits(a.masks + 7 * ms, a.dz + 3 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 7 * ms, dz + 3 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P3, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 6 * ms, a.dz + 2 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 6 * ms, dz + 2 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P2, false>(fp, x, none, y, bias_l, g,
-                             mask_bits(a.masks + 5 * ms, a.dz + 1 * hs, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 5 * ms, dz + 1 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P1, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 4 * ms, a.dz, 256, rows, N, g, inv));
+                             mask_bits(a.masks + 4 * ms, dz, 256, rows, N, g, inv));
   // d enc = W_0[:, :63]^T dZ_0 + the parked skip part, and pos_enc's backward (:205-212)
   EncBwd eb;
   eb.slot = slot;
@@ -204,20 +212,20 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
     float dv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? dx[e < 3 ? e : 0] * sd : 0.f;
-    split8(dv, ddx.hi[0][0], ddx.lo[0][0], ddx.ovf);
+    split8<BF>(dv, ddx.hi[0][0], ddx.lo[0][0], ddx.ovf);
   }
   // deformation head and MLP: d hd3 = W_dl^T dL/dx', then deformations_linear.3 .. 1
   layer_h<Net, AB_DL, false>(fp, none, ddx, y, bias_l, g,
-                             mask_bits(a.masks + 3 * ms, a.dzd + 3 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 3 * ms, dzd + 3 * ws, 128, rows, N, g, invd));
   layer_h<Net, AB_D3, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 2 * ms, a.dzd + 2 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 2 * ms, dzd + 2 * ws, 128, rows, N, g, invd));
   layer_h<Net, AB_D2, false>(fp, x, none, y, bias_l, g,
-                             mask_bits(a.masks + 1 * ms, a.dzd + 1 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 1 * ms, dzd + 1 * ws, 128, rows, N, g, invd));
   // (the last layer's outputs are only stored, the enc-column layers' fragments are consumed in
   // their epilogues: neither fp16 split is used, so neither is range-checked)
   const uint64_t used_ovf = x.ovf | y.ovf | drgb.ovf | dsig.ovf | ddx.ovf;
   layer_h<Net, AB_D1, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 0 * ms, a.dzd, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 0 * ms, dzd, 128, rows, N, g, invd));
   range_report(bias_g + Net::kBiasFloats, used_ovf);
 }
 
@@ -229,8 +237,8 @@ using namespace aon::mlp;
 
 extern "C" size_t aon_mlp_art_bwd_packed_bytes(void) { return NetArtBwdH::kPackedBytes; }
 
-extern "C" int aon_mlp_art_bwd_pack(const aon_mlp_art_params* prm, void* packed,
-                                    aon_stream_t stream) {
+static int art_bwd_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream,
+                        bool bf16) {
   AON_REQUIRE(prm && packed, "null pointer");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
   AON_REQUIRE(prm->ld_pts0 >= 63 && prm->ld_pts5 >= 319 && prm->ld_view0 >= 283,
@@ -259,12 +267,23 @@ extern "C" int aon_mlp_art_bwd_pack(const aon_mlp_art_params* prm, void* packed,
   a.n_layers = kNumLayersArtBwd;
   a.stream_blocks = NetArtBwdH::kStreamBlocks;
   a.bias_floats = NetArtBwdH::kBiasFloats;
+  a.bf16 = bf16 ? 1 : 0;
   return pack_h(a, packed, (hipStream_t)stream);
 }
 
-extern "C" int aon_mlp_art_bwd(const void* packed, const float* draw, const uint32_t* masks,
-                               const float* enc, int64_t N, float* dzv, float* dbot, float* dz,
-                               float* dxp, float* dzd, void* work, aon_stream_t stream) {
+extern "C" int aon_mlp_art_bwd_pack(const aon_mlp_art_params* prm, void* packed,
+                                    aon_stream_t stream) {
+  return art_bwd_pack(prm, packed, stream, false);
+}
+
+extern "C" int aon_mlp_art_bwd_pack_bf16(const aon_mlp_art_params* prm, void* packed,
+                                         aon_stream_t stream) {
+  return art_bwd_pack(prm, packed, stream, true);
+}
+
+static int art_bwd(const void* packed, const float* draw, const uint32_t* masks, const float* enc,
+                   int64_t N, float* dzv, float* dbot, float* dz, float* dxp, float* dzd,
+                   void* work, aon_stream_t stream, bool bf16) {
   AON_REQUIRE(packed && draw && masks && enc && dzv && dbot && dz && dxp && dzd && work,
               "null pointer");
   AON_REQUIRE(N >= 0, "bad shape");
@@ -284,6 +303,22 @@ extern "C" int aon_mlp_art_bwd(const void* packed, const float* draw, const uint
   const f4* wsp = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtBwdH::kStreamBytes);
-  hipLaunchKernelGGL(k_mlp_art_bwd_f16x3, (unsigned)grid, G::kThreads, 0, st, wsp, bias, args);
-  return launch_status(__func__);
+  if (bf16)
+    hipLaunchKernelGGL(k_mlp_art_bwd_f16x3<true>, (unsigned)grid, G::kThreads, 0, st, wsp, bias, args);
+  else
+    hipLaunchKernelGGL(k_mlp_art_bwd_f16x3<false>, (unsigned)grid, G::kThreads, 0, st, wsp, bias, args);
+  return launch_status(bf16 ? "aon_mlp_art_bwd_bf16" : "aon_mlp_art_bwd");
+}
+
+extern "C" int aon_mlp_art_bwd(const void* packed, const float* draw, const uint32_t* masks,
+                               const float* enc, int64_t N, float* dzv, float* dbot, float* dz,
+                               float* dxp, float* dzd, void* work, aon_stream_t stream) {
+  return art_bwd(packed, draw, masks, enc, N, dzv, dbot, dz, dxp, dzd, work, stream, false);
+}
+
+extern "C" int aon_mlp_art_bwd_bf16(const void* packed, const float* draw, const uint32_t* masks,
+                                    const float* enc, int64_t N, void* dzv, void* dbot, void* dz,
+                                    float* dxp, void* dzd, void* work, aon_stream_t stream) {
+  return art_bwd(packed, draw, masks, enc, N, static_cast<float*>(dzv), static_cast<float*>(dbot),
+                 static_cast<float*>(dz), dxp, static_cast<float*>(dzd), work, stream, true);
 }

@@ -219,16 +219,15 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
   const int64_t total = nhalf + a.bias_floats;
   const LayerDesc& last = a.layers[a.n_layers - 1];
   const int used_blocks = last.blk0 + (last.ka + last.kb) * last.u * 2;
+  const StreamMap map{a.bf16, a.mx_lo, a.mx_hi};
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e < nhalf) {
-      // bf16: compact stream -- element e of block c is element e of the fp16x3 hi block 2c;
-      // the second half of the stream region is unused (zero)
-      if (a.bf16 && e >= nhalf / 2) {
-        out[e] = static_cast<_Float16>(0.0f);
-        continue;
-      }
-      const int blk = static_cast<int>(a.bf16 ? 2 * (e >> 9) : (e >> 9));
+      // element e of stream block m is element e of fp16x3 block map.unmap(m) (StreamMap):
+      // past the used blocks (the compact modes' tail of the stream region) it maps past the
+      // weights and is zero
+      const int blk = map.unmap(static_cast<int>(e >> 9));
+      const bool bf = !map.f16(blk);  // a bf16 (hi-only) block
       const int l = static_cast<int>((e >> 3) & 63), jj = static_cast<int>(e & 7);
       float w = 0.f;
       bool lo_part = false;
@@ -267,7 +266,7 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
       }
 #if AON_F16X3_V2
       w *= kWS;  // exact (power of two)
-      if (a.bf16) {  // bf16 mode: bf16(w) in the compact (hi-only) stream
+      if (bf) {  // bf16 layer: bf16(w) in the compact (hi-only) stream
         out[e] = bf_bits(w);
         continue;
       }

@@ -118,17 +118,20 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, uint
 // w and w + 4 of an 8-wave workgroup share a SIMD; run in lockstep they reach the epilogue VALU
 // and the epilogue-free MFMA steps together, so neither wave's VALU rides beside the other's
 // MFMAs.  Waves 4-7 take EOFF = 4 (a stagger: MI355X_MICROARCH.md "Two waves per SIMD" item 9).
-// BF: bf16 numerics -- the stream's lo blocks are never read (and carry zeros).
-template <typename P, int D = AON_PREFETCH, int EOFF = 0, bool BF = false>
+// BF: bf16 numerics -- the compact stream (WeightPipeP) of hi blocks only.  MXL < MXH: the
+// mixed stream (StreamMap mode 2): layers in the fp16x3 blocks [MXL, MXH) run fp16x3, the
+// others bf16 (layer_h / head_h ask f16_block(d.blk0)).
+template <typename P, int D = AON_PREFETCH, int EOFF = 0, bool BF = false, int MXL = 0, int MXH = 0>
 struct FragPipe {
   static constexpr int kEpiOff = EOFF;
-  static constexpr bool kBF16 = BF;
+  static constexpr int kMode = MXH > MXL ? 2 : (BF ? 1 : 0);
+  __host__ __device__ static constexpr bool f16_block(int b) { return StreamMap{kMode, MXL, MXH}.f16(b); }
+  __host__ __device__ static constexpr int map_block(int b) { return StreamMap{kMode, MXL, MXH}.map(b); }
   P& p;
   f4 nh[D], nl[D];  // fragments of the next D steps
   __device__ __forceinline__ explicit FragPipe(P& pp) : p(pp) {}
   __device__ __forceinline__ void fetch_into(int blk_in, f4& h, f4& l) {
-    // BF: the compact stream (WeightPipeP): fp16x3 block 2c (a hi block) is block c
-    const int blk = BF ? blk_in >> 1 : blk_in;
+    const int blk = map_block(blk_in);
     if (blk >= P::kUsedBlocks) return;
 #ifdef AON_ABLATE_LDS  // timing-only build: reuse the first fragments (no LDS reads, wrong results)
     if (blk >= 2 * D) {
@@ -138,7 +141,7 @@ struct FragPipe {
 #endif
     if (blk % P::kChunk == 0) p.begin(blk / P::kChunk);
     h = p.block(blk);
-    if (!BF) l = p.block(blk + 1);
+    if (f16_block(blk_in)) l = p.block(blk + 1);
   }
   __device__ __forceinline__ void start() {
 #pragma unroll
@@ -426,7 +429,7 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
   constexpr int K = d.ka + d.kb;
   constexpr int NP = d.u / 2;
   constexpr int EO = P::kEpiOff;  // epilogue parts of pair p-1 at k-steps EO..EO+3 of pair p
-  constexpr bool BF = P::kBF16;   // bf16 numerics: one MFMA per k-step and tile
+  constexpr bool BF = !P::f16_block(d.blk0);  // bf16 numerics: one MFMA per k-step and tile
   constexpr int QIN = K - EO < 0 ? 0 : (K - EO > 4 ? 4 : K - EO);  // parts done inside the loop
   static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
   f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
@@ -502,7 +505,7 @@ template <typename Net, int LAYER, typename P, int NCOL, int NA>
 __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[NCOL],
                                        lds_float* bias_l, int g) {
   constexpr LayerDesc d = Net::layer(LAYER);
-  constexpr bool BF = P::kBF16;
+  constexpr bool BF = !P::f16_block(d.blk0);
   static_assert(d.u == 1 && d.kb == 0 && d.ka <= NA, "head shape");
   f4 hh[NCOL], xx[NCOL];
   const f4 bias = *reinterpret_cast<lds_f4*>(bias_l + d.bias0);

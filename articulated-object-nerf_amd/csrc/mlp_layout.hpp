@@ -254,8 +254,53 @@ struct PackArgsH {
   int tr[kMaxLayersH];
   LayerDesc layers[kMaxLayersH];
   int n_layers, stream_blocks, bias_floats;
-  int bf16;  // 1: bf16 weights in the hi blocks, zero lo blocks (the bf16 training mode)
+  // 0: fp16x3; 1: bf16 (compact, StreamMap mode 1); 2: mixed -- fp16x3 pairs for the blocks
+  // [mx_lo, mx_hi) of the fp16x3 numbering, compact bf16 for the rest (the articulated bf16
+  // training mode keeps the deformation MLP in fp16x3, StreamMap mode 2)
+  int bf16;
+  int mx_lo, mx_hi;
 };
+
+// Where the weight stream holds fp16x3 block b (even b: the hi block of a (hi, lo) pair, b + 1
+// its lo block) -- shared by k_pack_h and FragPipe.  mode 0: fp16x3, in place; 1: bf16 compact,
+// only hi blocks, block 2c at c; 2: mixed, [lo, hi) kept as fp16x3 pairs (lo even), every other
+// hi block compact bf16, all in consumption order (the ring's chunk starts are still met: a
+// chunk boundary is even, so it falls on a pair's hi block or a bf16 block).
+struct StreamMap {
+  int mode, lo, hi;
+  __host__ __device__ constexpr bool f16(int b) const {
+    return mode == 0 || (mode == 2 && b >= lo && b < hi);
+  }
+  __host__ __device__ constexpr int map(int b) const {
+    return mode == 0 ? b
+         : mode == 1 ? b >> 1
+         : b < lo    ? b >> 1
+         : b < hi    ? (lo >> 1) + b - lo
+                     : (lo >> 1) + (hi - lo) + ((b - hi) >> 1);
+  }
+  // stream block m -> its fp16x3 block
+  __host__ __device__ constexpr int unmap(int m) const {
+    return mode == 0 ? m
+         : mode == 1 ? 2 * m
+         : m < (lo >> 1)            ? 2 * m
+         : m < (lo >> 1) + hi - lo  ? lo + m - (lo >> 1)
+                                    : hi + 2 * (m - (lo >> 1) - (hi - lo));
+  }
+  // stream blocks carrying the `blocks` weight blocks of the fp16x3 numbering
+  __host__ __device__ constexpr int used(int blocks) const {
+    return mode == 0 ? blocks : mode == 1 ? blocks / 2 : (lo >> 1) + (hi - lo) + ((blocks - hi) >> 1);
+  }
+};
+// the articulated forward's mixed stream: the deformation MLP (kLayersArt blocks 0..215)
+// fp16x3 -- x' feeds pos_enc's sin(2^9 x'), where bf16's 2^-9 would cost whole radians -- the
+// trunk, heads and view branch compact bf16: 216 + 1268 = 1484 blocks, 1536 with the padding
+constexpr StreamMap kArtMix{2, 0, 216};
+constexpr int kArtMixUsed = kArtMix.used(2752);
+constexpr int kArtMixStream = (kArtMixUsed + 63) / 64 * 64;
+static_assert(kArtMixUsed == 1484 && kArtMixStream == 1536, "mixed articulated stream");
+static_assert(kArtMix.unmap(kArtMix.map(2750)) == 2750 && kArtMix.unmap(kArtMix.map(214)) == 214 &&
+                  kArtMix.map(216) == 216 && kArtMix.map(218) == 217,
+              "stream map round trip");
 
 // Training forward of the fused kernel (launch_f16x3 mode 2): every hidden activation goes to
 // HBM for the backward, as the layer-by-layer path keeps them: h (8, N, 256) post-ReLU

@@ -12,6 +12,7 @@ synchronize on both sides, max over ranks):
                     gradient all-reduce over RCCL on N > 1: weak scaling), f16x3 kernels
   "train_step_bf16" the same step in C5's bf16 mode (train.PRECISION = "bf16")
   "train_step_art"  C5 on the articulated auto-decoder (LitNeRF_AutoDecoder.training_step)
+  "train_step_art_bf16"  the same in the articulated bf16 mode (train_art.PRECISION = "bf16")
 each with its own ms_per_step and roofline (MFMA fraction of the fine-level MLP kernels,
 HBM byte fractions of the training kernels counting the stored activations).
 
@@ -131,6 +132,8 @@ def main():
         extra["train_step"] = bench_train(args, world, rank, local_rank)
         extra["train_step_bf16"] = bench_train(args, world, rank, local_rank, precision="bf16")
         extra["train_step_art"] = bench_train(args, world, rank, local_rank, art=True)
+        extra["train_step_art_bf16"] = bench_train(args, world, rank, local_rank, art=True,
+                                                   precision="bf16")
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -325,6 +328,10 @@ TRAIN_BYTES_BF16 = {"fwd_train": 4 + 16 + 2 * 2432 + 288, "bwd_chain": 16 + 288 
 ART_TRAIN_BYTES = {"art_fwd_train": 4 + 16 + 4 * (3328 + 63 + 3) + 512,
                    "art_bwd_chain": 16 + 512 + 4 * 63 + 4 * (3328 + 3),
                    "art_dweight": 4 * (3335 + 3484)}
+# bf16 mode: the kept activations and chain gradients 2 B (enc, points, d raw, dL/dx' fp32)
+ART_TRAIN_BYTES_BF16 = {"art_fwd_train": 4 + 16 + 2 * 3328 + 4 * (63 + 3) + 512,
+                        "art_bwd_chain": 16 + 512 + 4 * 63 + 2 * 3328 + 4 * 3,
+                        "art_dweight": 2 * (3328 + 3328) + 4 * (3 + 4 + 2 * 63 + 3 + 27)}
 ART_TRAIN_FLOP = {"art_fwd_train": 2 * 714_880, "art_bwd_chain": 2 * (714_880 - 3 * 128 - 128 * 27),
                   "art_dweight": 2 * 714_880}
 # dense MFMA peak in algorithmic FLOP/s per training precision: f16x3 issues 3 fp16 products
@@ -391,11 +398,15 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
 
     old_prec = train.PRECISION
     train.PRECISION = precision
+    if art:
+        old_art, train_art.PRECISION = train_art.PRECISION, precision
     try:
         el = timed(step, args.steps, args.warmup, world)
     finally:
         train.TIMERS = None
         train.PRECISION = old_prec
+        if art:
+            train_art.PRECISION = old_art
     mac = ART_MAC_ISSUED if art else MAC_PER_SAMPLE
     samples = nrays * (NC + 1 + NC + 1 + NF)
     ms = el / args.steps * 1e3
@@ -407,7 +418,10 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
                       "Adam (config C5)"),
            "value": nrays * world * args.steps / el, "unit": "rays/s", "n_gpus": world,
            "steps": args.steps, "ms_per_step": ms, "scaling": "weak",
-           "dtype": ("bf16 (bf16 MFMA, fp32 accumulate; bf16 activations and gradients, fp32 "
+           "dtype": ("bf16 (bf16 MFMA, fp32 accumulate; the deformation MLP's forward f16x3 for x'; "
+                     "bf16 activations and gradients, fp32 compositing / loss / Adam master "
+                     "weights)" if precision == "bf16" and art else
+                     "bf16 (bf16 MFMA, fp32 accumulate; bf16 activations and gradients, fp32 "
                      "compositing / loss / Adam master weights)" if precision == "bf16" else
                      "f16x3 (fp16 hi/lo split MFMA, fp32 accumulate; fp32 activations)"),
            "config": {"workload": "C5 training step" + (" (articulated)" if art else ""),
@@ -419,7 +433,8 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
     kern = {}
     hbm_bytes = 0.0
     names = ("art_fwd_train", "art_bwd_chain", "art_dweight") if art else ("fwd_train", "bwd_chain", "dweight")
-    nbytes = ART_TRAIN_BYTES if art else TRAIN_BYTES_BF16 if precision == "bf16" else TRAIN_BYTES
+    nbytes = ((ART_TRAIN_BYTES_BF16 if precision == "bf16" else ART_TRAIN_BYTES) if art else
+              TRAIN_BYTES_BF16 if precision == "bf16" else TRAIN_BYTES)
     nflop = ART_TRAIN_FLOP if art else TRAIN_FLOP
     for name in names:
         t_ms, rows = ev_ms(timers, f"{name}{NC + 1 + NF}")

@@ -282,6 +282,18 @@ int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* 
                           const float* noise, float* hd, float* h, float* bot, float* hv,
                           float* enc, float* xyz, float* raw, uint32_t* masks,
                           aon_stream_t stream);
+/* The articulated bf16 training mode (train_art.PRECISION = "bf16"; BASELINE config C5's
+ * "bf16" on the articulated model): hd, h, bot, hv are bf16 arrays of the shapes above, enc /
+ * xyz / raw / masks as above.  mixed != 0: packed by aon_mlp_art_pack_bf16 (a mixed stream in
+ * the same buffer size: the deformation MLP stays fp16x3 -- x' feeds sin(2^9 x') -- the trunk,
+ * heads and view branch are bf16), one bf16 MFMA per product past the deformation head;
+ * mixed == 0: packed by aon_mlp_art_pack, fp16x3 numerics throughout (only the stores bf16). */
+int aon_mlp_art_pack_bf16(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
+int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_o, const float* rays_d,
+                               const float* viewdirs, const float* t, int64_t B, int S,
+                               const float* noise, void* hd, void* h, void* bot, void* hv,
+                               float* enc, float* xyz, float* raw, uint32_t* masks, int mixed,
+                               aon_stream_t stream);
 
 /* Backward chain of one articulated level (autograd of model_autodecoder.py:168-239): from
  * dL/d raw (N, 4), the ReLU' bits (16, N, 4) of hd0..3, h0..7, hv0..3 and pos_enc(x') (enc) kept
@@ -297,6 +309,12 @@ int aon_mlp_art_bwd_pack(const aon_mlp_art_params* params, void* packed, aon_str
 int aon_mlp_art_bwd(const void* packed, const float* draw, const uint32_t* masks,
                     const float* enc, int64_t N, float* dzv, float* dbot, float* dz, float* dxp,
                     float* dzd, void* work, aon_stream_t stream);
+/* bf16 mode: the whole chain one bf16 MFMA per product on aon_mlp_art_bwd_pack_bf16's compact
+ * stream (same buffer size); dzv, dbot, dz, dzd are bf16 arrays of the shapes above, dxp fp32. */
+int aon_mlp_art_bwd_pack_bf16(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
+int aon_mlp_art_bwd_bf16(const void* packed, const float* draw, const uint32_t* masks,
+                         const float* enc, int64_t N, void* dzv, void* dbot, void* dz, float* dxp,
+                         void* dzd, void* work, aon_stream_t stream);
 
 /* The same on given sample points pos (B*S, 3) and encoded view directions condition (B, 27)
  * (NeRFMLP.forward(pos, condition, latents)). */
