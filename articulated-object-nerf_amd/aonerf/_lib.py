@@ -40,7 +40,8 @@ class AonGemmArgs(ctypes.Structure):
                 ("C", vp), ("ldc", c_i64), ("bias", vp), ("mask", vp), ("ldm", c_i64),
                 ("relu", c_int), ("accumulate", c_int), ("a_scale", c_float), ("b_scale", c_float),
                 ("k_splits", c_i64), ("rowsum", vp), ("a_amax", vp), ("mma_bf16", c_int),
-                ("a_bf16", c_int), ("b_bf16", c_int), ("a_tiled", c_int), ("b_tiled", c_int)]
+                ("a_bf16", c_int), ("b_bf16", c_int), ("a_tiled", c_int), ("b_tiled", c_int),
+                ("n_store", c_i64)]
 
 
 class AonAdamTensor(ctypes.Structure):
@@ -71,7 +72,7 @@ _SIGNATURES = {
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp]),
     "aon_mlp_fwd_train_bf16": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp,
-                                       vp]),
+                                       vp, vp]),
     "aon_mlp_bwd_pack_bf16": (c_int, [ctypes.POINTER(AonMlpParams), vp, vp]),
     "aon_mlp_bwd_bf16": (c_int, [vp, vp, vp, c_i64, vp, vp, vp, vp, vp]),
     "aon_relu_masks": (c_int, [vp, c_i64, c_int, vp, vp]),
@@ -125,7 +126,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.aon_abi_version() != 6:
+        if handle.aon_abi_version() != 7:
             raise ImportError("aonerf: ABI version mismatch")
         _lib = handle
     return _lib

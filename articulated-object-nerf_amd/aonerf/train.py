@@ -241,7 +241,7 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
     ReLU' bits of h0..h7, hv from the fused forward (built from the activations when None).
     h_tiled: h / bot / hv in the fused forward's tiled layout (tiles.py), else row-major (the
     layer-by-layer forward).  The chain's dz / dzb / dzv are always tiled."""
-    R, dev = enc.shape[0], enc.device
+    R, dev = draw.shape[0], draw.device
     bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
         acts = list(h) + [hv]
@@ -260,15 +260,22 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
     e0 = _ev()
     acts = ACT_SCALE
 
+    enc_t = enc.dtype == torch.bfloat16  # the bf16 forward's own tiled, 128-column copy
+
     def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None, a_t=True):
         # f16x3: dY rides at the chain's own per-call scale from max |d raw| (the word in
         # `work`); bf16: one bf16 MFMA per product, no scales needed.  dY: the chain's tiled
-        # gradients (a_t) or row-major d raw; X: a kept activation (tiled when h_tiled) or the
-        # row-major encodings
-        b_t = h_tiled and X is not enc and X is not venc
+        # gradients (a_t) or row-major d raw; X: a kept activation (tiled when h_tiled), the
+        # encodings (row-major (R, 63), or the bf16 forward's tiled (NR, 128): n_store 63) or
+        # the per-ray view encodings
+        b_t = (h_tiled and X is not enc and X is not venc) or (X is enc and enc_t)
+        n_store = 0
+        if X is enc and enc_t:
+            ldx, n_store, n_in = 128, n_in, 128
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
              b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=1.0, b_scale=1.0 if bf16 else acts,
-             rowsum=db, a_amax=None if bf16 else work, mma_bf16=bf16, a_tiled=a_t, b_tiled=b_t)
+             rowsum=db, a_amax=None if bf16 else work, mma_bf16=bf16, a_tiled=a_t, b_tiled=b_t,
+             n_store=n_store)
 
     dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1], a_t=False)    # rgb_layer
     dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0
@@ -287,11 +294,12 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
 
 
 def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, masks=None,
-                         bf16=False):
+                         bf16=False, enc=None):
     """_forward_level on the fused kernel: raw (R x 4) and the kept activations (tiled,
     tiles.rows(R) rows each); ``masks`` ((9, tiles.rows(R), 8) int32) receives their ReLU' bits
-    for the backward chain.  bf16: the bf16
-    training mode (activations kept as torch.bfloat16)."""
+    for the backward chain.  bf16: the bf16 training mode (activations kept as torch.bfloat16;
+    ``enc``, optional, (tiles.rows(R), 128) bfloat16, receives pos_enc(x) tiled, columns 63..
+    zero)."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
     NR = tiles.rows(R)  # kept tensors: the tiled layout (tiles.py)
@@ -305,10 +313,14 @@ def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, m
         if not (w.is_contiguous() and b.is_contiguous()):
             raise ValueError("MLP parameters must be contiguous")
     packed = _pack(P, dev, S, bf16)
-    L.call("aon_mlp_fwd_train_bf16" if bf16 else "aon_mlp_fwd_train", L.ptr(packed), L.ptr(rays_o),
-           L.ptr(rays_d), L.ptr(viewdirs),
-           L.ptr(t_vals), B, S, L.ptr(noise) if noise is not None else None, L.ptr(hbuf),
-           L.ptr(bot), L.ptr(hv), L.ptr(raw), L.ptr(masks), L.stream(dev))
+    args = (L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs), L.ptr(t_vals), B, S,
+            L.ptr(noise) if noise is not None else None, L.ptr(hbuf), L.ptr(bot), L.ptr(hv),
+            L.ptr(raw), L.ptr(masks))
+    if bf16:
+        L.call("aon_mlp_fwd_train_bf16", *args, L.ptr(enc) if enc is not None else None,
+               L.stream(dev))
+    else:
+        L.call("aon_mlp_fwd_train", *args, L.stream(dev))
     return list(hbuf.unbind(0)), bot, hv
 
 
@@ -320,10 +332,14 @@ class RenderLevel(torch.autograd.Function):
     def forward(ctx, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise, *params):
         B, S = t_vals.shape
         R, dev = B * S, t_vals.device
-        # xyz = o + t d (helper.py:25-26) straight into the encodings (helper.py:136-140)
-        enc = torch.empty((R, 63), device=dev)
-        L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0, None,
-               0, 10, L.ptr(enc), L.stream(dev))
+        bf16 = FUSED_FORWARD and PRECISION == "bf16"
+        if bf16:  # the bf16 training forward keeps pos_enc(x) itself (bf16, tiled, 128 columns)
+            enc = torch.empty((tiles.rows(R), 128), device=dev, dtype=torch.bfloat16)
+        else:
+            # xyz = o + t d (helper.py:25-26) straight into the encodings (helper.py:136-140)
+            enc = torch.empty((R, 63), device=dev)
+            L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
+                   None, 0, 10, L.ptr(enc), L.stream(dev))
         venc = torch.empty((B, 27), device=dev)
         L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, 4, L.ptr(venc), L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
@@ -335,7 +351,7 @@ class RenderLevel(torch.autograd.Function):
             e0 = _ev()
             h, bot, hv = _forward_level_fused(P, L.contig(rays_o), L.contig(rays_d),
                                               L.contig(viewdirs), L.contig(t_vals), raw, noise,
-                                              masks, bf16=PRECISION == "bf16")
+                                              masks, bf16=bf16, enc=enc if bf16 else None)
             _rec(f"fwd_train{S}", e0, R)
         else:
             h, bot, hv = _forward_level(P, enc, venc, S, raw, noise)
@@ -374,9 +390,11 @@ class RenderLevel(torch.autograd.Function):
         if FUSED_BACKWARD:
             _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, ctx.masks, ctx.h_tiled)
         else:
-            if ctx.h_tiled:  # the all-GEMM backward reads row-major activations
-                h = [tiles.untile(x, R) for x in h]
-                bot, hv = tiles.untile(bot, R), tiles.untile(hv, R)
+            if ctx.h_tiled:  # the all-GEMM backward reads row-major fp32 activations
+                h = [tiles.untile(x, R).float() for x in h]
+                bot, hv = tiles.untile(bot, R).float(), tiles.untile(hv, R).float()
+            if enc.dtype == torch.bfloat16:  # the bf16 forward's tiled copy
+                enc = tiles.untile(enc, R)[:, :63].float().contiguous()
             _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
         return (None, None, None, None, None, None, *grads)

@@ -61,6 +61,7 @@ struct Params {
   int tblocks;               // blocks of one K chunk's tile grid (tile_of's ids, with padding)
   int a_tiled, b_tiled;      // reduction-major operand in the fused training kernels' 16-row
                              // tiled layout (mlp_f16x3_core.hpp act_base; rdiv 1)
+  int64_t nstore;            // columns of C written: n < nstore (a zero-padded B, bf16 mode)
 };
 
 // start of the 4-element run (k, row .. row + 3) of a reduction-major operand (row % 4 == 0):
@@ -399,7 +400,7 @@ __global__ void k_gemm_reduce(Params p, int splits) {
     }
     const int64_t m = e / p.N, n = e - m * p.N;
     float v = sum_z4(p.part + e, total, splits, q);
-    if (q != 0) continue;
+    if (q != 0 || n >= p.nstore) continue;
     float* c = p.C + m * p.ldc + n;
     if (p.accumulate) v = __fadd_rn(*c, v);
     if (p.bias) v = __fadd_rn(v, p.bias[n]);
@@ -712,6 +713,7 @@ __global__ __launch_bounds__(THREADS, AON_GEMM_BF_OCC) void k_gemm_bf16_km(Param
           p.part[((int64_t)z * p.M + m) * p.N + n] = v;
           continue;
         }
+        if (n >= p.nstore) continue;
         float* c = p.C + m * p.ldc + n;
         if (p.accumulate) v = __fadd_rn(*c, v);
         *c = v;
@@ -893,13 +895,13 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_tt(Params p) {
           p.part[((int64_t)z * p.M + m) * p.N + n] = v;
           continue;
         }
+        if (n >= p.nstore) continue;
         float* c = p.C + m * p.ldc + n;
         if (p.accumulate) v = __fadd_rn(*c, v);
         *c = v;
       }
     }
 }
-
 
 // ---- the same product with the operand tiles copied HBM/L2 -> LDS by global_load_lds_dwordx4
 // (no register staging): a DNB-deep ring of [32 k][128 col] image pairs, DNB - 1 k-tiles in
@@ -1086,11 +1088,165 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_dma(Params p) {
           p.part[((int64_t)z * p.M + m) * p.N + n] = v;
           continue;
         }
+        if (n >= p.nstore) continue;
         float* c = p.C + m * p.ldc + n;
         if (p.accumulate) v = __fadd_rn(*c, v);
         *c = v;
       }
     }
+}
+
+// ---- bf16 weight gradients with M <= 4 rows (the rgb / density heads: dW = d raw^T X with
+// X = hv3 / h7): a 128 x 128 MFMA tile would run 97% empty and the km kernel's transposing
+// loads held these at ~130 us for 0.2-0.4 GB, so the product streams instead.  Thread (r, cg):
+// row phase r of every 16-row block of its K chunk, columns 8 cg .. 8 cg + 7 (one 16-B run of B:
+// a wave reads two whole 16 x 16 tiles, 1 KB contiguous, of the tiled layout); A's M values of
+// the row rounded to bf16 as the MFMA paths stage them, products exact in fp32, fp32 sums in
+// row order, then a fixed xor tree over the 16 row phases; one chunk's partial per workgroup
+// (k_gemm_reduce sums the chunks in z order: deterministic).
+constexpr int kSkinnyRows = 16;
+template <int M, typename TA, bool BT>
+__global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
+  const int tid = threadIdx.x, r = tid & 15, cg = tid >> 4;
+  const int64_t n0 = 8 * (int64_t)cg;
+  const int64_t kbeg = (int64_t)blockIdx.x * p.kchunk;
+  const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const TA* A = reinterpret_cast<const TA*>(p.A);
+  const __bf16* B = reinterpret_cast<const __bf16*>(p.B);
+  float acc[M][8], rs[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    rs[m] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
+  }
+  for (int64_t k = kbeg + r; k < kend; k += kSkinnyRows) {
+    const int64_t bo = BT ? (k & ~int64_t(15)) * p.ldb + 256 * (n0 >> 4) + 16 * (k & 15) + (n0 & 15)
+                          : k * p.ldb + n0;
+    const uint4 bv = *reinterpret_cast<const uint4*>(B + bo);
+    const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
+    float b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = __uint_as_float((j & 1) ? (bw[j >> 1] & 0xffff0000u) : (bw[j >> 1] << 16));
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float a = static_cast<float>(static_cast<__bf16>(static_cast<float>(A[k * p.lda + m])));
+      rs[m] = __fadd_rn(rs[m], a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[m][j] = fmaf(a, b[j], acc[m][j]);  // a * b exact in fp32
+    }
+  }
+  // the 16 row phases of a column group are lanes 16 q .. 16 q + 15 of one wave
+#pragma unroll
+  for (int sh = 1; sh < 16; sh <<= 1)
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      rs[m] = __fadd_rn(rs[m], __shfl_xor(rs[m], sh, 64));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[m][j] = __fadd_rn(acc[m][j], __shfl_xor(acc[m][j], sh, 64));
+    }
+  if (r != 0) return;
+  const bool split = p.zsplit > 1;
+  const int z = blockIdx.x;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (p.rowsum && cg == 0) {
+      if (split) p.rowsum_part[(int64_t)z * p.M + m] = rs[m];
+      else p.rowsum[m] = rs[m];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = acc[m][j];
+      if (split) {
+        p.part[((int64_t)z * p.M + m) * p.N + n0 + j] = v;
+        continue;
+      }
+      float* c = p.C + m * p.ldc + n0 + j;
+      if (p.accumulate) v = __fadd_rn(*c, v);
+      *c = v;
+    }
+  }
+}
+
+// ---- bf16 weight gradient against a per-ray operand: C = A^T B with row k of B at k / rdiv
+// (views_linear.0's enc_dir columns: B = pos_enc(viewdirs), one row per ray, rdiv = S).  Every
+// B row meets rdiv consecutive A rows, so C = sum_ray (sum_{s<rdiv} A[ray rdiv + s]) B[ray]:
+// thread (ray, cg) sums its ray's rdiv rows of columns 8 cg .. 8 cg + 7 in row order (A's
+// values rounded to bf16 as staged; fp32 sums, kept unrounded), the workgroup's RB rays' sums go
+// to LDS, and their outer products with bf16(B) make the chunk's partial of C (and of A's
+// column sums).  The km kernel read A with the reduction-major transposing loads at ~130 us for
+// the fine level's 0.2 GB; this reads A once, in 16-B runs, and does 1/rdiv of the products.
+template <typename TA, typename TB, bool AT>
+__global__ __launch_bounds__(256) void k_gemm_segsum_bf16(Params p) {
+  __shared__ float seg[256 * 8];  // [RB rays][M]: RB * M = 8 * 256
+  const int M = static_cast<int>(p.M), N = static_cast<int>(p.N);
+  const int cgs = M / 8, rb = 256 / cgs;
+  const int tid = threadIdx.x, cg = tid % cgs, rl = tid / cgs;
+  const int64_t rdiv = p.b_rdiv;
+  const int64_t ray = (int64_t)blockIdx.x * rb + rl;
+  const TA* A = reinterpret_cast<const TA*>(p.A);
+  const int64_t n0 = 8 * (int64_t)cg;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t kb = ray * rdiv, ke = kb + rdiv < p.K ? kb + rdiv : p.K;
+  for (int64_t k = kb; k < ke; ++k) {
+    const int64_t o = AT ? (k & ~int64_t(15)) * p.lda + 256 * (n0 >> 4) + 16 * (k & 15) + (n0 & 15)
+                         : k * p.lda + n0;
+    float v[8];
+    if (std::is_same<TA, __bf16>::value) {
+      const uint4 w = *reinterpret_cast<const uint4*>(A + o);
+      const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __uint_as_float((j & 1) ? (ww[j >> 1] & 0xffff0000u) : (ww[j >> 1] << 16));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = static_cast<float>(static_cast<__bf16>(static_cast<float>(A[o + j])));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = __fadd_rn(acc[j], v[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) seg[rl * M + n0 + j] = acc[j];
+  __syncthreads();
+  const int64_t ray0 = (int64_t)blockIdx.x * rb;
+  const int64_t nray = (p.K + rdiv - 1) / rdiv;
+  const int nr = static_cast<int>(nray - ray0 < rb ? nray - ray0 : rb);
+  const TB* Bm = reinterpret_cast<const TB*>(p.B);
+  const bool split = p.zsplit > 1;
+  const int z = blockIdx.x;
+  for (int e = tid; e < M * N + M; e += 256) {
+    float v = 0.f;
+    if (e < M * N) {
+      const int m = e / N, n = e - m * N;
+      for (int q = 0; q < nr; ++q) {
+        const float b = static_cast<float>(static_cast<__bf16>(static_cast<float>(Bm[(ray0 + q) * p.ldb + n])));
+        v = fmaf(seg[q * M + m], b, v);
+      }
+      if (split) {
+        p.part[((int64_t)z * M + m) * N + n] = v;
+        continue;
+      }
+      float* c = p.C + m * p.ldc + n;
+      if (p.accumulate) v = __fadd_rn(*c, v);
+      *c = v;
+    } else if (p.rowsum) {
+      const int m = e - M * N;
+      for (int q = 0; q < nr; ++q) v = __fadd_rn(v, seg[q * M + m]);
+      if (split) p.rowsum_part[(int64_t)z * M + m] = v;
+      else p.rowsum[m] = v;
+    }
+  }
+}
+
+template <typename TA, bool BT>
+static void launch_skinny(const Params& p, dim3 grid, hipStream_t st) {
+  const dim3 block((unsigned)(2 * p.N));  // 16 row phases x N / 8 column groups
+  switch (p.M) {
+    case 1: hipLaunchKernelGGL((k_gemm_skinny_bf16<1, TA, BT>), grid, block, 0, st, p); break;
+    case 2: hipLaunchKernelGGL((k_gemm_skinny_bf16<2, TA, BT>), grid, block, 0, st, p); break;
+    case 3: hipLaunchKernelGGL((k_gemm_skinny_bf16<3, TA, BT>), grid, block, 0, st, p); break;
+    default: hipLaunchKernelGGL((k_gemm_skinny_bf16<4, TA, BT>), grid, block, 0, st, p); break;
+  }
 }
 
 template <typename TA, typename TB>
@@ -1118,8 +1274,33 @@ static bool bf16_copy_path(const aon_gemm_args* a) {
          b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) && a->lda % 8 == 0 && a->ldb % 8 == 0;
 }
 
+// bf16 weight gradient of at most 4 rows on a bf16 B of up to 256 columns (k_gemm_skinny_bf16)
+static bool skinny_path(const aon_gemm_args* a) {
+  const int64_t b_rdiv = a->b_kc ? 1 : a->b_rdiv;
+  return a->mma_bf16 && a->M >= 1 && a->M <= 4 && a->b_bf16 && !a->a_tiled && b_rdiv == 1 &&
+         a->N % 8 == 0 && a->N <= 256 && aligned16(a->B) && a->ldb % 8 == 0 && !a->k_splits &&
+         (a->n_store == 0 || a->n_store == a->N);
+}
+
+// bf16 weight gradient against a per-ray B (rdiv > 1): k_gemm_segsum_bf16
+static bool segsum_path(const aon_gemm_args* a) {
+  return a->mma_bf16 && !a->a_kc && !a->b_kc && a->b_rdiv > 1 && !a->b_tiled && a->M % 8 == 0 &&
+         a->M >= 8 && a->M <= 256 && aligned16(a->A) && a->lda % 8 == 0 && !a->k_splits &&
+         (a->n_store == 0 || a->n_store == a->N);
+}
+
 static int64_t gemm_splits(const aon_gemm_args* a) {
   const int64_t tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
+  // the segment-sum kernel: one chunk of 2048 / M rays (whole segments) per workgroup
+  if (segsum_path(a)) {
+    const int64_t rays = (a->K + a->b_rdiv - 1) / a->b_rdiv, rb = 2048 / a->M;
+    return rays > 0 ? (rays + rb - 1) / rb : 1;
+  }
+  // the skinny kernel: ~512 chunks of whole 16-row blocks (two workgroups per CU)
+  if (skinny_path(a)) {
+    const int64_t kc = ((a->K + 511) / 512 + kSkinnyRows - 1) / kSkinnyRows * kSkinnyRows;
+    return a->K > 0 ? (a->K + kc - 1) / kc : 1;
+  }
   // split the reduction only when the tile grid alone cannot fill the chip and K is long
   if (a->k_splits > 0) return a->k_splits;
   if (tiles >= 512 || a->K < 8 * 1024 || a->A2) return 1;
@@ -1151,7 +1332,8 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   AON_REQUIRE(a, "null args");
   AON_REQUIRE(a->A && a->B && a->C, "null operand");
   AON_REQUIRE(a->M >= 0 && a->N >= 0 && a->K >= 0, "bad shape");
-  AON_REQUIRE(a->lda >= 1 && a->ldb >= 1 && a->ldc >= a->N, "bad leading dimension");
+  AON_REQUIRE(a->lda >= 1 && a->ldb >= 1 && a->ldc >= (a->n_store > 0 ? a->n_store : a->N),
+              "bad leading dimension");
   AON_REQUIRE(!a->A2 || (a->a_kc && a->K1 >= 0 && a->K1 <= a->K && a->lda2 >= 1 && a->a2_rdiv >= 1),
               "A2 needs a_kc, 0 <= K1 <= K, lda2 >= 1, a2_rdiv >= 1");
   AON_REQUIRE(!a->mask || a->ldm >= a->N, "bad mask leading dimension");
@@ -1169,10 +1351,15 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
               "a_tiled: reduction-major A of width lda = M (a multiple of 16)");
   AON_REQUIRE(!a->b_tiled || (!a->b_kc && a->b_rdiv == 1 && a->ldb == a->N && a->N % 16 == 0),
               "b_tiled: reduction-major B of width ldb = N (a multiple of 16), b_rdiv = 1");
+  AON_REQUIRE(a->n_store >= 0 && a->n_store <= a->N, "n_store must be in [0, N]");
+  AON_REQUIRE(a->n_store == 0 || a->n_store == a->N || bf16_copy_path(a),
+              "n_store < N: the bf16 LDS-DMA weight-gradient path only (both operands bf16, "
+              "M and N multiples of 128)");
   if (a->M == 0 || a->N == 0) return 0;
   Params p;
   p.a_tiled = a->a_tiled;
   p.b_tiled = a->b_tiled;
+  p.nstore = a->n_store > 0 ? a->n_store : a->N;
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = a->A; p.lda = a->lda;
   p.A2 = a->A2; p.lda2 = a->A2 ? a->lda2 : 0; p.K1 = a->A2 ? a->K1 : INT64_MAX;
@@ -1184,7 +1371,9 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   p.sa = a->a_scale; p.sb = a->b_scale; p.inv_s = 1.0f / (a->a_scale * a->b_scale);
   p.sa_bits = a->a_amax;
   const int64_t splits = gemm_splits(a);
-  p.kchunk = splits > 1 ? ((a->K + splits - 1) / splits + BK - 1) / BK * BK : (a->K > 0 ? a->K : 1);
+  const int64_t kround = skinny_path(a) ? kSkinnyRows : BK;
+  p.kchunk = splits > 1 ? ((a->K + splits - 1) / splits + kround - 1) / kround * kround : (a->K > 0 ? a->K : 1);
+  if (segsum_path(a)) p.kchunk = 2048 / a->M * a->b_rdiv;  // whole segments per workgroup
   const int64_t zs = a->K > 0 ? (a->K + p.kchunk - 1) / p.kchunk : 1;
   AON_REQUIRE(!a->rowsum || !a->a_kc, "rowsum needs a reduction-major A (a_kc = 0)");
   p.part = nullptr;
@@ -1219,7 +1408,21 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     const bool vb16 = a->b_bf16 ? (reinterpret_cast<uintptr_t>(a->B) & 7) == 0 && a->ldb % 4 == 0 : vb;
     // both bf16, whole 128 x 128 tiles, 16-B runs: the copy-staged kernels
     const bool tt = bf16_copy_path(a);
-    if (tt && AON_GEMM_BF_DMA) hipLaunchKernelGGL(k_gemm_bf16_dma, grid, dim3(THREADS), 0, st, p);
+    if (segsum_path(a)) {
+      const dim3 g((unsigned)zs, 1, 1);
+#define AON_SEG_L(TA_, TB_, AT_) hipLaunchKernelGGL((k_gemm_segsum_bf16<TA_, TB_, AT_>), g, dim3(256), 0, st, p)
+      if (a->a_bf16 && a->b_bf16) { if (a->a_tiled) AON_SEG_L(__bf16, __bf16, true); else AON_SEG_L(__bf16, __bf16, false); }
+      else if (a->a_bf16) { if (a->a_tiled) AON_SEG_L(__bf16, float, true); else AON_SEG_L(__bf16, float, false); }
+      else if (a->b_bf16) { if (a->a_tiled) AON_SEG_L(float, __bf16, true); else AON_SEG_L(float, __bf16, false); }
+      else { if (a->a_tiled) AON_SEG_L(float, float, true); else AON_SEG_L(float, float, false); }
+#undef AON_SEG_L
+    } else if (skinny_path(a)) {
+      const dim3 g((unsigned)zs, 1, 1);
+      if (a->a_bf16 && a->b_tiled) launch_skinny<__bf16, true>(p, g, st);
+      else if (a->a_bf16) launch_skinny<__bf16, false>(p, g, st);
+      else if (a->b_tiled) launch_skinny<float, true>(p, g, st);
+      else launch_skinny<float, false>(p, g, st);
+    } else if (tt && AON_GEMM_BF_DMA) hipLaunchKernelGGL(k_gemm_bf16_dma, grid, dim3(THREADS), 0, st, p);
     else if (tt) hipLaunchKernelGGL(k_gemm_bf16_tt, grid, dim3(THREADS), 0, st, p);
     else if (a->a_bf16 && a->b_bf16) launch_bf<__bf16, __bf16>(p, va16, vb16, grid, st);
     else if (a->a_bf16) launch_bf<__bf16, float>(p, va16, vb16, grid, st);

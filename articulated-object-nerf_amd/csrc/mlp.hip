@@ -372,18 +372,19 @@ extern "C" int aon_mlp_fwd_train_bf16(const void* packed, const float* rays_o,
                                       const float* rays_d, const float* viewdirs, const float* t,
                                       int64_t B, int S, const float* noise, uint16_t* h,
                                       uint16_t* bot, uint16_t* hv, float* raw, uint32_t* masks,
-                                      aon_stream_t stream) {
+                                      uint16_t* enc, aon_stream_t stream) {
   AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && h && bot && hv && raw && masks,
               "null pointer");
   AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
   AON_REQUIRE(aligned16(packed) && aligned16(raw) && aligned16(masks) && aligned16(h) &&
-                  aligned16(bot) && aligned16(hv),
+                  aligned16(bot) && aligned16(hv) && aligned16(enc),
               "packed / output buffers must be 16-byte aligned");
   const int64_t N = B * S;
   if (N == 0) return 0;
   AON_REQUIRE((N + 127) / 128 < (1ll << 31), "too many rows");
   const TrainStore ts{reinterpret_cast<float*>(h), reinterpret_cast<float*>(bot),
-                      reinterpret_cast<float*>(hv), noise, reinterpret_cast<uint2*>(masks)};
+                      reinterpret_cast<float*>(hv), noise, reinterpret_cast<uint2*>(masks),
+                      reinterpret_cast<__bf16*>(enc)};
   return launch_f16x3(3, 1, packed, rays_o, rays_d, viewdirs, t, B, S, AON_ACT_NONE, raw,
                       (hipStream_t)stream, &ts);
 }

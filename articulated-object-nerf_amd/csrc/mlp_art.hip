@@ -97,7 +97,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? px[c][e < 3 ? e : 0] * kActS : 0.f;
     split8(dv, din.hi[0][c], din.lo[0][c], din.ovf);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) vv[e] *= kActS;
+    for (int e = 0; e < 8; ++e) vv[e] *= act_scale<BFM>();
     split8<BFM>(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
     stash[64 * (6 * c + 4)] = __builtin_bit_cast(f4, venc.hi[0][c]);
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       for (int e = 0; e < 8; ++e) {
         const float f = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10);
         if (STORE && rows[c] < N && 32 * k + 8 * g + e < 63) ts.enc[63 * rows[c] + 32 * k + 8 * g + e] = f;
-        ev[k][e] = f * kActS;
+        ev[k][e] = f * act_scale<BFM>();
       }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {

@@ -43,6 +43,7 @@ struct EncStash {
     return v;
   }
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
+  __device__ __forceinline__ void put_bf(int, int, int, int, float, float, uint32_t) const {}
 };
 
 // Epilogue policy of pts_linears.0's enc columns: total d enc_f = this value + the parked skip
@@ -82,6 +83,7 @@ struct EncBwd {
     return v;
   }
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
+  __device__ __forceinline__ void put_bf(int, int, int, int, float, float, uint32_t) const {}
 };
 
 // BF: the bf16 training mode -- the whole chain one bf16 MFMA per product on the compact stream
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   p.start();
   for (int i = tid; i < Net::kBiasFloats; i += G::kThreads) bias_s[i] = bias_g[i];
 
-  const float s = grad_scale(*a.absmax);
+  const float s = BF ? 1.0f : grad_scale(*a.absmax);  // bf16: unscaled (fp32's exponent range)
   const float inv = 1.0f / s;  // exact: a power of two
 
   Frag<1, NCOL> drgb, dsig;
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
     for (int q = 0; q < 3; ++q) a.dxp[3 * row + q] = dx[q];
   }
   // dL/dx' carries pos_enc's 2^d factors: back into fp16 at this sample's own scale
-  const float sd = grad_scale(__float_as_uint(fmaxf(fabsf(dx[0]), fmaxf(fabsf(dx[1]), fabsf(dx[2])))));
+  const float sd = BF ? 1.0f : grad_scale(__float_as_uint(fmaxf(fabsf(dx[0]), fmaxf(fabsf(dx[1]), fabsf(dx[2])))));
   const float invd = 1.0f / sd;
   Frag<1, NCOL> ddx;
   {
@@ -296,7 +298,8 @@ static int art_bwd(const void* packed, const float* draw, const uint32_t* masks,
   AON_REQUIRE(grid < (1ll << 31), "too many rows");
   hipStream_t st = (hipStream_t)stream;
   uint32_t* amax = static_cast<uint32_t*>(work);
-  const int rc = absmax(draw, 4 * N, amax, st);
+  // the fp16x3 chain's per-call gradient scale (bf16 runs unscaled: no max pass)
+  const int rc = bf16 ? 0 : absmax(draw, 4 * N, amax, st);
   if (rc) return rc;
   const ArtBwdArgs args{draw, reinterpret_cast<const uint2*>(masks), enc, dzv, dbot, dz, dxp, dzd,
                         amax, N};

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   p.start();
   for (int i = tid; i < Net::kBiasFloats; i += G::kThreads) bias_s[i] = bias_g[i];
 
-  const float s = grad_scale(*a.absmax);
+  const float s = BF ? 1.0f : grad_scale(*a.absmax);  // bf16: unscaled (fp32's exponent range)
   const float inv = 1.0f / s;  // exact: a power of two
 
   // d raw_rgb -> segment B of rgb_layer^T (lane group 0, elements 0..2); d raw_sigma ->
@@ -212,7 +212,8 @@ static int bwd_launch(const void* packed, const float* draw, const uint32_t* mas
   AON_REQUIRE(grid < (1ll << 31), "too many rows");
   hipStream_t st = (hipStream_t)stream;
   uint32_t* amax = static_cast<uint32_t*>(work);
-  const int rc = absmax(draw, 4 * N, amax, st);
+  // the fp16x3 chain's per-call gradient scale (bf16 runs unscaled: no max pass)
+  const int rc = bf16 ? 0 : absmax(draw, 4 * N, amax, st);
   if (rc) return rc;
   BwdArgs args{draw, reinterpret_cast<const uint2*>(masks), static_cast<float*>(dzv),
                static_cast<float*>(dzb), static_cast<float*>(dz), amax, N};

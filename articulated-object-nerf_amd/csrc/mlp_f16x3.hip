@@ -171,14 +171,33 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
         vv[e] = f < 27 ? cd[f] : 0.f;
       }
     }
+    // bf16 training mode: pos_enc(x) kept for the weight gradients of pts_linears.0 and the skip
+    // layer's enc columns, bf16 in the tiled layout, 128 columns (63..127 zero) -- whole
+    // 128-column tiles for the LDS-DMA dW kernel (aon_gemm n_store); lane group g's 8 features
+    // 32 k + 8 g .. + 7 are one 16-B run of tile 2 k + g / 2, and k = 2, 3 write the zero tiles
+    if (STORE && BF && ts.enc_bf && rows[c] < N) {
+      __bf16* eb = ts.enc_bf + act_base(rows[c], 128, 0) + 8 * (g & 1) + 256 * (g >> 1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        if (k < 2) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bf2 pr = {static_cast<__bf16>(ev[k][2 * e]), static_cast<__bf16>(ev[k][2 * e + 1])};
+            w[e] = __builtin_bit_cast(uint32_t, pr);
+          }
+        }
+        *reinterpret_cast<uint4*>(eb + 512 * k) = uint4{w[0], w[1], w[2], w[3]};
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) ev[k][e] *= (AON_F16X3_V2 ? kActS : kActScale);
+      for (int e = 0; e < 8; ++e) ev[k][e] *= act_scale<BF>();
       split8<BF>(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) vv[e] *= (AON_F16X3_V2 ? kActS : kActScale);
+    for (int e = 0; e < 8; ++e) vv[e] *= act_scale<BF>();
     split8<BF>(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
   }
 
@@ -265,11 +284,11 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
           w = a.tr[li] ? src[(int64_t)col * ld + o] : src[(int64_t)o * ld + col];
       }
 #if AON_F16X3_V2
-      w *= kWS;  // exact (power of two)
-      if (bf) {  // bf16 layer: bf16(w) in the compact (hi-only) stream
+      if (bf) {  // bf16 layer: bf16(w), unscaled, in the compact (hi-only) stream
         out[e] = bf_bits(w);
         continue;
       }
+      w *= kWS;  // exact (power of two)
       const _Float16 h = static_cast<_Float16>(w);
       out[e] = lo_part ? static_cast<_Float16>(w - static_cast<float>(h)) : h;
       // range guard (mlp_f16x3_core.hpp): a weight whose scaled hi part is not a finite fp16
@@ -288,7 +307,9 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
       const int o = i - a.layers[li].bias0;
 #if AON_F16X3_V2
       // hidden layers add the bias at activation scale; the 1-tile heads at true scale
-      const float bs = a.layers[li].u == 1 ? 1.0f : kActS;
+      // (bf16 layers: at true scale, their activations are unscaled)
+      const StreamMap map{a.bf16, a.mx_lo, a.mx_hi};
+      const float bs = a.layers[li].u == 1 || !map.f16(a.layers[li].blk0) ? 1.0f : kActS;
 #else
       const float bs = kActScale;
 #endif

@@ -82,6 +82,11 @@ __device__ __forceinline__ void range_report(const float* bias_end, uint64_t ovf
   if (ovf && (threadIdx.x & 63) == 0) *reinterpret_cast<uint32_t*>(const_cast<float*>(bias_end)) = 1u;
 }
 
+// operand scale of a layer's input activations: 2^3 for fp16x3 (V2), 1 for bf16 layers (bf16
+// has fp32's exponent range: no scaling, and their weights are packed unscaled too)
+template <bool BF>
+__host__ __device__ constexpr float act_scale() { return BF ? 1.0f : (AON_F16X3_V2 ? kActS : kActScale); }
+
 // 8 fp32 values (already at activation scale) -> (hi, lo) fp16 fragments; ovf |= out of range.
 // BF: bf16 values in hi, no lo, no range test.
 template <bool BF = false>
@@ -180,7 +185,11 @@ struct NoStore {
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
+  __device__ __forceinline__ void put_bf(int, int, int, int, float, float, uint32_t) const {}
 };
+// put_bf (the bf16 layers' epilogue): the pair's values at TRUE scale (bf16 numerics carry no
+// operand scaling) with their packed bf16 dword -- the one the next layer's fragment gets -- so
+// a bf16 store writes that dword as it is: no rescale, no second conversion
 
 // two consecutive outputs at true scale: one 8-B fp32 store, or (bf16 mode) one 4-B bf16 store
 __device__ __forceinline__ void store2(float* p, float v0, float v1) {
@@ -240,6 +249,13 @@ struct Store4 {
       store4(rowp + kTileStride * (2 * pr + uu), pend[c][0], pend[c][1], v0, v1);
     }
   }
+  // bf16 layers: the packed pair as it is (parts r0 = 0, 2 of a tile row -> one 8-B store)
+  mutable uint32_t pendw[NCOL];
+  __device__ __forceinline__ void emit_bf(T* rowp, int pr, int uu, int r0, int c, uint32_t pk) const {
+    static_assert(std::is_same<T, __bf16>::value, "bf16 layers keep bf16 activations");
+    if (r0 == 0) pendw[c] = pk;
+    else if (rowp) *reinterpret_cast<uint2*>(rowp + kTileStride * (2 * pr + uu)) = uint2{pendw[c], pk};
+  }
 };
 
 template <int NCOL, typename T = float>
@@ -250,6 +266,9 @@ struct RowStore : Store4<NCOL, T> {
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     this->emit(rowp[c], pr, uu, r0, c, v0 * s, v1 * s);
+  }
+  __device__ __forceinline__ void put_bf(int pr, int uu, int r0, int c, float, float, uint32_t pk) const {
+    this->emit_bf(rowp[c], pr, uu, r0, c, pk);
   }
 };
 
@@ -263,8 +282,16 @@ struct RowStoreBits : RowStore<NCOL, T> {
   uint8_t* mrow[NCOL];  // bytes of word (row, g), nullptr when row >= N
   bool narrow;          // 4-pair (128-wide) layer: bytes 4..7 of the word are written as 0
   mutable uint32_t b[NCOL];  // the current pair's 8 bits (byte pr of the word)
+  __device__ __forceinline__ void put_bf(int pr, int uu, int r0, int c, float v0, float v1,
+                                         uint32_t pk) const {
+    RowStore<NCOL, T>::put_bf(pr, uu, r0, c, v0, v1, pk);
+    bits(pr, uu, r0, c, v0, v1);
+  }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     RowStore<NCOL, T>::put(pr, uu, r0, c, v0, v1);
+    bits(pr, uu, r0, c, v0, v1);
+  }
+  __device__ __forceinline__ void bits(int pr, int uu, int r0, int c, float v0, float v1) const {
     const uint32_t m = (v0 > 0.0f ? 1u : 0u) | (v1 > 0.0f ? 2u : 0u);  // v: post-ReLU, s > 0
     const int bit = 4 * uu + r0;  // within the pair's byte (compile-time after unrolling)
     b[c] = bit == 0 ? m : (b[c] | (m << bit));
@@ -296,6 +323,9 @@ struct MaskBits : Store4<NCOL, T> {
   }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     this->emit(rowp[c], pr, uu, r0, c, v0 * s, v1 * s);
+  }
+  __device__ __forceinline__ void put_bf(int pr, int uu, int r0, int c, float, float, uint32_t pk) const {
+    this->emit_bf(rowp[c], pr, uu, r0, c, pk);
   }
 };
 
@@ -359,7 +389,9 @@ struct StorePick<true, NCOL, T> {
 
 // epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
 // part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
-template <bool RELU, bool BF, int NCOL, int NO, typename Store = NoStore>
+// BF: a bf16 layer -- operands unscaled, the accumulator at true scale: + bias (nothing when
+// ZB, the backward chains' zero bias tables), ReLU, one v_cvt_pk_bf16_f32.
+template <bool RELU, bool BF, int NCOL, int NO, typename Store = NoStore, bool ZB = false>
 __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
                                          const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr,
                                          const Store& st = Store{}) {
@@ -370,8 +402,9 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
 #if AON_F16X3_V2
-      // one accumulator at scale 2^9 -> activation scale 2^3, plus the (pre-scaled) bias
-      float v = fmaf(hh[uu][c][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
+      // fp16x3: one accumulator at scale 2^9 -> activation scale 2^3, plus the (pre-scaled) bias
+      float v = BF ? (ZB ? hh[uu][c][r0 + e] : __fadd_rn(hh[uu][c][r0 + e], bias[uu][r0 + e]))
+                   : fmaf(hh[uu][c][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
       (void)xx;
 #else
       float v = fmaf(xx[uu][c][r0 + e], 1.0f / kLoScale, hh[uu][c][r0 + e]);
@@ -380,15 +413,16 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
       if (RELU) v = fmaxf(v, 0.0f);
       vv[e] = st.post(pr, uu, r0 + e, c, v);
     }
-    if (BF) {  // bf16 mode: the pair as one v_cvt_pk_bf16_f32, no lo part, no range limit
-      st.put(pr, uu, r0, c, vv[0], vv[1]);
+    if constexpr (BF) {  // bf16 mode: the pair as one v_cvt_pk_bf16_f32, no lo part, no range limit
       // the packed pair goes in as ONE dword of the fragment: ROCm 7.2's clang mis-lowers
       // bit_cast<_Float16>(pair[1]) of a <2 x bfloat> (it yields element 0;
       // tools/diag/bf16_pack_probe.hip), so no bf16 element is extracted
       typedef uint32_t u4 __attribute__((ext_vector_type(4)));
       const bf2 hb = {static_cast<__bf16>(vv[0]), static_cast<__bf16>(vv[1])};
+      const uint32_t pk = __builtin_bit_cast(uint32_t, hb);
+      st.put_bf(pr, uu, r0, c, vv[0], vv[1], pk);
       u4 w = __builtin_bit_cast(u4, out.hi[pr][c]);
-      w[q] = __builtin_bit_cast(uint32_t, hb);
+      w[q] = pk;
       out.hi[pr][c] = __builtin_bit_cast(h8, w);
       continue;
     }
@@ -480,11 +514,13 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
 #endif
         }
       }
-      if (pr > 0 && k >= EO && k - EO < 4) epi_part<RELU, BF>(k - EO, phh, pxx, pbias, out, pr - 1, st);
+      if (pr > 0 && k >= EO && k - EO < 4)
+        epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias>(k - EO, phh, pxx, pbias, out, pr - 1, st);
     }
     if (pr > 0) {
 #pragma unroll
-      for (int q = QIN; q < 4; ++q) epi_part<RELU, BF>(q, phh, pxx, pbias, out, pr - 1, st);
+      for (int q = QIN; q < 4; ++q)
+        epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias>(q, phh, pxx, pbias, out, pr - 1, st);
     }
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
@@ -497,7 +533,8 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) epi_part<RELU, BF>(q, phh, pxx, pbias, out, NP - 1, st);
+  for (int q = 0; q < 4; ++q)
+    epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias>(q, phh, pxx, pbias, out, NP - 1, st);
 }
 
 // single-tile head (density / rgb): returns the 16-row tile at activation scale
@@ -545,7 +582,8 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #if AON_F16X3_V2
-      res[c][r] = fmaf(hh[c][r], 1.0f / (kWS * kActS), bias[r]);  // true scale (head bias unscaled)
+      // true scale (head bias unscaled); bf16 heads: unscaled operands
+      res[c][r] = BF ? __fadd_rn(hh[c][r], bias[r]) : fmaf(hh[c][r], 1.0f / (kWS * kActS), bias[r]);
 #else
       res[c][r] = fmaf(xx[c][r], 1.0f / kLoScale, hh[c][r]);
 #endif

@@ -199,9 +199,11 @@ constexpr LayerDesc kLayersArtBwd[kNumLayersArtBwd] = {
 };
 
 // compile-time description of one fp16x3 network: its layer table and stream geometry
-template <const LayerDesc* TABLE, int NLAYERS, int BLOCKS, int STREAM_BLOCKS, int BIAS_FLOATS>
+template <const LayerDesc* TABLE, int NLAYERS, int BLOCKS, int STREAM_BLOCKS, int BIAS_FLOATS,
+          bool ZERO_BIAS = false>
 struct NetH {
   static constexpr const LayerDesc* kTable = TABLE;
+  static constexpr bool kZeroBias = ZERO_BIAS;  // the backward chains: an all-zero bias table
   static constexpr int kNumLayers = NLAYERS;
   static constexpr int kBlocks = BLOCKS;               // blocks carrying weights
   static constexpr int kStreamBlocks = STREAM_BLOCKS;  // padded to whole LDS chunks
@@ -226,8 +228,8 @@ struct NetH {
 
 using NetVanillaH = NetH<kLayersH, kNumLayers, kBlocks, kStreamBlocks, kBiasFloats>;
 using NetArtH = NetH<kLayersArt, kNumLayersArt, 2752, 2752, 3376>;
-using NetBwdH = NetH<kLayersBwd, kNumLayersBwd, 2224, 2240, 2432>;
-using NetArtBwdH = NetH<kLayersArtBwd, kNumLayersArtBwd, 2752, 2752, 3456>;
+using NetBwdH = NetH<kLayersBwd, kNumLayersBwd, 2224, 2240, 2432, true>;
+using NetArtBwdH = NetH<kLayersArtBwd, kNumLayersArtBwd, 2752, 2752, 3456, true>;
 static_assert(NetVanillaH::ok(), "inconsistent vanilla fp16x3 layout");
 static_assert(NetArtH::ok(), "inconsistent articulated fp16x3 layout");
 static_assert(NetBwdH::ok(), "inconsistent backward-chain fp16x3 layout");
@@ -312,6 +314,7 @@ struct TrainStore {
   float* hv;
   const float* noise;
   uint2* masks;  // (9, N, 4) ReLU' bits of h0..h7, hv (RowStoreBits)
+  __bf16* enc_bf;  // bf16 mode, optional: pos_enc(x) tiled (N, 128), columns 63.. zero
 };
 
 // activations the articulated training forward keeps (aon_mlp_art_fwd_train)

@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 6
+#define AON_ABI_VERSION 7
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -195,11 +195,14 @@ int aon_mlp_fwd_train(const void* packed, const float* rays_o, const float* rays
 /* The same training forward in the bf16 mode: packed = an AON_PREC_BF16 stream; one bf16
  * MFMA per weight product (fp32 accumulate, activations rounded to bf16 between layers) and
  * the kept activations h / bot / hv stored as bf16 (raw bits, same shapes): half the bytes of
- * the fp32 stores, and exactly the operands the next layer consumed. */
+ * the fp32 stores, and exactly the operands the next layer consumed.  enc (optional, NULL:
+ * not kept): pos_enc(x) as bf16 in the same tiled layout, (NR, 128), columns 63..127 zero --
+ * the B operand of pts_linears.0's and the skip layer's enc-column weight gradients (aon_gemm
+ * with n_store = 63), so no separate encoding pass. */
 int aon_mlp_fwd_train_bf16(const void* packed, const float* rays_o, const float* rays_d,
                            const float* viewdirs, const float* t, int64_t B, int S,
                            const float* noise, uint16_t* h, uint16_t* bot, uint16_t* hv,
-                           float* raw, uint32_t* masks, aon_stream_t stream);
+                           float* raw, uint32_t* masks, uint16_t* enc, aon_stream_t stream);
 
 /* ReLU' bits of a ROW-MAJOR activation tensor h (N x width, width a multiple of 32 up to 256)
  * in the tiled layout of aon_mlp_fwd_train's masks (NR, 4) pairs of uint32 -- for the fused backward chains
@@ -394,6 +397,10 @@ typedef struct aon_gemm_args {
    * aon_mlp_fwd_train): a_tiled needs lda == M, b_tiled ldb == N and b_rdiv 1, both widths
    * multiples of 16 */
   int a_tiled, b_tiled;
+  /* columns of C written (0: all N): a B zero-padded to whole 128-column tiles (the bf16 mode's
+   * pos_enc copy, 63 -> 128 columns) updates only the real columns of dW; n_store < N on the
+   * bf16 LDS-DMA path only (both operands bf16, M and N multiples of 128) */
+  int64_t n_store;
 } aon_gemm_args;
 
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);

@@ -215,3 +215,125 @@ def test_weight_gradient_gemm_tiled_operands(mma_bf16, dtype):
         out.append((C, rs))
     torch.cuda.synchronize()
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("K,M,N,a_off,b_tiled", [
+    (790528, 1, 256, 3, True),    # density: d raw_sigma (column 3 of d raw, ld 4) x h7
+    (790528, 3, 128, 0, True),    # rgb: d raw_rgb x hv3
+    (70001, 4, 64, 0, False),     # row-major B, ragged last 16-row block
+    (5, 2, 16, 1, True),          # fewer rows than one block
+])
+def test_bf16_skinny_weight_gradient(K, M, N, a_off, b_tiled):
+    """aon_gemm mma_bf16 with M <= 4 (k_gemm_skinny_bf16: the rgb / density heads' dW = d raw^T X)
+    against fp64 products of the bf16-rounded operands, C accumulated and the bias row sums, on
+    the fused kernels' tiled or row-major bf16 B."""
+    from aonerf import tiles
+    from aonerf.linalg import gemm
+
+    g = torch.Generator(device="cuda").manual_seed(K + 7 * M)
+    draw = torch.randn((K, 4), device="cuda", generator=g) * 1e-3
+    A = draw[:, a_off:]
+    Bst = torch.randn((K, N), device="cuda", generator=g).to(torch.bfloat16)
+    Bop = tiles.tile(Bst) if b_tiled else Bst
+    C0 = torch.randn((M, N), device="cuda", generator=g)
+    C = C0.clone()
+    rs = torch.empty((M,), device="cuda")
+    gemm(C, A, Bop, M, N, K, lda=4, a_kc=False, ldb=N, b_kc=False, ldc=N, accumulate=True,
+         rowsum=rs, mma_bf16=True, b_tiled=b_tiled)
+    torch.cuda.synchronize()
+    a64 = bf16_round(A[:, :M].cpu())
+    want = C0.cpu().double() + a64.T @ Bst.cpu().double()
+    err = rel_err(C.cpu().numpy(), want.numpy())
+    print(f"bf16 skinny dW K={K} M={M} N={N}: max-rel err {err:.2e}")
+    assert err < 2e-5
+    np.testing.assert_allclose(rs.cpu().numpy(), a64.sum(0).numpy(), rtol=0,
+                               atol=2e-5 * float(a64.abs().sum(0).max()))
+
+
+@pytest.mark.parametrize("K,rdiv,a_tiled,a_bf", [(4096 * 193, 193, True, True),
+                                                  (2000, 33, False, True),
+                                                  (29 * 65, 65, True, False)])
+def test_bf16_per_ray_weight_gradient(K, rdiv, a_tiled, a_bf):
+    """aon_gemm mma_bf16 against a per-ray B (row k of B = k / rdiv: views_linear.0's enc_dir
+    columns, k_gemm_segsum_bf16: per-ray sums of A, then their outer products) against fp64
+    products of the bf16-rounded operands, accumulated, with the row sums."""
+    from aonerf import tiles
+    from aonerf.linalg import gemm
+
+    M, N = 128, 27
+    g = torch.Generator(device="cuda").manual_seed(K)
+    A = torch.randn((K, M), device="cuda", generator=g) * 1e-3
+    if a_bf:
+        A = A.to(torch.bfloat16)
+    Bst = torch.randn(((K + rdiv - 1) // rdiv, N), device="cuda", generator=g)
+    C0 = torch.randn((M, 300), device="cuda", generator=g)
+    C = C0.clone()
+    rs = torch.empty((M,), device="cuda")
+    gemm(C[:, 256:], tiles.tile(A) if a_tiled else A, Bst, M, N, K, lda=M, a_kc=False, ldb=N,
+         b_kc=False, b_rdiv=rdiv, ldc=300, accumulate=True, rowsum=rs, mma_bf16=True,
+         a_tiled=a_tiled)
+    torch.cuda.synchronize()
+    a64 = bf16_round(A.float().cpu())
+    b64 = bf16_round(Bst.cpu())[torch.arange(K) // rdiv]
+    want = C0.cpu().double().clone()
+    want[:, 256:256 + N] += a64.T @ b64
+    err = rel_err(C.cpu().numpy(), want.numpy())
+    print(f"bf16 per-ray dW K={K} rdiv={rdiv}: max-rel err {err:.2e}")
+    assert err < 2e-5
+    assert torch.equal(C[:, :256], C0[:, :256]) and torch.equal(C[:, 256 + N:], C0[:, 256 + N:])
+    np.testing.assert_allclose(rs.cpu().numpy(), a64.sum(0).numpy(), rtol=0,
+                               atol=2e-5 * float(a64.abs().sum(0).max()))
+
+
+def test_bf16_n_store_padded_operand():
+    """aon_gemm n_store: a bf16 B zero-padded to 128 columns (the bf16 forward's pos_enc copy)
+    on the LDS-DMA kernel updates only the first 63 columns of a dW slice (the skip layer's enc
+    columns at 256..318 of a 319-wide weight) -- against fp64 products of the bf16 operands --
+    and leaves the rest of C untouched."""
+    from aonerf import tiles
+    from aonerf.linalg import gemm
+
+    K, M = 193 * 300, 256
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = tiles.tile((torch.randn((K, M), device="cuda", generator=g) * 1e-3).to(torch.bfloat16))
+    X = torch.randn((K, 63), device="cuda", generator=g).to(torch.bfloat16)
+    Xp = torch.zeros((K, 128), device="cuda", dtype=torch.bfloat16)
+    Xp[:, :63] = X
+    C0 = torch.randn((M, 319), device="cuda", generator=g)
+    C = C0.clone()
+    gemm(C[:, 256:], A, tiles.tile(Xp), M, 128, K, lda=M, a_kc=False, ldb=128, b_kc=False,
+         ldc=319, accumulate=True, mma_bf16=True, a_tiled=True, b_tiled=True, n_store=63)
+    torch.cuda.synchronize()
+    a64 = bf16_round(tiles.untile(A, K).float().cpu())
+    want = C0.cpu().double().clone()
+    want[:, 256:] += a64.T @ X.cpu().double()
+    err = rel_err(C.cpu().numpy(), want.numpy())
+    print(f"bf16 n_store dW: max-rel err {err:.2e}")
+    assert err < 2e-5
+    assert torch.equal(C[:, :256], C0[:, :256])
+
+
+def test_bf16_forward_keeps_encodings(bf16_mode):
+    """aon_mlp_fwd_train_bf16's enc output: pos_enc(o + t d) (aon_cast_rays, fp32) rounded to
+    bf16 exactly, in the tiled layout, columns 63..127 zero; rows past N untouched."""
+    from aonerf import _lib as L
+    from aonerf import tiles, train
+
+    net = _make_trainable(0)
+    batch, u_c, u_f = c5_batch(n=300)
+    B, S = 300, 65
+    t = torch.sort(torch.rand((B, S), device="cuda") * 4 + 2, -1)[0].contiguous()
+    R = B * S
+    P = [(w.detach(), b.detach()) for w, b in train._mlp_params(net.coarse_mlp)]
+    enc_ref = torch.empty((R, 63), device="cuda")
+    L.call("aon_cast_rays", L.ptr(batch["rays_o"]), L.ptr(batch["rays_d"]), L.ptr(t), B, S, None,
+           0, None, 0, 10, L.ptr(enc_ref), L.stream())
+    NR = tiles.rows(R)
+    enc = torch.full((NR, 128), 7.0, device="cuda", dtype=torch.bfloat16)
+    raw = torch.empty((R, 4), device="cuda")
+    train._forward_level_fused(P, batch["rays_o"], batch["rays_d"], batch["viewdirs"], t, raw,
+                               None, None, bf16=True, enc=enc)
+    torch.cuda.synchronize()
+    got = tiles.untile(enc, R)
+    assert torch.equal(got[:, :63], enc_ref.to(torch.bfloat16))
+    assert not got[:, 63:].float().any()
