@@ -41,7 +41,7 @@ class AonGemmArgs(ctypes.Structure):
                 ("relu", c_int), ("accumulate", c_int), ("a_scale", c_float), ("b_scale", c_float),
                 ("k_splits", c_i64), ("rowsum", vp), ("a_amax", vp), ("mma_bf16", c_int),
                 ("a_bf16", c_int), ("b_bf16", c_int), ("a_tiled", c_int), ("b_tiled", c_int),
-                ("n_store", c_i64)]
+                ("n_store", c_i64), ("exact_fp32", c_int)]
 
 
 class AonAdamTensor(ctypes.Structure):
@@ -93,7 +93,7 @@ _SIGNATURES = {
     "aon_mlp_art_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp,
                                       vp, vp, vp]),
     "aon_mlp_art_fwd_train_bf16": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp,
-                                           vp, vp, vp, vp, c_int, vp]),
+                                           vp, vp, vp, vp, vp, c_int, vp]),
     "aon_composite_fwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp,
                                   vp, vp, vp, vp]),
     "aon_image_mse": (c_int, [vp, vp, c_i64, c_i64, vp, c_int, vp, vp, vp]),

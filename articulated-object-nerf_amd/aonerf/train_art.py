@@ -69,11 +69,12 @@ class _Geo:
 
 
 def _fold(W, b, c0, lat):
-    """b + W[:, c0:c0+n] . lat (the latent columns of a layer as a per-call bias)."""
+    """b + W[:, c0:c0+n] . lat (the latent columns of a layer as a per-call bias); in the bf16
+    mode on aon_gemm's exact-fp32 tiny-product path."""
     N, n = W.shape[0], lat.shape[1]
     out = torch.empty((1, N), device=W.device)
     gemm(out, lat, W[:, c0:], 1, N, n, lda=n, a_kc=True, ldb=W.stride(0), b_kc=True, ldc=N,
-         bias=b, a_scale=1.0, b_scale=W_SCALE)
+         bias=b, a_scale=1.0, b_scale=W_SCALE, exact_fp32=PRECISION == "bf16")
     return out.reshape(-1)
 
 
@@ -213,12 +214,13 @@ def _pack_bwd(P, dev, tag="", bf16=False):
 
 
 def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None,
-                         masks=None, bf16=False):
+                         masks=None, bf16=False, enc_bf=None):
     """_forward_level on the fused kernel (aon_mlp_art_fwd_train): raw (R x 4) and the kept
     activations (tiled, tiles.rows(R) rows each), plus the sample points and pos_enc(x')
     (row-major); ``masks`` ((16, tiles.rows(R), 8) int32) receives the ReLU' bits of hd0..3,
     h0..7, hv0..3 for the backward chain.  bf16: the bf16 mode (aon_mlp_art_fwd_train_bf16;
-    hd / h / bot / hv kept as torch.bfloat16)."""
+    hd / h / bot / hv kept as torch.bfloat16; ``enc_bf``, optional, (tiles.rows(R), 128)
+    bfloat16, receives pos_enc(x') tiled, columns 63.. zero)."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
     NR = tiles.rows(R)
@@ -238,7 +240,8 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
             L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h), L.ptr(bot),
             L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks))
     if bf16:
-        L.call("aon_mlp_art_fwd_train_bf16", *args, int(mixed), L.stream(dev))
+        L.call("aon_mlp_art_fwd_train_bf16", *args, L.ptr(enc_bf) if enc_bf is not None else None,
+               int(mixed), L.stream(dev))
     else:
         L.call("aon_mlp_art_fwd_train", *args, L.stream(dev))
     _train._rec(f"art_fwd_train{S}", e0, R)
@@ -353,12 +356,13 @@ def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, dra
 
 
 def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
-                          masks=None, h_tiled=True):
+                          masks=None, h_tiled=True, enc_bf=None):
     """_backward_level with every input-gradient product (and pos_enc's backward) in one fused
     kernel (aon_mlp_art_bwd); the weight gradients dW = dZ^T X, db = sum_rows dZ and the latent
     terms stay GEMMs.  ``masks``: the fused forward's ReLU' bits (built from the activations
     when None); h_tiled: hd / h / bot / hv in the fused forward's tiled layout (else
-    row-major); the chain's dzv / dbot / dz / dzd are tiled."""
+    row-major); the chain's dzv / dbot / dz / dzd are tiled.  enc_bf: the bf16 forward's tiled
+    128-column pos_enc(x') (the enc-column weight gradients then run on the LDS-DMA kernel)."""
     R, dev = xyz.shape[0], xyz.device
     bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
@@ -384,28 +388,32 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     gs, acts = GRAD_SCALE, ACT_SCALE
 
     def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True, chain_scale=True, a_t=True):
+        n_store = 0
+        if X is enc and bf16 and enc_bf is not None:  # the tiled bf16 copy, 63 of 128 columns
+            X, ldx, n_store, n_in = enc_bf, 128, n_in, 128
         # chain_scale: dY is in the chain's d raw domain (draw, view/trunk outputs): A rides at
         # the chain's own per-call scale from max |d raw| (the word it left in `work`); the
         # deformation branch (dL/dx' carries pos_enc's 2^9, rescaled per sample) keeps 2^10.
         # a_t: dY is one of the chain's tiled gradients; X is tiled when it is a kept activation.
         # bf16: one bf16 MFMA per product, no scales (bf16 has fp32's exponent range)
         dW = G[i][0]
-        b_t = h_tiled and X is not enc and X is not venc and X is not xyz
+        b_t = (h_tiled and X is not enc and X is not venc and X is not xyz) or X is enc_bf
         gemm(dW[:, col0:] if col0 else dW, dY, X, dW.shape[0], n_in, R, lda=ldy, a_kc=False,
              ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0),
              a_scale=1.0 if (chain_scale or bf16) else gs, b_scale=1.0 if bf16 else acts,
              rowsum=G[i][1] if bias else None,
              a_amax=work if (chain_scale and not bf16) else None, mma_bf16=bf16, a_tiled=a_t,
-             b_tiled=b_t)
+             b_tiled=b_t, n_store=n_store)
 
     def dlatent(i, col0, l, dl, accumulate):
+        # (bf16 mode: the exact-fp32 tiny-product path)
         dW, db = G[i]
         W = P[i][0]
         n_out, n = W.shape[0], l.shape[1]
         gemm(dW[:, col0:], db, l, n_out, n, 1, lda=1, a_kc=True, ldb=n, b_kc=False,
-             ldc=dW.stride(0), a_scale=gs, b_scale=1.0)
+             ldc=dW.stride(0), a_scale=gs, b_scale=1.0, exact_fp32=bf16)
         gemm(dl, db, W[:, col0:], 1, n, n_out, lda=n_out, a_kc=True, ldb=W.stride(0), b_kc=False,
-             ldc=n, accumulate=accumulate, a_scale=gs, b_scale=W_SCALE)
+             ldc=n, accumulate=accumulate, a_scale=gs, b_scale=W_SCALE, exact_fp32=bf16)
 
     dweight(RGB, draw, 4, hv[3], wc, wc, a_t=False)                       # rgb_layer
     for i in range(3, 0, -1):                                             # views_linear.i
@@ -453,11 +461,15 @@ class ArtRenderLevel(torch.autograd.Function):
         raw = torch.empty((R, 4), device=dev)
         noise = L.contig(noise) if noise is not None else None
         masks = None  # ReLU' bits for the fused backward chain (built there when None)
+        enc_bf = None  # the bf16 forward's tiled pos_enc(x') copy
         if FUSED_FORWARD and _fused_ok(geo):
             masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device=dev)
+            bf16 = PRECISION == "bf16"
+            enc_bf = (torch.empty((tiles.rows(R), 128), device=dev, dtype=torch.bfloat16)
+                      if bf16 else None)
             xyz, hd, enc, h, bot, hv = _forward_level_fused(
                 geo, P, lat, L.contig(rays_o), L.contig(rays_d), L.contig(viewdirs),
-                L.contig(t_vals), raw, noise, masks, bf16=PRECISION == "bf16")
+                L.contig(t_vals), raw, noise, masks, bf16=bf16, enc_bf=enc_bf)
         else:
             xyz = torch.empty((R, 3), device=dev)
             L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
@@ -472,6 +484,7 @@ class ArtRenderLevel(torch.autograd.Function):
                L.ptr(weights), L.ptr(depth), L.stream(dev))
         ctx.save_for_backward(rays_d, t_vals, xyz, enc, venc, raw, hd, h, bot, hv, *lat, *params)
         ctx.masks = masks
+        ctx.enc_bf = enc_bf if masks is not None else None
         ctx.h_tiled = masks is not None  # the fused forward keeps its tensors tiled
         ctx.meta = (geo, B, S, bool(white_bkgd), tuple(x.shape for x in (shape, app, art)))
         ctx.mark_non_differentiable(weights)
@@ -497,7 +510,7 @@ class ArtRenderLevel(torch.autograd.Function):
         dlat = tuple(torch.empty_like(x) for x in lat)
         if FUSED_BACKWARD and _fused_ok(geo):
             _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
-                                  ctx.masks, ctx.h_tiled)
+                                  ctx.masks, ctx.h_tiled, ctx.enc_bf)
         else:
             if ctx.h_tiled:  # the all-GEMM backward reads row-major fp32 activations
                 hd, h, hv = (torch.stack([tiles.untile(x, R).float() for x in t]) for t in (hd, h, hv))

@@ -1238,6 +1238,46 @@ __global__ __launch_bounds__(256) void k_gemm_segsum_bf16(Params p) {
   }
 }
 
+// ---- tiny fp32 products (the latent-code terms of the articulated step: per-call folded biases
+// b + W_l l, dW_l = db l^T, dl = db^T W_l -- M x N <= 64K outputs, K <= 1024): the 128 x 128
+// tiled kernel spent 17-27 us on each (a K pass one or two k-tiles deep, PF register sets and
+// split epilogues for a few hundred outputs).  Exact fp32 fmaf (the operand scales are powers
+// of two and cancel exactly).  K <= 16: one thread per output, k in order; longer K: one wave
+// per output, lane l summing k = l, l + 64, ... in order, then a fixed xor tree (deterministic).
+__device__ __forceinline__ void small_store(const Params& p, int64_t m, int64_t n, float v) {
+  float* c = p.C + m * p.ldc + n;
+  if (p.accumulate) v = __fadd_rn(*c, v);
+  if (p.bias) v = __fadd_rn(v, p.bias[n]);
+  *c = v;
+}
+__global__ __launch_bounds__(256) void k_gemm_small_f32(Params p, int a_kc, int b_kc) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= p.M * p.N) return;
+  const int64_t m = e / p.N, n = e - m * p.N;
+  float v = 0.f;
+  for (int64_t k = 0; k < p.K; ++k) {
+    const float a = a_kc ? p.A[m * p.lda + k] : p.A[k * p.lda + m];
+    const float b = b_kc ? p.B[n * p.ldb + k] : p.B[k * p.ldb + n];
+    v = fmaf(a, b, v);
+  }
+  small_store(p, m, n, v);
+}
+__global__ __launch_bounds__(256) void k_gemm_small_f32_wave(Params p, int a_kc, int b_kc) {
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per output
+  const int lane = threadIdx.x & 63;
+  if (e >= p.M * p.N) return;  // wave-uniform
+  const int64_t m = e / p.N, n = e - m * p.N;
+  float v = 0.f;
+  for (int64_t k = lane; k < p.K; k += 64) {
+    const float a = a_kc ? p.A[m * p.lda + k] : p.A[k * p.lda + m];
+    const float b = b_kc ? p.B[n * p.ldb + k] : p.B[k * p.ldb + n];
+    v = fmaf(a, b, v);
+  }
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) v = __fadd_rn(v, __shfl_xor(v, sh, 64));
+  if (lane == 0) small_store(p, m, n, v);
+}
+
 template <typename TA, bool BT>
 static void launch_skinny(const Params& p, dim3 grid, hipStream_t st) {
   const dim3 block((unsigned)(2 * p.N));  // 16 row phases x N / 8 column groups
@@ -1282,6 +1322,13 @@ static bool skinny_path(const aon_gemm_args* a) {
          (a->n_store == 0 || a->n_store == a->N);
 }
 
+// tiny fp32 products (k_gemm_small_f32)
+static bool small_path(const aon_gemm_args* a) {
+  return a->exact_fp32 && !a->mma_bf16 && a->M * a->N <= 65536 && a->K <= 1024 && !a->A2 && !a->mask && !a->relu &&
+         !a->rowsum && !a->a_amax && !a->a_tiled && !a->b_tiled && (a->b_kc || a->b_rdiv == 1) &&
+         !a->k_splits && (a->n_store == 0 || a->n_store == a->N);
+}
+
 // bf16 weight gradient against a per-ray B (rdiv > 1): k_gemm_segsum_bf16
 static bool segsum_path(const aon_gemm_args* a) {
   return a->mma_bf16 && !a->a_kc && !a->b_kc && a->b_rdiv > 1 && !a->b_tiled && a->M % 8 == 0 &&
@@ -1291,6 +1338,7 @@ static bool segsum_path(const aon_gemm_args* a) {
 
 static int64_t gemm_splits(const aon_gemm_args* a) {
   const int64_t tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
+  if (small_path(a)) return 1;
   // the segment-sum kernel: one chunk of 2048 / M rays (whole segments) per workgroup
   if (segsum_path(a)) {
     const int64_t rays = (a->K + a->b_rdiv - 1) / a->b_rdiv, rb = 2048 / a->M;
@@ -1352,6 +1400,9 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   AON_REQUIRE(!a->b_tiled || (!a->b_kc && a->b_rdiv == 1 && a->ldb == a->N && a->N % 16 == 0),
               "b_tiled: reduction-major B of width ldb = N (a multiple of 16), b_rdiv = 1");
   AON_REQUIRE(a->n_store >= 0 && a->n_store <= a->N, "n_store must be in [0, N]");
+  AON_REQUIRE(!a->exact_fp32 || small_path(a),
+              "exact_fp32: tiny fp32 products only (M N <= 65536, K <= 1024, no A2 / mask / relu / "
+              "rowsum / a_amax / tiled operands / k_splits / n_store)");
   AON_REQUIRE(a->n_store == 0 || a->n_store == a->N || bf16_copy_path(a),
               "n_store < N: the bf16 LDS-DMA weight-gradient path only (both operands bf16, "
               "M and N multiples of 128)");
@@ -1402,6 +1453,15 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   const bool va = aligned16(a->A) && a->lda % 4 == 0 && (!a->A2 || a->K1 % 4 == 0);
   const bool vb = aligned16(a->B) && a->ldb % 4 == 0;
   hipStream_t st = (hipStream_t)stream;
+  if (small_path(a)) {
+    if (a->K <= 16)
+      hipLaunchKernelGGL(k_gemm_small_f32, grid_for(a->M * a->N, 256, 1 << 20), 256, 0, st, p,
+                         a->a_kc, a->b_kc);
+    else
+      hipLaunchKernelGGL(k_gemm_small_f32_wave, grid_for(a->M * a->N, 4, 1 << 20), 256, 0, st, p,
+                         a->a_kc, a->b_kc);
+    return launch_status(__func__);
+  }
   if (bf) {
     // element size of each operand: 8-B (bf16) or 16-B (fp32) runs of 4 rows
     const bool va16 = a->a_bf16 ? (reinterpret_cast<uintptr_t>(a->A) & 7) == 0 && a->lda % 4 == 0 : va;

@@ -130,15 +130,17 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     float q3[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) q3[q] = __fadd_rn(__shfl(dlt[c][q], j, 64), px[c][q]);
-    float ev[2][8];
+    float fv[2][8], ev[2][8];
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float f = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10);
         if (STORE && rows[c] < N && 32 * k + 8 * g + e < 63) ts.enc[63 * rows[c] + 32 * k + 8 * g + e] = f;
+        fv[k][e] = f;
         ev[k][e] = f * act_scale<BFM>();
       }
+    if (STORE && PREC != 0 && ts.enc_bf && rows[c] < N) store_enc_bf(ts.enc_bf, rows[c], g, fv);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       split8<BFM>(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
@@ -289,7 +291,7 @@ static int art_fwd_train(const void* packed, const float* rays_o, const float* r
                          const float* viewdirs, const float* t, int64_t B, int S,
                          const float* noise, float* hd, float* h, float* bot, float* hv,
                          float* enc, float* xyz, float* raw, uint32_t* masks, aon_stream_t stream,
-                         int prec) {
+                         int prec, __bf16* enc_bf = nullptr) {
   AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && raw, "null pointer");
   AON_REQUIRE(hd && h && bot && hv && enc && xyz && masks, "null activation buffer");
   AON_REQUIRE(aligned16(masks), "masks must be 16-byte aligned");
@@ -306,7 +308,7 @@ static int art_fwd_train(const void* packed, const float* rays_o, const float* r
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
-  const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise, reinterpret_cast<uint2*>(masks)};
+  const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise, reinterpret_cast<uint2*>(masks), enc_bf};
   if (prec == 2)
     hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 2>), (unsigned)grid, G::kThreads, 0,
                        (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
@@ -335,11 +337,12 @@ extern "C" int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_
                                           const float* rays_d, const float* viewdirs,
                                           const float* t, int64_t B, int S, const float* noise,
                                           void* hd, void* h, void* bot, void* hv, float* enc,
-                                          float* xyz, float* raw, uint32_t* masks, int mixed,
-                                          aon_stream_t stream) {
+                                          float* xyz, float* raw, uint32_t* masks, void* enc_bf,
+                                          int mixed, aon_stream_t stream) {
+  AON_REQUIRE(aligned16(enc_bf), "enc_bf must be 16-byte aligned");
   return art_fwd_train(packed, rays_o, rays_d, viewdirs, t, B, S, noise, static_cast<float*>(hd),
                        static_cast<float*>(h), static_cast<float*>(bot), static_cast<float*>(hv),
-                       enc, xyz, raw, masks, stream, mixed ? 2 : 1);
+                       enc, xyz, raw, masks, stream, mixed ? 2 : 1, static_cast<__bf16*>(enc_bf));
 }
 
 extern "C" int aon_mlp_art_fwd_points(const void* packed, const float* pos,

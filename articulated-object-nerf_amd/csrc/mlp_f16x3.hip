@@ -171,25 +171,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
         vv[e] = f < 27 ? cd[f] : 0.f;
       }
     }
-    // bf16 training mode: pos_enc(x) kept for the weight gradients of pts_linears.0 and the skip
-    // layer's enc columns, bf16 in the tiled layout, 128 columns (63..127 zero) -- whole
-    // 128-column tiles for the LDS-DMA dW kernel (aon_gemm n_store); lane group g's 8 features
-    // 32 k + 8 g .. + 7 are one 16-B run of tile 2 k + g / 2, and k = 2, 3 write the zero tiles
-    if (STORE && BF && ts.enc_bf && rows[c] < N) {
-      __bf16* eb = ts.enc_bf + act_base(rows[c], 128, 0) + 8 * (g & 1) + 256 * (g >> 1);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        if (k < 2) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bf2 pr = {static_cast<__bf16>(ev[k][2 * e]), static_cast<__bf16>(ev[k][2 * e + 1])};
-            w[e] = __builtin_bit_cast(uint32_t, pr);
-          }
-        }
-        *reinterpret_cast<uint4*>(eb + 512 * k) = uint4{w[0], w[1], w[2], w[3]};
-      }
-    }
+    if (STORE && BF && ts.enc_bf && rows[c] < N) store_enc_bf(ts.enc_bf, rows[c], g, ev);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
 #pragma unroll

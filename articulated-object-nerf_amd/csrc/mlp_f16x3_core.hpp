@@ -230,6 +230,28 @@ __device__ __forceinline__ int64_t mask_index(int64_t row, int g) {
 }
 constexpr int kTileStride = AON_TILED ? 256 : 16;  // elements between output tiles of one lane
 
+// bf16 training modes: pos_enc(x) kept for the weight gradients of pts_linears.0 and the skip
+// layer's enc columns, bf16 in the tiled layout (act_base) with 128 columns (63..127 zero) --
+// whole 128-column tiles for the LDS-DMA dW kernel (aon_gemm n_store).  Lane group g holds
+// features 32 k + 8 g .. + 7 of its sample (true scale): one 16-B run of tile 2 k + g / 2; the
+// k = 2, 3 runs are the zero tiles.
+__device__ __forceinline__ void store_enc_bf(__bf16* base, int64_t row, int g,
+                                             const float (&fv)[2][8]) {
+  __bf16* eb = base + act_base(row, 128, 0) + 8 * (g & 1) + 256 * (g >> 1);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (k < 2) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf2 pr = {static_cast<__bf16>(fv[k][2 * e]), static_cast<__bf16>(fv[k][2 * e + 1])};
+        w[e] = __builtin_bit_cast(uint32_t, pr);
+      }
+    }
+    *reinterpret_cast<uint4*>(eb + 512 * k) = uint4{w[0], w[1], w[2], w[3]};
+  }
+}
+
 // pairs (r0 = 0, 2) of a tile meet in one 4-value store
 template <int NCOL, typename T>
 struct Store4 {

@@ -327,6 +327,7 @@ struct TrainStoreArt {
   float* xyz;   // (N, 3) the sample points (deformation input)
   const float* noise;  // (N) added to raw_sigma, or nullptr
   uint2* masks;        // (16, N, 4) ReLU' bits of hd0..3, h0..7, hv0..3 (RowStoreBits)
+  __bf16* enc_bf;      // bf16 modes, optional: pos_enc(x') tiled (N, 128), columns 63.. zero
 };
 
 // fp16x3 path (mlp_f16x3.hip)

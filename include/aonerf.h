@@ -290,13 +290,15 @@ int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* 
  * xyz / raw / masks as above.  mixed != 0: packed by aon_mlp_art_pack_bf16 (a mixed stream in
  * the same buffer size: the deformation MLP stays fp16x3 -- x' feeds sin(2^9 x') -- the trunk,
  * heads and view branch are bf16), one bf16 MFMA per product past the deformation head;
- * mixed == 0: packed by aon_mlp_art_pack, fp16x3 numerics throughout (only the stores bf16). */
+ * mixed == 0: packed by aon_mlp_art_pack, fp16x3 numerics throughout (only the stores bf16).
+ * enc_bf (optional, NULL: not kept): pos_enc(x') as bf16, tiled (NR, 128), columns 63..127 zero
+ * (as aon_mlp_fwd_train_bf16's enc). */
 int aon_mlp_art_pack_bf16(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
 int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_o, const float* rays_d,
                                const float* viewdirs, const float* t, int64_t B, int S,
                                const float* noise, void* hd, void* h, void* bot, void* hv,
-                               float* enc, float* xyz, float* raw, uint32_t* masks, int mixed,
-                               aon_stream_t stream);
+                               float* enc, float* xyz, float* raw, uint32_t* masks,
+                               void* enc_bf, int mixed, aon_stream_t stream);
 
 /* Backward chain of one articulated level (autograd of model_autodecoder.py:168-239): from
  * dL/d raw (N, 4), the ReLU' bits (16, N, 4) of hd0..3, h0..7, hv0..3 and pos_enc(x') (enc) kept
@@ -401,6 +403,11 @@ typedef struct aon_gemm_args {
    * pos_enc copy, 63 -> 128 columns) updates only the real columns of dW; n_store < N on the
    * bf16 LDS-DMA path only (both operands bf16, M and N multiples of 128) */
   int64_t n_store;
+  /* exact_fp32 = 1: compute in exact fp32 fmaf, k in order (deterministic) instead of the fp16x3
+   * MFMA split -- tiny products only (M N <= 65536, K <= 1024, no A2 / mask / relu / rowsum /
+   * a_amax / tiled operands): the bf16 training mode's latent-code terms, which the 128 x 128
+   * tiled kernel ran at 17-27 us each */
+  int exact_fp32;
 } aon_gemm_args;
 
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);
