@@ -194,7 +194,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       }
     }
   }
-  range_report(bias_g + Net::kBiasFloats, x.ovf | y.ovf | enc.ovf | venc.ovf | din.ovf);
+  range_report(bias_g + Net::kBiasFloats, ovf_of(x) | ovf_of(y) | enc.ovf | venc.ovf | din.ovf);
 }
 
 }  // namespace mlp

@@ -15,6 +15,11 @@
 // arguments (x' 2^d and x' 2^d + pi/2f), summed over degrees -- and the four lane groups of a
 // sample are reduced with two shuffles.  dL/dx' then re-enters fp16 at a per-sample power-of-two
 // scale (it carries the 2^9 factors of pos_enc's top degree).
+// the round-2 per-pair range test (AON_GUARD_PK 0): with the deferred packed test this
+// 256-VGPR kernel spills
+#ifndef AON_GUARD_PK
+#define AON_GUARD_PK 0
+#endif
 #include "mlp_f16x3_core.hpp"
 
 namespace aon {
@@ -225,7 +230,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
                              mask_bits(a.masks + 1 * ms, dzd + 1 * ws, 128, rows, N, g, invd));
   // (the last layer's outputs are only stored, the enc-column layers' fragments are consumed in
   // their epilogues: neither fp16 split is used, so neither is range-checked)
-  const uint64_t used_ovf = x.ovf | y.ovf | drgb.ovf | dsig.ovf | ddx.ovf;
+  const uint64_t used_ovf = ovf_of(x) | ovf_of(y) | drgb.ovf | dsig.ovf | ddx.ovf;
   layer_h<Net, AB_D1, false>(fp, y, none, x, bias_l, g,
                              mask_bits(a.masks + 0 * ms, dzd, 128, rows, N, g, invd));
   range_report(bias_g + Net::kBiasFloats, used_ovf);

@@ -149,7 +149,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   layer_h<Net, B_2, false>(fp, y, none, x, bias_l, g,
                            mask_bits(a.masks + 1 * ms, dz + 1 * hs, 256, rows, N, g, inv));
   // (the last layer's outputs are only stored: its fp16 split is unused, so not range-checked)
-  const uint64_t used_ovf = x.ovf | y.ovf | drgb.ovf | dsig.ovf;
+  const uint64_t used_ovf = ovf_of(x) | ovf_of(y) | drgb.ovf | dsig.ovf;
   layer_h<Net, B_1, false>(fp, x, none, y, bias_l, g,
                            mask_bits(a.masks + 0 * ms, dz, 256, rows, N, g, inv));
   range_report(bias_g + Net::kBiasFloats, used_ovf);

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     FragPipe<WP, AON_PREFETCH, 0, BF> fp(p);
     vanilla_layers<NCOL, STORE, T>(fp, enc, venc, x, y, stash, bias_s, g, wave, rows, N, act, raw, ts);
   }
-  range_report(bias_g + kBiasFloats, x.ovf | y.ovf | enc.ovf | venc.ovf);
+  range_report(bias_g + kBiasFloats, ovf_of(x) | ovf_of(y) | enc.ovf | venc.ovf);
 }
 
 // ---- packing: torch [out][ldw] fp32 -> hi/lo fp16 blocks (+ biases at activation scale), for

@@ -167,11 +167,28 @@ struct FragPipe {
   }
 };
 
+#ifndef AON_GUARD_PK
+#define AON_GUARD_PK 1  // 0: A/B build with the round-2 per-pair fp32 range test in the epilogue
+#endif
 template <int N, int NCOL>
 struct Frag {
   h8 hi[N][NCOL], lo[N][NCOL];
   uint64_t ovf = 0;  // lanes that split a value out of fp16 range into this set (range guard)
+  // AON_GUARD_PK: the layer epilogues' test, deferred -- per lane, the packed i16 max of the
+  // |fp16 hi| bit patterns they produced (a value past the fp16 range rounds to inf, 0x7C00,
+  // and a NaN is above it), reduced to a ballot once, by ovf_of, at the kernel's range report
+  uint32_t m16 = 0;
 };
+typedef short s2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2v, a),
+                                                                __builtin_bit_cast(s2v, b)));
+}
+template <int N, int NCOL>
+__device__ __forceinline__ uint64_t ovf_of(const Frag<N, NCOL>& f) {
+  const bool bad = (f.m16 & 0x7FFFu) >= 0x7C00u || ((f.m16 >> 16) & 0x7FFFu) >= 0x7C00u;
+  return f.ovf | __builtin_amdgcn_ballot_w64(bad);
+}
 
 // Epilogue policies of layer_h.  begin_pair(pr) runs at the start of output pair pr (before its
 // MFMAs), post() maps a finished value (after the optional ReLU), put() sees the pair's values 2
@@ -448,7 +465,9 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
       out.hi[pr][c] = __builtin_bit_cast(h8, w);
       continue;
     }
+#if !(AON_GUARD_PK && AON_F16X3_V2 && AON_FMA_MIX)
     or_ballot(out.ovf, fmaxf(fabsf(vv[0]), fabsf(vv[1])) > kF16Max);
+#endif
     st.put(pr, uu, r0, c, vv[0], vv[1]);
 #if AON_F16X3_V2 && AON_FMA_MIX
     // hi pair by one v_cvt_pk_f16_f32; lo_e = v_e - hi_e by v_fma_mix_f32 reading the fp16 half
@@ -456,6 +475,12 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     const h2 hp = {static_cast<_Float16>(vv[0]), static_cast<_Float16>(vv[1])};
     const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
+#if AON_GUARD_PK
+    // range guard: one packed max per pair (ReLU outputs are >= 0: a -0 is negative as i16 and
+    // drops out; otherwise the sign bits are cleared first)
+    out.m16 = pk_max_i16(out.m16, RELU ? hu : (hu & 0x7FFF7FFFu));
+    asm("" : "+v"(out.m16));  // pinned per step, as the ballot chain's SGPRs (or_ballot)
+#endif
     float d0, d1;
     asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(vv[0]));
     asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(vv[1]));
