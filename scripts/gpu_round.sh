@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>: run, log, stop the session on crash/
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q -s -p no:cacheprovider
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 1100 python -u -m pytest tests -m gpu -q -s -p no:cacheprovider --timeout 300 --timeout-method thread
 step bench 600 python bench.py "$@"
 tail -1 "$OUT/bench.log" > "$OUT/bench.json"
 if [ "${EXTRA:-0}" = 1 ]; then

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a scripts/gpu_round.sh session into profiles/<name>/.
 
-    python scripts/pmc_summary.py gpurun_out/r01a profiles/r01_fp32 [--precision fp32]
+    python scripts/pmc_summary.py gpurun_out/r01a profiles/r01_fp32 [--precision fp32] (default f16x3, the headline)
 
 Copies the rocprofv3 kernel stats, and turns the FETCH_SIZE / WRITE_SIZE passes into per-launch
 HBM bytes per kernel (MI355X_MICROARCH.md "HBM": both counters in KiB; gfx950 FETCH_SIZE counts
@@ -28,7 +28,7 @@ def load(path, counter):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    precision = sys.argv[sys.argv.index("--precision") + 1] if "--precision" in sys.argv else "fp32"
+    precision = sys.argv[sys.argv.index("--precision") + 1] if "--precision" in sys.argv else "f16x3"
     os.makedirs(dst, exist_ok=True)
     for name in ("kt/run_kernel_stats.csv", "bench.json", "pytest_gpu.log"):
         p = os.path.join(src, name)
@@ -59,13 +59,15 @@ def main():
                      "hbm_bytes_per_launch": hbm, "duration_s_profiled": d,
                      "hbm_gbs": hbm / d / 1e9})
     json.dump(rows, open(os.path.join(dst, "pmc_hbm.json"), "w"), indent=1)
-    mlp = [r for r in rows if "mlp_fwd" in r["kernel"]]
+    tag = "mlp_fwd_f16x3<0, 1, false" if precision == "f16x3" else "mlp_fwd_f32"
+    mlp = [r for r in rows if tag in r["kernel"]]
     if mlp:
         fine = max(mlp, key=lambda r: r["grid"])
         json.dump({"precision": precision, "world": 1, "fine_mlp_hbm_bytes": fine["hbm_bytes_per_launch"],
                    "source": dst, "kernel": fine["kernel"], "grid": fine["grid"],
                    "note": "(2*FETCH_SIZE + WRITE_SIZE) KiB per launch, separate --pmc passes"},
-                  open(os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json"), "w"), indent=1)
+                  open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "profiles", "pmc_traffic.json"), "w"), indent=1)
     for r in rows:
         print(f"{r['kernel'][:40]:40s} grid {r['grid']:>10d}  {r['hbm_bytes_per_launch'] / 1e6:10.1f} MB"
               f"  {r['hbm_gbs']:8.1f} GB/s")
