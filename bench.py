@@ -318,8 +318,10 @@ TRAIN_BYTES = {"fwd_train": 4 + 16 + 4 * 2432 + 288, "bwd_chain": 16 + 288 + 4 *
 TRAIN_FLOP = {"fwd_train": 2 * MAC_PER_SAMPLE, "bwd_chain": 2 * (MAC_PER_SAMPLE - 256 * 63 - 128 * 27),
               "dweight": 2 * MAC_PER_SAMPLE}
 # bf16 mode: the kept activations and gradients are 2 B (encodings, d raw and masks unchanged)
-TRAIN_BYTES_BF16 = {"fwd_train": 4 + 16 + 2 * 2432 + 288, "bwd_chain": 16 + 288 + 2 * 2432,
-                    "dweight": 2 * (2432 + 2432) + 4 * (63 + 27)}
+# (round 3: the forward also keeps pos_enc(x) as bf16, tiled, 128 columns, read by the two
+# enc-column weight gradients)
+TRAIN_BYTES_BF16 = {"fwd_train": 4 + 16 + 2 * 2432 + 288 + 2 * 128, "bwd_chain": 16 + 288 + 2 * 2432,
+                    "dweight": 2 * (2432 + 2432) + 2 * 2 * 128 + 4 * 27}
 # articulated level (NeRF_AE_Art, model_autodecoder.py:168-239), bytes per sample: the fused
 # forward writes raw (16) + 3,328 activations (hd 4x128, h 8x256, bot 256, hv 4x128) + pos_enc(x')
 # (63) + the points (3) + ReLU' bits (16 x 32) and reads t; the chain reads d raw + bits + enc and
@@ -329,9 +331,9 @@ ART_TRAIN_BYTES = {"art_fwd_train": 4 + 16 + 4 * (3328 + 63 + 3) + 512,
                    "art_bwd_chain": 16 + 512 + 4 * 63 + 4 * (3328 + 3),
                    "art_dweight": 4 * (3335 + 3484)}
 # bf16 mode: the kept activations and chain gradients 2 B (enc, points, d raw, dL/dx' fp32)
-ART_TRAIN_BYTES_BF16 = {"art_fwd_train": 4 + 16 + 2 * 3328 + 4 * (63 + 3) + 512,
+ART_TRAIN_BYTES_BF16 = {"art_fwd_train": 4 + 16 + 2 * 3328 + 4 * (63 + 3) + 512 + 2 * 128,
                         "art_bwd_chain": 16 + 512 + 4 * 63 + 2 * 3328 + 4 * 3,
-                        "art_dweight": 2 * (3328 + 3328) + 4 * (3 + 4 + 2 * 63 + 3 + 27)}
+                        "art_dweight": 2 * (3328 + 3328) + 2 * 2 * 128 + 4 * (3 + 4 + 3 + 27)}
 ART_TRAIN_FLOP = {"art_fwd_train": 2 * 714_880, "art_bwd_chain": 2 * (714_880 - 3 * 128 - 128 * 27),
                   "art_dweight": 2 * 714_880}
 # dense MFMA peak in algorithmic FLOP/s per training precision: f16x3 issues 3 fp16 products
