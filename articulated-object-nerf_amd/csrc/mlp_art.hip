@@ -140,7 +140,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
         fv[k][e] = f;
         ev[k][e] = f * act_scale<BFM>();
       }
-    if (STORE && PREC != 0 && ts.enc_bf && rows[c] < N) store_enc_bf(ts.enc_bf, rows[c], g, fv);
+    if (STORE && PREC != 0 && ts.enc_bf && keep_row(rows[c], N)) store_enc_bf(ts.enc_bf, rows[c], g, fv);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       split8<BFM>(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);

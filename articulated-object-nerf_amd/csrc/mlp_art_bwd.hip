@@ -165,7 +165,8 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   // d bottleneck = W_view0[:, :256]^T dZ_view0 (linear layer: no mask)
   {
     RowStore<NCOL, T> st;
-    st.rowp[0] = row < N ? reinterpret_cast<T*>(a.dbot) + act_base(row, 256, g) : nullptr;
+    st.ok[0] = keep_row(row, N);
+    st.rowp[0] = reinterpret_cast<T*>(a.dbot) + act_base(row, 256, g);
     st.s = inv;
     layer_h<Net, AB_V0, false>(fp, y, none, x, bias_l, g, st);
   }

@@ -126,7 +126,8 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   // d bottleneck = W_view[:, :256]^T dZ_view (linear layer: no mask)
   {
     RowStore<NCOL, T> st;
-    st.rowp[0] = rows[0] < N ? dzb + act_base(rows[0], 256, g) : nullptr;
+    st.ok[0] = keep_row(rows[0], N);
+    st.rowp[0] = dzb + act_base(rows[0], 256, g);
     st.s = inv;
     layer_h<Net, B_VIEW, false>(fp, x, none, y, bias_l, g, st);
   }

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
         vv[e] = f < 27 ? cd[f] : 0.f;
       }
     }
-    if (STORE && BF && ts.enc_bf && rows[c] < N) store_enc_bf(ts.enc_bf, rows[c], g, ev);
+    if (STORE && BF && ts.enc_bf && keep_row(rows[c], N)) store_enc_bf(ts.enc_bf, rows[c], g, ev);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
 #pragma unroll

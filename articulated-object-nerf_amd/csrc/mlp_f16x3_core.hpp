@@ -246,6 +246,22 @@ __device__ __forceinline__ int64_t mask_index(int64_t row, int g) {
   return AON_TILED ? (row & ~int64_t(15)) * 4 + 16 * g + (row & 15) : row * 4 + g;
 }
 constexpr int kTileStride = AON_TILED ? 256 : 16;  // elements between output tiles of one lane
+// Whether a sample's kept values are stored.  Tiled: the whole 16-row tile is stored when it
+// starts below N -- the kept tensors hold act_rows(N) rows, so its rows past N land in the
+// padding (never read: the weight-gradient kernels stop at row N) -- and the test is
+// wave-uniform (readfirstlane of the tile's first row), so every store of the epilogues branches
+// on SCC instead of masking EXEC around itself (s_and_saveexec / s_cbranch_execz / s_or per
+// store).  Row-major (A/B build): row < N.
+__device__ __forceinline__ bool keep_row(int64_t row, int64_t N) {
+#if AON_TILED
+  const uint64_t t = static_cast<uint64_t>(row & ~int64_t(15));
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(t));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(t >> 32));
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo) < N;
+#else
+  return row < N;
+#endif
+}
 
 // bf16 training modes: pos_enc(x) kept for the weight gradients of pts_linears.0 and the skip
 // layer's enc columns, bf16 in the tiled layout (act_base) with 128 columns (63..127 zero) --
@@ -272,19 +288,20 @@ __device__ __forceinline__ void store_enc_bf(__bf16* base, int64_t row, int g,
 // pairs (r0 = 0, 2) of a tile meet in one 4-value store
 template <int NCOL, typename T>
 struct Store4 {
+  bool ok[NCOL];  // keep_row of each column's sample (wave-uniform when tiled)
   mutable float pend[NCOL][2];
   __device__ __forceinline__ void emit(T* rowp, int pr, int uu, int r0, int c, float v0,
                                        float v1) const {
     // fp32: one 8-B store per part (a lane's 16-B pair store measured slower); bf16: the two
     // parts of a tile row meet in one 8-B store (4-B stores: 1.73 -> 1.51 ms forward)
     if (std::is_same<T, float>::value) {
-      if (rowp) store2(rowp + kTileStride * (2 * pr + uu) + r0, v0, v1);
+      if (ok[c]) store2(rowp + kTileStride * (2 * pr + uu) + r0, v0, v1);
       return;
     }
     if (r0 == 0) {
       pend[c][0] = v0;
       pend[c][1] = v1;
-    } else if (rowp) {
+    } else if (ok[c]) {
       store4(rowp + kTileStride * (2 * pr + uu), pend[c][0], pend[c][1], v0, v1);
     }
   }
@@ -293,13 +310,13 @@ struct Store4 {
   __device__ __forceinline__ void emit_bf(T* rowp, int pr, int uu, int r0, int c, uint32_t pk) const {
     static_assert(std::is_same<T, __bf16>::value, "bf16 layers keep bf16 activations");
     if (r0 == 0) pendw[c] = pk;
-    else if (rowp) *reinterpret_cast<uint2*>(rowp + kTileStride * (2 * pr + uu)) = uint2{pendw[c], pk};
+    else if (ok[c]) *reinterpret_cast<uint2*>(rowp + kTileStride * (2 * pr + uu)) = uint2{pendw[c], pk};
   }
 };
 
 template <int NCOL, typename T = float>
 struct RowStore : Store4<NCOL, T> {
-  T* rowp[NCOL];  // act_base(row) of each column's sample, nullptr when row >= N
+  T* rowp[NCOL];  // act_base(row) of each column's sample (stored when ok)
   float s;        // to true scale (a power of two: exact)
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
@@ -318,7 +335,7 @@ struct RowStore : Store4<NCOL, T> {
 // so nothing is carried across pairs.
 template <int NCOL, typename T = float>
 struct RowStoreBits : RowStore<NCOL, T> {
-  uint8_t* mrow[NCOL];  // bytes of word (row, g), nullptr when row >= N
+  uint8_t* mrow[NCOL];  // bytes of word (row, g) (stored when ok)
   bool narrow;          // 4-pair (128-wide) layer: bytes 4..7 of the word are written as 0
   mutable uint32_t b[NCOL];  // the current pair's 8 bits (byte pr of the word)
   __device__ __forceinline__ void put_bf(int pr, int uu, int r0, int c, float v0, float v1,
@@ -334,7 +351,7 @@ struct RowStoreBits : RowStore<NCOL, T> {
     const uint32_t m = (v0 > 0.0f ? 1u : 0u) | (v1 > 0.0f ? 2u : 0u);  // v: post-ReLU, s > 0
     const int bit = 4 * uu + r0;  // within the pair's byte (compile-time after unrolling)
     b[c] = bit == 0 ? m : (b[c] | (m << bit));
-    if (uu == 1 && r0 == 2 && mrow[c]) {
+    if (uu == 1 && r0 == 2 && this->ok[c]) {
       mrow[c][pr] = static_cast<uint8_t>(b[c]);
       if (narrow) mrow[c][pr + 4] = 0;
     }
@@ -345,14 +362,14 @@ struct RowStoreBits : RowStore<NCOL, T> {
 // activations): the layer's word is loaded when its first pair starts.
 template <int NCOL, typename T = float>
 struct MaskBits : Store4<NCOL, T> {
-  const uint2* mrow[NCOL];  // masks + row * 4 + g, nullptr when row >= N
-  T* rowp[NCOL];            // out + row * ld + 4 g, nullptr when row >= N
+  const uint2* mrow[NCOL];  // masks + row * 4 + g (read and stored when ok)
+  T* rowp[NCOL];            // out + row * ld + 4 g
   float s;
   mutable uint2 m[NCOL];
   __device__ __forceinline__ void begin_pair(int pr) const {
     if (pr == 0) {
 #pragma unroll
-      for (int c = 0; c < NCOL; ++c) m[c] = mrow[c] ? *mrow[c] : uint2{0u, 0u};
+      for (int c = 0; c < NCOL; ++c) m[c] = this->ok[c] ? *mrow[c] : uint2{0u, 0u};
     }
   }
   __device__ __forceinline__ float post(int pr, int uu, int r, int c, float v) const {
@@ -375,9 +392,10 @@ __device__ __forceinline__ MaskBits<NCOL, T> mask_bits(const uint2* mbase, T* ob
   MaskBits<NCOL, T> mb;
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
-    const bool ok = rows[c] < N;
-    mb.mrow[c] = ok ? mbase + mask_index(rows[c], g) : nullptr;
-    mb.rowp[c] = ok ? obase + act_base(rows[c], ld, g) : nullptr;
+    const bool ok = keep_row(rows[c], N);
+    mb.ok[c] = ok;
+    mb.mrow[c] = mbase + mask_index(rows[c], g);
+    mb.rowp[c] = obase + act_base(rows[c], ld, g);
   }
   mb.s = s;
   return mb;
@@ -402,7 +420,10 @@ struct StorePick<true, NCOL, T> {
                                                            int g) {
     RowStore<NCOL, T> r;
 #pragma unroll
-    for (int c = 0; c < NCOL; ++c) r.rowp[c] = rows[c] < N ? base + act_base(rows[c], ld, g) : nullptr;
+    for (int c = 0; c < NCOL; ++c) {
+      r.ok[c] = keep_row(rows[c], N);
+      r.rowp[c] = base + act_base(rows[c], ld, g);
+    }
     r.s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;
     return r;
   }
@@ -414,7 +435,7 @@ struct StorePick<true, NCOL, T> {
     static_cast<RowStore<NCOL, T>&>(r) = make(base, ld, rows, N, g);
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
-      r.mrow[c] = rows[c] < N ? reinterpret_cast<uint8_t*>(mbase + mask_index(rows[c], g)) : nullptr;
+      r.mrow[c] = reinterpret_cast<uint8_t*>(mbase + mask_index(rows[c], g));
       r.b[c] = 0u;
     }
     r.narrow = ld == 128;
