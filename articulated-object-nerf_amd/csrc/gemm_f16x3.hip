@@ -1096,6 +1096,197 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_dma(Params p) {
     }
 }
 
+// ---- fp16x3 weight gradients on the LDS-DMA ring (fp32 operands, both reduction-major):
+// k_gemm_f16x3<false, false> staged each k-tile through registers (global loads -> transpose ->
+// split -> LDS), one tile ahead, and ran the fine level's 256 x 256 x 790k products at ~3 TB/s
+// (0.38 of HBM): like the bf16 kernel before its DMA rewrite, too few bytes in flight for the
+// HBM latency.  Here global_load_lds_dwordx4 copies each operand's [32 k][128 col] fp32 image
+// into a DNBF-deep ring (DNBF - 1 k-tiles in flight per workgroup); once a tile has landed every
+// thread reads ITS 4 x 4 block of it from LDS -- the same block the register loader held -- and
+// runs the same row sums, split and [row][k] hi / lo plane stores (TileLoad::add_rows / store),
+// and the MFMA loop reads the planes exactly as k_gemm_f16x3: every value, every product and
+// every sum in the same order, so the result is bit-identical to the register-staged kernel.
+// Two barriers per k-tile (tile landed + previous MFMAs done; planes written).  LDS: ring
+// DNBF x 32 KB + one 40-KB plane stage -- one workgroup per CU where the register-staged kernel
+// runs two, and that costs more than the deeper ring gains: 0.68-0.71 ms (DNBF 2 / 3) against
+// 0.57-0.59 ms for the fine product, same sha (profiles/r03/ab_gemm_f16).  Off by default
+// (AON_GEMM_F16_DMA = 1 selects it for A/B).
+#ifndef AON_GEMM_F16_DNB
+#define AON_GEMM_F16_DNB 3
+#endif
+constexpr int DNBF = AON_GEMM_F16_DNB;
+constexpr int F32_IMG = BK * BM * 4;  // bytes of one operand's [32 k][128 col] fp32 image
+
+// one operand's copies of a k-tile: wave w, copy c (0..3) fills image rows 8 w + 2 c + lane / 32,
+// 16-B chunk lane % 32 (4 columns)
+struct DmaOperandF32 {
+  const char* gbase;  // byte address of k-tile 0's (k row 0, column col0) origin, kbeg applied
+  int64_t tstep;      // bytes between k-tiles
+  uint32_t voff[4];   // per-lane byte offset of copy c within a k-tile
+  __device__ __forceinline__ DmaOperandF32(const float* p, int64_t ld, int64_t col0, int64_t kbeg,
+                                           int wave, int lane, bool tiled) {
+    gbase = reinterpret_cast<const char*>(p) + 4 * (kbeg * ld + (tiled ? 16 * col0 : col0));
+    tstep = 4 * BK * ld;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int r = 8 * wave + 2 * c + (lane >> 5), col = 4 * (lane & 31);
+      const int64_t e = tiled ? (int64_t)(r & 16) * ld + 256 * (col >> 4) + 16 * (r & 15) + (col & 15)
+                              : (int64_t)r * ld + col;
+      voff[c] = static_cast<uint32_t>(4 * e);
+    }
+  }
+  __device__ __forceinline__ void issue(uint32_t img, int wave, int kt) const {
+    const char* g = gbase + kt * tstep;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane(img + 512u * (8 * wave + 2 * c));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :
+                   : "s"(m0), "v"(voff[c]), "s"(g)
+                   : "memory", "m0");
+#pragma clang diagnostic pop
+    }
+  }
+  // the ragged last tile through registers: k rows at or past rows_left read as zero
+  __device__ __forceinline__ void issue_ragged(char* img, int wave, int lane, int kt,
+                                               int64_t rows_left) const {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int r = 8 * wave + 2 * c + (lane >> 5);
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (r < rows_left) v = *reinterpret_cast<const uint4*>(gbase + kt * tstep + voff[c]);
+      *reinterpret_cast<uint4*>(img + 512 * (8 * wave + 2 * c) + 16 * lane) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+};
+
+__global__ __launch_bounds__(THREADS, 1) void k_gemm_f16x3_dma(Params p) {
+  float sa = p.sa, inv_s = p.inv_s;
+  if (p.sa_bits) {
+    const float gs = grad_scale(*p.sa_bits);
+    sa = __fmul_rn(sa, gs);
+    inv_s = __fdiv_rn(inv_s, gs);
+  }
+  __shared__ __align__(16) char smem[DNBF * 2 * F32_IMG + STAGE * 2];  // ring | A hi, A lo, B hi, B lo
+  _Float16* planes = reinterpret_cast<_Float16*>(smem + DNBF * 2 * F32_IMG);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn, tile, z;
+  if (!split_of(p, tile, z)) return;
+  if (!tile_of(p, tile, tm, tn)) return;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)z * p.kchunk;
+  const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
+  const DmaOperandF32 da(p.A, p.lda, m0, kbeg, wave, lane, p.a_tiled);
+  const DmaOperandF32 db(p.B, p.ldb, n0, kbeg, wave, lane, p.b_tiled);
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
+  auto issue = [&](int kt) {
+    const int st = kt % DNBF;
+    const int64_t left = kend - (kbeg + (int64_t)kt * BK);
+    if (left >= BK) {
+      da.issue(lds0 + st * 2 * F32_IMG, wave, kt);
+      db.issue(lds0 + st * 2 * F32_IMG + F32_IMG, wave, kt);
+    } else {
+      dma_wait_vm(0);
+      da.issue_ragged(smem + st * 2 * F32_IMG, wave, lane, kt, left);
+      db.issue_ragged(smem + st * 2 * F32_IMG + F32_IMG, wave, lane, kt, left);
+    }
+  };
+  f4 acc_h[4][4], acc_x[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc_h[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+      acc_x[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  const bool want_rows = p.rowsum && tn == 0;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  // this thread's 4 x 4 block of an image: rows rq .. rq + 3 (16 B) of k rows kq .. kq + 3
+  const int kq = 4 * ((tid >> 2) & 7), rq = 16 * (tid >> 5) + 4 * (tid & 3);
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int kt = 0; kt < DNBF - 1 && kt < nk; ++kt) issue(kt);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's copies of tile kt have landed once only the later tiles' may be pending
+    const int later = (kt + DNBF - 2 < nk - 1 ? kt + DNBF - 2 : nk - 1) - kt;
+    dma_wait_vm(8 * later);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile kt in LDS for every wave; the planes' readers are done
+    asm volatile("" ::: "memory");
+    if (kt + DNBF - 1 < nk) issue(kt + DNBF - 1);  // its stage held tile kt - 1, split last step
+    const char* img = smem + (kt % DNBF) * 2 * F32_IMG;
+    TileLoad<false, true> ta, tb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ta.r[i] = *reinterpret_cast<const f4*>(img + 512 * (kq + i) + 4 * rq);
+      tb.r[i] = *reinterpret_cast<const f4*>(img + F32_IMG + 512 * (kq + i) + 4 * rq);
+    }
+    if (want_rows) ta.add_rows(rs);
+    ta.store(planes, planes + PLANE, sa, tid);
+    tb.store(planes + 2 * PLANE, planes + 3 * PLANE, p.sb, tid);
+    __syncthreads();  // planes written
+    h8 bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wn * 64 + 16 * j + r16;
+      bh[j] = *reinterpret_cast<const h8*>(planes + 2 * PLANE + row * ROWH + 8 * g);
+      bl[j] = *reinterpret_cast<const h8*>(planes + 3 * PLANE + row * ROWH + 8 * g);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + 16 * i + r16;
+      const h8 ah = *reinterpret_cast<const h8*>(planes + row * ROWH + 8 * g);
+      const h8 al = *reinterpret_cast<const h8*>(planes + PLANE + row * ROWH + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc_h[i][j] = mfma16(ah, bh[j], acc_h[i][j]);
+        acc_x[i][j] = mfma16(ah, bl[j], acc_x[i][j]);
+        acc_x[i][j] = mfma16(al, bh[j], acc_x[i][j]);
+      }
+    }
+  }
+  dma_wait_vm(0);
+  __syncthreads();  // LDS free for the row-sum reduction
+  const bool split = p.zsplit > 1;
+  if (want_rows) {
+    float* red = reinterpret_cast<float*>(smem);  // [8 k quads][128 rows]
+    const int kqi = (tid >> 2) & 7;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[kqi * BM + rq + j] = rs[j];
+    __syncthreads();
+    if (tid < BM) {
+      float v = red[tid];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v = __fadd_rn(v, red[q * BM + tid]);
+      if (split) p.rowsum_part[(int64_t)z * p.M + m0 + tid] = v;
+      else p.rowsum[m0 + tid] = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + 16 * j + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+        float v = __fmul_rn(__fadd_rn(acc_h[i][j][r], __fmul_rn(acc_x[i][j][r], kInvLo)), inv_s);
+        if (split) {
+          p.part[((int64_t)z * p.M + m) * p.N + n] = v;
+          continue;
+        }
+        if (n >= p.nstore) continue;
+        float* c = p.C + m * p.ldc + n;
+        if (p.accumulate) v = __fadd_rn(*c, v);
+        *c = v;
+      }
+    }
+}
+
 // ---- bf16 weight gradients with M <= 4 rows (the rgb / density heads: dW = d raw^T X with
 // X = hv3 / h7): a 128 x 128 MFMA tile would run 97% empty and the km kernel's transposing
 // loads held these at ~130 us for 0.2-0.4 GB, so the product streams instead.  Thread (r, cg):
@@ -1336,6 +1527,18 @@ static bool segsum_path(const aon_gemm_args* a) {
          (a->n_store == 0 || a->n_store == a->N);
 }
 
+// fp32 reduction-major x reduction-major weight gradients in whole 128 x 128 tiles with 16-B
+// runs: the fp16x3 LDS-DMA kernel (k_gemm_f16x3_dma)
+#ifndef AON_GEMM_F16_DMA
+#define AON_GEMM_F16_DMA 0  // 1: A/B build of k_gemm_f16x3_dma (bit-identical, measured slower)
+#endif
+static bool f16_copy_path(const aon_gemm_args* a) {
+  const int64_t b_rdiv = a->b_kc ? 1 : a->b_rdiv;
+  return AON_GEMM_F16_DMA && !a->mma_bf16 && !a->a_bf16 && !a->b_bf16 && !a->a_kc && !a->b_kc &&
+         !a->A2 && !a->bias && !a->mask && !a->relu && a->M % BM == 0 && a->N % BN == 0 &&
+         b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) && a->lda % 4 == 0 && a->ldb % 4 == 0;
+}
+
 static int64_t gemm_splits(const aon_gemm_args* a) {
   const int64_t tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
   if (small_path(a)) return 1;
@@ -1488,6 +1691,8 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     else if (a->a_bf16) launch_bf<__bf16, float>(p, va16, vb16, grid, st);
     else if (a->b_bf16) launch_bf<float, __bf16>(p, va16, vb16, grid, st);
     else launch_bf<float, float>(p, va16, vb16, grid, st);
+  } else if (f16_copy_path(a)) {
+    hipLaunchKernelGGL(k_gemm_f16x3_dma, grid, dim3(THREADS), 0, st, p);
   } else if (a->a_kc && a->b_kc) launch_v<true, true>(p, va, vb, grid, st);
   else if (a->a_kc) launch_v<true, false>(p, va, vb, grid, st);
   else if (a->b_kc) launch_v<false, true>(p, va, vb, grid, st);

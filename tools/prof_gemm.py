@@ -3,7 +3,8 @@
 K = 4096 x 193 = 790,528 rows, M = N = 256, both operands in the fused kernels' tiled layout)
 in the bf16 mode and the f16x3 mode, with HIP events on the launch stream; prints ms, the
 algorithmic HBM fraction (K (M + N) operand bytes) and the MFMA fraction.  AONERF_LIB selects
-the library (A/B of builds)."""
+the library (A/B of builds); "sha" hashes C and the row sums (bit-identity across builds)."""
+import hashlib
 import json
 import os
 import sys
@@ -49,8 +50,11 @@ def main():
 
         ms = timed(run)
         nbytes = K * (M + N) * A.element_size()
+        run()
+        torch.cuda.synchronize()
+        sha = hashlib.sha256(C.cpu().numpy().tobytes() + rs.cpu().numpy().tobytes()).hexdigest()[:16]
         res[mode] = {"ms": ms, "hbm_frac": nbytes / (ms * 1e-3) / 8e12,
-                     "mfma_frac": 2 * K * M * N / (ms * 1e-3) / 1e12 / peak}
+                     "mfma_frac": 2 * K * M * N / (ms * 1e-3) / 1e12 / peak, "sha": sha}
     print(json.dumps(res))
 
 
