@@ -432,6 +432,11 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
            "roofline": {"bound": "hbm+mfma", "kernel": "whole step (3 x forward FLOP)",
                         "achieved": ach, "peak": TRAIN_PEAK[precision], "unit": "TFLOP/s",
                         "frac": ach / TRAIN_PEAK[precision]}}
+    if art and precision == "bf16":
+        rec["roofline"]["note"] = ("the articulated bf16 mode keeps its forward in fp16x3 "
+                                   "(train_art.BF16_TRUNK = False: 3 fp16 products per MAC, peak "
+                                   "833 TF/s for that third of the FLOP); frac is against the "
+                                   "bf16 peak for the whole step")
     kern = {}
     hbm_bytes = 0.0
     names = ("art_fwd_train", "art_bwd_chain", "art_dweight") if art else ("fwd_train", "bwd_chain", "dweight")
