@@ -1096,6 +1096,194 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_dma(Params p) {
     }
 }
 
+// ---- the same product with a 256 x 256 C tile per workgroup (k_gemm_bf16_dma256): the
+// training step's 256 x 256 weight gradients (pts_linears, bottleneck) are ONE tile, so every
+// workgroup is a K chunk and each operand byte crosses into a CU once -- the 128 x 128 kernel
+// reads every k-tile of both operands into two workgroups (the 2 x 2 tile grid), twice the
+// bytes per CU for the same product (0.195 ms per fine-level product at ~15 B/cycle/CU).
+// 512 threads = 8 waves in 4 (m) x 2 (n), each wave 64 x 128 = 4 x 8 MFMA tiles (128 fp32
+// accumulator VGPRs), one workgroup per CU: DNB2 stages of a [32 k][256 col] image pair
+// (32 KB), the same XOR swizzle on the low four 16-B chunks of each 512-B image row
+// (ds_read_b64_tr_b16 banks repeat every 256 B, so the 128-column analysis holds).
+#ifndef AON_GEMM_DMA256
+#define AON_GEMM_DMA256 1  // 0: the 256 x 256 products take the 128 x 128 kernel (A/B)
+#endif
+#ifndef AON_GEMM_DMA256_NBUF
+#define AON_GEMM_DMA256_NBUF 3
+#endif
+constexpr int DNB2 = AON_GEMM_DMA256_NBUF;
+constexpr int BM2 = 256, THREADS2 = 512;
+constexpr int TT_PLANE2 = BK * 512;  // bytes of one operand's [32 k][256 col] bf16 image
+
+__device__ __forceinline__ int tt_off2(int row, int ch) {  // byte offset of 16-B chunk ch of row
+  return 512 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ bf8 tt_frag2(const char* plane, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  tt_v4s h[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const char* a = plane + tt_off2(8 * g + 4 * hh + q, c0 + (p >> 1)) + 8 * (p & 1);
+    h[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        reinterpret_cast<__attribute__((address_space(3))) tt_v4s*>(
+            reinterpret_cast<uintptr_t>(a)));
+  }
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s w = {h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]};
+  return __builtin_bit_cast(bf8, w);
+}
+
+// one operand's copies into a 256-column image: copy c of wave w fills image rows
+// 2 (2 w + c) + lane / 32, physical chunk lane % 32 <- logical chunk (lane % 32) ^ swz(row)
+struct DmaOperand2 {
+  const char* gbase;
+  int64_t tstep;
+  uint32_t voff[2];
+  __device__ __forceinline__ DmaOperand2(const __bf16* p, int64_t ld, int64_t col0, int64_t kbeg,
+                                         int wave, int lane, bool tiled) {
+    gbase = reinterpret_cast<const char*>(p) + 2 * (kbeg * ld + (tiled ? 16 * col0 : col0));
+    tstep = 2 * BK * ld;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int r = 2 * (2 * wave + c) + (lane >> 5);
+      const int ch = (lane & 31) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int64_t e = tiled ? (int64_t)(r & 16) * ld + 256 * (ch >> 1) + 16 * (r & 15) + 8 * (ch & 1)
+                              : (int64_t)r * ld + 8 * ch;
+      voff[c] = static_cast<uint32_t>(2 * e);
+    }
+  }
+  __device__ __forceinline__ void issue(uint32_t plane, int wave, int kt) const {
+    const char* g = gbase + kt * tstep;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane(plane + 1024u * (2 * wave + c));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :
+                   : "s"(m0), "v"(voff[c]), "s"(g)
+                   : "memory", "m0");
+#pragma clang diagnostic pop
+    }
+  }
+  __device__ __forceinline__ void issue_ragged(char* plane, int wave, int lane, int kt,
+                                               int64_t rows_left) const {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int r = 2 * (2 * wave + c) + (lane >> 5);
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (r < rows_left) v = *reinterpret_cast<const uint4*>(gbase + kt * tstep + voff[c]);
+      *reinterpret_cast<uint4*>(plane + 1024 * (2 * wave + c) + 16 * lane) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+};
+
+__global__ __launch_bounds__(THREADS2, 2) void k_gemm_bf16_dma256(Params p) {
+  __shared__ __align__(16) char smem[DNB2 * 2 * TT_PLANE2];  // DNB2 stages x (A, B) images
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn, tile, z;
+  if (!split_of(p, tile, z)) return;
+  if (!tile_of(p, tile, tm, tn)) return;
+  const int64_t m0 = (int64_t)tm * BM2, n0 = (int64_t)tn * BM2;
+  const int64_t kbeg = (int64_t)z * p.kchunk;
+  const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
+  const DmaOperand2 da(reinterpret_cast<const __bf16*>(p.A), p.lda, m0, kbeg, wave, lane, p.a_tiled);
+  const DmaOperand2 db(reinterpret_cast<const __bf16*>(p.B), p.ldb, n0, kbeg, wave, lane, p.b_tiled);
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
+  auto issue = [&](int kt) {
+    const int st = kt % DNB2;
+    const int64_t left = kend - (kbeg + (int64_t)kt * BK);
+    if (left >= BK) {
+      da.issue(lds0 + st * 2 * TT_PLANE2, wave, kt);
+      db.issue(lds0 + st * 2 * TT_PLANE2 + TT_PLANE2, wave, kt);
+    } else {
+      dma_wait_vm(0);
+      da.issue_ragged(smem + st * 2 * TT_PLANE2, wave, lane, kt, left);
+      db.issue_ragged(smem + st * 2 * TT_PLANE2 + TT_PLANE2, wave, lane, kt, left);
+    }
+  };
+  f4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const bool want_rows = p.rowsum && tn == 0;
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // this thread's column-sum runs in the A image: rows kl0, kl0 + 16, columns cl .. cl + 7
+  const int kl0 = tid >> 5, cl = 8 * (tid & 31);
+  for (int kt = 0; kt < DNB2 - 1 && kt < nk; ++kt) issue(kt);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int later = (kt + DNB2 - 2 < nk - 1 ? kt + DNB2 - 2 : nk - 1) - kt;
+    dma_wait_vm(4 * later);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + DNB2 - 1 < nk) issue(kt + DNB2 - 1);
+    const char* s = smem + (kt % DNB2) * 2 * TT_PLANE2;
+    if (want_rows) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint4 v = *reinterpret_cast<const uint4*>(s + tt_off2(kl0 + 16 * j, cl >> 3));
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t d = w[e >> 1];
+          rs[e] = __fadd_rn(rs[e], __uint_as_float((e & 1) ? (d & 0xffff0000u) : (d << 16)));
+        }
+      }
+    }
+    bf8 b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = tt_frag2(s + TT_PLANE2, 16 * wn + 2 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf8 a = tt_frag2(s, 8 * wm + 2 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  dma_wait_vm(0);
+  __syncthreads();  // LDS free for the row-sum reduction
+  const bool split = p.zsplit > 1;
+  if (want_rows) {
+    float* red = reinterpret_cast<float*>(smem);  // [16][256]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[kl0 * BM2 + cl + e] = rs[e];
+    __syncthreads();
+    if (tid < BM2) {
+      float v = red[tid];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) v = __fadd_rn(v, red[q * BM2 + tid]);
+      if (split) p.rowsum_part[(int64_t)z * p.M + m0 + tid] = v;
+      else p.rowsum[m0 + tid] = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t n = n0 + wn * 128 + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        float v = acc[i][j][r];
+        if (split) {
+          p.part[((int64_t)z * p.M + m) * p.N + n] = v;
+          continue;
+        }
+        if (n >= p.nstore) continue;
+        float* c = p.C + m * p.ldc + n;
+        if (p.accumulate) v = __fadd_rn(*c, v);
+        *c = v;
+      }
+    }
+}
+
 // ---- fp16x3 weight gradients on the LDS-DMA ring (fp32 operands, both reduction-major):
 // k_gemm_f16x3<false, false> staged each k-tile through registers (global loads -> transpose ->
 // split -> LDS), one tile ahead, and ran the fine level's 256 x 256 x 790k products at ~3 TB/s
@@ -1505,6 +1693,12 @@ static bool bf16_copy_path(const aon_gemm_args* a) {
          b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) && a->lda % 8 == 0 && a->ldb % 8 == 0;
 }
 
+// ... in whole 256 x 256 tiles: k_gemm_bf16_dma256 (one tile per 256 x 256 weight gradient)
+static bool bf16_copy256_path(const aon_gemm_args* a) {
+  return AON_GEMM_DMA256 && AON_GEMM_BF_DMA && bf16_copy_path(a) && a->M % BM2 == 0 &&
+         a->N % BM2 == 0;
+}
+
 // bf16 weight gradient of at most 4 rows on a bf16 B of up to 256 columns (k_gemm_skinny_bf16)
 static bool skinny_path(const aon_gemm_args* a) {
   const int64_t b_rdiv = a->b_kc ? 1 : a->b_rdiv;
@@ -1542,6 +1736,15 @@ static bool f16_copy_path(const aon_gemm_args* a) {
 static int64_t gemm_splits(const aon_gemm_args* a) {
   const int64_t tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
   if (small_path(a)) return 1;
+  if (bf16_copy256_path(a) && a->k_splits <= 0) {
+    // one workgroup per CU: 256 K chunks of a single 256 x 256 tile (chunks of >= 1024 rows;
+    // the coarse level's 266k rows still fill the chip -- 2048-row chunks left half of it idle)
+    const int64_t t2 = (a->M / BM2) * (a->N / BM2);
+    if (t2 >= 256 || a->K < 8 * 1024) return 1;
+    const int64_t cap = a->K / 1024 < 256 ? a->K / 1024 : 256;
+    const int64_t s = 256 / t2 < cap ? 256 / t2 : cap;
+    return s >= 8 ? s / 8 * 8 : (s < 1 ? 1 : s);
+  }
   // the segment-sum kernel: one chunk of 2048 / M rays (whole segments) per workgroup
   if (segsum_path(a)) {
     const int64_t rays = (a->K + a->b_rdiv - 1) / a->b_rdiv, rb = 2048 / a->M;
@@ -1639,7 +1842,9 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     p.part = static_cast<float*>(work);
     p.rowsum_part = p.part + zs * a->M * a->N;
   }
-  const int64_t tiles_m = (a->M + BM - 1) / BM, tiles_n = (a->N + BN - 1) / BN;
+  const bool t256 = a->mma_bf16 && bf16_copy256_path(a);
+  const int64_t bmt = t256 ? BM2 : BM;  // C tile edge of the kernel that runs
+  const int64_t tiles_m = (a->M + bmt - 1) / bmt, tiles_n = (a->N + bmt - 1) / bmt;
   const int64_t gm = tiles_m < 8 ? tiles_m : 8;
   const int64_t blocks = (tiles_m + gm - 1) / gm * gm * tiles_n;
   AON_REQUIRE(blocks < (1ll << 31), "too large");
@@ -1685,7 +1890,8 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
       else if (a->a_bf16) launch_skinny<__bf16, false>(p, g, st);
       else if (a->b_tiled) launch_skinny<float, true>(p, g, st);
       else launch_skinny<float, false>(p, g, st);
-    } else if (tt && AON_GEMM_BF_DMA) hipLaunchKernelGGL(k_gemm_bf16_dma, grid, dim3(THREADS), 0, st, p);
+    } else if (t256) hipLaunchKernelGGL(k_gemm_bf16_dma256, grid, dim3(THREADS2), 0, st, p);
+    else if (tt && AON_GEMM_BF_DMA) hipLaunchKernelGGL(k_gemm_bf16_dma, grid, dim3(THREADS), 0, st, p);
     else if (tt) hipLaunchKernelGGL(k_gemm_bf16_tt, grid, dim3(THREADS), 0, st, p);
     else if (a->a_bf16 && a->b_bf16) launch_bf<__bf16, __bf16>(p, va16, vb16, grid, st);
     else if (a->a_bf16) launch_bf<__bf16, float>(p, va16, vb16, grid, st);

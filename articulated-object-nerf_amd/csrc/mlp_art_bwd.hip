@@ -41,6 +41,7 @@ struct ArtBwdArgs {
 // Epilogue policy of the skip layer's enc columns: park each value (scale s) in this lane's LDS
 // slots [tile][reg]; nothing goes to the output fragments' consumer.
 struct EncStash {
+  static constexpr bool kPkEpi = false;  // sees the fp32 values (post)
   float* slot;  // lane-private: float index (t * 64) * 4 + r of the lane's f4 slot t
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int pr, int uu, int r, int, float v) const {
@@ -48,7 +49,7 @@ struct EncStash {
     return v;
   }
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
-  __device__ __forceinline__ void put_bf(int, int, int, int, float, float, uint32_t) const {}
+  __device__ __forceinline__ void put_pk(int, int, int, int, uint32_t) const {}
 };
 
 // Epilogue policy of pts_linears.0's enc columns: total d enc_f = this value + the parked skip
@@ -56,6 +57,7 @@ struct EncStash {
 // f < 3 identity; 3 <= f < 33 sin(x_c 2^d); 33 <= f < 63 sin(x_c 2^d + pi/2f), (f - 3) mod 30 =
 // 3 d + c.
 struct EncBwd {
+  static constexpr bool kPkEpi = false;
   const float* slot;
   float x0, x1, x2;  // x' of this lane's sample
   int g;
@@ -88,7 +90,7 @@ struct EncBwd {
     return v;
   }
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
-  __device__ __forceinline__ void put_bf(int, int, int, int, float, float, uint32_t) const {}
+  __device__ __forceinline__ void put_pk(int, int, int, int, uint32_t) const {}
 };
 
 // BF: the bf16 training mode -- the whole chain one bf16 MFMA per product on the compact stream
@@ -167,6 +169,7 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
     RowStore<NCOL, T> st;
     st.ok[0] = keep_row(row, N);
     st.rowp[0] = reinterpret_cast<T*>(a.dbot) + act_base(row, 256, g);
+    st.off16 = st16_off(g);
     st.s = inv;
     layer_h<Net, AB_V0, false>(fp, y, none, x, bias_l, g, st);
   }

@@ -61,20 +61,22 @@ int absmax(const float* x, int64_t n, uint32_t* out, hipStream_t stream) {
 
 // BF: the bf16 training mode -- one bf16 MFMA per product, dZ stored as bf16 (BwdArgs' output
 // pointers then address bf16 arrays of the same shapes)
+// (the bf16 chain runs 16 kBfNcolBwd samples per wave, 8 waves: GeomH<kBfNcolBwd, true>)
 template <bool BF = false>
-__global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
+__global__ __launch_bounds__((GeomH<BF ? kBfNcolBwd : 1, BF>::kThreads), 2) void k_mlp_bwd_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, BwdArgs a) {
-  constexpr int NCOL = 1;
+  constexpr int NCOL = BF ? kBfNcolBwd : 1;
   using T = typename std::conditional<BF, __bf16, float>::type;
   T* const dzv = reinterpret_cast<T*>(a.dzv);
   T* const dzb = reinterpret_cast<T*>(a.dzb);
   T* const dz = reinterpret_cast<T*>(a.dz);
-  using G = GeomH<NCOL>;
+  using G = GeomH<NCOL, BF>;
   using Net = NetBwdH;
-  constexpr int kStash = G::kWaves * 64 * 2;  // f4: d raw_sigma fragment, hi & lo
+  constexpr int kPer = (BF ? 1 : 2) * NCOL;  // f4 per lane: d raw_sigma fragments, hi (& lo)
+  constexpr int kStash = G::kWaves * 64 * kPer;
   __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + kStash];
   float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
-  f4* stash = smem + kLdsWeights + Net::kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 2 +
+  f4* stash = smem + kLdsWeights + Net::kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * kPer +
               (threadIdx.x & 63);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -96,9 +98,10 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   // segment B of [bottleneck | density]^T (lane group 0, element 0)
   Frag<1, NCOL> drgb, dsig;
   int64_t rows[NCOL];
-  {
-    const int64_t row = (int64_t)blockIdx.x * G::kRowsPerBlock + wave * G::kRowsPerWave + j;
-    rows[0] = row;
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    const int64_t row = (int64_t)blockIdx.x * G::kRowsPerBlock + wave * G::kRowsPerWave + 16 * c + j;
+    rows[c] = row;
     const int64_t rr = row < N ? row : N - 1;
     const f4 d = *reinterpret_cast<const f4*>(a.draw + 4 * rr);
     float dv[8], sv[8];
@@ -107,10 +110,10 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
       dv[e] = (g == 0 && e < 3) ? d[e < 3 ? e : 0] * s : 0.f;
       sv[e] = (g == 0 && e == 0) ? d[3] * s : 0.f;
     }
-    split8<BF>(dv, drgb.hi[0][0], drgb.lo[0][0], drgb.ovf);
-    split8<BF>(sv, dsig.hi[0][0], dsig.lo[0][0], dsig.ovf);
-    stash[0] = __builtin_bit_cast(f4, dsig.hi[0][0]);
-    stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
+    split8<BF>(dv, drgb.hi[0][c], drgb.lo[0][c], drgb.ovf);
+    split8<BF>(sv, dsig.hi[0][c], dsig.lo[0][c], dsig.ovf);
+    stash[64 * (kPer / NCOL) * c] = __builtin_bit_cast(f4, dsig.hi[0][c]);
+    if (!BF) stash[64 * (2 * c + 1)] = __builtin_bit_cast(f4, dsig.lo[0][c]);
   }
 
   FragPipe<WeightPipeP<Net, G::kThreads, BF>, AON_PREFETCH, 0, BF> fp(p);
@@ -126,13 +129,20 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_bwd_f16x3(
   // d bottleneck = W_view[:, :256]^T dZ_view (linear layer: no mask)
   {
     RowStore<NCOL, T> st;
-    st.ok[0] = keep_row(rows[0], N);
-    st.rowp[0] = dzb + act_base(rows[0], 256, g);
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+      st.ok[c] = keep_row(rows[c], N);
+      st.rowp[c] = dzb + act_base(rows[c], 256, g);
+    }
+    st.off16 = st16_off(g);
     st.s = inv;
     layer_h<Net, B_VIEW, false>(fp, x, none, y, bias_l, g, st);
   }
-  dsig.hi[0][0] = __builtin_bit_cast(h8, stash[0]);
-  dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    dsig.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (kPer / NCOL) * c]);
+    if (!BF) dsig.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (2 * c + 1)]);
+  }
   // d h7 = W_bot^T dZ_bot + W_den^T d sigma, * ReLU'(h7) -> dZ_7
   layer_h<Net, B_BOTDEN, false>(fp, y, dsig, x, bias_l, g,
                                 mask_bits(a.masks + 7 * ms, dz + 7 * hs, 256, rows, N, g, inv));
@@ -208,8 +218,10 @@ static int bwd_launch(const void* packed, const float* draw, const uint32_t* mas
                   aligned16(dzb) && aligned16(dz),
               "buffers must be 16-byte aligned");
   if (N == 0) return 0;
-  using G = GeomH<1>;
-  const int64_t grid = (N + G::kRowsPerBlock - 1) / G::kRowsPerBlock;
+  using G1 = GeomH<1>;
+  using GB = GeomH<kBfNcolBwd, true>;
+  const int64_t rpb = bf16 ? GB::kRowsPerBlock : G1::kRowsPerBlock;
+  const int64_t grid = (N + rpb - 1) / rpb;
   AON_REQUIRE(grid < (1ll << 31), "too many rows");
   hipStream_t st = (hipStream_t)stream;
   uint32_t* amax = static_cast<uint32_t*>(work);
@@ -222,9 +234,9 @@ static int bwd_launch(const void* packed, const float* draw, const uint32_t* mas
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetBwdH::kStreamBytes);
   if (bf16)
-    hipLaunchKernelGGL(k_mlp_bwd_f16x3<true>, (unsigned)grid, G::kThreads, 0, st, ws, bias, args);
+    hipLaunchKernelGGL(k_mlp_bwd_f16x3<true>, (unsigned)grid, GB::kThreads, 0, st, ws, bias, args);
   else
-    hipLaunchKernelGGL(k_mlp_bwd_f16x3<false>, (unsigned)grid, G::kThreads, 0, st, ws, bias, args);
+    hipLaunchKernelGGL(k_mlp_bwd_f16x3<false>, (unsigned)grid, G1::kThreads, 0, st, ws, bias, args);
   return launch_status(bf16 ? "aon_mlp_bwd_bf16" : "aon_mlp_bwd");
 }
 

@@ -34,12 +34,22 @@ namespace mlp {
 
 // The layer sequence of k_mlp_fwd_f16x3 (model.py:95-120), instantiated per FragPipe type: the
 // two halves of the workgroup differ in the k-step of their epilogues (FragPipe EOFF).
+// per-lane LDS stash of the encodings: enc k-steps 0, 1 and venc, hi and lo (fp16x3) or hi only
+// (bf16: no lo part); slot (c, i) at stash[64 (kStashPer c + i)]
+template <bool BF>
+__host__ __device__ constexpr int stash_per() { return BF ? 3 : 6; }
+template <bool BF>
+__device__ __forceinline__ int enc_slot(int c, int k, int lo) { return BF ? 3 * c + k : 6 * c + 2 * k + lo; }
+template <bool BF>
+__device__ __forceinline__ int venc_slot(int c, int lo) { return BF ? 3 * c + 2 : 6 * c + 4 + lo; }
+
 template <int NCOL, bool STORE, typename T, typename FP>
 __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<1, NCOL>& venc,
                                                Frag<8, NCOL>& x, Frag<8, NCOL>& y, f4* stash,
                                                float* bias_s, int g, int wave,
                                                const int64_t (&rows)[NCOL], int64_t N, int act,
                                                float* __restrict__ raw, const TrainStore& ts) {
+  constexpr bool BF = std::is_same<T, __bf16>::value;
   fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
 #if AON_PRIO_HALF
   if (wave >= GeomH<NCOL>::kWaves / 2) __builtin_amdgcn_s_setprio(AON_PRIO_HALF);
@@ -63,8 +73,8 @@ __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<
   for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k)]);
-      enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 2 * k + 1)]);
+      enc.hi[k][c] = __builtin_bit_cast(h8, stash[64 * enc_slot<BF>(c, k, 0)]);
+      if (!BF) enc.lo[k][c] = __builtin_bit_cast(h8, stash[64 * enc_slot<BF>(c, k, 1)]);
     }
   // skip: cat[h, enc] (model.py:102-103)
   layer_h<NetVanillaH, L5, true>(fp, x, enc, y, bias_l, g, SP::make(th + 5 * hs, 256, rows, N, g, ts.masks + 5 * ms));
@@ -76,8 +86,8 @@ __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<
   layer_h<NetVanillaH, LBOT, false>(fp, y, none, x, bias_l, g, SP::make(tbot, 256, rows, N, g));
 #pragma unroll
   for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c) {
-    venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
-    venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 5)]);
+    venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * venc_slot<BF>(c, 0)]);
+    if (!BF) venc.lo[0][c] = __builtin_bit_cast(h8, stash[64 * venc_slot<BF>(c, 1)]);
   }
   // cat[bottleneck, enc_dir] + ReLU (:110-116)
   layer_h<NetVanillaH, LVIEW, true>(fp, x, venc, y, bias_l, g, SP::make(thv, 128, rows, N, g, ts.masks + 8 * ms));
@@ -105,16 +115,18 @@ __device__ __forceinline__ void vanilla_layers(FP& fp, Frag<2, NCOL>& enc, Frag<
 // BF: bf16 numerics (one bf16 MFMA per k-step; the kept activations stored as bf16) -- the
 // bf16 training mode; the stream then carries bf16 weights in its hi blocks (k_pack_h bf16).
 template <int MODE, int NCOL, bool STORE = false, bool BF = false>
-__global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_fwd_f16x3(
+__global__ __launch_bounds__((GeomH<NCOL, BF>::kThreads), (GeomH<NCOL, BF>::kWavesPerSimd)) void k_mlp_fwd_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
     int64_t B, int S, int act, float* __restrict__ raw, TrainStore ts = {}) {
-  using G = GeomH<NCOL>;
+  using G = GeomH<NCOL, BF>;
   // ONE __shared__ object: weight ring | bias table | per-lane stash of the encodings
-  constexpr int kStash = AON_STASH_REGS ? 0 : G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
+  constexpr int kPer = stash_per<BF>() * NCOL;  // f4 per lane: enc 2 k-steps + venc 1, hi (& lo)
+  constexpr int kStash = AON_STASH_REGS ? 0 : G::kWaves * 64 * kPer;
+  static_assert((kLdsWeights + kBiasFloats / 4 + kStash) * 16 <= 160 * 1024, "LDS");
   __shared__ f4 smem[kLdsWeights + kBiasFloats / 4 + kStash];
   float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
-  f4* stash = smem + kLdsWeights + kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * 6 * NCOL +
+  f4* stash = smem + kLdsWeights + kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * kPer +
               (threadIdx.x & 63);  // lane-private slots: written and read by the same lane
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -189,11 +201,11 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   for (int c = 0; c < NCOL && !AON_STASH_REGS; ++c) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      stash[64 * (6 * c + 2 * k)] = __builtin_bit_cast(f4, enc.hi[k][c]);
-      stash[64 * (6 * c + 2 * k + 1)] = __builtin_bit_cast(f4, enc.lo[k][c]);
+      stash[64 * enc_slot<BF>(c, k, 0)] = __builtin_bit_cast(f4, enc.hi[k][c]);
+      if (!BF) stash[64 * enc_slot<BF>(c, k, 1)] = __builtin_bit_cast(f4, enc.lo[k][c]);
     }
-    stash[64 * (6 * c + 4)] = __builtin_bit_cast(f4, venc.hi[0][c]);
-    stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
+    stash[64 * venc_slot<BF>(c, 0)] = __builtin_bit_cast(f4, venc.hi[0][c]);
+    if (!BF) stash[64 * venc_slot<BF>(c, 1)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
 
   Frag<8, NCOL> x, y;
@@ -340,10 +352,12 @@ int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const 
                      GeomH<C>::kThreads, 0, stream, ws, bias, a0, a1, a2, a3, B, S, act, raw)
   if (mode == 2 || mode == 3) {  // training forward: MODE 0 inputs + activation stores
     const int grid = static_cast<int>((N + GeomH<1>::kRowsPerBlock - 1) / GeomH<1>::kRowsPerBlock);
-    if (mode == 3)  // bf16 training mode
-      hipLaunchKernelGGL((k_mlp_fwd_f16x3<0, 1, true, true>), grid, GeomH<1>::kThreads, 0, stream,
-                         ws, bias, a0, a1, a2, a3, B, S, act, raw, *ts);
-    else
+    if (mode == 3) {  // bf16 training mode: 16 kBfNcolFwd samples per wave
+      using GB = GeomH<kBfNcolFwd, true>;
+      hipLaunchKernelGGL((k_mlp_fwd_f16x3<0, kBfNcolFwd, true, true>),
+                         static_cast<int>((N + GB::kRowsPerBlock - 1) / GB::kRowsPerBlock),
+                         GB::kThreads, 0, stream, ws, bias, a0, a1, a2, a3, B, S, act, raw, *ts);
+    } else
       hipLaunchKernelGGL((k_mlp_fwd_f16x3<0, 1, true>), grid, GeomH<1>::kThreads, 0, stream, ws,
                          bias, a0, a1, a2, a3, B, S, act, raw, *ts);
     return launch_status("aon_mlp_fwd_train");

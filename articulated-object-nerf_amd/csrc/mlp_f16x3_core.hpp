@@ -179,11 +179,6 @@ struct Frag {
   // and a NaN is above it), reduced to a ballot once, by ovf_of, at the kernel's range report
   uint32_t m16 = 0;
 };
-typedef short s2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2v, a),
-                                                                __builtin_bit_cast(s2v, b)));
-}
 template <int N, int NCOL>
 __device__ __forceinline__ uint64_t ovf_of(const Frag<N, NCOL>& f) {
   const bool bad = (f.m16 & 0x7FFFu) >= 0x7C00u || ((f.m16 >> 16) & 0x7FFFu) >= 0x7C00u;
@@ -199,14 +194,50 @@ __device__ __forceinline__ uint64_t ovf_of(const Frag<N, NCOL>& f) {
 // output it flows into was > 0 (torch's threshold_backward on the ReLU output) and the product
 // (true scale) is stored for the weight-gradient GEMMs.
 struct NoStore {
+  static constexpr bool kPkEpi = true;
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
+  __device__ __forceinline__ uint32_t post_pk(int, int, int, int, uint32_t pk) const { return pk; }
   __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
-  __device__ __forceinline__ void put_bf(int, int, int, int, float, float, uint32_t) const {}
+  __device__ __forceinline__ void put_pk(int, int, int, int, uint32_t) const {}
 };
-// put_bf (the bf16 layers' epilogue): the pair's values at TRUE scale (bf16 numerics carry no
-// operand scaling) with their packed bf16 dword -- the one the next layer's fragment gets -- so
-// a bf16 store writes that dword as it is: no rescale, no second conversion
+// The bf16 layers' epilogue works on the PACKED pair (kPkEpi policies): the accumulator already
+// holds the bias (layer_h seeds it), one v_cvt_pk_bf16_f32 makes the dword the next layer's
+// fragment gets, ReLU is one v_pk_max_i16 on it (a negative bf16 is a negative i16; bf16
+// rounding is sign-symmetric, so max_i16(bf16(v), 0) = bf16(max(v, 0))), post_pk masks it (the
+// backward chains' ReLU'), put_pk stores it as it is and derives the ReLU' bits from it.
+// Policies with kPkEpi = false (the articulated chain's enc-column stashes) see fp32 values.
+typedef short s2v __attribute__((ext_vector_type(2)));
+typedef unsigned short u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2v, a),
+                                                                __builtin_bit_cast(s2v, b)));
+}
+// The packed bit forms are written as instructions (they only read VALU results): left to
+// itself hipcc rewrites min(h, 1) into per-half compares + cndmask + v_perm (3x the VALU).
+// per 16-bit half: 1 if the (non-negative) bf16 is non-zero, else 0 -- ReLU' of a ReLU output
+// (op_sel_hi:[1,0]: the constant's low half feeds the high lane too; its high half is 0)
+__device__ __forceinline__ uint32_t pk_nonzero(uint32_t a) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(r) : "v"(a));
+  return r;
+}
+// (m << s) | a in one v_lshl_or_b32
+__device__ __forceinline__ uint32_t lshl_or(uint32_t m, int s, uint32_t a) {
+  uint32_t r;
+  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "i"(s), "v"(a));
+  return r;
+}
+// (bf16(lo), bf16(hi)) round to nearest even as one v_cvt_pk_bf16_f32: the empty asm pins the
+// packed dword (without it hipcc pushes the packed ReLU back through the conversion and emits
+// two one-value conversions joined by a v_perm); the conversion itself stays compiler-visible,
+// as it reads MFMA results (the MFMA-to-VALU wait states are the compiler's to insert)
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  const bf2 hb = {static_cast<__bf16>(lo), static_cast<__bf16>(hi)};
+  uint32_t r = __builtin_bit_cast(uint32_t, hb);
+  asm("" : "+v"(r));
+  return r;
+}
 
 // two consecutive outputs at true scale: one 8-B fp32 store, or (bf16 mode) one 4-B bf16 store
 __device__ __forceinline__ void store2(float* p, float v0, float v1) {
@@ -253,6 +284,9 @@ constexpr int kTileStride = AON_TILED ? 256 : 16;  // elements between output ti
 // on SCC instead of masking EXEC around itself (s_and_saveexec / s_cbranch_execz / s_or per
 // store).  Row-major (A/B build): row < N.
 __device__ __forceinline__ bool keep_row(int64_t row, int64_t N) {
+#ifdef AON_ABL_NO_KEEP  // timing-only A/B build: the training kernels store nothing they keep
+  return false;
+#endif
 #if AON_TILED
   const uint64_t t = static_cast<uint64_t>(row & ~int64_t(15));
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(t));
@@ -285,6 +319,9 @@ __device__ __forceinline__ void store_enc_bf(__bf16* base, int64_t row, int g,
   }
 }
 
+#ifndef AON_BF_ST16
+#define AON_BF_ST16 1
+#endif
 // pairs (r0 = 0, 2) of a tile meet in one 4-value store
 template <int NCOL, typename T>
 struct Store4 {
@@ -305,14 +342,44 @@ struct Store4 {
       store4(rowp + kTileStride * (2 * pr + uu), pend[c][0], pend[c][1], v0, v1);
     }
   }
-  // bf16 layers: the packed pair as it is (parts r0 = 0, 2 of a tile row -> one 8-B store)
+  // bf16 layers: the packed pair as it is.  AON_BF_ST16 (tiled): the pair's two tiles meet in
+  // ONE 16-B store per lane -- lane (g, j) holds 4 features of tile 2pr and 4 of tile 2pr + 1
+  // (4g.., 16 + 4g.. of sample j); one v_permlane16_swap per dword trades the odd lane groups'
+  // tile-2pr values for the even groups' tile-(2pr + 1) values, after which group g holds 8
+  // consecutive features of one tile (g even: features 8 (g / 2).. of tile 2pr; g odd: of tile
+  // 2pr + 1) -- a wave's store is the pair's whole 1-KB run, half the store instructions of the
+  // 8-B form (the bf16 chain was store-issue-bound: ~6 B/cycle/CU with 8-B stores).  off16:
+  // this lane group's element offset of that run from rowp (set by the makers; 0 or 252).
+  // Else: parts r0 = 0, 2 of a tile row -> one 8-B store.
+  static constexpr bool kPkEpi = true;
+  __device__ __forceinline__ uint32_t post_pk(int, int, int, int, uint32_t pk) const { return pk; }
   mutable uint32_t pendw[NCOL];
+  mutable uint2 pend0[NCOL];
+  int off16 = 0;
   __device__ __forceinline__ void emit_bf(T* rowp, int pr, int uu, int r0, int c, uint32_t pk) const {
     static_assert(std::is_same<T, __bf16>::value, "bf16 layers keep bf16 activations");
-    if (r0 == 0) pendw[c] = pk;
-    else if (ok[c]) *reinterpret_cast<uint2*>(rowp + kTileStride * (2 * pr + uu)) = uint2{pendw[c], pk};
+    if (r0 == 0) {
+      pendw[c] = pk;
+      return;
+    }
+#if AON_BF_ST16 && AON_TILED
+    if (uu == 0) {
+      pend0[c] = uint2{pendw[c], pk};
+      return;
+    }
+    // every lane takes part in the swaps (EXEC full): only the store is predicated
+    const auto s0 = __builtin_amdgcn_permlane16_swap(pend0[c].x, pendw[c], false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(pend0[c].y, pk, false, false);
+    if (ok[c])
+      *reinterpret_cast<uint4*>(rowp + kTileStride * 2 * pr + off16) = uint4{s0[0], s1[0], s0[1], s1[1]};
+#else
+    if (ok[c]) *reinterpret_cast<uint2*>(rowp + kTileStride * (2 * pr + uu)) = uint2{pendw[c], pk};
+#endif
   }
 };
+// Store4::off16 of lane group g: 16-B run of 8 features of tile 2pr + (g & 1) at column 8 (g / 2),
+// relative to act_base(row, ld, g) (which includes 4 g)
+__device__ __forceinline__ int st16_off(int g) { return 256 * (g & 1) + 8 * (g >> 1) - 4 * g; }
 
 template <int NCOL, typename T = float>
 struct RowStore : Store4<NCOL, T> {
@@ -323,7 +390,7 @@ struct RowStore : Store4<NCOL, T> {
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     this->emit(rowp[c], pr, uu, r0, c, v0 * s, v1 * s);
   }
-  __device__ __forceinline__ void put_bf(int pr, int uu, int r0, int c, float, float, uint32_t pk) const {
+  __device__ __forceinline__ void put_pk(int pr, int uu, int r0, int c, uint32_t pk) const {
     this->emit_bf(rowp[c], pr, uu, r0, c, pk);
   }
 };
@@ -338,10 +405,21 @@ struct RowStoreBits : RowStore<NCOL, T> {
   uint8_t* mrow[NCOL];  // bytes of word (row, g) (stored when ok)
   bool narrow;          // 4-pair (128-wide) layer: bytes 4..7 of the word are written as 0
   mutable uint32_t b[NCOL];  // the current pair's 8 bits (byte pr of the word)
-  __device__ __forceinline__ void put_bf(int pr, int uu, int r0, int c, float v0, float v1,
-                                         uint32_t pk) const {
-    RowStore<NCOL, T>::put_bf(pr, uu, r0, c, v0, v1, pk);
-    bits(pr, uu, r0, c, v0, v1);
+  // bf16 layers: the bits from the packed ReLU output -- part q = 2 uu + r0 / 2 of the pair has
+  // its two values' bits at 2q (element 0) and 2q + 1 (element 1): one v_pk_min_u16 gives them at
+  // 0 and 16, one v_lshl_or_b32 per part gathers them at 2q and 16 + 2q, and the byte folds the
+  // upper ones down by 15 (9 VALU per pair against 25 for the fp32 compares).  A positive fp32
+  // below bf16's smallest subnormal rounds to 0 here and its bit reads 0; the bf16 training mode
+  // keeps that 0, so the backward masks exactly what the forward stored.
+  __device__ __forceinline__ void put_pk(int pr, int uu, int r0, int c, uint32_t pk) const {
+    RowStore<NCOL, T>::put_pk(pr, uu, r0, c, pk);
+    const uint32_t m = pk_nonzero(pk);
+    const int q = 2 * uu + (r0 >> 1);  // compile-time after unrolling
+    b[c] = q == 0 ? m : lshl_or(m, 2 * q, b[c]);
+    if (q == 3 && this->ok[c]) {
+      mrow[c][pr] = static_cast<uint8_t>(b[c] | (b[c] >> 15));
+      if (narrow) mrow[c][pr + 4] = 0;
+    }
   }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     RowStore<NCOL, T>::put(pr, uu, r0, c, v0, v1);
@@ -380,7 +458,22 @@ struct MaskBits : Store4<NCOL, T> {
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     this->emit(rowp[c], pr, uu, r0, c, v0 * s, v1 * s);
   }
-  __device__ __forceinline__ void put_bf(int pr, int uu, int r0, int c, float, float, uint32_t pk) const {
+  // bf16 layers: the mask applied to the packed pair (bf16(0) = 0, so masking after the
+  // conversion gives the same bits).  Part q of pair pr needs bits 2q, 2q + 1 of the pair's byte
+  // as 16-bit all-ones / zero halves: the byte and its copy shifted up by 15 put them at 2q of
+  // each half (once per pair: hipcc shares it between the four parts), then one packed shift
+  // left moves bit 2q to the sign and one packed arithmetic shift right spreads it.
+  __device__ __forceinline__ uint32_t post_pk(int pr, int uu, int r0, int c, uint32_t pk) const {
+    const uint32_t w = pr < 4 ? m[c].x : m[c].y;
+    const uint32_t byte = (w >> (8 * (pr & 3))) & 0xFFu;
+    const uint32_t z = byte | (byte << 15);
+    const short q = static_cast<short>(2 * uu + (r0 >> 1));
+    const s2v sel = (__builtin_bit_cast(s2v, z) << s2v{static_cast<short>(15 - 2 * q),
+                                                         static_cast<short>(15 - 2 * q)}) >>
+                    s2v{15, 15};
+    return pk & __builtin_bit_cast(uint32_t, sel);
+  }
+  __device__ __forceinline__ void put_pk(int pr, int uu, int r0, int c, uint32_t pk) const {
     this->emit_bf(rowp[c], pr, uu, r0, c, pk);
   }
 };
@@ -397,6 +490,7 @@ __device__ __forceinline__ MaskBits<NCOL, T> mask_bits(const uint2* mbase, T* ob
     mb.mrow[c] = mbase + mask_index(rows[c], g);
     mb.rowp[c] = obase + act_base(rows[c], ld, g);
   }
+  mb.off16 = st16_off(g);
   mb.s = s;
   return mb;
 }
@@ -424,6 +518,7 @@ struct StorePick<true, NCOL, T> {
       r.ok[c] = keep_row(rows[c], N);
       r.rowp[c] = base + act_base(rows[c], ld, g);
     }
+    r.off16 = st16_off(g);
     r.s = AON_F16X3_V2 ? 1.0f / kActS : 1.0f / kActScale;
     return r;
   }
@@ -449,22 +544,33 @@ struct StorePick<true, NCOL, T> {
 
 // epilogue of a finished pair, in 4 parts of 2 values (so it can ride between MFMA steps):
 // part q converts v[2q], v[2q+1] of the pair's 8 per-lane values (v[4uu + r] = tile uu, reg r)
-// BF: a bf16 layer -- operands unscaled, the accumulator at true scale: + bias (nothing when
-// ZB, the backward chains' zero bias tables), ReLU, one v_cvt_pk_bf16_f32.
+// BF: a bf16 layer -- operands unscaled, the accumulator at true scale and already holding the
+// bias (layer_h seeds it): one v_cvt_pk_bf16_f32, then ReLU / mask / store on the packed pair
+// (kPkEpi policies, see NoStore).
 template <bool RELU, bool BF, int NCOL, int NO, typename Store = NoStore, bool ZB = false>
 __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
                                          const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr,
                                          const Store& st = Store{}) {
   const int uu = q >> 1, r0 = (q & 1) * 2;
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
+    if constexpr (BF && Store::kPkEpi) {
+      uint32_t pk = cvt_pk_bf16(hh[uu][c][r0], hh[uu][c][r0 + 1]);
+      if (RELU) pk = pk_max_i16(pk, 0u);
+      pk = st.post_pk(pr, uu, r0, c, pk);
+      st.put_pk(pr, uu, r0, c, pk);
+      u4 w = __builtin_bit_cast(u4, out.hi[pr][c]);
+      w[q] = pk;
+      out.hi[pr][c] = __builtin_bit_cast(h8, w);
+      continue;
+    }
     float vv[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
 #if AON_F16X3_V2
       // fp16x3: one accumulator at scale 2^9 -> activation scale 2^3, plus the (pre-scaled) bias
-      float v = BF ? (ZB ? hh[uu][c][r0 + e] : __fadd_rn(hh[uu][c][r0 + e], bias[uu][r0 + e]))
-                   : fmaf(hh[uu][c][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
+      float v = BF ? hh[uu][c][r0 + e] : fmaf(hh[uu][c][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
       (void)xx;
 #else
       float v = fmaf(xx[uu][c][r0 + e], 1.0f / kLoScale, hh[uu][c][r0 + e]);
@@ -477,10 +583,9 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
       // the packed pair goes in as ONE dword of the fragment: ROCm 7.2's clang mis-lowers
       // bit_cast<_Float16>(pair[1]) of a <2 x bfloat> (it yields element 0;
       // tools/diag/bf16_pack_probe.hip), so no bf16 element is extracted
-      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
       const bf2 hb = {static_cast<__bf16>(vv[0]), static_cast<__bf16>(vv[1])};
       const uint32_t pk = __builtin_bit_cast(uint32_t, hb);
-      st.put_bf(pr, uu, r0, c, vv[0], vv[1], pk);
+      st.put_pk(pr, uu, r0, c, pk);
       u4 w = __builtin_bit_cast(u4, out.hi[pr][c]);
       w[q] = pk;
       out.hi[pr][c] = __builtin_bit_cast(h8, w);
@@ -536,22 +641,41 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
   static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
   f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
   f4 pbias[2];                     // V2: that pair's biases, added in its epilogue
+  // bf16 layers seed the accumulators with the bias (no epilogue add); each pair's bias is read
+  // from LDS one pair ahead, so the first MFMA does not wait on it (zero-bias chains: nothing)
+  constexpr bool kBiasC = BF && !Net::kZeroBias;
+  f4 nbias[2];
+  if (kBiasC) {
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) nbias[uu] = *reinterpret_cast<lds_f4*>(bias_l + d.bias0 + 16 * uu);
+  }
 #pragma unroll
   for (int pr = 0; pr < NP; ++pr) {
     st.begin_pair(pr);
     f4 hh[2][NCOL], xx[2][NCOL], bias[2];
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
-      bias[uu] = *reinterpret_cast<lds_f4*>(bias_l + d.bias0 + 16 * (2 * pr + uu));
+      if (kBiasC)
+        bias[uu] = nbias[uu];
+      else if (!BF)
+        bias[uu] = *reinterpret_cast<lds_f4*>(bias_l + d.bias0 + 16 * (2 * pr + uu));
+      else
+        bias[uu] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < NCOL; ++c) {
 #if AON_F16X3_V2
-        hh[uu][c] = f4{0.f, 0.f, 0.f, 0.f};  // bias joins in the epilogue: no LDS read to wait on
+        // fp16x3: the bias joins in the epilogue (no LDS read to wait on); bf16: in the accumulator
+        hh[uu][c] = kBiasC ? bias[uu] : f4{0.f, 0.f, 0.f, 0.f};
 #else
         hh[uu][c] = bias[uu];
 #endif
         xx[uu][c] = f4{0.f, 0.f, 0.f, 0.f};
       }
+    }
+    if (kBiasC && pr + 1 < NP) {
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu)
+        nbias[uu] = *reinterpret_cast<lds_f4*>(bias_l + d.bias0 + 16 * (2 * (pr + 1) + uu));
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -685,12 +809,23 @@ constexpr int kLdsWeights = kRing * kChunkH * 64;  // f4
 #define AON_WAVES_H 8  // waves per workgroup at 16 samples per wave (2 waves per SIMD either way)
 #endif
 
-template <int NCOL>
+// BF: the bf16 training kernels -- at 32 samples per wave (NCOL = 2) they keep 8 waves (2 per
+// SIMD): bf16 activations carry no lo part, so a wave's input and output fragments take 64 + 64
+// VGPRs where fp16x3 needs 256 (its NCOL = 2 runs 4 waves, one per SIMD)
+#ifndef AON_BF_NCOL_FWD
+#define AON_BF_NCOL_FWD 1  // samples per wave / 16 of the bf16 training forward
+#endif
+#ifndef AON_BF_NCOL_BWD
+#define AON_BF_NCOL_BWD 2  // ... and of the bf16 backward chain
+#endif
+constexpr int kBfNcolFwd = AON_BF_NCOL_FWD, kBfNcolBwd = AON_BF_NCOL_BWD;
+template <int NCOL, bool BF = false>
 struct GeomH {
-  static constexpr int kWaves = NCOL == 1 ? AON_WAVES_H : 4;
+  static constexpr int kWaves = (NCOL == 1 || BF) ? AON_WAVES_H : 4;
   static constexpr int kThreads = 64 * kWaves;
   static constexpr int kRowsPerWave = 16 * NCOL;
   static constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
+  static constexpr int kWavesPerSimd = kWaves / 4;  // __launch_bounds__' occupancy request
 };
 
 }  // namespace mlp

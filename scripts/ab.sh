@@ -15,6 +15,7 @@
 #   train      tools/prof_train_step.py                       (C5 step; --art, --precision ...)
 #   bench      bench.py --no-cpu-baseline                     (every bench record)
 #   bf16-sha   tools/diag/bf16_ab_outputs.py                  (sha of every bf16-step output)
+#   trainrec   tools/prof_train_records.py                    (C5 records + fine-level kernel ms)
 # env: ROUNDS (default 2), TOOL_ARGS (extra arguments), LIMIT (seconds per run, default 300).
 # Writes OUT/NAME.ROUND.log under gpurun_out/ and prints each run's last line; stops at the
 # first failing run (no retries).
@@ -28,6 +29,7 @@ case $TOOL in
   train) CMD="tools/prof_train_step.py" ;;
   bench) CMD="bench.py --no-cpu-baseline" ;;
   bf16-sha) CMD="tools/diag/bf16_ab_outputs.py" ;;
+  trainrec) CMD="tools/prof_train_records.py" ;;
   *) echo "unknown TOOL $TOOL"; exit 2 ;;
 esac
 V=articulated-object-nerf_amd/lib/variants

@@ -34,7 +34,9 @@ def bf16_round(x):
 
 
 @pytest.mark.parametrize("K,M,N,rdiv,a_bf,b_bf", [
-    (70000, 256, 256, 1, True, True),     # a fine-level dW (split-K)
+    (70000, 256, 256, 1, True, True),     # a fine-level dW (split-K; the 256 x 256-tile kernel)
+    (250003, 256, 256, 1, True, True),    # 256 K chunks with a ragged last k-tile
+    (70000, 128, 256, 1, True, True),     # the 128 x 128-tile kernel
     (1000, 3, 128, 1, False, True),       # rgb_layer: dY = fp32 d raw (strided, 3 of 4 columns)
     (2000, 128, 27, 33, True, False),     # views_linear.0's enc_dir columns: B row k // S
     (517, 256, 63, 1, True, False),       # pts_linears.0: fp32 encodings (ld 63, scalar loads)
@@ -192,16 +194,18 @@ def test_bf16_loss_trajectory():
 
 @pytest.mark.parametrize("mma_bf16,dtype", [(False, torch.float32), (True, torch.float32),
                                             (True, torch.bfloat16)])
-def test_weight_gradient_gemm_tiled_operands(mma_bf16, dtype):
+@pytest.mark.parametrize("M", [128, 256])
+def test_weight_gradient_gemm_tiled_operands(mma_bf16, dtype, M):
     """aon_gemm a_tiled / b_tiled: dW = dZ^T X read in place from the fused training kernels'
     16-row tiled layout (aonerf/tiles.py; 70,003 rows: a partial last block, split-K) is
     bit-identical to the same product on row-major copies -- the staged values and their
-    order are the same."""
+    order are the same.  M = 256 with bf16 operands: the 256 x 256-tile kernel
+    (k_gemm_bf16_dma256)."""
     from aonerf import tiles
     from aonerf.linalg import gemm
 
     g = torch.Generator(device="cuda").manual_seed(11)
-    K, M, N = 70003, 128, 256
+    K, N = 70003, 256
     A = (torch.randn((K, M), device="cuda", generator=g) * 1e-3).to(dtype)
     B = torch.randn((K, N), device="cuda", generator=g).to(dtype)
     At, Bt = tiles.tile(A), tiles.tile(B)
