@@ -49,6 +49,7 @@ class AonAdamTensor(ctypes.Structure):
 
 
 ADAM_MAX_TENSORS = 64
+GEMM_BATCH_MAX = 8  # AON_GEMM_BATCH_MAX
 
 _SIGNATURES = {
     "aon_abi_version": (c_int, []),
@@ -100,6 +101,8 @@ _SIGNATURES = {
     "aon_to8b": (c_int, [vp, c_i64, vp, vp]),
     "aon_gemm_workspace_bytes": (c_size, [ctypes.POINTER(AonGemmArgs)]),
     "aon_gemm": (c_int, [ctypes.POINTER(AonGemmArgs), vp, c_size, vp]),
+    "aon_gemm_batch_workspace_bytes": (c_size, [ctypes.POINTER(AonGemmArgs), c_int]),
+    "aon_gemm_batch": (c_int, [ctypes.POINTER(AonGemmArgs), c_int, vp, c_size, vp]),
     "aon_composite_bwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp, vp,
                                   vp, vp, vp, c_i64, vp]),
     "aon_mse": (c_int, [vp, vp, c_i64, c_float, vp, vp, vp]),
@@ -126,7 +129,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.aon_abi_version() != 7:
+        if handle.aon_abi_version() != 8:
             raise ImportError("aonerf: ABI version mismatch")
         _lib = handle
     return _lib

@@ -2,7 +2,9 @@
 layer-by-layer paths: the training forward/backward (train.py) and the articulated
 NeRF_AE_Art MLP (model_autodecoder.py).  Operands are tensor views passed as pointers +
 leading dimensions; workspace for split reductions is cached per device."""
+import contextlib
 import ctypes
+import os
 
 import torch
 
@@ -48,9 +50,55 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
                       b_bf16=int(B.dtype == torch.bfloat16), a_tiled=int(bool(a_tiled)),
                       b_tiled=int(bool(b_tiled)), n_store=n_store,
                       exact_fp32=int(bool(exact_fp32)))
+    if (_batch is not None and mma_bf16 and M % 128 == 0 and N % 128 == 0 and K >= 8192
+            and not k_splits and b_rdiv == 1 and A.dtype == torch.bfloat16
+            and B.dtype == torch.bfloat16):
+        # operands kept alive until the flush; class: one 256 x 256 tile, or 128 x 128 tiles
+        cls = 256 if M == 256 and N == 256 else 128
+        if cls == 256 or BATCH128:
+            _batch.append((a, C.device, cls, (A, B, C, rowsum)))
+            return
     nbytes = L.lib().aon_gemm_workspace_bytes(ctypes.byref(a))
     ws = _workspace(nbytes, C.device) if nbytes else None
     L.call("aon_gemm", ctypes.byref(a), L.ptr(ws), nbytes, L.stream(C.device))
+
+
+_batch = None
+# AONERF_NO_GEMM_BATCH=1: batched() defers nothing (A/B of aon_gemm_batch against separate launches)
+BATCH = os.environ.get("AONERF_NO_GEMM_BATCH", "0") != "1"
+# AONERF_NO_GEMM_BATCH128=1: only the 256 x 256 products are deferred (A/B of the 128-tile class)
+BATCH128 = os.environ.get("AONERF_NO_GEMM_BATCH128", "0") != "1"
+
+
+@contextlib.contextmanager
+def batched():
+    """Defer the bf16 weight-gradient products in whole 128-column tiles issued inside (dW =
+    dZ^T X of pts_linears / bottleneck / views_linear.0, the enc-column products) to
+    aon_gemm_batch launches -- the 256 x 256 ones together, the others together, up to
+    GEMM_BATCH_MAX products of equal K each -- flushed at exit; every other product runs at
+    once.  The deferred products only read kept tensors and write their own dW / db (callers
+    flush before reading a deferred db), so the reordering is safe."""
+    global _batch
+    if not BATCH:
+        yield
+        return
+    outer, _batch = _batch, []
+    try:
+        yield
+        items = _batch
+    finally:
+        _batch = outer
+    groups = {}
+    for it in items:
+        groups.setdefault((it[2], it[0].K, str(it[1])), []).append(it)
+    for grp in groups.values():
+        for i in range(0, len(grp), L.GEMM_BATCH_MAX):
+            chunk = grp[i:i + L.GEMM_BATCH_MAX]
+            arr = (L.AonGemmArgs * len(chunk))(*[it[0] for it in chunk])
+            dev = chunk[0][1]
+            nbytes = L.lib().aon_gemm_batch_workspace_bytes(arr, len(chunk))
+            ws = _workspace(nbytes, dev) if nbytes else None
+            L.call("aon_gemm_batch", arr, len(chunk), L.ptr(ws), nbytes, L.stream(dev))
 
 
 def colsum(out, X, M, N, ldx, accumulate=False):

@@ -27,7 +27,7 @@ import torch.optim.optimizer as _torch_optim
 from . import _lib as L
 from . import tiles
 
-from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, colsum, gemm, linear_fwd  # noqa: F401
+from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, batched, colsum, gemm, linear_fwd  # noqa: F401
 
 # ---------------------------------------------------------------------------- one render level
 def _mlp_params(mlp):
@@ -277,19 +277,21 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
              rowsum=db, a_amax=None if bf16 else work, mma_bf16=bf16, a_tiled=a_t, b_tiled=b_t,
              n_store=n_store)
 
-    dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1], a_t=False)    # rgb_layer
-    dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0
-    dweight(G[10][0], dzv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
-    dweight(G[9][0], dzb, 256, 256, h[7], 256, 256, db=G[9][1])            # bottleneck
-    dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256, db=G[8][1], a_t=False)  # density
-    for i in range(7, -1, -1):                                             # pts_linears.i
-        if i == 5:
-            dweight(G[5][0], dz[5], 256, 256, h[4], 256, 256, db=G[5][1])
-            dweight(G[5][0], dz[5], 256, 256, enc, 63, 63, col0=256)
-        elif i == 0:
-            dweight(G[0][0], dz[0], 256, 256, enc, 63, 63, db=G[0][1])
-        else:
-            dweight(G[i][0], dz[i], 256, 256, h[i - 1], 256, 256, db=G[i][1])
+    # bf16: the eight 256 x 256 products (bottleneck, pts_linears.1-7) run as one aon_gemm_batch
+    with batched():
+        dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1], a_t=False)    # rgb_layer
+        dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0
+        dweight(G[10][0], dzv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
+        dweight(G[9][0], dzb, 256, 256, h[7], 256, 256, db=G[9][1])            # bottleneck
+        dweight(G[8][0], draw[:, 3:], 4, 1, h[7], 256, 256, db=G[8][1], a_t=False)  # density
+        for i in range(7, -1, -1):                                             # pts_linears.i
+            if i == 5:
+                dweight(G[5][0], dz[5], 256, 256, h[4], 256, 256, db=G[5][1])
+                dweight(G[5][0], dz[5], 256, 256, enc, 63, 63, col0=256)
+            elif i == 0:
+                dweight(G[0][0], dz[0], 256, 256, enc, 63, 63, db=G[0][1])
+            else:
+                dweight(G[i][0], dz[i], 256, 256, h[i - 1], 256, 256, db=G[i][1])
     _rec(f"dweight{S}", e0, R)
 
 

@@ -33,7 +33,7 @@ import torch
 from . import _lib as L
 from . import tiles
 from . import train as _train
-from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, gemm
+from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, batched, gemm
 from .train import Adam, _amax_word, img2mse, learning_rate, mse2psnr, relu_masks  # noqa: F401 (shared)
 
 # parameter layout of one articulated NeRFMLP in ArtRenderLevel: 20 layers x (weight, bias)
@@ -421,10 +421,13 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     dweight(VIEW0, dzv[0], wc, bot, nw, nw)                               # views_linear.0
     dweight(VIEW0, dzv[0], wc, venc, nv, nv, col0=nw, rdiv=S, bias=False)
     dlatent(VIEW0, nw + nv, app, dapp, False)
-    dweight(BOT, dbot, nw, h[7], nw, nw)                                  # bottleneck
-    dweight(DENS, draw[:, 3:], 4, h[7], nw, nw, a_t=False)                # density
-    for i in range(7, 0, -1):                                             # pts_linears.i
-        dweight(PTS0 + i, dz[i], nw, h[i - 1], nw, nw)
+    # bf16: the eight 256 x 256 products (bottleneck, pts_linears.1-7) as one aon_gemm_batch,
+    # flushed before dlatent reads pts_linears.5's bias gradient
+    with batched():
+        dweight(BOT, dbot, nw, h[7], nw, nw)                              # bottleneck
+        dweight(DENS, draw[:, 3:], 4, h[7], nw, nw, a_t=False)            # density
+        for i in range(7, 0, -1):                                         # pts_linears.i
+            dweight(PTS0 + i, dz[i], nw, h[i - 1], nw, nw)
     dweight(PTS0 + 5, dz[5], nw, enc, ne, ne, col0=nw, bias=False)
     dlatent(PTS0 + 5, nw + ne, shape, dshape, False)
     dweight(PTS0, dz[0], nw, enc, ne, ne)                                 # pts_linears.0

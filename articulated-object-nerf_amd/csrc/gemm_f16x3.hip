@@ -382,7 +382,7 @@ __device__ __forceinline__ float sum_z4(const float* src, int64_t stride, int sp
   return (q & 2) ? __fadd_rn(other, pair) : __fadd_rn(pair, other);
 }
 
-__global__ void k_gemm_reduce(Params p, int splits) {
+__device__ __forceinline__ void reduce_body(const Params& p, int splits) {
   const int64_t total = p.M * p.N;
   const int64_t extra = p.rowsum ? p.M : 0;  // rowsum entries ride along as e >= total
   const int q = threadIdx.x & 3;
@@ -409,6 +409,19 @@ __global__ void k_gemm_reduce(Params p, int splits) {
     *c = v;
   }
 }
+
+__global__ void k_gemm_reduce(Params p, int splits) { reduce_body(p, splits); }
+
+// aon_gemm_batch: up to AON_GEMM_BATCH_MAX products in one launch, selected by a wave-uniform
+// index into the kernel-argument table
+struct ParamsBatch {
+  Params p[AON_GEMM_BATCH_MAX];
+  int count, zsplit;
+  int tile0[AON_GEMM_BATCH_MAX + 1];  // 128 x 128-tile batch: first tile of each product
+};
+
+// the batch's split-K reduce: grid.y = product
+__global__ void k_gemm_reduce_batch(ParamsBatch pb) { reduce_body(pb.p[blockIdx.y], pb.zsplit); }
 
 template <bool AKC, bool BKC, bool VA, bool VB>
 static void launch(const Params& p, dim3 grid, hipStream_t st) {
@@ -989,13 +1002,9 @@ struct DmaOperand {
   }
 };
 
-__global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_dma(Params p) {
-  __shared__ __align__(16) char smem[DNB * 2 * TT_PLANE];  // DNB stages x (A, B) images
+__device__ __forceinline__ void dma128_body(const Params& p, int tm, int tn, int z, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  int tm, tn, tile, z;
-  if (!split_of(p, tile, z)) return;
-  if (!tile_of(p, tile, tm, tn)) return;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kbeg = (int64_t)z * p.kchunk;
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
@@ -1096,6 +1105,29 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_dma(Params p) {
     }
 }
 
+__global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_dma(Params p) {
+  __shared__ __align__(16) char smem[DNB * 2 * TT_PLANE];  // DNB stages x (A, B) images
+  int tm, tn, tile, z;
+  if (!split_of(p, tile, z)) return;
+  if (!tile_of(p, tile, tm, tn)) return;
+  dma128_body(p, tm, tn, z, smem);
+}
+
+// A batch of products in whole 128 x 128 tiles over the same K (aon_gemm_batch): T = all the
+// products' tiles, chunk z of every tile on one XCD (split_of's order), product b owning tiles
+// tile0[b] .. tile0[b + 1] - 1 (its own grid, m fastest)
+__global__ __launch_bounds__(THREADS, 2) void k_gemm_bf16_dma_batch(ParamsBatch pb) {
+  __shared__ __align__(16) char smem[DNB * 2 * TT_PLANE];
+  const int T = pb.tile0[pb.count], L = blockIdx.x, x = L & 7, q = L >> 3;
+  const int z = 8 * (q / T) + x, t = q - (q / T) * T;
+  if (z >= pb.zsplit) return;  // padding block of the last chunk group (uniform exit)
+  int b = 0;
+  while (b + 1 < pb.count && t >= pb.tile0[b + 1]) ++b;
+  const Params& p = pb.p[b];
+  const int lt = t - pb.tile0[b];
+  dma128_body(p, lt % p.tiles_m, lt / p.tiles_m, z, smem);
+}
+
 // ---- the same product with a 256 x 256 C tile per workgroup (k_gemm_bf16_dma256): the
 // training step's 256 x 256 weight gradients (pts_linears, bottleneck) are ONE tile, so every
 // workgroup is a K chunk and each operand byte crosses into a CU once -- the 128 x 128 kernel
@@ -1180,13 +1212,9 @@ struct DmaOperand2 {
   }
 };
 
-__global__ __launch_bounds__(THREADS2, 2) void k_gemm_bf16_dma256(Params p) {
-  __shared__ __align__(16) char smem[DNB2 * 2 * TT_PLANE2];  // DNB2 stages x (A, B) images
+__device__ __forceinline__ void dma256_body(const Params& p, int tm, int tn, int z, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  int tm, tn, tile, z;
-  if (!split_of(p, tile, z)) return;
-  if (!tile_of(p, tile, tm, tn)) return;
   const int64_t m0 = (int64_t)tm * BM2, n0 = (int64_t)tn * BM2;
   const int64_t kbeg = (int64_t)z * p.kchunk;
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
@@ -1282,6 +1310,28 @@ __global__ __launch_bounds__(THREADS2, 2) void k_gemm_bf16_dma256(Params p) {
         *c = v;
       }
     }
+}
+
+__global__ __launch_bounds__(THREADS2, 2) void k_gemm_bf16_dma256(Params p) {
+  __shared__ __align__(16) char smem[DNB2 * 2 * TT_PLANE2];  // DNB2 stages x (A, B) images
+  int tm, tn, tile, z;
+  if (!split_of(p, tile, z)) return;
+  if (!tile_of(p, tile, tm, tn)) return;
+  dma256_body(p, tm, tn, z, smem);
+}
+
+// A batch of one-tile (256 x 256) products over the same K (one level's weight gradients): the
+// 256 workgroups are count products x zsplit K chunks -- chunk z of every product on one XCD
+// (split_of's order, the product index in place of the tile) -- so each product's chunks are
+// count times longer than in its own launch: count times fewer fp32 partials written and summed
+// (each launch of a lone product wrote 256 x 257 KB = 67 MB of partials for 0.27-0.81 GB of
+// operands), and one launch + one reduce per level instead of count of each.
+__global__ __launch_bounds__(THREADS2, 2) void k_gemm_bf16_dma256_batch(ParamsBatch pb) {
+  __shared__ __align__(16) char smem[DNB2 * 2 * TT_PLANE2];
+  const int T = pb.count, L = blockIdx.x, x = L & 7, q = L >> 3;
+  const int z = 8 * (q / T) + x, b = q - (q / T) * T;
+  if (z >= pb.zsplit) return;  // padding block of the last chunk group (uniform exit)
+  dma256_body(pb.p[b], 0, 0, z, smem);
 }
 
 // ---- fp16x3 weight gradients on the LDS-DMA ring (fp32 operands, both reduction-major):
@@ -1909,4 +1959,155 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     hipLaunchKernelGGL(k_gemm_reduce, grid_for(4 * (a->M * a->N + a->M), 256, 16384), 256, 0, st, p, (int)zs);
   }
   return launch_status(__func__);
+}
+
+// ---- aon_gemm_batch: one level's bf16 weight gradients in two launches (+ their reduces):
+// the one-tile 256 x 256 products on k_gemm_bf16_dma256_batch, the other whole-128 x 128-tile
+// products on k_gemm_bf16_dma_batch; any other product runs as aon_gemm.
+enum { kBatchNone = 0, kBatch256 = 1, kBatch128 = 2 };
+
+static int batch_class(const aon_gemm_args* a) {
+  if (!a->mma_bf16 || a->k_splits > 0 || a->K < 8 * 1024) return kBatchNone;
+  if (bf16_copy256_path(a) && a->M == BM2 && a->N == BM2) return kBatch256;
+  if (AON_GEMM_BF_DMA && bf16_copy_path(a) && !bf16_copy256_path(a) &&
+      (a->M / BM) * (a->N / BN) < 512)
+    return kBatch128;
+  return kBatchNone;
+}
+
+struct BatchPlan {
+  int idx[AON_GEMM_BATCH_MAX];  // products of the class, in argument order
+  int n;
+  int64_t K, kchunk, zs, tiles;
+};
+
+static BatchPlan plan_class(const aon_gemm_args* a, int count, int cls) {
+  BatchPlan pl{};
+  for (int i = 0; i < count; ++i)
+    if (batch_class(&a[i]) == cls) {
+      if (pl.n == 0) pl.K = a[i].K;
+      if (a[i].K == pl.K) pl.idx[pl.n++] = i;  // other K: run alone (aon_gemm)
+    }
+  if (pl.n < 2) { pl.n = 0; return pl; }
+  for (int j = 0; j < pl.n; ++j) {
+    const aon_gemm_args* g = &a[pl.idx[j]];
+    pl.tiles += cls == kBatch256 ? 1 : (g->M / BM) * (g->N / BN);
+  }
+  // 256 x 256 tiles: one workgroup per CU (256 in all), chunks >= 1024 rows; 128 x 128 tiles:
+  // two per CU (512), chunks >= 2048 rows -- each product's chunks longer by the batch size
+  const int64_t wgs = cls == kBatch256 ? 256 : 512, minrows = cls == kBatch256 ? 1024 : 2048;
+  const int64_t cap = pl.K / minrows < 256 ? pl.K / minrows : 256;
+  int64_t s = wgs / pl.tiles < cap ? wgs / pl.tiles : cap;
+  s = s >= 8 ? s / 8 * 8 : (s < 1 ? 1 : s);
+  pl.kchunk = s > 1 ? ((pl.K + s - 1) / s + BK - 1) / BK * BK : pl.K;
+  pl.zs = (pl.K + pl.kchunk - 1) / pl.kchunk;
+  return pl;
+}
+
+static size_t plan_bytes(const aon_gemm_args* a, const BatchPlan& pl) {
+  if (pl.n == 0 || pl.zs <= 1) return 0;
+  size_t f = 0;
+  for (int j = 0; j < pl.n; ++j) f += (size_t)pl.zs * (a[pl.idx[j]].M * a[pl.idx[j]].N + a[pl.idx[j]].M);
+  return f * sizeof(float);
+}
+
+static bool in_plan(const BatchPlan& pl, int i) {
+  for (int j = 0; j < pl.n; ++j)
+    if (pl.idx[j] == i) return true;
+  return false;
+}
+
+extern "C" size_t aon_gemm_batch_workspace_bytes(const aon_gemm_args* a, int count) {
+  if (!a || count < 1 || count > AON_GEMM_BATCH_MAX) return 0;
+  const BatchPlan p2 = plan_class(a, count, kBatch256), p1 = plan_class(a, count, kBatch128);
+  // the launches are stream-ordered: one workspace serves each in turn
+  size_t m = plan_bytes(a, p2) > plan_bytes(a, p1) ? plan_bytes(a, p2) : plan_bytes(a, p1);
+  for (int i = 0; i < count; ++i)
+    if (!in_plan(p2, i) && !in_plan(p1, i)) {
+      const size_t b = aon_gemm_workspace_bytes(&a[i]);
+      m = b > m ? b : m;
+    }
+  return m;
+}
+
+static int run_plan(const aon_gemm_args* a, const BatchPlan& pl, int cls, void* work,
+                    size_t work_bytes, hipStream_t st) {
+  ParamsBatch pb;
+  pb.count = pl.n;
+  pb.zsplit = (int)pl.zs;
+  pb.tile0[0] = 0;
+  AON_REQUIRE(pl.zs == 1 || (work && work_bytes >= plan_bytes(a, pl)),
+              "aon_gemm_batch needs aon_gemm_batch_workspace_bytes() of workspace");
+  float* part = static_cast<float*>(work);
+  for (int j = 0; j < pl.n; ++j) {
+    const aon_gemm_args* g = &a[pl.idx[j]];
+    AON_REQUIRE(g->A && g->B && g->C && g->ldc >= (g->n_store > 0 ? g->n_store : g->N),
+                "null operand or bad leading dimension");
+    AON_REQUIRE(!g->a_tiled || (g->lda == g->M && g->M % 16 == 0), "a_tiled: lda = M");
+    AON_REQUIRE(!g->b_tiled || (g->ldb == g->N && g->N % 16 == 0), "b_tiled: ldb = N");
+    AON_REQUIRE(g->n_store >= 0 && g->n_store <= g->N, "n_store must be in [0, N]");
+    AON_REQUIRE(g->K < (int64_t(1) << 32), "K must be below 2^32");
+    Params& p = pb.p[j];
+    p = Params{};
+    p.a_tiled = g->a_tiled;
+    p.b_tiled = g->b_tiled;
+    p.nstore = g->n_store > 0 ? g->n_store : g->N;
+    p.M = g->M; p.N = g->N; p.K = g->K;
+    p.A = g->A; p.lda = g->lda;
+    p.K1 = INT64_MAX; p.a2_rdiv = 1;
+    p.B = g->B; p.ldb = g->ldb; p.b_rdiv = 1;
+    p.C = g->C; p.ldc = g->ldc;
+    p.accumulate = g->accumulate;
+    p.sa = p.sb = p.inv_s = 1.0f;
+    p.kchunk = pl.kchunk;
+    p.rowsum = g->rowsum;
+    p.zsplit = (int)pl.zs;
+    const int bmt = cls == kBatch256 ? BM2 : BM;
+    p.tiles_m = (int)(g->M / bmt);
+    p.tiles_n = (int)(g->N / bmt);
+    p.gm = p.tiles_m;
+    p.tblocks = p.tiles_m * p.tiles_n;
+    pb.tile0[j + 1] = pb.tile0[j] + p.tblocks;
+    if (pl.zs > 1) {
+      p.part = part;
+      p.rowsum_part = p.part + pl.zs * g->M * g->N;
+      part += pl.zs * (g->M * g->N + g->M);
+    }
+  }
+  const dim3 grid((unsigned)(8 * pb.tile0[pl.n] * ((pl.zs + 7) / 8)), 1, 1);
+  if (cls == kBatch256) hipLaunchKernelGGL(k_gemm_bf16_dma256_batch, grid, dim3(THREADS2), 0, st, pb);
+  else hipLaunchKernelGGL(k_gemm_bf16_dma_batch, grid, dim3(THREADS), 0, st, pb);
+  if (pl.zs > 1) {
+    const int rc = launch_status("aon_gemm_batch");
+    if (rc) return rc;
+    int64_t mx = 0;
+    for (int j = 0; j < pl.n; ++j) {
+      const int64_t w = 4 * (pb.p[j].M * pb.p[j].N + pb.p[j].M);
+      mx = w > mx ? w : mx;
+    }
+    const dim3 rg((unsigned)grid_for(mx, 256, 16384), (unsigned)pl.n, 1);
+    hipLaunchKernelGGL(k_gemm_reduce_batch, rg, dim3(256), 0, st, pb);
+  }
+  return launch_status("aon_gemm_batch");
+}
+
+extern "C" int aon_gemm_batch(const aon_gemm_args* a, int count, void* work, size_t work_bytes,
+                              aon_stream_t stream) {
+  AON_REQUIRE(a && count >= 0 && count <= AON_GEMM_BATCH_MAX, "bad batch");
+  hipStream_t st = (hipStream_t)stream;
+  const BatchPlan p2 = plan_class(a, count, kBatch256), p1 = plan_class(a, count, kBatch128);
+  if (p2.n) {
+    const int rc = run_plan(a, p2, kBatch256, work, work_bytes, st);
+    if (rc) return rc;
+  }
+  if (p1.n) {
+    const int rc = run_plan(a, p1, kBatch128, work, work_bytes, st);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < count; ++i)
+    if (!in_plan(p2, i) && !in_plan(p1, i)) {
+      const int rc = aon_gemm(&a[i], work, work_bytes, stream);
+      if (rc) return rc;
+    }
+  return 0;
 }

@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 7
+#define AON_ABI_VERSION 8
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -412,6 +412,19 @@ typedef struct aon_gemm_args {
 
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);
 int aon_gemm(const aon_gemm_args* args, void* work, size_t work_bytes, aon_stream_t stream);
+
+/* `count` (<= AON_GEMM_BATCH_MAX) independent aon_gemm products (no product reads what another
+ * writes), stream-ordered, with one workspace: one level's bf16 weight gradients, the loop of
+ * LitNeRF.training_step's backward (model.py:256-282).  The bf16 256 x 256 products (mma_bf16,
+ * both operands bf16, M = N = 256, k_splits 0, equal K >= 8192: pts_linears / bottleneck) run
+ * as ONE launch of count x (256 / count) K chunks and one split-K reduce -- count times fewer
+ * fp32 partials than count launches; the other bf16 products in whole 128 x 128 tiles
+ * (views_linear.0, the enc columns) likewise as one launch; the rest one by one as aon_gemm.
+ * Deterministic; the chunking, and so the fp32 summation order, differs from aon_gemm's. */
+#define AON_GEMM_BATCH_MAX 8
+size_t aon_gemm_batch_workspace_bytes(const aon_gemm_args* args, int count);
+int aon_gemm_batch(const aon_gemm_args* args, int count, void* work, size_t work_bytes,
+                   aon_stream_t stream);
 
 /* Backward of volumetric_rendering (helper.py:157-195) and of the activations `act` applied to
  * the raw MLP outputs (model.py:186-187): given dL/dcomp_rgb (B,3) and optionally dL/dacc,

@@ -341,3 +341,105 @@ def test_bf16_forward_keeps_encodings(bf16_mode):
     got = tiles.untile(enc, R)
     assert torch.equal(got[:, :63], enc_ref.to(torch.bfloat16))
     assert not got[:, 63:].float().any()
+
+
+@pytest.mark.parametrize("count,K", [(8, 70003), (3, 266240), (8, 790528)])
+def test_bf16_weight_gradient_batch(count, K):
+    """aon_gemm_batch (linalg.batched): one level's 256 x 256 bf16 weight gradients in ONE launch
+    (k_gemm_bf16_dma256_batch: count products x 256 / count K chunks, one split-K reduce) --
+    every product against fp64 products of its bf16 operands (tiled, as the fused kernels keep
+    them; one C a 256-column slice of a 319-wide weight), with its bias row sums, deterministic
+    (two runs bit-equal); a lone deferred product of each class (here a 256 x 256 and a
+    128 x 256 one) runs as aon_gemm, bit-identical to separate calls."""
+    from aonerf import tiles
+    from aonerf.linalg import batched, gemm
+
+    g = torch.Generator(device="cuda").manual_seed(count + K)
+    As = [tiles.tile((torch.randn((K, 256), device="cuda", generator=g) * 1e-3).to(torch.bfloat16))
+          for _ in range(count)]
+    Bs = [tiles.tile(torch.randn((K, 256), device="cuda", generator=g).to(torch.bfloat16))
+          for _ in range(count)]
+
+    def run():
+        Cs = [torch.zeros((256, 319 if i == 1 else 256), device="cuda") for i in range(count)]
+        rss = [torch.empty((256,), device="cuda") for _ in range(count)]
+        with batched():
+            for i in range(count):
+                gemm(Cs[i], As[i], Bs[i], 256, 256, K, lda=256, a_kc=False, ldb=256, b_kc=False,
+                     ldc=Cs[i].shape[1], rowsum=rss[i], mma_bf16=True, a_tiled=True, b_tiled=True)
+        torch.cuda.synchronize()
+        return Cs, rss
+
+    Cs, rss = run()
+    Cs2, rss2 = run()
+    worst = 0.0
+    for i in range(count):
+        assert torch.equal(Cs[i], Cs2[i]) and torch.equal(rss[i], rss2[i])
+        a64 = bf16_round(tiles.untile(As[i], K).float().cpu())
+        b64 = bf16_round(tiles.untile(Bs[i], K).float().cpu())
+        err = rel_err(Cs[i][:, :256].cpu().numpy(), (a64.T @ b64).numpy())
+        worst = max(worst, err)
+        assert err < 2e-5
+        np.testing.assert_allclose(rss[i].cpu().numpy(), a64.sum(0).numpy(), rtol=0,
+                                   atol=2e-5 * float(a64.abs().sum(0).max()))
+        if i == 1:
+            assert not Cs[i][:, 256:].any()
+    print(f"bf16 dW batch of {count}, K={K}: max-rel err {worst:.2e}")
+
+    # a 128-row product in the set: every product on aon_gemm, bit-identical to separate calls
+    A128 = tiles.tile((torch.randn((K, 128), device="cuda", generator=g) * 1e-3).to(torch.bfloat16))
+    out = []
+    for use_batch in (True, False):
+        C1, C2 = torch.zeros((256, 256), device="cuda"), torch.zeros((128, 256), device="cuda")
+        with batched() if use_batch else torch.no_grad():
+            gemm(C1, As[0], Bs[0], 256, 256, K, lda=256, a_kc=False, ldb=256, b_kc=False,
+                 ldc=256, mma_bf16=True, a_tiled=True, b_tiled=True)
+            gemm(C2, A128, Bs[0], 128, 256, K, lda=128, a_kc=False, ldb=256, b_kc=False,
+                 ldc=256, mma_bf16=True, a_tiled=True, b_tiled=True)
+        out.append((C1, C2))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][0], out[1][0])
+
+
+@pytest.mark.parametrize("K", [70003, 790528])
+def test_bf16_weight_gradient_batch_128_tiles(K):
+    """aon_gemm_batch's 128 x 128-tile class (k_gemm_bf16_dma_batch): one level's views_linear.0
+    (dZv 128 wide x bottleneck 256), skip-layer enc columns (dZ5 x the 128-column zero-padded
+    bf16 pos_enc copy, n_store 63 into columns 256.. of a 319-wide weight) and pts_linears.0
+    (likewise, with its bias row sums) in ONE launch -- each against fp64 products of its bf16
+    operands; the columns past n_store untouched."""
+    from aonerf import tiles
+    from aonerf.linalg import batched, gemm
+
+    g = torch.Generator(device="cuda").manual_seed(K + 1)
+
+    def rnd(w, s=1.0):
+        return (torch.randn((K, w), device="cuda", generator=g) * s).to(torch.bfloat16)
+
+    dzv, bot, dz5, dz0 = rnd(128, 1e-3), rnd(256), rnd(256, 1e-3), rnd(256, 1e-3)
+    enc = torch.zeros((K, 128), device="cuda", dtype=torch.bfloat16)
+    enc[:, :63] = rnd(63)
+    Cv = torch.zeros((128, 283), device="cuda")
+    C5 = torch.full((256, 319), 7.0, device="cuda")
+    C0 = torch.zeros((256, 63), device="cuda")
+    rs_v, rs_0 = torch.empty((128,), device="cuda"), torch.empty((256,), device="cuda")
+    with batched():
+        gemm(Cv, tiles.tile(dzv), tiles.tile(bot), 128, 256, K, lda=128, a_kc=False, ldb=256,
+             b_kc=False, ldc=283, rowsum=rs_v, mma_bf16=True, a_tiled=True, b_tiled=True)
+        gemm(C5[:, 256:], tiles.tile(dz5), tiles.tile(enc), 256, 128, K, lda=256, a_kc=False,
+             ldb=128, b_kc=False, ldc=319, mma_bf16=True, a_tiled=True, b_tiled=True, n_store=63)
+        gemm(C0, tiles.tile(dz0), tiles.tile(enc), 256, 128, K, lda=256, a_kc=False, ldb=128,
+             b_kc=False, ldc=63, rowsum=rs_0, mma_bf16=True, a_tiled=True, b_tiled=True,
+             n_store=63)
+    torch.cuda.synchronize()
+    d = lambda t: t.float().cpu().double()  # noqa: E731
+    checks = [(Cv[:, :256], d(dzv).T @ d(bot)), (C5[:, 256:], d(dz5).T @ d(enc)[:, :63]),
+              (C0, d(dz0).T @ d(enc)[:, :63])]
+    for got, want in checks:
+        err = rel_err(got.cpu().numpy(), want.numpy())
+        print(f"bf16 dW 128-tile batch K={K}: max-rel err {err:.2e}")
+        assert err < 2e-5
+    assert not Cv[:, 256:].any() and torch.equal(C5[:, :256], torch.full((256, 256), 7.0, device="cuda"))
+    for rs, a in ((rs_v, dzv), (rs_0, dz0)):
+        np.testing.assert_allclose(rs.cpu().numpy(), d(a).sum(0).numpy(), rtol=0,
+                                   atol=2e-5 * float(d(a).abs().sum(0).max()))
