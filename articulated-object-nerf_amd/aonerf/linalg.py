@@ -50,12 +50,16 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
                       b_bf16=int(B.dtype == torch.bfloat16), a_tiled=int(bool(a_tiled)),
                       b_tiled=int(bool(b_tiled)), n_store=n_store,
                       exact_fp32=int(bool(exact_fp32)))
-    if (_batch is not None and mma_bf16 and M % 128 == 0 and N % 128 == 0 and K >= 8192
-            and not k_splits and b_rdiv == 1 and A.dtype == torch.bfloat16
-            and B.dtype == torch.bfloat16):
-        # operands kept alive until the flush; class: one 256 x 256 tile, or 128 x 128 tiles
-        cls = 256 if M == 256 and N == 256 else 128
-        if cls == 256 or BATCH128:
+    bf = mma_bf16 and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16
+    f16 = (not mma_bf16 and A.dtype == torch.float32 and B.dtype == torch.float32 and not a_kc
+           and not b_kc and A2 is None and bias is None and mask is None and not relu
+           and not exact_fp32 and n_store in (0, N))
+    if (_batch is not None and (bf or f16) and M % 128 == 0 and N % 128 == 0 and K >= 8192
+            and not k_splits and b_rdiv == 1):
+        # operands kept alive until the flush; class: bf16 one 256 x 256 tile, bf16 128 x 128
+        # tiles, or fp16x3
+        cls = "f16" if f16 else 256 if M == 256 and N == 256 else 128
+        if cls != 128 or BATCH128:
             _batch.append((a, C.device, cls, (A, B, C, rowsum)))
             return
     nbytes = L.lib().aon_gemm_workspace_bytes(ctypes.byref(a))
@@ -72,11 +76,11 @@ BATCH128 = os.environ.get("AONERF_NO_GEMM_BATCH128", "0") != "1"
 
 @contextlib.contextmanager
 def batched():
-    """Defer the bf16 weight-gradient products in whole 128-column tiles issued inside (dW =
-    dZ^T X of pts_linears / bottleneck / views_linear.0, the enc-column products) to
-    aon_gemm_batch launches -- the 256 x 256 ones together, the others together, up to
-    GEMM_BATCH_MAX products of equal K each -- flushed at exit; every other product runs at
-    once.  The deferred products only read kept tensors and write their own dW / db (callers
+    """Defer the weight-gradient products in whole 128-column tiles issued inside (dW = dZ^T X
+    of pts_linears / bottleneck / views_linear.0, the bf16 enc-column products) to
+    aon_gemm_batch launches -- bf16 256 x 256, other bf16, and fp16x3 ones, up to
+    GEMM_BATCH_MAX products of equal K per launch -- flushed at exit; every other product runs
+    at once.  The deferred products only read kept tensors and write their own dW / db (callers
     flush before reading a deferred db), so the reordering is safe."""
     global _batch
     if not BATCH:

@@ -211,7 +211,7 @@ struct TileLoad {
 };
 
 template <bool AKC, bool BKC, bool VA, bool VB>
-__global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
+__device__ __forceinline__ void f16x3_body(const Params& p, int tm, int tn, int z, _Float16* smem) {
   // A's prescale: a constant, or per call from the gradient's max |x| (exact powers of two)
   float sa = p.sa, inv_s = p.inv_s;
   if (p.sa_bits) {
@@ -219,13 +219,8 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
     sa = __fmul_rn(sa, gs);
     inv_s = __fdiv_rn(inv_s, gs);
   }
-  __shared__ __align__(16) _Float16 smem[2 * STAGE];  // 2 stages x (A hi, A lo, B hi, B lo)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  int tm, tn;
-  int tile, z;
-  if (!split_of(p, tile, z)) return;      // padding block of the last chunk group
-  if (!tile_of(p, tile, tm, tn)) return;  // padding block of the last XCD group (uniform exit)
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kbeg = (int64_t)z * p.kchunk;
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
@@ -350,6 +345,15 @@ __global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
     }
 }
 
+template <bool AKC, bool BKC, bool VA, bool VB>
+__global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3(Params p) {
+  __shared__ __align__(16) _Float16 smem[2 * STAGE];  // 2 stages x (A hi, A lo, B hi, B lo)
+  int tm, tn, tile, z;
+  if (!split_of(p, tile, z)) return;      // padding block of the last chunk group
+  if (!tile_of(p, tile, tm, tn)) return;  // padding block of the last XCD group (uniform exit)
+  f16x3_body<AKC, BKC, VA, VB>(p, tm, tn, z, smem);
+}
+
 // split-K: C = epilogue(sum_z part[z]) in z order (deterministic); rowsum likewise.  The loads
 // of 8 consecutive z are issued before their (in-order) adds: a thread walks up to 256 partials
 // spaced M*N apart, and one load at a time left this kernel latency-bound (~50 us at any size).
@@ -422,6 +426,20 @@ struct ParamsBatch {
 
 // the batch's split-K reduce: grid.y = product
 __global__ void k_gemm_reduce_batch(ParamsBatch pb) { reduce_body(pb.p[blockIdx.y], pb.zsplit); }
+
+// fp16x3 weight gradients of one level (aon_gemm_batch): every product's 128 x 128 tiles, chunk z
+// of all of them on one XCD (split_of's order), product b owning tiles tile0[b] .. tile0[b+1]-1
+__global__ __launch_bounds__(THREADS, 2) void k_gemm_f16x3_batch(ParamsBatch pb) {
+  __shared__ __align__(16) _Float16 smem[2 * STAGE];
+  const int T = pb.tile0[pb.count], L = blockIdx.x, x = L & 7, q = L >> 3;
+  const int z = 8 * (q / T) + x, t = q - (q / T) * T;
+  if (z >= pb.zsplit) return;  // padding block of the last chunk group (uniform exit)
+  int b = 0;
+  while (b + 1 < pb.count && t >= pb.tile0[b + 1]) ++b;
+  const Params& p = pb.p[b];
+  const int lt = t - pb.tile0[b];
+  f16x3_body<false, false, true, true>(p, lt % p.tiles_m, lt / p.tiles_m, z, smem);
+}
 
 template <bool AKC, bool BKC, bool VA, bool VB>
 static void launch(const Params& p, dim3 grid, hipStream_t st) {
@@ -1549,21 +1567,48 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
   }
-  for (int64_t k = kbeg + r; k < kend; k += kSkinnyRows) {
-    const int64_t bo = BT ? (k & ~int64_t(15)) * p.ldb + 256 * (n0 >> 4) + 16 * (k & 15) + (n0 & 15)
-                          : k * p.ldb + n0;
-    const uint4 bv = *reinterpret_cast<const uint4*>(B + bo);
+  auto boff = [&](int64_t k) {
+    return BT ? (k & ~int64_t(15)) * p.ldb + 256 * (n0 >> 4) + 16 * (k & 15) + (n0 & 15)
+              : k * p.ldb + n0;
+  };
+  auto row = [&](const uint4& bv, const TA* ar) {
     const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
     float b[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) b[j] = __uint_as_float((j & 1) ? (bw[j >> 1] & 0xffff0000u) : (bw[j >> 1] << 16));
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const float a = static_cast<float>(static_cast<__bf16>(static_cast<float>(A[k * p.lda + m])));
+      const float a = static_cast<float>(static_cast<__bf16>(static_cast<float>(ar[m])));
       rs[m] = __fadd_rn(rs[m], a);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[m][j] = fmaf(a, b[j], acc[m][j]);  // a * b exact in fp32
     }
+  };
+  // SK rows per thread in flight: their loads are issued before the first is consumed (one
+  // dependent load per row left this kernel latency-bound: rgb's 0.27 GB at ~2.2 TB/s); the
+  // rows are still summed in k order (bit-identical)
+#ifndef AON_GEMM_SKINNY_SK
+#define AON_GEMM_SKINNY_SK 4  // 1: one row in flight per thread (the round-3 kernel; A/B)
+#endif
+  constexpr int SK = AON_GEMM_SKINNY_SK;
+  int64_t k = kbeg + r;
+  for (; k + (SK - 1) * kSkinnyRows < kend; k += SK * kSkinnyRows) {
+    uint4 bv[SK];
+    TA av[SK][M];
+#pragma unroll
+    for (int u = 0; u < SK; ++u) {
+      bv[u] = *reinterpret_cast<const uint4*>(B + boff(k + u * kSkinnyRows));
+#pragma unroll
+      for (int m = 0; m < M; ++m) av[u][m] = A[(k + u * kSkinnyRows) * p.lda + m];
+    }
+#pragma unroll
+    for (int u = 0; u < SK; ++u) row(bv[u], av[u]);
+  }
+  for (; k < kend; k += kSkinnyRows) {
+    TA av[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) av[m] = A[k * p.lda + m];
+    row(*reinterpret_cast<const uint4*>(B + boff(k)), av);
   }
   // the 16 row phases of a column group are lanes 16 q .. 16 q + 15 of one wave
 #pragma unroll
@@ -1964,10 +2009,20 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
 // ---- aon_gemm_batch: one level's bf16 weight gradients in two launches (+ their reduces):
 // the one-tile 256 x 256 products on k_gemm_bf16_dma256_batch, the other whole-128 x 128-tile
 // products on k_gemm_bf16_dma_batch; any other product runs as aon_gemm.
-enum { kBatchNone = 0, kBatch256 = 1, kBatch128 = 2 };
+enum { kBatchNone = 0, kBatch256 = 1, kBatch128 = 2, kBatchF16 = 3 };
 
 static int batch_class(const aon_gemm_args* a) {
-  if (!a->mma_bf16 || a->k_splits > 0 || a->K < 8 * 1024) return kBatchNone;
+  if (a->k_splits > 0 || a->K < 8 * 1024) return kBatchNone;
+  if (!a->mma_bf16) {
+    // fp16x3 weight gradients dW = dY^T X: fp32 reduction-major operands in 16-B runs, whole
+    // 128 x 128 tiles, no epilogue beyond accumulate (k_gemm_f16x3<false, false, true, true>)
+    const bool ok = !a->a_bf16 && !a->b_bf16 && !a->a_kc && !a->b_kc && !a->A2 && !a->bias &&
+                    !a->mask && !a->relu && !a->exact_fp32 && a->b_rdiv == 1 &&
+                    a->M % BM == 0 && a->N % BN == 0 && (a->n_store == 0 || a->n_store == a->N) &&
+                    aligned16(a->A) && a->lda % 4 == 0 && aligned16(a->B) && a->ldb % 4 == 0 &&
+                    !f16_copy_path(a) && (a->M / BM) * (a->N / BN) < 512;
+    return ok ? kBatchF16 : kBatchNone;
+  }
   if (bf16_copy256_path(a) && a->M == BM2 && a->N == BM2) return kBatch256;
   if (AON_GEMM_BF_DMA && bf16_copy_path(a) && !bf16_copy256_path(a) &&
       (a->M / BM) * (a->N / BN) < 512)
@@ -1994,10 +2049,12 @@ static BatchPlan plan_class(const aon_gemm_args* a, int count, int cls) {
     pl.tiles += cls == kBatch256 ? 1 : (g->M / BM) * (g->N / BN);
   }
   // 256 x 256 tiles: one workgroup per CU (256 in all), chunks >= 1024 rows; 128 x 128 tiles:
-  // two per CU (512), chunks >= 2048 rows -- each product's chunks longer by the batch size
+  // two per CU (512), chunks >= 2048 rows -- each product's chunks longer by the batch size;
+  // fp16x3: whole rounds of 512 as aon_gemm's split (two when K is long enough)
   const int64_t wgs = cls == kBatch256 ? 256 : 512, minrows = cls == kBatch256 ? 1024 : 2048;
   const int64_t cap = pl.K / minrows < 256 ? pl.K / minrows : 256;
   int64_t s = wgs / pl.tiles < cap ? wgs / pl.tiles : cap;
+  if (cls == kBatchF16 && cap * pl.tiles >= 1024) s = 1024 / pl.tiles;
   s = s >= 8 ? s / 8 * 8 : (s < 1 ? 1 : s);
   pl.kchunk = s > 1 ? ((pl.K + s - 1) / s + BK - 1) / BK * BK : pl.K;
   pl.zs = (pl.K + pl.kchunk - 1) / pl.kchunk;
@@ -2019,11 +2076,13 @@ static bool in_plan(const BatchPlan& pl, int i) {
 
 extern "C" size_t aon_gemm_batch_workspace_bytes(const aon_gemm_args* a, int count) {
   if (!a || count < 1 || count > AON_GEMM_BATCH_MAX) return 0;
-  const BatchPlan p2 = plan_class(a, count, kBatch256), p1 = plan_class(a, count, kBatch128);
+  const BatchPlan p2 = plan_class(a, count, kBatch256), p1 = plan_class(a, count, kBatch128),
+                  pf = plan_class(a, count, kBatchF16);
   // the launches are stream-ordered: one workspace serves each in turn
   size_t m = plan_bytes(a, p2) > plan_bytes(a, p1) ? plan_bytes(a, p2) : plan_bytes(a, p1);
+  m = plan_bytes(a, pf) > m ? plan_bytes(a, pf) : m;
   for (int i = 0; i < count; ++i)
-    if (!in_plan(p2, i) && !in_plan(p1, i)) {
+    if (!in_plan(p2, i) && !in_plan(p1, i) && !in_plan(pf, i)) {
       const size_t b = aon_gemm_workspace_bytes(&a[i]);
       m = b > m ? b : m;
     }
@@ -2059,6 +2118,11 @@ static int run_plan(const aon_gemm_args* a, const BatchPlan& pl, int cls, void* 
     p.C = g->C; p.ldc = g->ldc;
     p.accumulate = g->accumulate;
     p.sa = p.sb = p.inv_s = 1.0f;
+    if (cls == kBatchF16) {
+      AON_REQUIRE(g->a_scale > 0.f && g->b_scale > 0.f, "operand scales must be positive");
+      p.sa = g->a_scale; p.sb = g->b_scale; p.inv_s = 1.0f / (g->a_scale * g->b_scale);
+      p.sa_bits = g->a_amax;
+    }
     p.kchunk = pl.kchunk;
     p.rowsum = g->rowsum;
     p.zsplit = (int)pl.zs;
@@ -2076,7 +2140,8 @@ static int run_plan(const aon_gemm_args* a, const BatchPlan& pl, int cls, void* 
   }
   const dim3 grid((unsigned)(8 * pb.tile0[pl.n] * ((pl.zs + 7) / 8)), 1, 1);
   if (cls == kBatch256) hipLaunchKernelGGL(k_gemm_bf16_dma256_batch, grid, dim3(THREADS2), 0, st, pb);
-  else hipLaunchKernelGGL(k_gemm_bf16_dma_batch, grid, dim3(THREADS), 0, st, pb);
+  else if (cls == kBatch128) hipLaunchKernelGGL(k_gemm_bf16_dma_batch, grid, dim3(THREADS), 0, st, pb);
+  else hipLaunchKernelGGL(k_gemm_f16x3_batch, grid, dim3(THREADS), 0, st, pb);
   if (pl.zs > 1) {
     const int rc = launch_status("aon_gemm_batch");
     if (rc) return rc;
@@ -2095,7 +2160,12 @@ extern "C" int aon_gemm_batch(const aon_gemm_args* a, int count, void* work, siz
                               aon_stream_t stream) {
   AON_REQUIRE(a && count >= 0 && count <= AON_GEMM_BATCH_MAX, "bad batch");
   hipStream_t st = (hipStream_t)stream;
-  const BatchPlan p2 = plan_class(a, count, kBatch256), p1 = plan_class(a, count, kBatch128);
+  const BatchPlan p2 = plan_class(a, count, kBatch256), p1 = plan_class(a, count, kBatch128),
+                  pf = plan_class(a, count, kBatchF16);
+  if (pf.n) {
+    const int rc = run_plan(a, pf, kBatchF16, work, work_bytes, st);
+    if (rc) return rc;
+  }
   if (p2.n) {
     const int rc = run_plan(a, p2, kBatch256, work, work_bytes, st);
     if (rc) return rc;
@@ -2105,7 +2175,7 @@ extern "C" int aon_gemm_batch(const aon_gemm_args* a, int count, void* work, siz
     if (rc) return rc;
   }
   for (int i = 0; i < count; ++i)
-    if (!in_plan(p2, i) && !in_plan(p1, i)) {
+    if (!in_plan(p2, i) && !in_plan(p1, i) && !in_plan(pf, i)) {
       const int rc = aon_gemm(&a[i], work, work_bytes, stream);
       if (rc) return rc;
     }

@@ -419,7 +419,9 @@ int aon_gemm(const aon_gemm_args* args, void* work, size_t work_bytes, aon_strea
  * both operands bf16, M = N = 256, k_splits 0, equal K >= 8192: pts_linears / bottleneck) run
  * as ONE launch of count x (256 / count) K chunks and one split-K reduce -- count times fewer
  * fp32 partials than count launches; the other bf16 products in whole 128 x 128 tiles
- * (views_linear.0, the enc columns) likewise as one launch; the rest one by one as aon_gemm.
+ * (views_linear.0, the enc columns) likewise as one launch, the fp16x3 weight gradients (fp32
+ * reduction-major operands in whole 128 x 128 tiles, no A2 / bias / mask / relu) as one more;
+ * the rest one by one as aon_gemm.
  * Deterministic; the chunking, and so the fp32 summation order, differs from aon_gemm's. */
 #define AON_GEMM_BATCH_MAX 8
 size_t aon_gemm_batch_workspace_bytes(const aon_gemm_args* args, int count);

@@ -443,3 +443,48 @@ def test_bf16_weight_gradient_batch_128_tiles(K):
     for rs, a in ((rs_v, dzv), (rs_0, dz0)):
         np.testing.assert_allclose(rs.cpu().numpy(), d(a).sum(0).numpy(), rtol=0,
                                    atol=2e-5 * float(d(a).abs().sum(0).max()))
+
+
+def test_f16x3_weight_gradient_batch():
+    """aon_gemm_batch's fp16x3 class (k_gemm_f16x3_batch): the parity mode's weight gradients
+    (fp32 tiled operands, the activation prescale 2^-8 and a per-call gradient scale word, one
+    product accumulating) in ONE launch -- each product against fp64 and within 1e-6 of its own
+    aon_gemm launch (the same fp16x3 numerics, other K chunks); deterministic."""
+    from aonerf import tiles
+    from aonerf.linalg import ACT_SCALE, batched, gemm
+
+    K = 70003
+    g = torch.Generator(device="cuda").manual_seed(3)
+    shapes = [(256, 256), (128, 256), (256, 256)]
+    As = [torch.randn((K, m), device="cuda", generator=g) * 1e-3 for m, _ in shapes]
+    Bs = [torch.relu(torch.randn((K, n), device="cuda", generator=g)) for _, n in shapes]
+    C_init = torch.randn((256, 256), device="cuda", generator=g)
+    word = torch.zeros((1,), dtype=torch.int32, device="cuda")
+    from aonerf import _lib as L
+    L.call("aon_absmax", L.ptr(As[0]), As[0].numel(), L.ptr(word), L.stream())
+
+    def run(use_batch):
+        Cs = [torch.zeros((m, n), device="cuda") for m, n in shapes]
+        Cs[2].copy_(C_init)
+        rss = [torch.empty((m,), device="cuda") for m, _ in shapes]
+        with batched() if use_batch else torch.no_grad():
+            for i, (m, n) in enumerate(shapes):
+                gemm(Cs[i], tiles.tile(As[i]), tiles.tile(Bs[i]), m, n, K, lda=m, a_kc=False,
+                     ldb=n, b_kc=False, ldc=n, rowsum=rss[i], accumulate=i == 2, a_scale=1.0,
+                     b_scale=ACT_SCALE, a_amax=word if i == 0 else None, a_tiled=True,
+                     b_tiled=True)
+        torch.cuda.synchronize()
+        return Cs, rss
+
+    (Cb, rb), (Cb2, rb2), (Cs, rs) = run(True), run(True), run(False)
+    for i in range(3):
+        assert torch.equal(Cb[i], Cb2[i]) and torch.equal(rb[i], rb2[i])
+        want = As[i].cpu().double().T @ Bs[i].cpu().double()
+        if i == 2:
+            want += C_init.cpu().double()
+        err = rel_err(Cb[i].cpu().numpy(), want.numpy())
+        err_own = rel_err(Cb[i].cpu().numpy(), Cs[i].cpu().numpy())
+        print(f"f16x3 dW batch product {i}: max-rel err {err:.2e} (vs its own launch {err_own:.2e})")
+        assert err < 2e-6 and err_own < 1e-6
+        np.testing.assert_allclose(rb[i].cpu().numpy(), rs[i].cpu().numpy(), rtol=0,
+                                   atol=1e-6 * float(As[i].abs().sum(0).max()))
