@@ -179,6 +179,12 @@ def contig(t):
 # status word into its device's sticky word, so the re-pack cannot erase an overflow.
 PENDING_PACKS = {}
 _STICKY = {}
+# data pointers of the parameters each pending pack was packed from (the tensor objects an
+# autograd Function sees are not always the optimizer's, their storage is), and per device those of the packs
+# OR-ed into its sticky word: an optimizer step checks only the packs of ITS parameters, so an
+# unrelated model's optimizer neither pays the sync nor consumes (hides) this model's overflow
+PACK_PARAMS = {}
+_STICKY_PARAMS = {}
 
 
 def status_word(buf):
@@ -186,9 +192,10 @@ def status_word(buf):
     return buf.view(torch.int32)[-4]
 
 
-def register_pack(key, buf):
+def register_pack(key, buf, params=()):
     """Call BEFORE (re)packing ``buf`` on the current stream: keep the status a pending pack
-    still holds (stream-ordered device OR, no sync), then mark ``buf`` pending."""
+    still holds (stream-ordered device OR, no sync), then mark ``buf`` pending.  ``params``: the
+    parameter tensors packed into ``buf`` (empty: the pack concerns every optimizer)."""
     dev = str(buf.device)
     k = (key[0], key[1], dev)
     if k in PENDING_PACKS:
@@ -196,7 +203,22 @@ def register_pack(key, buf):
         if w is None:
             w = _STICKY[dev] = torch.zeros((), dtype=torch.int32, device=buf.device)
         w.bitwise_or_(status_word(PENDING_PACKS[k]))
+        _STICKY_PARAMS.setdefault(dev, set()).update(PACK_PARAMS.get(k) or {None})
     PENDING_PACKS[k] = buf
+    PACK_PARAMS[k] = frozenset(p.data_ptr() for p in params)
+
+
+def _concerns(ids, param_ids):
+    # a pack registered without parameters (or a sticky word holding one) concerns everyone
+    return param_ids is None or not ids or None in ids or bool(ids & param_ids)
+
+
+def has_pending(devices=None, param_ids=None):
+    """Whether check_pending(devices, param_ids) would look at anything (no sync)."""
+    return (any((devices is None or k[2] in devices) and _concerns(PACK_PARAMS.get(k), param_ids)
+                for k in PENDING_PACKS) or
+            any((devices is None or d in devices) and _concerns(_STICKY_PARAMS.get(d), param_ids)
+                for d in _STICKY))
 
 
 def range_overflow(bufs):
@@ -207,14 +229,21 @@ def range_overflow(bufs):
     return bool(torch.stack([status_word(b) for b in bufs]).any().item())
 
 
-def check_pending(devices=None):
-    """Consume the pending training packs (and sticky words) of ``devices`` (str, None = all):
+def check_pending(devices=None, param_ids=None):
+    """Consume the pending training packs (and sticky words) of ``devices`` (str, None = all)
+    that concern ``param_ids`` (data pointers of an optimizer's parameters; None = all):
     True if any saw an overflow since the last check (one sync; False without a sync when
     nothing is pending)."""
-    keys = [k for k in PENDING_PACKS if devices is None or k[2] in devices]
-    words = [status_word(PENDING_PACKS.pop(k)) for k in keys]
-    for dev in [d for d in _STICKY if devices is None or d in devices]:
+    keys = [k for k in PENDING_PACKS if (devices is None or k[2] in devices)
+            and _concerns(PACK_PARAMS.get(k), param_ids)]
+    words = []
+    for k in keys:
+        words.append(status_word(PENDING_PACKS.pop(k)))
+        PACK_PARAMS.pop(k, None)
+    for dev in [d for d in _STICKY if (devices is None or d in devices)
+                and _concerns(_STICKY_PARAMS.get(d), param_ids)]:
         words.append(_STICKY.pop(dev))
+        _STICKY_PARAMS.pop(dev, None)
     if not words:
         return False
     return bool(torch.stack(words).any().item())

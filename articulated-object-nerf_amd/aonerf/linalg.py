@@ -60,7 +60,17 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
         # tiles, or fp16x3
         cls = "f16" if f16 else 256 if M == 256 and N == 256 else 128
         if cls != 128 or BATCH128:
-            _batch.append((a, C.device, cls, (A, B, C, rowsum)))
+            writes = [_span(C)] + ([_span(rowsum)] if rowsum is not None else [])
+            reads = [_span(A), _span(B)] + ([_span(a_amax)] if a_amax is not None else [])
+            if any(_overlaps(w, it[4]) or _overlaps(w, it[5]) or _overlaps(r, it[4])
+                   for it in _batch for w in writes for r in reads):
+                # a pending product writes what this one reads or writes, or reads what it
+                # writes (incl. accumulate into a pending C): run the pending ones first
+                _flush(_batch)
+                _batch.clear()
+            # every operand (a_amax too: a temporary scale word must not be recycled by the
+            # caching allocator before the flush) stays alive until the product runs
+            _batch.append((a, C.device, cls, (A, B, C, rowsum, a_amax), writes, reads))
             return
     nbytes = L.lib().aon_gemm_workspace_bytes(ctypes.byref(a))
     ws = _workspace(nbytes, C.device) if nbytes else None
@@ -92,6 +102,44 @@ def batched():
         items = _batch
     finally:
         _batch = outer
+    _flush(items)
+
+
+def _span(t):
+    """What a product may touch of a tensor view: (start, end) bytes, and for a 2-D view with
+    unit column stride also (storage base, row pitch, first row, rows, first byte in the row,
+    bytes per row), so that column slices of one dW tensor do not count as overlapping."""
+    if t.numel() == 0:
+        return (0, 0, None)
+    es = t.element_size()
+    last = sum((n - 1) * st for n, st in zip(t.shape, t.stride()))
+    start = t.data_ptr()
+    grid = None
+    if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]:
+        base = t.untyped_storage().data_ptr()
+        pitch = t.stride(0) * es
+        off = start - base
+        grid = (base, pitch, off // pitch, t.shape[0], off % pitch, t.shape[1] * es)
+    return (start, start + (last + 1) * es, grid)
+
+
+def _overlaps(x, ys):
+    for y in ys:
+        if not (x[0] < y[1] and y[0] < x[1]):
+            continue
+        gx, gy = x[2], y[2]
+        if (gx is not None and gy is not None and gx[:2] == gy[:2]
+                and gx[4] + gx[5] <= gx[1] and gy[4] + gy[5] <= gy[1]):
+            rows = gx[2] < gy[2] + gy[3] and gy[2] < gx[2] + gx[3]
+            cols = gx[4] < gy[4] + gy[5] and gy[4] < gx[4] + gx[5]
+            if not (rows and cols):
+                continue
+        return True
+    return False
+
+
+def _flush(items):
+    """Launch deferred products grouped by class and K, GEMM_BATCH_MAX per aon_gemm_batch."""
     groups = {}
     for it in items:
         groups.setdefault((it[2], it[0].K, str(it[1])), []).append(it)

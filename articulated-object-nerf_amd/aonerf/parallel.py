@@ -87,10 +87,12 @@ class GradAllReduce:
         self.sizes = [p.numel() for p in self.params]
         self.flat = None
         self.flat32 = None
+        self.calls = 0  # collectives issued (bench.py records it with the DDP step)
 
     def __call__(self):
         if not dist.is_initialized():  # (a process group of one still runs the all-reduce)
             return
+        self.calls += 1
         world = dist.get_world_size(self.group)
         dev = self.params[0].device
         if self.flat is None or self.flat.device != dev:

@@ -162,15 +162,16 @@ def _params_struct(P):
     return prm
 
 
-def _buffer(key, nbytes, dev, guard=False):
+def _buffer(key, nbytes, dev, guard=False, params=()):
     # one buffer per kind and device: a pack and the kernel reading it are stream-ordered.
-    # guard: a packed weight stream whose range-status word the next Adam.step checks
+    # guard: a packed weight stream whose range-status word the next optimizer step over
+    # ``params`` (the packed parameters) checks
     buf = _packed.get((key, str(dev)))
     if buf is None:
         buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
         _packed[(key, str(dev))] = buf
     if guard:
-        L.register_pack(("train", key), buf)
+        L.register_pack(("train", key), buf, params)
     return buf
 
 
@@ -185,20 +186,25 @@ _RANGE_MSG = ("a fp16x3 training kernel met a value beyond its fp16 hi/lo range 
               "operands carry a 2^-8 scale (range 1.6e7), or in train.PRECISION = 'bf16'.")
 
 
-def check_range(devices=None):
-    """Raise FloatingPointError if a fused fp16x3 training kernel on ``devices`` overflowed since
-    the last check (consumes the pending packs)."""
-    if RANGE_CHECK and L.check_pending(devices):
+def check_range(devices=None, params=None):
+    """Raise FloatingPointError if a fused fp16x3 training kernel on ``devices`` that packed any
+    of ``params`` (None: any) overflowed since the last check (consumes those pending packs)."""
+    ids = None if params is None else {p.data_ptr() for p in params}
+    if RANGE_CHECK and L.check_pending(devices, ids):
         raise FloatingPointError(_RANGE_MSG)
 
 
 def _optimizer_step_pre_hook(optimizer, args, kwargs):
     # the reference trains through Lightning with torch.optim.Adam (configure_optimizers,
-    # model.py:386-389): the guard must hold for any optimizer, not only aonerf's Adam
+    # model.py:386-389): the guard must hold for any optimizer, not only aonerf's Adam -- but only
+    # for the packs of the parameters it steps (ADVICE r03): an unrelated optimizer neither pays
+    # the sync nor consumes this model's overflow
     if not L.PENDING_PACKS and not L._STICKY:
         return
-    devs = {str(p.device) for g in optimizer.param_groups for p in g["params"]}
-    check_range(devs)
+    params = [p for g in optimizer.param_groups for p in g["params"]]
+    devs = {str(p.device) for p in params}
+    if L.has_pending(devs, {p.data_ptr() for p in params}):
+        check_range(devs, params)
 
 
 _HOOK = _torch_optim.register_optimizer_step_pre_hook(_optimizer_step_pre_hook)
@@ -210,7 +216,7 @@ def _pack(P, dev, tag="", bf16=False):
     buffer per level (its range-status word must survive until the optimizer step)."""
     prec = L.PREC_BF16 if bf16 else L.PREC["f16x3"]
     buf = _buffer(f"fwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_packed_bytes(prec), dev,
-                  guard=not bf16)
+                  guard=not bf16, params=[t for wb in P for t in wb])
     L.call("aon_mlp_pack", L.ctypes.byref(_params_struct(P)), prec, L.ptr(buf), L.stream(dev))
     return buf
 
@@ -218,7 +224,7 @@ def _pack(P, dev, tag="", bf16=False):
 def _pack_bwd(P, dev, tag="", bf16=False):
     """The transposed weight stream of the fused backward chain (aon_mlp_bwd_pack[_bf16])."""
     buf = _buffer(f"bwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_bwd_packed_bytes(), dev,
-                  guard=not bf16)
+                  guard=not bf16, params=[t for wb in P for t in wb])
     L.call("aon_mlp_bwd_pack_bf16" if bf16 else "aon_mlp_bwd_pack",
            L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
     return buf
@@ -473,7 +479,7 @@ class Adam:
 
     @torch.no_grad()
     def step(self, lr=None):
-        check_range({str(p.device) for p in self.params})
+        check_range({str(p.device) for p in self.params}, self.params)
         self.step_count += 1
         for p in self.params:
             if p.grad is None:

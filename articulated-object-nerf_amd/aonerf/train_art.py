@@ -174,15 +174,16 @@ def _params_struct(P, fb=None):
     return prm
 
 
-def _buffer(key, nbytes, dev, guard=False):
+def _buffer(key, nbytes, dev, guard=False, params=()):
     # one buffer per kind and device: a pack and the kernel reading it are stream-ordered.
-    # guard: a packed weight stream whose range-status word train.Adam.step checks
+    # guard: a packed weight stream whose range-status word the next optimizer step over
+    # ``params`` (the packed parameters) checks
     buf = _packed.get((key, str(dev)))
     if buf is None:
         buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
         _packed[(key, str(dev))] = buf
     if guard:
-        L.register_pack(("train_art", key), buf)
+        L.register_pack(("train_art", key), buf, params)
     return buf
 
 
@@ -198,7 +199,7 @@ def _pack(geo, P, lat, tag="", bf16=False):
           PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
           VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
     buf = _buffer(f"fwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_art_packed_bytes(), dev,
-                  guard=True)
+                  guard=True, params=[t for wb in P for t in wb])
     L.call("aon_mlp_art_pack_bf16" if bf16 else "aon_mlp_art_pack",
            L.ctypes.byref(_params_struct(P, fb)), L.ptr(buf), L.stream(dev))
     return buf
@@ -207,7 +208,7 @@ def _pack(geo, P, lat, tag="", bf16=False):
 def _pack_bwd(P, dev, tag="", bf16=False):
     """The transposed weight stream of the fused backward chain (aon_mlp_art_bwd_pack[_bf16])."""
     buf = _buffer(f"bwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_art_bwd_packed_bytes(), dev,
-                  guard=not bf16)
+                  guard=not bf16, params=[t for wb in P for t in wb])
     L.call("aon_mlp_art_bwd_pack_bf16" if bf16 else "aon_mlp_art_bwd_pack",
            L.ctypes.byref(_params_struct(P)), L.ptr(buf), L.stream(dev))
     return buf

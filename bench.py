@@ -16,8 +16,14 @@ synchronize on both sides, max over ranks):
 each with its own ms_per_step and roofline (MFMA fraction of the fine-level MLP kernels,
 HBM byte fractions of the training kernels counting the stored activations).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32] [--backend gloo]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+``--gpus N`` (N > 1) without an external launcher spawns the N ranks itself, one process per
+GPU, before anything touches the GPU (aonerf.launch; run.py:101-111 takes devices=num_gpus the
+same way); under torchrun the launcher's WORLD_SIZE must equal N.  ``--backend gloo`` lets the
+ranks share one device (the one-GPU test box rehearses the N-rank path that way; RCCL refuses
+two ranks on one device); the default is nccl (RCCL over xGMI).
 
 A step = generate the frame's rays, coarse sample, coarse MLP, the fused coarse composite +
 pdf resample (aon_composite_march), fine MLP, composite, gather.  value = 307,200 rays x steps / max-over-ranks wall time.  Rank 0 prints
@@ -70,17 +76,21 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_TFLOPS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-chunks", type=int, default=4, help="3840-ray chunks in the CPU sample")
+    ap.add_argument("--cpu-chunks", type=int, default=16,
+                    help="3840-ray chunks in the CPU sample (SURVEY.md 8(d): 16)")
     ap.add_argument("--no-extra", action="store_true", help="headline C2 render only")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend for N > 1 (gloo: ranks may share one GPU)")
+    ap.add_argument("--dump-frame", default=None,
+                    help="rank 0 saves the gathered frame of the last timed step (.npy)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from aonerf import launch
+
+    if args.gpus > 1 and not launch.launched_externally():
+        # one process per GPU, started before any GPU call in this process
+        sys.exit(launch.spawn_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus))
+    world, rank, local_rank, _ = launch.init_rank(args.backend, expect_world=args.gpus)
 
     from aonerf.model import NeRF
     from aonerf.parallel import render_frame_sharded
@@ -107,11 +117,9 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], device="cuda")
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = el.item()
+    elapsed = launch.max_over_ranks(time.perf_counter() - t0)
+    if rank == 0 and args.dump_frame:
+        np.save(args.dump_frame, frame.cpu().numpy())
 
     # per-launch kernel times from HIP events on the launch stream
     def avg_ms(key):
@@ -155,6 +163,7 @@ def main():
         "value": value, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "backend": args.backend if world > 1 else None,
         "dtype": "fp32" if args.precision == "fp32" else "f16x3 (fp16 hi/lo split MFMA, fp32 accumulate)",
         "data": "synthetic",
         "config": {"workload": "sapien vanilla 640x480 frame render, 64c+128f (65+193 MLP "
@@ -221,10 +230,9 @@ def timed(step, steps, warmup, world):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], device="cuda")
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    return el.item()
+    from aonerf import launch
+
+    return launch.max_over_ranks(time.perf_counter() - t0)
 
 
 def ev_ms(timers, key):
@@ -355,7 +363,7 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
     from aonerf.render import create_spheric_poses, sapien_focal
     from aonerf.synthetic import init_like_reference
 
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", torch.cuda.current_device())  # (gloo ranks may share one GPU)
     nrays = 4096
     if art:
         from aonerf import train_art
@@ -409,6 +417,21 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
         train.PRECISION = old_prec
         if art:
             train_art.PRECISION = old_art
+    ddp = None
+    if world > 1:
+        # the all-reduce is part of every timed step: the ranks draw different batches, so their
+        # parameters stay identical after Adam only if every step averaged the gradients
+        import hashlib
+
+        flat = torch.cat([p.detach().reshape(-1).float() for p in params]).cpu().numpy()
+        digests = [None] * world
+        dist.all_gather_object(digests, hashlib.sha256(flat.tobytes()).hexdigest())
+        ddp = {"collective": "GradAllReduce (one flat-bucket all_reduce per step)",
+               "backend": dist.get_backend(), "world": world,
+               "bucket_dtype": "bf16" if precision == "bf16" else "fp32",
+               "bucket_values": sum(sync.sizes), "calls": sync.calls,
+               "params_identical_across_ranks": len(set(digests)) == 1,
+               "param_sha256_rank0": digests[0]}
     mac = ART_MAC_ISSUED if art else MAC_PER_SAMPLE
     samples = nrays * (NC + 1 + NC + 1 + NF)
     ms = el / args.steps * 1e3
@@ -432,6 +455,8 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
            "roofline": {"bound": "hbm+mfma", "kernel": "whole step (3 x forward FLOP)",
                         "achieved": ach, "peak": TRAIN_PEAK[precision], "unit": "TFLOP/s",
                         "frac": ach / TRAIN_PEAK[precision]}}
+    if ddp is not None:
+        rec["ddp"] = ddp
     if art and precision == "bf16":
         rec["roofline"]["note"] = ("the articulated bf16 mode keeps its forward in fp16x3 "
                                    "(train_art.BF16_TRUNK = False: 3 fp16 products per MAC, peak "

@@ -403,8 +403,10 @@ typedef struct aon_gemm_args {
    * pos_enc copy, 63 -> 128 columns) updates only the real columns of dW; n_store < N on the
    * bf16 LDS-DMA path only (both operands bf16, M and N multiples of 128) */
   int64_t n_store;
-  /* exact_fp32 = 1: compute in exact fp32 fmaf, k in order (deterministic) instead of the fp16x3
-   * MFMA split -- tiny products only (M N <= 65536, K <= 1024, no A2 / mask / relu / rowsum /
+  /* exact_fp32 = 1: compute in exact fp32 fmaf instead of the fp16x3 MFMA split, in a fixed
+   * (deterministic) order: K <= 16 one fma chain in k order per output; K > 16 one wave per
+   * output, lane-strided partial chains (lane l sums k = l, l + 64, ...) combined by a fixed
+   * xor-butterfly -- not k order -- tiny products only (M N <= 65536, K <= 1024, no A2 / mask / relu / rowsum /
    * a_amax / tiled operands): the bf16 training mode's latent-code terms, which the 128 x 128
    * tiled kernel ran at 17-27 us each */
   int exact_fp32;

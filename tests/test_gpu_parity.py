@@ -737,14 +737,16 @@ def test_composite_march_equals_two_kernels(S, Ns):
         np.testing.assert_array_equal(npy(t1[:64]), t_ref.numpy())
 
 
-def test_composite_march_ray_loop():
-    """The fused kernel's grid caps at 65,536 workgroups and loops: a 270,000-ray launch equals
-    900-ray launches bit for bit."""
+@pytest.mark.parametrize("B,S,Ns", [(600000, 65, 128), (270000, 65, 96)])
+def test_composite_march_ray_loop(B, S, Ns):
+    """The fused kernels' grids cap at 65,536 workgroups and loop: k_march_rows
+    (S = 65, Ns = 128: 8 rays per workgroup) loops only past 524,288 rays -- an 800x800 frame --
+    so it runs at 600,000 rays; the one-ray-per-wave k_composite_march (any other shape) at
+    270,000.  Each whole launch equals 900-ray launches bit for bit."""
     from aonerf import _lib as L
     from aonerf import helper
 
     g = torch.Generator().manual_seed(5)
-    B, S, Ns = 270000, 65, 128
     t = cuda(torch.sort(2.0 + 4.0 * torch.rand((B, S), generator=g), -1).values)
     raw = cuda(torch.cat([torch.rand((B, S, 3), generator=g), 3.0 * torch.rand((B, S, 1), generator=g)],
                          -1).reshape(-1, 4))

@@ -1,0 +1,74 @@
+"""linalg.batched() deferral bookkeeping (CPU): deferred products keep every operand
+alive (a_amax included) and a product that reads or writes what a pending product writes (or
+writes what one reads, or accumulates into a pending C) flushes the pending ones first; column
+slices of one dW tensor do not count as overlapping.  No kernel runs: _flush is recorded."""
+import torch
+
+from aonerf import linalg
+
+
+def _rec(monkeypatch):
+    log = []
+    monkeypatch.setattr(linalg, "_flush", lambda items: log.append([it[3][2] for it in items]))
+    return log
+
+
+def _dw(C, A, B, **kw):
+    M, N, K = C.shape[0], C.shape[1], A.shape[0]
+    linalg.gemm(C, A, B, M, N, K, lda=A.shape[1], a_kc=False, ldb=B.shape[1], b_kc=False,
+                ldc=C.stride(0), mma_bf16=True, **kw)
+
+
+def test_disjoint_products_share_one_flush(monkeypatch):
+    log = _rec(monkeypatch)
+    K = 8192
+    A = torch.zeros(K, 256, dtype=torch.bfloat16)
+    B = torch.zeros(K, 512, dtype=torch.bfloat16)
+    C = torch.zeros(256, 512)
+    with linalg.batched():
+        _dw(C[:, :256], A, B[:, :256])
+        _dw(C[:, 256:], A, B[:, 256:])  # other columns of the same dW: no conflict
+    assert len(log) == 1 and len(log[0]) == 2
+
+
+def test_accumulate_into_pending_output_flushes_first(monkeypatch):
+    log = _rec(monkeypatch)
+    K = 8192
+    A = torch.zeros(K, 256, dtype=torch.bfloat16)
+    B = torch.zeros(K, 256, dtype=torch.bfloat16)
+    C = torch.zeros(256, 256)
+    with linalg.batched():
+        _dw(C, A, B)
+        _dw(C, A, B, accumulate=True)
+    assert [len(g) for g in log] == [1, 1]
+
+
+def test_read_after_pending_write_flushes_first(monkeypatch):
+    log = _rec(monkeypatch)
+    K = 8192
+    A = torch.zeros(K, 256)
+    buf = torch.zeros(K, 256)  # fp16x3 class: fp32 operands
+    with linalg.batched():
+        linalg.gemm(buf[:256], A, A, 256, 256, K, lda=256, a_kc=False, ldb=256, b_kc=False, ldc=256)
+        other = torch.zeros(256, 256)
+        linalg.gemm(other, A, torch.zeros(K, 256), 256, 256, K, lda=256, a_kc=False, ldb=256,
+                    b_kc=False, ldc=256)
+        assert log == []  # independent
+        linalg.gemm(torch.zeros(256, 256), A, buf, 256, 256, K, lda=256, a_kc=False, ldb=256,
+                    b_kc=False, ldc=256)  # reads what the first writes
+        assert [len(g) for g in log] == [2]
+    assert [len(g) for g in log] == [2, 1]
+
+
+def test_a_amax_kept_alive(monkeypatch):
+    seen = []
+    monkeypatch.setattr(linalg, "_flush", lambda items: seen.extend(items))
+    K = 8192
+    A = torch.zeros(K, 256)
+    B = torch.zeros(K, 256)
+    C = torch.zeros(256, 256)
+    amax = torch.zeros(1, dtype=torch.int32)
+    with linalg.batched():
+        linalg.gemm(C, A, B, 256, 256, K, lda=256, a_kc=False, ldb=256, b_kc=False, ldc=256,
+                    a_amax=amax)
+    assert len(seen) == 1 and seen[0][3][4] is amax

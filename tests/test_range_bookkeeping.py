@@ -16,11 +16,11 @@ def _buf(status=0):
 def L():
     from aonerf import _lib
 
-    _lib.PENDING_PACKS.clear()
-    _lib._STICKY.clear()
+    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib._STICKY_PARAMS):
+        d.clear()
     yield _lib
-    _lib.PENDING_PACKS.clear()
-    _lib._STICKY.clear()
+    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib._STICKY_PARAMS):
+        d.clear()
 
 
 def test_pending_consumed_once(L):
@@ -60,3 +60,39 @@ def test_torch_optimizer_hook_refuses(L):
     opt.step()  # consumed: the next step goes through
     assert torch.allclose(p.detach(), torch.full((3,), 0.9))
     assert train.RANGE_CHECK
+
+
+def test_hook_limited_to_packed_parameters(L):
+    """an optimizer over parameters no pending pack was packed from neither raises
+    nor consumes the overflow; the model's own optimizer then still refuses its step."""
+    from aonerf import train  # noqa: F401  (installs the hook)
+
+    mine = torch.nn.Parameter(torch.ones(3))
+    other = torch.nn.Parameter(torch.ones(3))
+    for p in (mine, other):
+        p.grad = torch.ones(3)
+    L.register_pack(("train", "fwd65"), _buf(1), [mine])
+    torch.optim.SGD([other], lr=0.1).step()  # unrelated model: goes through
+    assert torch.allclose(other.detach(), torch.full((3,), 0.9))
+    assert L.PENDING_PACKS  # not consumed
+    with pytest.raises(FloatingPointError):
+        torch.optim.SGD([mine], lr=0.1).step()
+    assert torch.equal(mine.detach(), torch.ones(3))
+
+
+def test_sticky_keeps_its_parameters(L):
+    from aonerf import train  # noqa: F401
+
+    mine = torch.nn.Parameter(torch.ones(3))
+    other = torch.nn.Parameter(torch.ones(3))
+    for p in (mine, other):
+        p.grad = torch.ones(3)
+    b = _buf(1)
+    L.register_pack(("train", "fwd65"), b, [mine])
+    L.register_pack(("train", "fwd65"), b, [mine])  # re-pack: the 1 goes to the sticky word
+    b.view(torch.int32)[-4] = 0
+    torch.optim.SGD([other], lr=0.1).step()
+    assert L._STICKY
+    with pytest.raises(FloatingPointError):
+        torch.optim.SGD([mine], lr=0.1).step()
+    assert not L._STICKY and not L.PENDING_PACKS

@@ -7,7 +7,8 @@ model_autodecoder.py:395-477: NeRF_AE_Art + CodeLibraryArticulated, latent regul
 over the MLPs and the code tables).
 
     python tools/bench_train.py [--model vanilla|art] [--rays 4096] [--steps 10] [--warmup 3]
-    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_train.py
+    python tools/bench_train.py --gpus N [--backend gloo]     (spawns the N ranks itself)
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_train.py --gpus N
 
 A step = draw a batch of pixels of a synthetic 640x480 view (8 poses of create_spheric_poses,
 target image PCG64 seed 3), coarse + fine training forward, loss, HIP backward, gradient
@@ -42,14 +43,14 @@ def main():
     ap.add_argument("--max-steps", type=int, default=200000, help="schedule length (run_max_steps)")
     ap.add_argument("--precision", choices=("f16x3", "bf16"), default="f16x3",
                     help="train.PRECISION of the vanilla step (bf16: C5's bf16 mode)")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     args = ap.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from aonerf import launch
+
+    if args.gpus > 1 and not launch.launched_externally():
+        sys.exit(launch.spawn_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus))
+    world, rank, local_rank, dev = launch.init_rank(args.backend, expect_world=args.gpus)
     from aonerf import train
     from aonerf.model import NeRF
 
@@ -59,7 +60,6 @@ def main():
     from aonerf.render import create_spheric_poses, sapien_focal
     from aonerf.synthetic import init_like_reference  # same initial weights as bench.py
 
-    dev = torch.device("cuda", local_rank)
     art = args.model == "art"
     if art:
         import types
@@ -117,11 +117,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
+    dt = launch.max_over_ranks(time.perf_counter() - t0)
     rays = args.rays * args.steps * world
     flop = 3 * 2 * MAC[args.model] * (65 + 193) * rays
     if rank == 0:
