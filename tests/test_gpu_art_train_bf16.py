@@ -202,22 +202,11 @@ def _art_trajectory_gpu(precision, batch, steps, lr, trunk=False):
         train_art.PRECISION, train_art.BF16_TRUNK = old
 
 
-def test_art_bf16_loss_trajectory():
-    """20 Adam steps (lr 2e-4 over the MLPs and the code library, eval sampling so every run
-    sees the same schedule) on a 128-ray batch with a colour-ramp target (loss 0.169 -> 0.106):
-    the f16x3 trajectory tracks the fp32 oracle's (torch autograd + torch.optim.Adam on the
-    reference's arithmetic) within 5e-3 relative at every step, the bf16 one (both forward
-    numerics) within 2%.  The run is sensitive to the last bits: the fp64 oracle itself parts
-    from the fp32 one by 9.7e-4 (printed), and the f16x3 run measured 1.05e-3 with f16x3
-    latent-term GEMMs, 3.0e-3 with exact-fp32 ones (k_gemm_small_f32); bf16 2.0e-3 / 6.1e-3,
-    bf16 trunk 4.9e-3 / 6.3e-3.  At lr 1e-3 the articulated
-    run's loss oscillates on this target and even the f16x3 run parted from the fp32 oracle by
-    26% within 10 steps (profiles/r03/art_bf16/traj_lr1e-3.log), so a step-for-step gate is set
-    where the trajectory is smooth."""
+def _traj_batch():
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, sapien_focal
 
-    H, Wd, steps, lr = 48, 64, 20, 2e-4
+    H, Wd = 48, 64
     rays = frame_rays(torch.as_tensor(create_spheric_poses(4.0)[2]), H, Wd, sapien_focal(H))
     sel = torch.arange(0, H * Wd, 24, device="cuda")
     batch = {k: v[sel].contiguous() for k, v in rays.items()}
@@ -228,41 +217,95 @@ def test_art_bf16_loss_trajectory():
     # trajectory's relative spread is the noise floor): a smooth colour ramp over the pixels
     g = torch.linspace(0.0, 1.0, batch["rays_o"].shape[0], device="cuda")
     batch["target"] = torch.stack([g, 1.0 - g, 0.5 + 0.4 * torch.sin(12.0 * g)], -1).contiguous()
-    # the oracle trajectories (torch autograd + torch.optim.Adam): fp32 (the reference's
-    # arithmetic) and fp64 (their spread is the envelope any fp32-class run sits in)
-    traj = {}
-    for dtype in (torch.float32, torch.float64):
-        params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
-                  for p in O.split_state_dict(W.art_state_dict(0))]
-        tables = {k: torch.from_numpy(v).to(dtype).requires_grad_(True)
-                  for k, v in W.code_library_state_dict(0).items()}
-        flat = [v for p in params for v in p.values()] + list(tables.values())
-        opt = torch.optim.Adam(flat, lr=lr, betas=(0.9, 0.999))
-        rc = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
-        tgt = batch["target"].cpu().to(dtype)
-        out = []
-        for _ in range(steps):
-            opt.zero_grad()
-            loss = O.art_training_loss(params, tables, rc, tgt, 7, 3, False, True, 2.0, 6.0)[0]
-            loss.backward()
-            opt.step()
-            out.append(loss.item())
-        traj[dtype] = np.array(out)
-    ref, ref64 = traj[torch.float32], traj[torch.float64]
+    return batch
+
+
+def _oracle_trajectory(batch, steps, lr, dtype, perturb_seed=None):
+    """The oracle's trajectory (torch autograd + torch.optim.Adam on the reference's arithmetic,
+    model_autodecoder.py:395-477): fp32 = the reference, fp64 = its exact-arithmetic limit.
+    perturb_seed: every MLP weight multiplied by (1 + 2^-24 n), n ~ N(0, 1) -- an fp32 run
+    that differs from the reference by one rounding per weight, as any re-associated fp32-class
+    evaluation does."""
+    gen = torch.Generator().manual_seed(perturb_seed) if perturb_seed is not None else None
+
+    def leaf(v):
+        v = torch.as_tensor(v)
+        if gen is not None:
+            v = v.double() * (1 + 2.0 ** -24 * torch.randn(v.shape, generator=gen, dtype=torch.float64))
+        return v.to(dtype).requires_grad_(True)
+
+    params = [{k: leaf(v) for k, v in p.items()} for p in O.split_state_dict(W.art_state_dict(0))]
+    tables = {k: torch.from_numpy(v).to(dtype).requires_grad_(True)
+              for k, v in W.code_library_state_dict(0).items()}
+    flat = [v for p in params for v in p.values()] + list(tables.values())
+    opt = torch.optim.Adam(flat, lr=lr, betas=(0.9, 0.999))
+    rc = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
+    tgt = batch["target"].cpu().to(dtype)
+    out = []
+    for _ in range(steps):
+        opt.zero_grad()
+        loss = O.art_training_loss(params, tables, rc, tgt, 7, 3, False, True, 2.0, 6.0)[0]
+        loss.backward()
+        opt.step()
+        out.append(loss.item())
+    return np.array(out)
+
+
+def test_art_bf16_loss_trajectory():
+    """20 Adam steps (lr 2e-4 over the MLPs and the code library, eval sampling so every run
+    sees the same schedule) on a 128-ray batch with a colour-ramp target (loss 0.169 -> 0.106):
+    the f16x3 trajectory tracks the fp32 oracle's within max(2 env, 1e-3) relative at every
+    step, env = the fp64 oracle's own distance from the fp32 one (9.7e-4, printed; f16x3 measured
+    1.05e-3 with f16x3 latent-term GEMMs), the bf16 ones (both forward numerics) within 2%
+    (measured 2.0e-3 / 6.1e-3, bf16 trunk 4.9e-3 / 6.3e-3).  At lr 1e-3 the reference's own
+    trajectory is chaotic: test_art_trajectory_lr1e3_is_the_references_chaos."""
+    steps, lr = 20, 2e-4
+    batch = _traj_batch()
+    ref = _oracle_trajectory(batch, steps, lr, torch.float32)
+    ref64 = _oracle_trajectory(batch, steps, lr, torch.float64)
     f16 = _art_trajectory_gpu("f16x3", batch, steps, lr)
     bf = _art_trajectory_gpu("bf16", batch, steps, lr)
     bft = _art_trajectory_gpu("bf16", batch, steps, lr, trunk=True)
+    env = float(np.abs(ref64 / ref - 1).max())
     for i in range(0, steps, 4):
         print(f"step {i:2d}: oracle {ref[i]:.6f}  f16x3 {f16[i]:.6f}  bf16 {bf[i]:.6f}  "
               f"bf16 trunk {bft[i]:.6f}")
     print(f"final: oracle {ref[-1]:.6f}  f16x3 {f16[-1]:.6f}  bf16 {bf[-1]:.6f}  bf16 trunk "
-          f"{bft[-1]:.6f}; max rel to the fp32 oracle: fp64 oracle {np.abs(ref64 / ref - 1).max():.2e}  "
-          f"f16x3 {np.abs(f16 / ref - 1).max():.2e}  bf16 {np.abs(bf / ref - 1).max():.2e}  "
-          f"bf16 trunk {np.abs(bft / ref - 1).max():.2e}")
+          f"{bft[-1]:.6f}; max rel to the fp32 oracle: fp64 oracle {env:.2e}  "
+          f"f16x3 {np.abs(f16 / ref - 1).max():.2e} (gate {max(2 * env, 1e-3):.2e})  "
+          f"bf16 {np.abs(bf / ref - 1).max():.2e}  bf16 trunk {np.abs(bft / ref - 1).max():.2e}")
     assert ref[-1] < 0.8 * ref[0], "the oracle run must actually train"
-    np.testing.assert_allclose(f16, ref, rtol=5e-3)
+    np.testing.assert_allclose(f16, ref, rtol=max(2 * env, 1e-3))
     np.testing.assert_allclose(bf, ref, rtol=2e-2)
     np.testing.assert_allclose(bft, ref, rtol=2e-2)
+
+
+def test_art_trajectory_lr1e3_is_the_references_chaos():
+    """Verdict r03 #2: at lr 1e-3 the f16x3 run parted from the fp32 oracle by 26% within 10
+    steps (profiles/r03/art_bf16/traj_lr1e-3.log).  That is the reference's own behaviour, shown
+    here: the fp64 oracle and fp32 oracles whose weights differ from the reference's by one
+    rounding each (2^-24 relative, seeded) -- an ensemble of fp32-class evaluations that agree
+    to the last bit at step 0 -- part from the fp32 oracle by 7-57% within 12 steps (measured on
+    CPU: fp64 14%).  Gate, per step i: |f16x3 / ref - 1| <= max(2 x the ensemble's largest
+    distance up to step i, 1e-3) -- ours stays inside the spread the reference's own
+    arithmetic produces, and step for step where that spread is small."""
+    steps, lr = 12, 1e-3
+    batch = _traj_batch()
+    ref = _oracle_trajectory(batch, steps, lr, torch.float32)
+    ens = {"fp64": _oracle_trajectory(batch, steps, lr, torch.float64)}
+    for seed in (1, 2, 3):
+        ens[f"fp32 ulp seed {seed}"] = _oracle_trajectory(batch, steps, lr, torch.float32, seed)
+    f16 = _art_trajectory_gpu("f16x3", batch, steps, lr)
+    dist = {k: np.abs(v / ref - 1) for k, v in ens.items()}
+    env = np.maximum.accumulate(np.max(np.stack(list(dist.values())), 0))
+    ours = np.abs(f16 / ref - 1)
+    for i in range(steps):
+        print(f"step {i:2d}: fp32 oracle {ref[i]:.6f}  f16x3 {f16[i]:.6f}  |rel| {ours[i]:.2e}  "
+              + "  ".join(f"{k} {d[i]:.2e}" for k, d in dist.items()) + f"  env {env[i]:.2e}")
+    print(f"max: f16x3 {ours.max():.2e}; " + "  ".join(f"{k} {d.max():.2e}" for k, d in dist.items()))
+    assert env[-1] > 1e-2, "lr 1e-3 should be chaotic in the reference itself"
+    gate = np.maximum(2 * env, 1e-3)
+    assert (ours <= gate).all(), list(zip(ours, gate))
 
 
 _LAYERS = (["deformations_linear.%d" % i for i in range(4)] + ["deformation_layer"]
