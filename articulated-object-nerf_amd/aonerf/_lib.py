@@ -70,6 +70,7 @@ _SIGNATURES = {
     "aon_mlp_read_status": (c_int, [vp, c_size, ctypes.POINTER(ctypes.c_uint32), vp]),
     "aon_mlp_pack": (c_int, [ctypes.POINTER(AonMlpParams), c_int, vp, vp]),
     "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
+    "aon_mlp_set_dataflow": (c_int, [c_int]),
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp]),
     "aon_mlp_fwd_train_bf16": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp,

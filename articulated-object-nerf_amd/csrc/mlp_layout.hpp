@@ -339,6 +339,10 @@ int absmax(const float* x, int64_t n, uint32_t* out, hipStream_t stream);
 int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const float* a1,
                  const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
                  hipStream_t stream, const TrainStore* ts = nullptr);
+// the weight-streamed fp16x3 render forward (mlp_ws.hip; MODE 0 inputs, bit-identical to
+// launch_f16x3 mode 0)
+int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
+                    const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream);
 
 }  // namespace mlp
 }  // namespace aon

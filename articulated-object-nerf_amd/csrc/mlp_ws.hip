@@ -1,0 +1,341 @@
+// Fused NeRFMLP forward on fp16x3 MFMA, WEIGHT-STREAMED dataflow ("ws") -- the render path's
+// alternative to k_mlp_fwd_f16x3 (mlp_f16x3.hip), same numerics, bit-identical outputs.
+//
+// Why ("Fine MLP: LDS bytes per MAC"): k_mlp_fwd_f16x3 keeps each wave's 16
+// samples in registers and streams the WEIGHTS through LDS, so every wave reads the whole 2.37-MB
+// stream per 16 samples: 683 B of LDS per MFMA, 19 MB per 128-sample pass per CU -- with the
+// ring's DMA writes ~100k LDS cycles against ~112k MFMA cycles.  The LDS is co-critical with the
+// matrix cores (MFMA busy 0.69; a build without the fragment reads runs in half the time).
+//
+// Here the roles swap.  A workgroup (8 waves, 2 per SIMD) owns 128 samples whose activations
+// live in LDS (hi / lo planes, 128 KB) and are shared by all its waves; each wave owns 32 OUTPUT
+// rows (one pair of 16-row tiles) of a layer and reads its weight fragments straight from the
+// packed stream in global memory (L2-resident: every CU reads the same 2.37 MB) into registers.
+// Per 32-deep k-step a wave loads 4 KB of A from L2 and 16 KB of B (8 sample tiles, hi + lo) from
+// LDS for 48 MFMAs: 341 B of LDS per MFMA (half of the streamed kernel's) and 21 B/clk/CU of
+// L2 -> CU traffic.  A layer ends with two barriers: all waves past their reads of the input
+// planes -> epilogue (bias, ReLU, fp16 hi/lo split) written in place -> all waves past their
+// writes.  The accumulator tile (2 pr + uu, sample tile t) of lane (g, j) holds rows
+// 16 (2 pr + uu) + 4 g + r, which are exactly elements 4 uu + r of the next layer's k-step-pr
+// B fragment of that lane (the stream's feature order, mlp_layout.hpp) -- the epilogue writes
+// each lane's own 16 B, no shuffles.
+//
+// Accumulation order per output: k-steps in order, hi*hi, hi*lo, lo*hi into ONE fp32 accumulator,
+// the same epilogue arithmetic -- every raw value equals k_mlp_fwd_f16x3's bit for bit
+// (tests/test_gpu_parity.py::test_mlp_ws_equals_streamed).  MODE 0 (rays + t) inference only;
+// selected by AON_MLP_WS (env, mlp.hip) for the A/B.
+#include "mlp_f16x3_core.hpp"
+
+namespace aon {
+namespace mlp {
+namespace ws {
+
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kTiles = 8;            // 16-sample tiles per workgroup pass
+constexpr int kNb = 16 * kTiles;     // 128 samples
+constexpr int kActPlane = 8 * 4 * kNb;  // f4: [k-step 8][lane group 4][sample 128] = 64 KB
+constexpr int kEncPlane = 2 * 4 * kNb;  // f4: pos_enc(x) (2 k-steps), later pos_enc(dir) (1)
+constexpr int kLdsF4 = 2 * kActPlane + 2 * kEncPlane;
+static_assert(kLdsF4 * 16 <= 160 * 1024, "LDS");
+
+#ifndef AON_WS_PREFETCH
+#define AON_WS_PREFETCH 2  // k-steps of A fragments in flight ahead of the one in use
+#endif
+
+// the per-wave step sequence: layer of each 32-deep k-step, in execution order
+// (the layer enum's order: sequence index == layer index)
+constexpr int kLayerSeq[] = {L0, L1, L2, L3, L4, L5, L6, L7, LDEN, LBOT, LVIEW, LRGB};
+static_assert(LDEN == 8 && LBOT == 9 && LVIEW == 10 && LRGB == 11, "layer order");
+constexpr int kNumSeq = sizeof(kLayerSeq) / sizeof(int);
+__host__ __device__ constexpr int layer_k(int l) { return kLayersH[l].ka + kLayersH[l].kb; }
+__host__ __device__ constexpr int step0_of(int i) { return i == 0 ? 0 : step0_of(i - 1) + layer_k(kLayerSeq[i - 1]); }
+constexpr int kSteps = step0_of(kNumSeq);
+__host__ __device__ constexpr int seq_of_step(int s) {
+  int i = 0;
+  while (i + 1 < kNumSeq && step0_of(i + 1) <= s) ++i;
+  return i;
+}
+
+// A fragments straight from the packed stream (global, L2-resident), D k-steps ahead.
+// Pair layers: wave w owns pair w (tiles 2w, 2w + 1); the 128-row view layer: pair w & 3 (its 4
+// pairs x 2 halves of the sample tiles); the 1-tile heads: tile 0, on every wave.
+template <int D>
+struct APipe {
+  const f4* __restrict__ ws;
+  int lane, w;
+  f4 qh[D][2], ql[D][2];
+  __device__ __forceinline__ void fetch(int s, f4 (&h)[2], f4 (&l)[2]) {
+    if (s >= kSteps) return;
+    const int L = kLayerSeq[seq_of_step(s)];
+    const int k = s - step0_of(seq_of_step(s));
+    const LayerDesc d = kLayersH[L];
+    const int K = d.ka + d.kb;
+    if (d.u == 1) {
+      const int b = d.blk0 + 2 * k;
+      h[0] = ws[(size_t)b * 64 + lane];
+      l[0] = ws[(size_t)(b + 1) * 64 + lane];
+      return;
+    }
+    const int pr = L == LVIEW ? (w & 3) : w;
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) {
+      const int b = d.blk0 + 2 * ((pr * K + k) * 2 + uu);
+      h[uu] = ws[(size_t)b * 64 + lane];
+      l[uu] = ws[(size_t)(b + 1) * 64 + lane];
+    }
+  }
+  __device__ __forceinline__ void start() {
+#pragma unroll
+    for (int i = 0; i < D; ++i) fetch(i, qh[i], ql[i]);
+  }
+  __device__ __forceinline__ void take(int s, h8 (&wh)[2], h8 (&wl)[2]) {
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) {
+      wh[uu] = as_h8(qh[0][uu]);
+      wl[uu] = as_h8(ql[0][uu]);
+    }
+#pragma unroll
+    for (int i = 0; i + 1 < D; ++i)
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu) {
+        qh[i][uu] = qh[i + 1][uu];
+        ql[i][uu] = ql[i + 1][uu];
+      }
+    fetch(s + D, qh[D - 1], ql[D - 1]);
+  }
+};
+
+// every wave's LDS writes (and reads) done, then the workgroup barrier; the A prefetch (global
+// loads into registers) stays in flight across it
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");  // no LDS access moves across (the builtin itself is IntrNoMem)
+  wait_vm<0>(31);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct Planes {
+  f4* act_hi;  // [8][4][kNb] (+ g * kNb + j applied)
+  f4* act_lo;
+  f4* enc_hi;  // [2][4][kNb]
+  f4* enc_lo;
+};
+
+// MFMAs of one layer for NT sample tiles starting at tile T0 and the tiles uu < NU of pair pr:
+// acc[uu][t] = sum_k W[k] . B[k] (3 products per k-step into one accumulator)
+template <int L, int S0, int NT, int NU, typename AP>
+__device__ __forceinline__ void layer_mfma(AP& ap, const Planes& pl, int T0, f4 (&acc)[2][NT]) {
+  constexpr LayerDesc d = kLayersH[L];
+  constexpr int K = d.ka + d.kb;
+#pragma unroll
+  for (int uu = 0; uu < NU; ++uu)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[uu][t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    h8 wh[2], wl[2];
+    ap.take(S0 + k, wh, wl);
+    const f4* bh = k < d.ka ? pl.act_hi + k * 4 * kNb : pl.enc_hi + (k - d.ka) * 4 * kNb;
+    const f4* bl = k < d.ka ? pl.act_lo + k * 4 * kNb : pl.enc_lo + (k - d.ka) * 4 * kNb;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const h8 xh = as_h8(bh[16 * (T0 + t)]);
+      const h8 xl = as_h8(bl[16 * (T0 + t)]);
+#pragma unroll
+      for (int uu = 0; uu < NU; ++uu) {
+        acc[uu][t] = mfma16(wh[uu], xh, acc[uu][t]);
+        acc[uu][t] = mfma16(wh[uu], xl, acc[uu][t]);
+        acc[uu][t] = mfma16(wl[uu], xh, acc[uu][t]);
+      }
+    }
+  }
+}
+
+// epilogue of a pair's tiles (hidden / bottleneck / view layer): bias at activation scale,
+// ReLU, fp16 hi / lo split (mlp_f16x3_core.hpp epi_part, V2 + fma_mix), written as the lane's
+// k-step-pr B fragment of the next layer; m16: the range guard's packed max of the hi bits
+template <bool RELU, int NT>
+__device__ __forceinline__ void pair_epilogue(const f4 (&acc)[2][NT], const f4 (&bias)[2],
+                                              const Planes& pl, int pr, int T0, uint32_t& m16) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    u4 hw, lw;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int uu = q >> 1, r0 = (q & 1) * 2;
+      float vv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float v = fmaf(acc[uu][t][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
+        if (RELU) v = fmaxf(v, 0.0f);
+        vv[e] = v;
+      }
+      const h2 hp = {static_cast<_Float16>(vv[0]), static_cast<_Float16>(vv[1])};
+      const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
+      m16 = pk_max_i16(m16, RELU ? hu : (hu & 0x7FFF7FFFu));
+      asm("" : "+v"(m16));
+      float d0, d1;
+      asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(vv[0]));
+      asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(vv[1]));
+      const h2 lp = {static_cast<_Float16>(d0), static_cast<_Float16>(d1)};
+      hw[q] = hu;
+      lw[q] = __builtin_bit_cast(uint32_t, lp);
+    }
+    pl.act_hi[pr * 4 * kNb + 16 * (T0 + t)] = __builtin_bit_cast(f4, hw);
+    pl.act_lo[pr * 4 * kNb + 16 * (T0 + t)] = __builtin_bit_cast(f4, lw);
+  }
+}
+
+__device__ __forceinline__ f4 ldg_f4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+// a 256-row layer (16 tiles = 8 pairs, wave w -> pair w) over all 8 sample tiles
+template <int L, bool RELU, typename AP>
+__device__ __forceinline__ void pair_layer(AP& ap, const Planes& pl, const float* bias_g, int w,
+                                           int g, uint32_t& m16) {
+  constexpr LayerDesc d = kLayersH[L];
+  static_assert(d.u == 16, "256-row layer");
+  f4 bias[2];
+#pragma unroll
+  for (int uu = 0; uu < 2; ++uu) bias[uu] = ldg_f4(bias_g + d.bias0 + 16 * (2 * w + uu) + 4 * g);
+  f4 acc[2][kTiles];
+  layer_mfma<L, step0_of(L), kTiles, 2>(ap, pl, 0, acc);
+  lds_barrier();  // every wave past its reads of the input planes
+  pair_epilogue<RELU, kTiles>(acc, bias, pl, w, 0, m16);
+  lds_barrier();  // the layer's output complete
+}
+
+// a 1-tile head (density / rgb) on this wave's sample tile: (4 rows at true scale)
+template <int L, typename AP>
+__device__ __forceinline__ f4 head(AP& ap, const Planes& pl, const float* bias_g, int w, int g) {
+  constexpr LayerDesc d = kLayersH[L];
+  static_assert(d.u == 1 && d.kb == 0, "head");
+  const f4 bias = ldg_f4(bias_g + d.bias0 + 4 * g);
+  f4 acc[2][1];
+  layer_mfma<L, step0_of(L), 1, 1>(ap, pl, w, acc);
+  f4 res;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) res[r] = fmaf(acc[0][0][r], 1.0f / (kWS * kActS), bias[r]);
+  return res;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
+    const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
+    const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
+    int64_t B, int S, int act, float* __restrict__ raw) {
+  static_assert(MODE == 0, "rays + t inputs");
+  __shared__ f4 smem[kLdsF4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int64_t N = B * S;
+
+  APipe<AON_WS_PREFETCH> ap;
+  ap.ws = wstream;
+  ap.lane = lane;
+  ap.w = w;
+  ap.start();
+
+  Planes pl;
+  pl.act_hi = smem + g * kNb + j;
+  pl.act_lo = smem + kActPlane + g * kNb + j;
+  pl.enc_hi = smem + 2 * kActPlane + g * kNb + j;
+  pl.enc_lo = smem + 2 * kActPlane + kEncPlane + g * kNb + j;
+
+  // pos_enc(x) of this wave's sample tile (samples 16 w + j), natural feature order (segment B)
+  const int64_t row = (int64_t)blockIdx.x * kNb + 16 * w + j;
+  const int64_t rr = row < N ? row : N - 1;
+  const int64_t ray = rr / S;
+  uint64_t ovf = 0;
+  {
+    const float* ro = in0 + 3 * ray;
+    const float* rd = in1 + 3 * ray;
+    const float tt = in3[rr];
+    const float x0 = __fadd_rn(ro[0], __fmul_rn(tt, rd[0]));
+    const float x1 = __fadd_rn(ro[1], __fmul_rn(tt, rd[1]));
+    const float x2 = __fadd_rn(ro[2], __fmul_rn(tt, rd[2]));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float ev[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ev[e] = pos_enc_feature(x0, x1, x2, 32 * k + 8 * g + e, 0, 10) * kActS;
+      h8 hi, lo;
+      split8<false>(ev, hi, lo, ovf);
+      pl.enc_hi[k * 4 * kNb + 16 * w] = __builtin_bit_cast(f4, hi);
+      pl.enc_lo[k * 4 * kNb + 16 * w] = __builtin_bit_cast(f4, lo);
+    }
+  }
+  lds_barrier();
+
+  uint32_t m16 = 0;
+  pair_layer<L0, true>(ap, pl, bias_g, w, g, m16);
+  pair_layer<L1, true>(ap, pl, bias_g, w, g, m16);
+  pair_layer<L2, true>(ap, pl, bias_g, w, g, m16);
+  pair_layer<L3, true>(ap, pl, bias_g, w, g, m16);
+  pair_layer<L4, true>(ap, pl, bias_g, w, g, m16);
+  {
+    // skip layer cat[h4, enc]; in its epilogue phase the enc planes are free: pos_enc(viewdirs)
+    // of this wave's tile goes to enc k-step 0 for the view layer
+    constexpr LayerDesc d = kLayersH[L5];
+    f4 bias[2];
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) bias[uu] = ldg_f4(bias_g + d.bias0 + 16 * (2 * w + uu) + 4 * g);
+    f4 acc[2][kTiles];
+    layer_mfma<L5, step0_of(L5), kTiles, 2>(ap, pl, 0, acc);
+    lds_barrier();
+    pair_epilogue<true, kTiles>(acc, bias, pl, w, 0, m16);
+    const float* vd = in2 + 3 * ray;
+    float vv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4) * kActS;
+    h8 hi, lo;
+    split8<false>(vv, hi, lo, ovf);
+    pl.enc_hi[16 * w] = __builtin_bit_cast(f4, hi);
+    pl.enc_lo[16 * w] = __builtin_bit_cast(f4, lo);
+    lds_barrier();
+  }
+  pair_layer<L6, true>(ap, pl, bias_g, w, g, m16);
+  pair_layer<L7, true>(ap, pl, bias_g, w, g, m16);
+  // density head on h7 (this wave's tile), then the bottleneck (no activation) on h7
+  const f4 dens = head<LDEN>(ap, pl, bias_g, w, g);
+  pair_layer<LBOT, false>(ap, pl, bias_g, w, g, m16);
+  {
+    // views_linear.0: cat[bottleneck, enc_dir] + ReLU, 128 rows = 4 pairs; wave w -> pair w & 3
+    // on sample tiles 4 (w >> 2) .. + 3
+    constexpr LayerDesc d = kLayersH[LVIEW];
+    const int pr = w & 3, T0 = 4 * (w >> 2);
+    f4 bias[2];
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) bias[uu] = ldg_f4(bias_g + d.bias0 + 16 * (2 * pr + uu) + 4 * g);
+    f4 acc[2][4];
+    layer_mfma<LVIEW, step0_of(LVIEW), 4, 2>(ap, pl, T0, acc);
+    lds_barrier();
+    pair_epilogue<true, 4>(acc, bias, pl, pr, T0, m16);
+    lds_barrier();
+  }
+  const f4 rgb = head<LRGB>(ap, pl, bias_g, w, g);
+  if (g == 0 && row < N) {
+    const f4 o = {act_rgb(rgb[0], act), act_rgb(rgb[1], act), act_rgb(rgb[2], act), act_sigma(dens[0], act)};
+    *reinterpret_cast<f4*>(raw + 4 * row) = o;
+  }
+  const bool bad = (m16 & 0x7FFFu) >= 0x7C00u || ((m16 >> 16) & 0x7FFFu) >= 0x7C00u;
+  range_report(bias_g + kBiasFloats, ovf | __builtin_amdgcn_ballot_w64(bad));
+}
+
+}  // namespace ws
+
+int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
+                    const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream) {
+  const int64_t N = B * S;
+  const f4* wsp = static_cast<const f4*>(packed);
+  const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + kStreamBytesF32);
+  hipLaunchKernelGGL(ws::k_mlp_ws_f16x3<0>, static_cast<int>((N + ws::kNb - 1) / ws::kNb),
+                     ws::kThreads, 0, stream, wsp, bias, a0, a1, a2, a3, B, S, act, raw);
+  return launch_status("aon_mlp_fwd");
+}
+
+}  // namespace mlp
+}  // namespace aon

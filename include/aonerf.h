@@ -167,6 +167,16 @@ int aon_mlp_fwd(const void* packed, int precision, const float* rays_o, const fl
                 const float* viewdirs, const float* t, int64_t B, int S, int act, float* out,
                 aon_stream_t stream);
 
+/* Dataflow of aon_mlp_fwd's fp16x3 kernel (process-wide; returns the previous setting, or < 0
+ * for an unknown value): AON_DATAFLOW_STREAMED -- each wave keeps 16 samples in registers and
+ * the weights stream through an LDS ring (mlp_f16x3.hip); AON_DATAFLOW_WS -- a workgroup's 128
+ * samples live in LDS and each wave reads its 32 output rows' weights from L2 (mlp_ws.hip).
+ * Both give bit-identical outputs.  Initial value: AON_MLP_WS=1 / 0 in the environment, else the
+ * build's default (AON_DATAFLOW_STREAMED). */
+#define AON_DATAFLOW_STREAMED 0
+#define AON_DATAFLOW_WS 1
+int aon_mlp_set_dataflow(int dataflow);
+
 /* NeRFMLP.forward on pre-encoded inputs: x (B*S, 63), condition (B, 27) -> out (B*S, 4). */
 int aon_mlp_fwd_encoded(const void* packed, int precision, const float* x,
                         const float* condition, int64_t B, int S, int act, float* out,

@@ -22,6 +22,12 @@ def agg(path):
     return per
 
 
+def agg_opt(path, k):
+    if not glob.glob(f"{path}/**/*counter_collection.csv", recursive=True):
+        return None
+    return agg(path).get(k)
+
+
 def main():
     src = sys.argv[1]
     a, b = agg(f"{src}/A"), agg(f"{src}/B")
@@ -33,7 +39,19 @@ def main():
         if cyc < 1e5:
             continue
         w = b[k]["waves"]
-        res[k] = {"mfma_busy": a[k]["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc),
+        c_, d_ = agg_opt(f"{src}/C", k), agg_opt(f"{src}/D", k)
+        e_ = agg_opt(f"{src}/E", k)
+        disp = len(b[k]["disp"])
+        extra = {}
+        if c_ and d_:  # HBM bytes per dispatch: FETCH_SIZE doubled (gfx950), KiB units
+            extra["fetch_bytes_per_dispatch"] = 2 * 1024 * c_["FETCH_SIZE"] / disp
+            extra["write_bytes_per_dispatch"] = 1024 * d_["WRITE_SIZE"] / disp
+        if e_:
+            extra["vmem_wr_per_wave"] = e_["SQ_INSTS_VMEM_WR"] / w
+            extra["vmem_rd_per_wave"] = e_["SQ_INSTS_VMEM_RD"] / w
+            extra["salu_per_wave"] = e_["SQ_INSTS_SALU"] / w
+            extra["vmem_wr_issue_frac"] = e_["SQ_INST_CYCLES_VMEM_WR"] / e_["SQ_WAVE_CYCLES"]
+        res[k] = {"dispatches": disp, "mfma_busy": a[k]["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc),
                   "lds_busy": b[k]["SQ_LDS_IDX_ACTIVE"] / (256 * cyc),
                   "wait_inst_any_frac": a[k]["SQ_WAIT_INST_ANY"] / a[k]["SQ_WAVE_CYCLES"],
                   "wait_inst_lds_frac": a[k]["SQ_WAIT_INST_LDS"] / a[k]["SQ_WAVE_CYCLES"],
@@ -41,7 +59,7 @@ def main():
                   "valu_non_mfma_per_wave": (b[k]["SQ_INSTS_VALU"] - b[k]["SQ_INSTS_MFMA"]) / w,
                   "lds_per_wave": b[k]["SQ_INSTS_LDS"] / w,
                   "valu_mfma_coexec_frac": b[k]["SQ_VALU_MFMA_COEXEC_CYCLES"] / (1024 * cyc),
-                  "active_valu_frac": b[k]["SQ_ACTIVE_INST_VALU"] / (1024 * cyc)}
+                  "active_valu_frac": b[k]["SQ_ACTIVE_INST_VALU"] / (1024 * cyc), **extra}
     print(json.dumps(res, indent=1))
     if len(sys.argv) > 2:
         json.dump(res, open(sys.argv[2], "w"), indent=1)
