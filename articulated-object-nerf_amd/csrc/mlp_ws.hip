@@ -40,7 +40,7 @@ constexpr int kLdsF4 = 2 * kActPlane + 2 * kEncPlane;
 static_assert(kLdsF4 * 16 <= 160 * 1024, "LDS");
 
 #ifndef AON_WS_PREFETCH
-#define AON_WS_PREFETCH 2  // k-steps of A fragments in flight ahead of the one in use
+#define AON_WS_PREFETCH 3  // k-steps of A fragments in flight ahead of the one in use
 #endif
 
 // the per-wave step sequence: layer of each 32-deep k-step, in execution order
@@ -115,39 +115,69 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// LDS plane pointers: each plane gets its own base register (opaque to the compiler), so every
+// access is base + an immediate offset < 64 KB -- ds_read / ds_write's offset field stops at
+// 64 KB, and past it hipcc materialises one address VGPR per access (40+ registers here)
+typedef __attribute__((address_space(3))) f4 lds_f4w;
+__device__ __forceinline__ lds_f4w* lds_base(f4* p) {
+  uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p));
+  asm volatile("" : "+v"(a));
+  return reinterpret_cast<lds_f4w*>(static_cast<uintptr_t>(a));
+}
 struct Planes {
-  f4* act_hi;  // [8][4][kNb] (+ g * kNb + j applied)
-  f4* act_lo;
-  f4* enc_hi;  // [2][4][kNb]
-  f4* enc_lo;
+  lds_f4w* act_hi;  // [8][4][kNb] (+ g * kNb + j applied)
+  lds_f4w* act_lo;
+  lds_f4w* enc_hi;  // [2][4][kNb]
+  lds_f4w* enc_lo;
 };
 
+#ifndef AON_WS_BPF
+#define AON_WS_BPF 2  // B fragments (one sample tile's hi + lo) read from LDS ahead of their MFMAs
+#endif
+
 // MFMAs of one layer for NT sample tiles starting at tile T0 and the tiles uu < NU of pair pr:
-// acc[uu][t] = sum_k W[k] . B[k] (3 products per k-step into one accumulator)
+// acc[uu][t] = sum_k W[k] . B[k] (3 products per k-step into one accumulator).  The (k, t) loop
+// runs flat with the B fragments of the next AON_WS_BPF (k, t) steps already read from LDS (the
+// sched_barrier keeps those reads above the current step's MFMAs: left alone, hipcc sinks each
+// ds_read to its use and waits lgkmcnt(0) in front of every sample tile's MFMAs).
 template <int L, int S0, int NT, int NU, typename AP>
 __device__ __forceinline__ void layer_mfma(AP& ap, const Planes& pl, int T0, f4 (&acc)[2][NT]) {
   constexpr LayerDesc d = kLayersH[L];
   constexpr int K = d.ka + d.kb;
+  constexpr int NS = K * NT;
+  constexpr int P = AON_WS_BPF < NS ? AON_WS_BPF : NS;
 #pragma unroll
   for (int uu = 0; uu < NU; ++uu)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[uu][t] = f4{0.f, 0.f, 0.f, 0.f};
+  auto bsrc = [&](int i, f4& xh, f4& xl) {
+    const int k = i / NT, t = i % NT;
+    const lds_f4w* bh = k < d.ka ? pl.act_hi + k * 4 * kNb : pl.enc_hi + (k - d.ka) * 4 * kNb;
+    const lds_f4w* bl = k < d.ka ? pl.act_lo + k * 4 * kNb : pl.enc_lo + (k - d.ka) * 4 * kNb;
+    xh = bh[16 * (T0 + t)];
+    xl = bl[16 * (T0 + t)];
+  };
+  f4 qh[P], ql[P];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    h8 wh[2], wl[2];
-    ap.take(S0 + k, wh, wl);
-    const f4* bh = k < d.ka ? pl.act_hi + k * 4 * kNb : pl.enc_hi + (k - d.ka) * 4 * kNb;
-    const f4* bl = k < d.ka ? pl.act_lo + k * 4 * kNb : pl.enc_lo + (k - d.ka) * 4 * kNb;
+  for (int i = 0; i < P; ++i) bsrc(i, qh[i], ql[i]);
+  h8 wh[2], wl[2];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const h8 xh = as_h8(bh[16 * (T0 + t)]);
-      const h8 xl = as_h8(bl[16 * (T0 + t)]);
+  for (int i = 0; i < NS; ++i) {
+    const int t = i % NT;
+    if (t == 0) ap.take(S0 + i / NT, wh, wl);
+    const h8 xh = as_h8(qh[0]), xl = as_h8(ql[0]);
 #pragma unroll
-      for (int uu = 0; uu < NU; ++uu) {
-        acc[uu][t] = mfma16(wh[uu], xh, acc[uu][t]);
-        acc[uu][t] = mfma16(wh[uu], xl, acc[uu][t]);
-        acc[uu][t] = mfma16(wl[uu], xh, acc[uu][t]);
-      }
+    for (int p = 0; p + 1 < P; ++p) {
+      qh[p] = qh[p + 1];
+      ql[p] = ql[p + 1];
+    }
+    if (i + P < NS) bsrc(i + P, qh[P - 1], ql[P - 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int uu = 0; uu < NU; ++uu) {
+      acc[uu][t] = mfma16(wh[uu], xh, acc[uu][t]);
+      acc[uu][t] = mfma16(wh[uu], xl, acc[uu][t]);
+      acc[uu][t] = mfma16(wl[uu], xh, acc[uu][t]);
     }
   }
 }
@@ -240,10 +270,10 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
   ap.start();
 
   Planes pl;
-  pl.act_hi = smem + g * kNb + j;
-  pl.act_lo = smem + kActPlane + g * kNb + j;
-  pl.enc_hi = smem + 2 * kActPlane + g * kNb + j;
-  pl.enc_lo = smem + 2 * kActPlane + kEncPlane + g * kNb + j;
+  pl.act_hi = lds_base(smem + g * kNb + j);
+  pl.act_lo = lds_base(smem + kActPlane + g * kNb + j);
+  pl.enc_hi = lds_base(smem + 2 * kActPlane + g * kNb + j);
+  pl.enc_lo = lds_base(smem + 2 * kActPlane + kEncPlane + g * kNb + j);
 
   // pos_enc(x) of this wave's sample tile (samples 16 w + j), natural feature order (segment B)
   const int64_t row = (int64_t)blockIdx.x * kNb + 16 * w + j;
