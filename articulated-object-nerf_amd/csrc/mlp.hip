@@ -284,7 +284,7 @@ static int f16x3_ncol() {
 #endif
 constexpr int kDefaultDataflow = AON_DATAFLOW_DEFAULT;
 static int g_dataflow = -1;
-static bool mlp_ws() {
+bool aon::mlp::mlp_dataflow_ws() {
   if (g_dataflow < 0) {
     const char* e = getenv("AON_MLP_WS");
     g_dataflow = e ? (atoi(e) == 1 ? AON_DATAFLOW_WS : AON_DATAFLOW_STREAMED) : kDefaultDataflow;
@@ -294,7 +294,7 @@ static bool mlp_ws() {
 
 extern "C" int aon_mlp_set_dataflow(int dataflow) {
   AON_REQUIRE(dataflow == AON_DATAFLOW_STREAMED || dataflow == AON_DATAFLOW_WS, "bad dataflow");
-  const int prev = mlp_ws() ? AON_DATAFLOW_WS : AON_DATAFLOW_STREAMED;
+  const int prev = mlp_dataflow_ws() ? AON_DATAFLOW_WS : AON_DATAFLOW_STREAMED;
   g_dataflow = dataflow;
   return prev;
 }
@@ -343,7 +343,7 @@ static int mlp_launch(int mode, const void* packed, int precision, const float* 
   const int64_t N = B * S;
   if (N == 0) return 0;
   AON_REQUIRE((N + kRowsPerBlock - 1) / kRowsPerBlock < (1ll << 31), "too many rows");
-  if (precision == AON_PREC_F16X3 && mode == 0 && mlp_ws())
+  if (precision == AON_PREC_F16X3 && mode == 0 && mlp_dataflow_ws())
     return launch_ws_f16x3(packed, a0, a1, a2, a3, B, S, act, raw, (hipStream_t)stream);
   if (precision == AON_PREC_F16X3)
     return launch_f16x3(mode, f16x3_ncol(), packed, a0, a1, a2, a3, B, S, act, raw,

@@ -271,6 +271,8 @@ static int art_launch(int mode, const void* packed, const float* a0, const float
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
+  if (mode == 0 && mlp_dataflow_ws())
+    return launch_art_ws_f16x3(packed, a0, a1, a2, a3, B, S, act, raw, (hipStream_t)stream);
   if (mode == 0)
     hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1>), (unsigned)grid, G::kThreads, 0,
                        (hipStream_t)stream, ws, bias, a0, a1, a2, a3, B, S, act, raw);

@@ -343,6 +343,10 @@ int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const 
 // launch_f16x3 mode 0)
 int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
                     const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream);
+int launch_art_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
+                        const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream);
+// the render forward's dataflow (aon_mlp_set_dataflow, mlp.hip): true = weight-streamed
+bool mlp_dataflow_ws();
 
 }  // namespace mlp
 }  // namespace aon

@@ -43,33 +43,37 @@ static_assert(kLdsF4 * 16 <= 160 * 1024, "LDS");
 #define AON_WS_PREFETCH 3  // k-steps of A fragments in flight ahead of the one in use
 #endif
 
-// the per-wave step sequence: layer of each 32-deep k-step, in execution order
-// (the layer enum's order: sequence index == layer index)
-constexpr int kLayerSeq[] = {L0, L1, L2, L3, L4, L5, L6, L7, LDEN, LBOT, LVIEW, LRGB};
-static_assert(LDEN == 8 && LBOT == 9 && LVIEW == 10 && LRGB == 11, "layer order");
-constexpr int kNumSeq = sizeof(kLayerSeq) / sizeof(int);
-__host__ __device__ constexpr int layer_k(int l) { return kLayersH[l].ka + kLayersH[l].kb; }
-__host__ __device__ constexpr int step0_of(int i) { return i == 0 ? 0 : step0_of(i - 1) + layer_k(kLayerSeq[i - 1]); }
-constexpr int kSteps = step0_of(kNumSeq);
-__host__ __device__ constexpr int seq_of_step(int s) {
-  int i = 0;
-  while (i + 1 < kNumSeq && step0_of(i + 1) <= s) ++i;
-  return i;
+// The per-wave step sequence of a network: its layers in table order (both layer tables list
+// them in execution order), each ka + kb 32-deep k-steps.
+template <typename Net>
+__host__ __device__ constexpr int layer_k(int l) { return Net::layer(l).ka + Net::layer(l).kb; }
+template <typename Net>
+__host__ __device__ constexpr int step0_of(int l) { return l == 0 ? 0 : step0_of<Net>(l - 1) + layer_k<Net>(l - 1); }
+template <typename Net>
+__host__ __device__ constexpr int layer_of_step(int s) {
+  int l = 0;
+  while (l + 1 < Net::kNumLayers && step0_of<Net>(l + 1) <= s) ++l;
+  return l;
 }
+template <typename Net>
+constexpr int kStepsOf = step0_of<Net>(Net::kNumLayers);
+
+// Which rows a wave computes: a 256-row layer (16 tiles) -> pair w over all 8 sample tiles; a
+// 128-row layer (8 tiles) -> pair w & 3 over sample tiles 4 (w >> 2) .. + 3; a 1-tile head ->
+// tile 0 over sample tile w (every wave: its own tile).
+__host__ __device__ constexpr int pair_of(int u, int w) { return u == 16 ? w : (w & 3); }
 
 // A fragments straight from the packed stream (global, L2-resident), D k-steps ahead.
-// Pair layers: wave w owns pair w (tiles 2w, 2w + 1); the 128-row view layer: pair w & 3 (its 4
-// pairs x 2 halves of the sample tiles); the 1-tile heads: tile 0, on every wave.
-template <int D>
+template <typename Net, int D>
 struct APipe {
   const f4* __restrict__ ws;
   int lane, w;
   f4 qh[D][2], ql[D][2];
   __device__ __forceinline__ void fetch(int s, f4 (&h)[2], f4 (&l)[2]) {
-    if (s >= kSteps) return;
-    const int L = kLayerSeq[seq_of_step(s)];
-    const int k = s - step0_of(seq_of_step(s));
-    const LayerDesc d = kLayersH[L];
+    if (s >= kStepsOf<Net>) return;
+    const int L = layer_of_step<Net>(s);
+    const int k = s - step0_of<Net>(L);
+    const LayerDesc d = Net::layer(L);
     const int K = d.ka + d.kb;
     if (d.u == 1) {
       const int b = d.blk0 + 2 * k;
@@ -77,7 +81,7 @@ struct APipe {
       l[0] = ws[(size_t)(b + 1) * 64 + lane];
       return;
     }
-    const int pr = L == LVIEW ? (w & 3) : w;
+    const int pr = pair_of(d.u, w);
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
       const int b = d.blk0 + 2 * ((pr * K + k) * 2 + uu);
@@ -127,7 +131,7 @@ __device__ __forceinline__ lds_f4w* lds_base(f4* p) {
 struct Planes {
   lds_f4w* act_hi;  // [8][4][kNb] (+ g * kNb + j applied)
   lds_f4w* act_lo;
-  lds_f4w* enc_hi;  // [2][4][kNb]
+  lds_f4w* enc_hi;  // [2][4][kNb]: segment B (pos_enc(x), pos_enc(x'), xyz, pos_enc(dir))
   lds_f4w* enc_lo;
 };
 
@@ -135,17 +139,19 @@ struct Planes {
 #define AON_WS_BPF 2  // B fragments (one sample tile's hi + lo) read from LDS ahead of their MFMAs
 #endif
 
-// MFMAs of one layer for NT sample tiles starting at tile T0 and the tiles uu < NU of pair pr:
-// acc[uu][t] = sum_k W[k] . B[k] (3 products per k-step into one accumulator).  The (k, t) loop
-// runs flat with the B fragments of the next AON_WS_BPF (k, t) steps already read from LDS (the
-// sched_barrier keeps those reads above the current step's MFMAs: left alone, hipcc sinks each
-// ds_read to its use and waits lgkmcnt(0) in front of every sample tile's MFMAs).
-template <int L, int S0, int NT, int NU, typename AP>
+// MFMAs of one layer for NT sample tiles starting at tile T0 and the tiles uu < NU of the wave's
+// pair: acc[uu][t] = sum_k W[k] . B[k] (3 products per k-step into one accumulator, k-steps in
+// order).  The (k, t) loop runs flat with the B fragments of the next AON_WS_BPF (k, t) steps
+// already read from LDS (the sched_barrier keeps those reads above the current step's MFMAs:
+// left alone, hipcc sinks each ds_read to its use and waits lgkmcnt(0) in front of every sample
+// tile's MFMAs).
+template <typename Net, int L, int NT, int NU, typename AP>
 __device__ __forceinline__ void layer_mfma(AP& ap, const Planes& pl, int T0, f4 (&acc)[2][NT]) {
-  constexpr LayerDesc d = kLayersH[L];
+  constexpr LayerDesc d = Net::layer(L);
   constexpr int K = d.ka + d.kb;
   constexpr int NS = K * NT;
   constexpr int P = AON_WS_BPF < NS ? AON_WS_BPF : NS;
+  constexpr int S0 = step0_of<Net>(L);
 #pragma unroll
   for (int uu = 0; uu < NU; ++uu)
 #pragma unroll
@@ -182,9 +188,9 @@ __device__ __forceinline__ void layer_mfma(AP& ap, const Planes& pl, int T0, f4 
   }
 }
 
-// epilogue of a pair's tiles (hidden / bottleneck / view layer): bias at activation scale,
-// ReLU, fp16 hi / lo split (mlp_f16x3_core.hpp epi_part, V2 + fma_mix), written as the lane's
-// k-step-pr B fragment of the next layer; m16: the range guard's packed max of the hi bits
+// epilogue of a pair's tiles: bias at activation scale, ReLU, fp16 hi / lo split
+// (mlp_f16x3_core.hpp epi_part, V2 + fma_mix), written as the lane's k-step-pr B fragment of the
+// next layer; m16: the range guard's packed max of the hi bits
 template <bool RELU, int NT>
 __device__ __forceinline__ void pair_epilogue(const f4 (&acc)[2][NT], const f4 (&bias)[2],
                                               const Planes& pl, int pr, int T0, uint32_t& m16) {
@@ -221,69 +227,103 @@ __device__ __forceinline__ void pair_epilogue(const f4 (&acc)[2][NT], const f4 (
 
 __device__ __forceinline__ f4 ldg_f4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
-// a 256-row layer (16 tiles = 8 pairs, wave w -> pair w) over all 8 sample tiles
-template <int L, bool RELU, typename AP>
-__device__ __forceinline__ void pair_layer(AP& ap, const Planes& pl, const float* bias_g, int w,
-                                           int g, uint32_t& m16) {
-  constexpr LayerDesc d = kLayersH[L];
-  static_assert(d.u == 16, "256-row layer");
+// One hidden layer (256 or 128 rows) of the wave's rows and sample tiles (pair_of), output in
+// place: MFMAs; barrier (every wave past its reads of the input planes); epilogue; `mid` (work
+// that needs the input planes free, e.g. the next segment B into the enc planes); barrier.
+struct NoMid {
+  __device__ __forceinline__ void operator()() const {}
+};
+template <typename Net, int L, bool RELU, typename AP, typename MID = NoMid>
+__device__ __forceinline__ void hidden_layer(AP& ap, const Planes& pl, const float* bias_g, int w,
+                                             int g, uint32_t& m16, const MID& mid = MID{}) {
+  constexpr LayerDesc d = Net::layer(L);
+  static_assert(d.u == 16 || d.u == 8, "hidden layer of 256 or 128 rows");
+  constexpr int NT = d.u == 16 ? kTiles : kTiles / 2;
+  const int pr = pair_of(d.u, w), T0 = d.u == 16 ? 0 : NT * (w >> 2);
   f4 bias[2];
 #pragma unroll
-  for (int uu = 0; uu < 2; ++uu) bias[uu] = ldg_f4(bias_g + d.bias0 + 16 * (2 * w + uu) + 4 * g);
-  f4 acc[2][kTiles];
-  layer_mfma<L, step0_of(L), kTiles, 2>(ap, pl, 0, acc);
-  lds_barrier();  // every wave past its reads of the input planes
-  pair_epilogue<RELU, kTiles>(acc, bias, pl, w, 0, m16);
-  lds_barrier();  // the layer's output complete
+  for (int uu = 0; uu < 2; ++uu) bias[uu] = ldg_f4(bias_g + d.bias0 + 16 * (2 * pr + uu) + 4 * g);
+  f4 acc[2][NT];
+  layer_mfma<Net, L, NT, 2>(ap, pl, T0, acc);
+  lds_barrier();
+  pair_epilogue<RELU, NT>(acc, bias, pl, pr, T0, m16);
+  mid();
+  lds_barrier();
 }
 
-// a 1-tile head (density / rgb) on this wave's sample tile: (4 rows at true scale)
-template <int L, typename AP>
+// a 1-tile head (density / rgb / deformation) on the wave's own sample tile: 4 rows at true scale
+template <typename Net, int L, typename AP>
 __device__ __forceinline__ f4 head(AP& ap, const Planes& pl, const float* bias_g, int w, int g) {
-  constexpr LayerDesc d = kLayersH[L];
+  constexpr LayerDesc d = Net::layer(L);
   static_assert(d.u == 1 && d.kb == 0, "head");
   const f4 bias = ldg_f4(bias_g + d.bias0 + 4 * g);
   f4 acc[2][1];
-  layer_mfma<L, step0_of(L), 1, 1>(ap, pl, w, acc);
+  layer_mfma<Net, L, 1, 1>(ap, pl, w, acc);
   f4 res;
 #pragma unroll
   for (int r = 0; r < 4; ++r) res[r] = fmaf(acc[0][0][r], 1.0f / (kWS * kActS), bias[r]);
   return res;
 }
 
-template <int MODE>
+// 8 fp32 features (true scale) of a segment-B k-step of this lane -> the enc planes (hi / lo at
+// activation scale, split8's range test into ovf)
+__device__ __forceinline__ void put_segb(const Planes& pl, int k, int w, const float (&v)[8],
+                                         uint64_t& ovf) {
+  float ev[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ev[e] = v[e] * kActS;
+  h8 hi, lo;
+  split8<false>(ev, hi, lo, ovf);
+  pl.enc_hi[k * 4 * kNb + 16 * w] = __builtin_bit_cast(f4, hi);
+  pl.enc_lo[k * 4 * kNb + 16 * w] = __builtin_bit_cast(f4, lo);
+}
+
+struct WsSetup {
+  Planes pl;
+  int lane, w, g, j;
+  int64_t row, rr, ray;
+};
+__device__ __forceinline__ WsSetup ws_setup(f4* smem, int64_t N, int S) {
+  WsSetup c;
+  const int tid = threadIdx.x;
+  c.lane = tid & 63;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  c.g = c.lane >> 4;
+  c.j = c.lane & 15;
+  const int gj = c.g * kNb + c.j;
+  c.pl.act_hi = lds_base(smem + gj);
+  c.pl.act_lo = lds_base(smem + kActPlane + gj);
+  c.pl.enc_hi = lds_base(smem + 2 * kActPlane + gj);
+  c.pl.enc_lo = lds_base(smem + 2 * kActPlane + kEncPlane + gj);
+  c.row = (int64_t)blockIdx.x * kNb + 16 * c.w + c.j;  // this lane's sample (wave w's tile)
+  c.rr = c.row < N ? c.row : N - 1;
+  c.ray = c.rr / S;
+  return c;
+}
+
+// ---- vanilla NeRFMLP (model.py:95-120), MODE 0 inputs: rays_o, rays_d, viewdirs, t
 __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
     int64_t B, int S, int act, float* __restrict__ raw) {
-  static_assert(MODE == 0, "rays + t inputs");
+  using Net = NetVanillaH;
   __shared__ f4 smem[kLdsF4];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, j = lane & 15;
   const int64_t N = B * S;
-
-  APipe<AON_WS_PREFETCH> ap;
+  const WsSetup c = ws_setup(smem, N, S);
+  const int w = c.w, g = c.g;
+  const Planes& pl = c.pl;
+  APipe<Net, AON_WS_PREFETCH> ap;
   ap.ws = wstream;
-  ap.lane = lane;
+  ap.lane = c.lane;
   ap.w = w;
   ap.start();
 
-  Planes pl;
-  pl.act_hi = lds_base(smem + g * kNb + j);
-  pl.act_lo = lds_base(smem + kActPlane + g * kNb + j);
-  pl.enc_hi = lds_base(smem + 2 * kActPlane + g * kNb + j);
-  pl.enc_lo = lds_base(smem + 2 * kActPlane + kEncPlane + g * kNb + j);
-
-  // pos_enc(x) of this wave's sample tile (samples 16 w + j), natural feature order (segment B)
-  const int64_t row = (int64_t)blockIdx.x * kNb + 16 * w + j;
-  const int64_t rr = row < N ? row : N - 1;
-  const int64_t ray = rr / S;
+  // pos_enc(x) of this wave's sample tile, natural feature order (segment B)
   uint64_t ovf = 0;
   {
-    const float* ro = in0 + 3 * ray;
-    const float* rd = in1 + 3 * ray;
-    const float tt = in3[rr];
+    const float* ro = in0 + 3 * c.ray;
+    const float* rd = in1 + 3 * c.ray;
+    const float tt = in3[c.rr];
     const float x0 = __fadd_rn(ro[0], __fmul_rn(tt, rd[0]));
     const float x1 = __fadd_rn(ro[1], __fmul_rn(tt, rd[1]));
     const float x2 = __fadd_rn(ro[2], __fmul_rn(tt, rd[2]));
@@ -291,68 +331,127 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
     for (int k = 0; k < 2; ++k) {
       float ev[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) ev[e] = pos_enc_feature(x0, x1, x2, 32 * k + 8 * g + e, 0, 10) * kActS;
-      h8 hi, lo;
-      split8<false>(ev, hi, lo, ovf);
-      pl.enc_hi[k * 4 * kNb + 16 * w] = __builtin_bit_cast(f4, hi);
-      pl.enc_lo[k * 4 * kNb + 16 * w] = __builtin_bit_cast(f4, lo);
+      for (int e = 0; e < 8; ++e) ev[e] = pos_enc_feature(x0, x1, x2, 32 * k + 8 * g + e, 0, 10);
+      put_segb(pl, k, w, ev, ovf);
     }
   }
   lds_barrier();
 
   uint32_t m16 = 0;
-  pair_layer<L0, true>(ap, pl, bias_g, w, g, m16);
-  pair_layer<L1, true>(ap, pl, bias_g, w, g, m16);
-  pair_layer<L2, true>(ap, pl, bias_g, w, g, m16);
-  pair_layer<L3, true>(ap, pl, bias_g, w, g, m16);
-  pair_layer<L4, true>(ap, pl, bias_g, w, g, m16);
-  {
-    // skip layer cat[h4, enc]; in its epilogue phase the enc planes are free: pos_enc(viewdirs)
-    // of this wave's tile goes to enc k-step 0 for the view layer
-    constexpr LayerDesc d = kLayersH[L5];
-    f4 bias[2];
-#pragma unroll
-    for (int uu = 0; uu < 2; ++uu) bias[uu] = ldg_f4(bias_g + d.bias0 + 16 * (2 * w + uu) + 4 * g);
-    f4 acc[2][kTiles];
-    layer_mfma<L5, step0_of(L5), kTiles, 2>(ap, pl, 0, acc);
-    lds_barrier();
-    pair_epilogue<true, kTiles>(acc, bias, pl, w, 0, m16);
-    const float* vd = in2 + 3 * ray;
+  hidden_layer<Net, L0, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, L1, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, L2, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, L3, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, L4, true>(ap, pl, bias_g, w, g, m16);
+  // skip layer cat[h4, enc]; once it has read the enc planes, pos_enc(viewdirs) of this wave's
+  // tile goes to enc k-step 0 for the view layer
+  hidden_layer<Net, L5, true>(ap, pl, bias_g, w, g, m16, [&] {
+    const float* vd = in2 + 3 * c.ray;
     float vv[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4) * kActS;
-    h8 hi, lo;
-    split8<false>(vv, hi, lo, ovf);
-    pl.enc_hi[16 * w] = __builtin_bit_cast(f4, hi);
-    pl.enc_lo[16 * w] = __builtin_bit_cast(f4, lo);
-    lds_barrier();
-  }
-  pair_layer<L6, true>(ap, pl, bias_g, w, g, m16);
-  pair_layer<L7, true>(ap, pl, bias_g, w, g, m16);
+    for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
+    put_segb(pl, 0, w, vv, ovf);
+  });
+  hidden_layer<Net, L6, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, L7, true>(ap, pl, bias_g, w, g, m16);
   // density head on h7 (this wave's tile), then the bottleneck (no activation) on h7
-  const f4 dens = head<LDEN>(ap, pl, bias_g, w, g);
-  pair_layer<LBOT, false>(ap, pl, bias_g, w, g, m16);
-  {
-    // views_linear.0: cat[bottleneck, enc_dir] + ReLU, 128 rows = 4 pairs; wave w -> pair w & 3
-    // on sample tiles 4 (w >> 2) .. + 3
-    constexpr LayerDesc d = kLayersH[LVIEW];
-    const int pr = w & 3, T0 = 4 * (w >> 2);
-    f4 bias[2];
-#pragma unroll
-    for (int uu = 0; uu < 2; ++uu) bias[uu] = ldg_f4(bias_g + d.bias0 + 16 * (2 * pr + uu) + 4 * g);
-    f4 acc[2][4];
-    layer_mfma<LVIEW, step0_of(LVIEW), 4, 2>(ap, pl, T0, acc);
-    lds_barrier();
-    pair_epilogue<true, 4>(acc, bias, pl, pr, T0, m16);
-    lds_barrier();
-  }
-  const f4 rgb = head<LRGB>(ap, pl, bias_g, w, g);
-  if (g == 0 && row < N) {
+  const f4 dens = head<Net, LDEN>(ap, pl, bias_g, w, g);
+  hidden_layer<Net, LBOT, false>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, LVIEW, true>(ap, pl, bias_g, w, g, m16);  // cat[bottleneck, enc_dir] + ReLU
+  const f4 rgb = head<Net, LRGB>(ap, pl, bias_g, w, g);
+  if (g == 0 && c.row < N) {
     const f4 o = {act_rgb(rgb[0], act), act_rgb(rgb[1], act), act_rgb(rgb[2], act), act_sigma(dens[0], act)};
-    *reinterpret_cast<f4*>(raw + 4 * row) = o;
+    *reinterpret_cast<f4*>(raw + 4 * c.row) = o;
   }
   const bool bad = (m16 & 0x7FFFu) >= 0x7C00u || ((m16 >> 16) & 0x7FFFu) >= 0x7C00u;
-  range_report(bias_g + kBiasFloats, ovf | __builtin_amdgcn_ballot_w64(bad));
+  range_report(bias_g + Net::kBiasFloats, ovf | __builtin_amdgcn_ballot_w64(bad));
+}
+
+// ---- articulated NeRFMLP (model_autodecoder.py:168-239, latents folded into the biases as in
+// mlp_art.hip), MODE 0 inputs.  The deformation MLP's 128-row layers and the view branch run as
+// 4 pairs x 2 sample-tile halves; the deformation head gives each wave its tile's delta in lane
+// group 0, broadcast to the sample's lanes with ds_bpermute (as mlp_art.hip does), x' =
+// delta + xyz in fp32, pos_enc(x') into the enc planes.
+__global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_art_ws_f16x3(
+    const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
+    const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
+    int64_t B, int S, int act, float* __restrict__ raw) {
+  using Net = NetArtH;
+  __shared__ f4 smem[kLdsF4];
+  const int64_t N = B * S;
+  const WsSetup c = ws_setup(smem, N, S);
+  const int w = c.w, g = c.g;
+  const Planes& pl = c.pl;
+  APipe<Net, AON_WS_PREFETCH> ap;
+  ap.ws = wstream;
+  ap.lane = c.lane;
+  ap.w = w;
+  ap.start();
+
+  uint64_t ovf = 0;
+  float px[3];
+  {
+    const float* ro = in0 + 3 * c.ray;
+    const float* rd = in1 + 3 * c.ray;
+    const float tt = in3[c.rr];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) px[q] = __fadd_rn(ro[q], __fmul_rn(tt, rd[q]));
+    // deformation input: xyz in lane group 0, elements 0..2 (natural order), the rest 0
+    float dv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? px[e < 3 ? e : 0] : 0.f;
+    put_segb(pl, 0, w, dv, ovf);
+  }
+  lds_barrier();
+
+  uint32_t m16 = 0;
+  hidden_layer<Net, A_D0, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_D1, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_D2, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_D3, true>(ap, pl, bias_g, w, g, m16);
+  {
+    const f4 dlt = head<Net, A_DOUT>(ap, pl, bias_g, w, g);
+    // x' = deformation + xyz (:205), pos_enc(x') (:207-212) of this wave's tile -> enc planes
+    // (the xyz segment there was last read by deformations_linear.0, long past its barriers)
+    float q3[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) q3[q] = __fadd_rn(__shfl(dlt[q], c.j, 64), px[q]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float ev[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ev[e] = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10);
+      put_segb(pl, k, w, ev, ovf);
+    }
+    lds_barrier();
+  }
+  hidden_layer<Net, A_P0, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_P1, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_P2, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_P3, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_P4, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_P5, true>(ap, pl, bias_g, w, g, m16, [&] {
+    const float* vd = in2 + 3 * c.ray;
+    float vv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
+    put_segb(pl, 0, w, vv, ovf);
+  });
+  hidden_layer<Net, A_P6, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_P7, true>(ap, pl, bias_g, w, g, m16);
+  const f4 dens = head<Net, A_DEN>(ap, pl, bias_g, w, g);
+  hidden_layer<Net, A_BOT, false>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_V0, true>(ap, pl, bias_g, w, g, m16);  // cat[bottleneck, enc_dir, app]
+  hidden_layer<Net, A_V1, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_V2, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, A_V3, true>(ap, pl, bias_g, w, g, m16);
+  const f4 rgb = head<Net, A_RGB>(ap, pl, bias_g, w, g);
+  if (g == 0 && c.row < N) {
+    const f4 o = {act_rgb(rgb[0], act), act_rgb(rgb[1], act), act_rgb(rgb[2], act), act_sigma(dens[0], act)};
+    *reinterpret_cast<f4*>(raw + 4 * c.row) = o;
+  }
+  const bool bad = (m16 & 0x7FFFu) >= 0x7C00u || ((m16 >> 16) & 0x7FFFu) >= 0x7C00u;
+  range_report(bias_g + Net::kBiasFloats, ovf | __builtin_amdgcn_ballot_w64(bad));
 }
 
 }  // namespace ws
@@ -362,9 +461,19 @@ int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const 
   const int64_t N = B * S;
   const f4* wsp = static_cast<const f4*>(packed);
   const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + kStreamBytesF32);
-  hipLaunchKernelGGL(ws::k_mlp_ws_f16x3<0>, static_cast<int>((N + ws::kNb - 1) / ws::kNb),
+  hipLaunchKernelGGL(ws::k_mlp_ws_f16x3, static_cast<int>((N + ws::kNb - 1) / ws::kNb),
                      ws::kThreads, 0, stream, wsp, bias, a0, a1, a2, a3, B, S, act, raw);
   return launch_status("aon_mlp_fwd");
+}
+
+int launch_art_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
+                        const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream) {
+  const int64_t N = B * S;
+  const f4* wsp = static_cast<const f4*>(packed);
+  const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
+  hipLaunchKernelGGL(ws::k_mlp_art_ws_f16x3, static_cast<int>((N + ws::kNb - 1) / ws::kNb),
+                     ws::kThreads, 0, stream, wsp, bias, a0, a1, a2, a3, B, S, act, raw);
+  return launch_status("aon_mlp_art_fwd");
 }
 
 }  // namespace mlp

@@ -55,7 +55,8 @@ def main():
     L.call("aon_pos_enc", L.ptr(batch["viewdirs"]), venc.shape[0], 0, 4, L.ptr(venc), L.stream())
     tgt64 = batch["target"].cpu().double()
     sd = W.art_state_dict(0)
-    for level in range(2):
+    levels = [int(x) for x in os.environ.get("ATTR_LEVELS", "0,1").split(",")]
+    for level in levels:
         t = ret[level][3]["t_vals"].contiguous()
         B, S = t.shape
         R = B * S
@@ -138,7 +139,9 @@ def main():
             print(f"   ReLU' flips vs K64, {src}: {flips}")
         variants = {"K64": kept["K64"], "K32": kept["K32"], "Kours": kept["Kours"],
                     "K64.masks_ours": with_masks("Kours"), "K64.masks_32": with_masks("K32")}
-        for g in ("hd", "h", "hv"):
+        for g in os.environ.get("ATTR_GROUPS", "hd,h,hv").split(","):
+            if not g:
+                continue
             v = dict(kept["K64"])
             v[g] = kept["Kours"][g]
             variants[f"K64+ours.{g}"] = v
