@@ -1552,6 +1552,9 @@ __global__ __launch_bounds__(THREADS, 1) void k_gemm_f16x3_dma(Params p) {
 // row order, then a fixed xor tree over the 16 row phases; one chunk's partial per workgroup
 // (k_gemm_reduce sums the chunks in z order: deterministic).
 constexpr int kSkinnyRows = 16;
+#ifndef AON_GEMM_SKINNY_SK
+#define AON_GEMM_SKINNY_SK 4  // rows in flight per thread (skinny and segment-sum kernels); 1: A/B
+#endif
 template <int M, typename TA, bool BT>
 __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
   const int tid = threadIdx.x, r = tid & 15, cg = tid >> 4;
@@ -1587,9 +1590,6 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
   // SK rows per thread in flight: their loads are issued before the first is consumed (one
   // dependent load per row left this kernel latency-bound: rgb's 0.27 GB at ~2.2 TB/s); the
   // rows are still summed in k order (bit-identical)
-#ifndef AON_GEMM_SKINNY_SK
-#define AON_GEMM_SKINNY_SK 4  // 1: one row in flight per thread (the round-3 kernel; A/B)
-#endif
   constexpr int SK = AON_GEMM_SKINNY_SK;
   int64_t k = kbeg + r;
   for (; k + (SK - 1) * kSkinnyRows < kend; k += SK * kSkinnyRows) {
@@ -1662,12 +1662,13 @@ __global__ __launch_bounds__(256) void k_gemm_segsum_bf16(Params p) {
   const int64_t n0 = 8 * (int64_t)cg;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int64_t kb = ray * rdiv, ke = kb + rdiv < p.K ? kb + rdiv : p.K;
-  for (int64_t k = kb; k < ke; ++k) {
-    const int64_t o = AT ? (k & ~int64_t(15)) * p.lda + 256 * (n0 >> 4) + 16 * (k & 15) + (n0 & 15)
-                         : k * p.lda + n0;
+  auto aoff = [&](int64_t k) {
+    return AT ? (k & ~int64_t(15)) * p.lda + 256 * (n0 >> 4) + 16 * (k & 15) + (n0 & 15)
+              : k * p.lda + n0;
+  };
+  auto add_row = [&](int64_t o, const uint4& w) {
     float v[8];
     if (std::is_same<TA, __bf16>::value) {
-      const uint4 w = *reinterpret_cast<const uint4*>(A + o);
       const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = __uint_as_float((j & 1) ? (ww[j >> 1] & 0xffff0000u) : (ww[j >> 1] << 16));
@@ -1678,6 +1679,26 @@ __global__ __launch_bounds__(256) void k_gemm_segsum_bf16(Params p) {
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = __fadd_rn(acc[j], v[j]);
+  };
+  int64_t k = kb;
+  if (std::is_same<TA, __bf16>::value) {
+    // AON_GEMM_SKINNY_SK rows' 16-B loads in flight per thread before the first is summed (one
+    // dependent load per row left one workgroup of 4 waves per CU latency-bound); the rows are
+    // still summed in k order (bit-identical)
+    constexpr int SK = AON_GEMM_SKINNY_SK;
+    for (; k + SK - 1 < ke; k += SK) {
+      uint4 w[SK];
+#pragma unroll
+      for (int u = 0; u < SK; ++u) w[u] = *reinterpret_cast<const uint4*>(A + aoff(k + u));
+#pragma unroll
+      for (int u = 0; u < SK; ++u) add_row(0, w[u]);
+    }
+  }
+  for (; k < ke; ++k) {
+    const int64_t o = aoff(k);
+    uint4 w = {0u, 0u, 0u, 0u};
+    if (std::is_same<TA, __bf16>::value) w = *reinterpret_cast<const uint4*>(A + o);
+    add_row(o, w);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) seg[rl * M + n0 + j] = acc[j];
