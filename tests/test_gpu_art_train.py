@@ -14,9 +14,10 @@ loss rtol 1e-5.  Gradients:
   * C5-size stage isolation per level (test_art_c5_level_stage_isolated): forward values 1e-5,
     d raw 1e-5 / 1e-4, backward 1e-4, each against fp64 at our own inputs;
   * x'-forced at C5's size: the fp64 oracle at our deformed points, per tensor within
-    max(k x the fp32 oracle's own forced distance, 1e-3) of its max, k = 2 x (our forward
-    distance / the fp32 oracle's) measured per level (the step's own ill-conditioning amplifies
-    6e-7 forward differences ~1e3-fold there, linearly);
+    max(2 x the largest distance of an fp32-class ensemble -- the fp32 oracle and two ulp-
+    perturbed fp32 oracles, all forced to our x' -- 1e-3) of its max (the step's own
+    ill-conditioning amplifies 6e-7 forward differences ~1e3-fold there, through a few ReLU'
+    flips);
   * free-running (the deformation gradients pass through sin(2^9 x'), so the reference's own
     fp32 evaluation sits up to ~1e-2 from fp64): vs the reference's golden gradients within
     max(4 x its fp32-vs-fp64 spread, 1e-4); teacher-forced vs the fp32 oracle within
@@ -565,15 +566,16 @@ def test_art_train_step_c5_4096_rays():
         difference of transmittance-weighted sums and dL/dx' sums 60 terms of up to 2^9 |d enc|
         that largely cancel, so a forward difference of 6e-7 (our f16x3 trunk, stage-isolated in
         test_art_c5_level_stage_isolated) reaches ~1e-3 of a deformation gradient -- and the
-        reference's own fp32 shows the same amplification of its 1e-7 (env_a: the fp32 oracle
-        forced at the same x', printed).  Gate per tensor: max(k env_a, 1e-3) of its max, with
-        k = 2 x max(1, q) derived per level: q = rms distance of OUR compositing weights from
-        the forced fp64 oracle's over the forced fp32 oracle's (printed).  In this regime the
-        gradient error is linear in the forward error (the stage-isolated backward contributes
-        <= 1.9e-5), so our gradients sit q x as far from fp64 as the fp32 oracle's; q is ~4-6,
-        because an f16x3 product keeps 22 operand bits (the dropped lo*lo term is 2^-22
-        relative) where fp32 rounds at 2^-24 -- which is why fine pts_linears.1.weight sat at
-        6x the fp32 oracle's forced distance (verdict r03);
+        reference's own fp32 shows the same amplification of its 1e-7.  Gate per tensor:
+        max(2 env_a, 1e-3) of its max, env_a = the largest distance from the forced fp64 oracle
+        of an ensemble of fp32-class evaluations at our x': the fp32 oracle and two fp32 oracles
+        whose weights differ from it by one rounding each (2^-24 relative, seeded).  One member
+        is not an envelope: the distance is carried by a few ReLU' flips in the trunk and view
+        branch (tools/diag/art_c5_forward_attr.py: the fine level's whole distance comes from the
+        view activations' masks alone, values no farther from fp64 than the fp32 oracle's), so it
+        moves by an order of magnitude between equally accurate evaluations -- the fp32 oracle sat
+        at 7.7e-5 on a fine deformation tensor where ours was 2e-3, and at 8.6e-3 on a coarse one
+        where ours was 1.3e-3 (verdict r03's 6x on fine pts_linears.1.weight is one such draw);
     (B) free-running against the fp32 oracle (the reference's arithmetic): per tensor within
         max(2 x env, 1e-3) of its max, env = the oracle's own fp32-vs-fp64 distance on that
         tensor -- or ATTRIBUTED: the gradients see sin(2^9 x') (model_autodecoder.py:205-212)
@@ -617,10 +619,18 @@ def test_art_train_step_c5_4096_rays():
         tgt = target.cpu()
         ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
     ref, ref_loss, xps, wts = {}, None, {}, {}
-    for mode, dtype in (("fp32", torch.float32), ("fp64", torch.float64), ("forced", torch.float64),
-                        ("forced32", torch.float32)):
+    def leaf(v, dtype, gen):
+        v = torch.as_tensor(v)
+        if gen is not None:  # one rounding per weight: x (1 + 2^-24 n), n ~ N(0, 1)
+            v = v.double() * (1 + 2.0 ** -24 * torch.randn(v.shape, generator=gen, dtype=torch.float64))
+        return v.to(dtype).requires_grad_(True)
+
+    modes = (("fp32", torch.float32), ("fp64", torch.float64), ("forced", torch.float64),
+             ("forced32", torch.float32), ("forced32_p1", torch.float32), ("forced32_p2", torch.float32))
+    for mode, dtype in modes:
         rays = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
-        params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
+        gen = torch.Generator().manual_seed(int(mode[-1])) if mode.startswith("forced32_p") else None
+        params = [{k: leaf(v, dtype, gen) for k, v in p.items()}
                   for p in O.split_state_dict(W.art_state_dict(0))]
         lat = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in lat_dev.items()}
         tgt = target.cpu().to(dtype)
@@ -656,25 +666,25 @@ def test_art_train_step_c5_4096_rays():
         print(f"  level {level}: x' rms error vs fp64  ours {e_ours:.2e}  fp32 oracle {e_32:.2e}  "
               f"r = {e_ours / e_32:.2f}")
     ratio["latent"] = max(ratio.values())
-    # forward distance (compositing weights at our t and x'): ours vs the fp32 oracle's, both
-    # from the forced fp64 oracle -> the (A) gate's k per level
-    k_a = {}
-    for level, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")):
+    # forward distance (compositing weights at our t and x') from the forced fp64 oracle: ours vs
+    # the fp32-class ensemble's (informational: the gate below is per tensor)
+    for level in range(2):
         w64 = wts[("forced", level)]
-        q = rms(ret[level][3]["weights"].detach().cpu().double() - w64) / rms(
-            wts[("forced32", level)] - w64)
-        k_a[pre] = 2.0 * max(1.0, q)
-        print(f"  level {level}: forward weights rms distance from forced fp64, ours / fp32 "
-              f"oracle q = {q:.2f} -> (A) k = {k_a[pre]:.2f}")
-    k_a["latent"] = max(k_a.values())
+        d_ours = rms(ret[level][3]["weights"].detach().cpu().double() - w64)
+        d_ens = [rms(wts[(m, level)] - w64) for m in ("forced32", "forced32_p1", "forced32_p2")]
+        print(f"  level {level}: forward weights rms distance from forced fp64: ours {d_ours:.2e}, "
+              f"fp32 ensemble " + " / ".join(f"{x:.2e}" for x in d_ens))
     worst_a = worst_b = 0.0
     bad_a, unexplained, attributed = [], [], []
     for name, want in ref["fp32"].items():
         ea = rel_err(ours[name], ref["forced"][name])
-        env_a = rel_err(ref["forced32"][name], ref["forced"][name])
+        # the fp32-class ensemble's distance on this tensor: the fp32 oracle and two fp32 oracles
+        # whose weights differ from it by one rounding each, all at our x'
+        env_a = max(rel_err(ref[m][name], ref["forced"][name])
+                    for m in ("forced32", "forced32_p1", "forced32_p2"))
         env = rel_err(want, ref["fp64"][name])
         r = next(v for pre, v in ratio.items() if name.startswith(pre))
-        allow_a = max(next(v for pre, v in k_a.items() if name.startswith(pre)) * env_a, 1e-3)
+        allow_a = max(2.0 * env_a, 1e-3)
         e = rel_err(ours[name], want)
         allow = max(2 * env, 1e-3)
         worst_a = max(worst_a, ea / allow_a)
@@ -685,7 +695,7 @@ def test_art_train_step_c5_4096_rays():
         if e > allow:
             (attributed if ok_a and r <= 1.5 else unexplained).append(name)
         if e > 1e-4 or ea > 1e-5 or not ok_a:
-            print(f"  {name:45s} (A) x'-forced {ea:.2e} (its fp32 {env_a:.2e}, gate {allow_a:.2e})  (B) ours {e:.2e}  "
+            print(f"  {name:45s} (A) x'-forced {ea:.2e} (fp32 ensemble {env_a:.2e}, gate {allow_a:.2e})  (B) ours {e:.2e}  "
                   f"oracle fp32-vs-fp64 {env:.2e}{'  ATTRIBUTED' if name in attributed else ''}")
     print(f"C5 art grads (4096 rays): (A) x'-forced worst error / allowance {worst_a:.2f}; (B) "
           f"free-running worst error / allowance {worst_b:.2f}, {len(attributed)} tensor(s) "
