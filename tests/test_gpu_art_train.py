@@ -13,11 +13,9 @@ loss rtol 1e-5.  Gradients:
     fp32 noise;
   * C5-size stage isolation per level (test_art_c5_level_stage_isolated): forward values 1e-5,
     d raw 1e-5 / 1e-4, backward 1e-4, each against fp64 at our own inputs;
-  * x'-forced at C5's size: the fp64 oracle at our deformed points, per tensor within
-    max(2 x the largest distance of an fp32-class ensemble -- the fp32 oracle and two ulp-
-    perturbed fp32 oracles, all forced to our x' -- 1e-3) of its max (the step's own
-    ill-conditioning amplifies 6e-7 forward differences ~1e3-fold there, through a few ReLU'
-    flips);
+  * x'- and mask-forced at C5's size: the fp64 oracle at our deformed points and our ReLU'
+    pattern, 1e-4 of each tensor's max; our ReLU' flips against fp64 at most twice the fp32
+    oracle's (the x'-forced distance alone, ~1e-3, is a lottery of those flips);
   * free-running (the deformation gradients pass through sin(2^9 x'), so the reference's own
     fp32 evaluation sits up to ~1e-2 from fp64): vs the reference's golden gradients within
     max(4 x its fp32-vs-fp64 spread, 1e-4); teacher-forced vs the fp32 oracle within
@@ -559,23 +557,21 @@ def test_art_train_step_c5_4096_rays():
     (rtol 1e-4), and every MLP parameter's and latent code's gradient against the oracle on our
     sample positions, twice:
 
-    (A) x'-forced: the oracle with pos_enc evaluated at OUR deformed points x' (gradients
-        straight through to its own deformation MLP, oracle.pos_enc_at) in fp64 -- nothing is
-        amplified by sin(2^9 x'), so the whole level's chain is compared at C5's size.  The
-        step's gradients are still ill-conditioned in the forward values: dL/dsigma is a
-        difference of transmittance-weighted sums and dL/dx' sums 60 terms of up to 2^9 |d enc|
-        that largely cancel, so a forward difference of 6e-7 (our f16x3 trunk, stage-isolated in
-        test_art_c5_level_stage_isolated) reaches ~1e-3 of a deformation gradient -- and the
-        reference's own fp32 shows the same amplification of its 1e-7.  Gate per tensor:
-        max(2 env_a, 1e-3) of its max, env_a = the largest distance from the forced fp64 oracle
-        of an ensemble of fp32-class evaluations at our x': the fp32 oracle and two fp32 oracles
-        whose weights differ from it by one rounding each (2^-24 relative, seeded).  One member
-        is not an envelope: the distance is carried by a few ReLU' flips in the trunk and view
-        branch (tools/diag/art_c5_forward_attr.py: the fine level's whole distance comes from the
-        view activations' masks alone, values no farther from fp64 than the fp32 oracle's), so it
-        moves by an order of magnitude between equally accurate evaluations -- the fp32 oracle sat
-        at 7.7e-5 on a fine deformation tensor where ours was 2e-3, and at 8.6e-3 on a coarse one
-        where ours was 1.3e-3 (verdict r03's 6x on fine pts_linears.1.weight is one such draw);
+    (A) x'- and mask-forced: the fp64 oracle with pos_enc evaluated at OUR deformed points x'
+        (oracle.pos_enc_at; gradients straight through to its own deformation MLP) and with OUR
+        ReLU' pattern (oracle.art_mlp_forward_kept on its own fp64 forward values, the units whose
+        sign differs from ours set to our side of zero), its own fp64 compositor and loss: every
+        parameter's and latent's gradient within 1e-4 of its max.  Forcing x' alone is not enough:
+        tools/diag/art_c5_forward_attr.py (profiles/r04/art_attr.log) shows the x'-forced distance
+        (~1e-3) is carried entirely by ReLU' flips -- ours 20 / 98 / 35 units of hd / h / hv on
+        the fine level, the fp32 oracle's 30 / 137 / 41 -- each a discrete event that the step's
+        ill-conditioning (dL/dx' sums 60 terms of up to 2^9 |d enc|) turns into ~1e-3 of a
+        deformation gradient, so one evaluation lands 20x closer than another of equal accuracy
+        (the fp32 oracle: 7.7e-5 on a fine deformation tensor where ours is 2e-3, 8.6e-3 on a
+        coarse one where ours is 1.3e-3; verdict r03's "6x" was one such draw).  With the pattern
+        shared the distance drops to <= 2.7e-7 (diagnostic), the backward kernels' own 3.5e-6
+        (test_art_c5_level_stage_isolated) on top.  And the flips themselves are gated: ours at
+        most max(2 x the fp32 oracle's count, 16) per group and level;
     (B) free-running against the fp32 oracle (the reference's arithmetic): per tensor within
         max(2 x env, 1e-3) of its max, env = the oracle's own fp32-vs-fp64 distance on that
         tensor -- or ATTRIBUTED: the gradients see sin(2^9 x') (model_autodecoder.py:205-212)
@@ -602,35 +598,35 @@ def test_art_train_step_c5_4096_rays():
     lat_dev = {k: v.detach().cpu() for k, v in latents.items()}
     # our x' per level: the fused forward at the level's t (deterministic: the values the
     # autograd forward saw)
-    xp_ours = []
+    from aonerf import tiles
+
+    xp_ours, relu_ours = [], []
     with torch.no_grad():
         lat_t = tuple(L_contig(latents[k]) for k in ("density", "color", "articulation"))
         for level, mlp in enumerate((net.coarse_mlp, net.fine_mlp)):
             t = ret[level][3]["t_vals"].contiguous()
+            R = t.numel()
             P = [(m.weight.detach(), m.bias.detach()) for m in train_art.art_layers(mlp)]
-            raw = torch.empty((t.numel(), 4), device="cuda")
-            enc = train_art._forward_level_fused(train_art._Geo(mlp), P, lat_t, batch["rays_o"],
-                                                 batch["rays_d"], batch["viewdirs"], t, raw)[2]
+            raw = torch.empty((R, 4), device="cuda")
+            _, hd, enc, h, _, hv = train_art._forward_level_fused(
+                train_art._Geo(mlp), P, lat_t, batch["rays_o"], batch["rays_d"], batch["viewdirs"],
+                t, raw)
             xp_ours.append(enc[:, :3].cpu())
+            # the ReLU' pattern our forward fed the backward: the sign of each kept activation
+            relu_ours.append({grp: [tiles.untile(x, R).cpu() > 0 for x in tt]
+                              for grp, tt in (("hd", hd), ("h", h), ("hv", hv))})
+            del hd, enc, h, hv
         rays = {k: batch[k].cpu() for k in ("rays_o", "rays_d", "viewdirs")}
         params = O.split_state_dict(W.art_state_dict(0))
         e2e = O.art_nerf_forward(params, rays, True, True, 2.0, 6.0, lat_dev, u_coarse=u_c.cpu(),
                                  u_fine=u_f.cpu())
         tgt = target.cpu()
         ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
-    ref, ref_loss, xps, wts = {}, None, {}, {}
-    def leaf(v, dtype, gen):
-        v = torch.as_tensor(v)
-        if gen is not None:  # one rounding per weight: x (1 + 2^-24 n), n ~ N(0, 1)
-            v = v.double() * (1 + 2.0 ** -24 * torch.randn(v.shape, generator=gen, dtype=torch.float64))
-        return v.to(dtype).requires_grad_(True)
-
-    modes = (("fp32", torch.float32), ("fp64", torch.float64), ("forced", torch.float64),
-             ("forced32", torch.float32), ("forced32_p1", torch.float32), ("forced32_p2", torch.float32))
-    for mode, dtype in modes:
+    ref, ref_loss, xps = {}, None, {}
+    for mode, dtype in (("fp32", torch.float32), ("fp64", torch.float64), ("forced", torch.float64),
+                        ("forced32", torch.float32)):
         rays = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
-        gen = torch.Generator().manual_seed(int(mode[-1])) if mode.startswith("forced32_p") else None
-        params = [{k: leaf(v, dtype, gen) for k, v in p.items()}
+        params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
                   for p in O.split_state_dict(W.art_state_dict(0))]
         lat = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in lat_dev.items()}
         tgt = target.cpu().to(dtype)
@@ -640,7 +636,6 @@ def test_art_train_step_c5_4096_rays():
             out = O.art_render_level(params, rays, t, level, True, lat, return_xp=True,
                                      xp_fixed=xp_ours[level] if mode.startswith("forced") else None)
             xps[(mode, level)] = out[4].detach().double()
-            wts[(mode, level)] = out[2].detach().double()
             lv_loss = lv_loss + O.img2mse(out[0], tgt)
         lv_loss.backward()
         if mode == "fp32":
@@ -666,40 +661,83 @@ def test_art_train_step_c5_4096_rays():
         print(f"  level {level}: x' rms error vs fp64  ours {e_ours:.2e}  fp32 oracle {e_32:.2e}  "
               f"r = {e_ours / e_32:.2f}")
     ratio["latent"] = max(ratio.values())
-    # forward distance (compositing weights at our t and x') from the forced fp64 oracle: ours vs
-    # the fp32-class ensemble's (informational: the gate below is per tensor)
+    # (A) the fp64 oracle forced to our x' AND our ReLU' pattern (values its own): the forced fp64
+    # forward's kept values, each hidden activation whose sign differs from ours replaced by ours
+    # (oracle.art_mlp_forward_kept: ReLU' from the sign), its fp64 backward through its own
+    # compositor and loss.  Mask flips are discrete events of the forward's last bits (counted
+    # below, ours against the fp32 oracle's); with the pattern shared, what is left is the
+    # continuous part, which the step does not amplify.
+    names3 = ("density", "color", "articulation")
+    l64 = {k: lat_dev[k].double().requires_grad_(True) for k in names3}
+    p64 = [{k: v.double().requires_grad_(True) for k, v in p.items()}
+           for p in O.split_state_dict(W.art_state_dict(0))]
+    o64, d64, v64 = (batch[k].cpu().double() for k in ("rays_o", "rays_d", "viewdirs"))
+    venc64 = O.pos_enc(v64, 0, 4)
+    loss_m = 0.0
+    flips = {}
     for level in range(2):
-        w64 = wts[("forced", level)]
-        d_ours = rms(ret[level][3]["weights"].detach().cpu().double() - w64)
-        d_ens = [rms(wts[(m, level)] - w64) for m in ("forced32", "forced32_p1", "forced32_p2")]
-        print(f"  level {level}: forward weights rms distance from forced fp64: ours {d_ours:.2e}, "
-              f"fp32 ensemble " + " / ".join(f"{x:.2e}" for x in d_ens))
+        t64 = ret[level][3]["t_vals"].cpu().double()
+        B_, S_ = t64.shape
+        recs = {}
+        with torch.no_grad():
+            for tag, dt in (("64", torch.float64), ("32", torch.float32)):
+                rec = {}
+                O.art_mlp_forward({k: v.detach().to(dt) for k, v in p64[level].items()},
+                                  O.cast_rays(t64.to(dt), o64.to(dt), d64.to(dt)), venc64.to(dt),
+                                  {k: v.detach().to(dt) for k, v in l64.items()},
+                                  xp_fixed=xp_ours[level], record=rec)
+                recs[tag] = rec
+        r64 = recs["64"]
+        kept = {"xyz": r64["xyz"], "xp": xp_ours[level], "enc": r64["enc"], "bot": r64["bot"]}
+        for grp in ("hd", "h", "hv"):
+            # a flipped unit takes 1e-30 (ours > 0: fp64 had it at 0, ~1e-7 from the edge) or 0
+            kept[grp] = [torch.where(m == (v > 0), v, torch.where(m, torch.full_like(v, 1e-30),
+                                                                 torch.zeros_like(v)))
+                         for m, v in zip(relu_ours[level][grp], r64[grp])]
+            flips[(level, grp)] = (
+                sum(int((m != (v > 0)).sum()) for m, v in zip(relu_ours[level][grp], r64[grp])),
+                sum(int(((a > 0) != (v > 0)).sum()) for a, v in zip(recs["32"][grp], r64[grp])))
+        del recs
+        r_rgb, r_sig = O.art_mlp_forward_kept(p64[level], kept, venc64, l64, S_)
+        rgb_a, sig_a = O.art_activations(r_rgb.reshape(B_, S_, 3), r_sig.reshape(B_, S_, 1))
+        comp = O.volumetric_rendering(rgb_a, sig_a, t64, d64, True)[0]
+        loss_m = loss_m + O.img2mse(comp, target.cpu().double())
+        del kept, r_rgb, r_sig
+    loss_m.backward()
+    ref["masked"] = {f"{pre}{n}": v.grad.double().numpy()
+                     for lv, pre in ((0, "coarse_mlp."), (1, "fine_mlp.")) for n, v in p64[lv].items()}
+    ref["masked"].update({f"latent {k}": v.grad.double().numpy() for k, v in l64.items()})
+    bad_flips = []
+    for (level, grp), (fo, f32) in sorted(flips.items()):
+        print(f"  level {level} {grp}: ReLU' flips against the forced fp64 forward: ours {fo}, fp32 "
+              f"oracle {f32}")
+        if fo > max(2 * f32, 16):
+            bad_flips.append((level, grp, fo, f32))
     worst_a = worst_b = 0.0
     bad_a, unexplained, attributed = [], [], []
     for name, want in ref["fp32"].items():
-        ea = rel_err(ours[name], ref["forced"][name])
-        # the fp32-class ensemble's distance on this tensor: the fp32 oracle and two fp32 oracles
-        # whose weights differ from it by one rounding each, all at our x'
-        env_a = max(rel_err(ref[m][name], ref["forced"][name])
-                    for m in ("forced32", "forced32_p1", "forced32_p2"))
+        ea = rel_err(ours[name], ref["masked"][name])
+        lottery = rel_err(ours[name], ref["forced"][name])
+        lottery32 = rel_err(ref["forced32"][name], ref["forced"][name])
         env = rel_err(want, ref["fp64"][name])
         r = next(v for pre, v in ratio.items() if name.startswith(pre))
-        allow_a = max(2.0 * env_a, 1e-3)
         e = rel_err(ours[name], want)
         allow = max(2 * env, 1e-3)
-        worst_a = max(worst_a, ea / allow_a)
+        worst_a = max(worst_a, ea / 1e-4)
         worst_b = max(worst_b, e / allow)
-        ok_a = ea <= allow_a
+        ok_a = ea <= 1e-4
         if not ok_a:
-            bad_a.append((name, ea, env_a))
+            bad_a.append((name, ea))
         if e > allow:
             (attributed if ok_a and r <= 1.5 else unexplained).append(name)
         if e > 1e-4 or ea > 1e-5 or not ok_a:
-            print(f"  {name:45s} (A) x'-forced {ea:.2e} (fp32 ensemble {env_a:.2e}, gate {allow_a:.2e})  (B) ours {e:.2e}  "
-                  f"oracle fp32-vs-fp64 {env:.2e}{'  ATTRIBUTED' if name in attributed else ''}")
-    print(f"C5 art grads (4096 rays): (A) x'-forced worst error / allowance {worst_a:.2f}; (B) "
+            print(f"  {name:45s} (A) mask-forced {ea:.2e}, unforced {lottery:.2e} (fp32 oracle "
+                  f"{lottery32:.2e})  (B) ours {e:.2e}  oracle fp32-vs-fp64 {env:.2e}"
+                  f"{'  ATTRIBUTED' if name in attributed else ''}")
+    print(f"C5 art grads (4096 rays): (A) x'- and mask-forced worst error / 1e-4 {worst_a:.2f}; (B) "
           f"free-running worst error / allowance {worst_b:.2f}, {len(attributed)} tensor(s) "
           f"outside it attributed to x' rounding")
+    assert not bad_flips, bad_flips
     assert not bad_a, bad_a
     assert not unexplained, unexplained
 

@@ -53,8 +53,7 @@ print("streamed run-to-run equal:", torch.equal(outs[0], outs[2]), " ws run-to-r
 if not a.art:  # the fused TRAINING forward (same epilogue arithmetic, fp32 kept tensors) on the same rows
     from aonerf import train
 
-    ps = [p.detach() for p in mlp.parameters()]
-    P = [(ps[2 * i], ps[2 * i + 1]) for i in range(12)]
+    P = [(m.weight.detach(), m.bias.detach()) for m in mlp._layers()]
     raw_t = torch.empty((B * S, 4), device="cuda")
     h, bot, hv = train._forward_level_fused(P, o, d, d, t, raw_t)
     raw_t = raw_t.cpu()
