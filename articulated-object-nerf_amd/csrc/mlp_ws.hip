@@ -135,6 +135,10 @@ struct Planes {
   lds_f4w* enc_lo;
 };
 
+#ifndef AON_WS_VENC_EARLY
+#define AON_WS_VENC_EARLY 0
+#endif
+
 #ifndef AON_WS_BPF
 #define AON_WS_BPF 2  // B fragments (one sample tile's hi + lo) read from LDS ahead of their MFMAs
 #endif
@@ -206,6 +210,11 @@ __device__ __forceinline__ void pair_epilogue(const f4 (&acc)[2][NT], const f4 (
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         float v = fmaf(acc[uu][t][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
+        // pinned: without an activation between them hipcc folds this fma and the fp16
+        // conversion of the hi part into one v_fma_mixlo_f16 -- ONE rounding of the exact fma
+        // to fp16 where the split (and k_mlp_fwd_f16x3) rounds to fp32 first: 1-ulp different
+        // hi / lo pairs in the bottleneck (tools/diag/ws_diff2.py)
+        asm("" : "+v"(v));
         if (RELU) v = fmaxf(v, 0.0f);
         vv[e] = v;
       }
@@ -345,6 +354,20 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
   hidden_layer<Net, L4, true>(ap, pl, bias_g, w, g, m16);
   // skip layer cat[h4, enc]; once it has read the enc planes, pos_enc(viewdirs) of this wave's
   // tile goes to enc k-step 0 for the view layer
+#if AON_WS_VENC_EARLY  // A/B: pos_enc(viewdirs) computed at the start, parked in registers
+  h8 vhi, vlo;
+  {
+    const float* vd = in2 + 3 * c.ray;
+    float vv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4) * kActS;
+    split8<false>(vv, vhi, vlo, ovf);
+  }
+  hidden_layer<Net, L5, true>(ap, pl, bias_g, w, g, m16, [&] {
+    pl.enc_hi[16 * w] = __builtin_bit_cast(f4, vhi);
+    pl.enc_lo[16 * w] = __builtin_bit_cast(f4, vlo);
+  });
+#else
   hidden_layer<Net, L5, true>(ap, pl, bias_g, w, g, m16, [&] {
     const float* vd = in2 + 3 * c.ray;
     float vv[8];
@@ -352,6 +375,7 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
     for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
     put_segb(pl, 0, w, vv, ovf);
   });
+#endif
   hidden_layer<Net, L6, true>(ap, pl, bias_g, w, g, m16);
   hidden_layer<Net, L7, true>(ap, pl, bias_g, w, g, m16);
   // density head on h7 (this wave's tile), then the bottleneck (no activation) on h7

@@ -22,14 +22,30 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rays", type=int, default=307200)
 ap.add_argument("--samples", type=int, default=193)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--art", action="store_true", help="the articulated MLP (NeRF_AE_Art fine level)")
 a = ap.parse_args()
 g = torch.Generator(device="cuda").manual_seed(0)
 B, S = a.rays, a.samples
 o = torch.randn(B, 3, device="cuda", generator=g) * 0.1 + torch.tensor([0.0, -3.5, 2.0], device="cuda")
 d = torch.nn.functional.normalize(torch.randn(B, 3, device="cuda", generator=g), dim=-1)
 t = torch.sort(torch.rand(B, S, device="cuda", generator=g) * 4 + 2, dim=-1).values
-net = init_like_reference(NeRF()).cuda()
-net.set_precision("f16x3")
+if a.art:
+    from aonerf.model_autodecoder import NeRF_AE_Art
+    from aonerf.synthetic import art_latents
+
+    net = init_like_reference(NeRF_AE_Art()).cuda()
+    lat = art_latents(0, device="cuda")
+    MAC = 714_880
+
+    def fwd():
+        return net.fine_mlp.forward_rays(o, d, d, t, lat)
+else:
+    net = init_like_reference(NeRF()).cuda()
+    net.set_precision("f16x3")
+    MAC = 593_408
+
+    def fwd():
+        return net.fine_mlp.forward_rays(o, d, d, t)
 lib = L.lib()
 ms = {0: [], 1: []}
 same = True
@@ -39,7 +55,7 @@ for r in range(a.reps):
         lib.aon_mlp_set_dataflow(df)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        raw = net.fine_mlp.forward_rays(o, d, d, t)
+        raw = fwd()
         e1.record()
         torch.cuda.synchronize()
         ms[df].append(e0.elapsed_time(e1))
@@ -51,7 +67,7 @@ for r in range(a.reps):
         print(f"rep {r}: MISMATCH max {diff.max().item():.3e} at {int(diff.argmax())}, "
               f"{int((diff > 0).sum())} values differ", flush=True)
     print(f"rep {r}: streamed {ms[0][-1]:.2f} ms  ws {ms[1][-1]:.2f} ms  bit-equal {eq}", flush=True)
-flop = 2 * 593408 * B * S
+flop = 2 * MAC * B * S
 res = {k: {"median_ms": float(np.median(v[1:] or v)),
            "tflops": flop / float(np.median(v[1:] or v)) / 1e9,
            "frac_f16x3_peak": flop / float(np.median(v[1:] or v)) / 1e9 / (2500 / 3)}
