@@ -30,18 +30,40 @@ namespace aon {
 namespace mlp {
 namespace ws {
 
-constexpr int kWaves = 8;
-constexpr int kThreads = 64 * kWaves;
-constexpr int kTiles = 8;            // 16-sample tiles per workgroup pass
-constexpr int kNb = 16 * kTiles;     // 128 samples
-constexpr int kActPlane = 8 * 4 * kNb;  // f4: [k-step 8][lane group 4][sample 128] = 64 KB
-constexpr int kEncPlane = 2 * 4 * kNb;  // f4: pos_enc(x) (2 k-steps), later pos_enc(dir) (1)
-constexpr int kLdsF4 = 2 * kActPlane + 2 * kEncPlane;
-static_assert(kLdsF4 * 16 <= 160 * 1024, "LDS");
-
 #ifndef AON_WS_PREFETCH
-#define AON_WS_PREFETCH 3  // k-steps of A fragments in flight ahead of the one in use
+#define AON_WS_PREFETCH 3  // k-steps of A fragments in flight ahead of the one in use (8 waves)
 #endif
+
+// Workgroup geometry.  WAVES = 8: one workgroup of 128 samples per CU (160 KB of LDS), 2 waves
+// per SIMD; WAVES = 4: 64 samples (80 KB), two workgroups per CU, one wave of each per SIMD --
+// their barriers and epilogues fall at different times, so one workgroup's MFMAs run while the
+// other's waves wait (the 8-wave kernel's SIMD-mates reach every barrier and epilogue together).
+template <int WAVES>
+struct Geo {
+  static constexpr int kWaves = WAVES;
+  static constexpr int kThreads = 64 * WAVES;
+  static constexpr int kTiles = WAVES;              // 16-sample tiles per workgroup pass
+  static constexpr int kNb = 16 * kTiles;           // samples per pass
+  static constexpr int kActPlane = 8 * 4 * kNb;     // f4: [k-step 8][lane group 4][sample]
+  static constexpr int kEncPlane = 2 * 4 * kNb;     // f4: segment B, 2 k-steps
+  static constexpr int kLdsF4 = 2 * kActPlane + 2 * kEncPlane;
+  static constexpr int kWavesPerSimd = 2;           // __launch_bounds__: 256 VGPRs per wave
+  // A-fragment k-steps in flight (AON_WS_PREFETCH): 4 row tiles per wave at WAVES = 4 hold twice
+  // the registers per k-step, so one step less fits in 256 VGPRs without spills
+  static constexpr int kPrefetch = WAVES == 8 ? AON_WS_PREFETCH : AON_WS_PREFETCH - 1;
+  static_assert(kLdsF4 * 16 * (8 / WAVES) <= 160 * 1024, "LDS");
+  // the rows a wave computes in a layer of u row tiles: row tiles [rt0, rt0 + TU) over sample
+  // tiles [T0, T0 + NT).  Pairs per layer P = u / 2; P >= WAVES: P / WAVES pairs each over every
+  // sample tile; P < WAVES: WAVES / P waves share a pair, splitting the sample tiles.
+  __host__ __device__ static constexpr int tu(int u) { return u / 2 >= WAVES ? u / WAVES : 2; }
+  __host__ __device__ static constexpr int nt(int u) { return u / 2 >= WAVES ? kTiles : kTiles * (u / 2) / WAVES; }
+  __host__ __device__ static constexpr int rt0(int u, int w) {
+    return u / 2 >= WAVES ? tu(u) * w : 2 * (w % (u / 2));
+  }
+  __host__ __device__ static constexpr int t0(int u, int w) {
+    return u / 2 >= WAVES ? 0 : nt(u) * (w / (u / 2));
+  }
+};
 
 // The per-wave step sequence of a network: its layers in table order (both layer tables list
 // them in execution order), each ka + kb 32-deep k-steps.
@@ -58,18 +80,15 @@ __host__ __device__ constexpr int layer_of_step(int s) {
 template <typename Net>
 constexpr int kStepsOf = step0_of<Net>(Net::kNumLayers);
 
-// Which rows a wave computes: a 256-row layer (16 tiles) -> pair w over all 8 sample tiles; a
-// 128-row layer (8 tiles) -> pair w & 3 over sample tiles 4 (w >> 2) .. + 3; a 1-tile head ->
-// tile 0 over sample tile w (every wave: its own tile).
-__host__ __device__ constexpr int pair_of(int u, int w) { return u == 16 ? w : (w & 3); }
-
-// A fragments straight from the packed stream (global, L2-resident), D k-steps ahead.
-template <typename Net, int D>
+// A fragments straight from the packed stream (global, L2-resident), D k-steps ahead: the
+// wave's TU row tiles of each k-step (a 1-tile head: tile 0, on every wave).
+template <typename Net, typename G, int D>
 struct APipe {
+  static constexpr int TM = G::tu(16);  // most row tiles a wave holds
   const f4* __restrict__ ws;
   int lane, w;
-  f4 qh[D][2], ql[D][2];
-  __device__ __forceinline__ void fetch(int s, f4 (&h)[2], f4 (&l)[2]) {
+  f4 qh[D][TM], ql[D][TM];
+  __device__ __forceinline__ void fetch(int s, f4 (&h)[TM], f4 (&l)[TM]) {
     if (s >= kStepsOf<Net>) return;
     const int L = layer_of_step<Net>(s);
     const int k = s - step0_of<Net>(L);
@@ -81,30 +100,32 @@ struct APipe {
       l[0] = ws[(size_t)(b + 1) * 64 + lane];
       return;
     }
-    const int pr = pair_of(d.u, w);
+    const int r0 = G::rt0(d.u, w);
 #pragma unroll
-    for (int uu = 0; uu < 2; ++uu) {
-      const int b = d.blk0 + 2 * ((pr * K + k) * 2 + uu);
-      h[uu] = ws[(size_t)b * 64 + lane];
-      l[uu] = ws[(size_t)(b + 1) * 64 + lane];
+    for (int i = 0; i < TM; ++i) {
+      if (i >= G::tu(d.u)) break;
+      const int u = r0 + i;
+      const int b = d.blk0 + 2 * (((u >> 1) * K + k) * 2 + (u & 1));
+      h[i] = ws[(size_t)b * 64 + lane];
+      l[i] = ws[(size_t)(b + 1) * 64 + lane];
     }
   }
   __device__ __forceinline__ void start() {
 #pragma unroll
     for (int i = 0; i < D; ++i) fetch(i, qh[i], ql[i]);
   }
-  __device__ __forceinline__ void take(int s, h8 (&wh)[2], h8 (&wl)[2]) {
+  __device__ __forceinline__ void take(int s, h8 (&wh)[TM], h8 (&wl)[TM]) {
 #pragma unroll
-    for (int uu = 0; uu < 2; ++uu) {
-      wh[uu] = as_h8(qh[0][uu]);
-      wl[uu] = as_h8(ql[0][uu]);
+    for (int i = 0; i < TM; ++i) {
+      wh[i] = as_h8(qh[0][i]);
+      wl[i] = as_h8(ql[0][i]);
     }
 #pragma unroll
-    for (int i = 0; i + 1 < D; ++i)
+    for (int q = 0; q + 1 < D; ++q)
 #pragma unroll
-      for (int uu = 0; uu < 2; ++uu) {
-        qh[i][uu] = qh[i + 1][uu];
-        ql[i][uu] = ql[i + 1][uu];
+      for (int i = 0; i < TM; ++i) {
+        qh[q][i] = qh[q + 1][i];
+        ql[q][i] = ql[q + 1][i];
       }
     fetch(s + D, qh[D - 1], ql[D - 1]);
   }
@@ -143,25 +164,25 @@ struct Planes {
 #define AON_WS_BPF 2  // B fragments (one sample tile's hi + lo) read from LDS ahead of their MFMAs
 #endif
 
-// MFMAs of one layer for NT sample tiles starting at tile T0 and the tiles uu < NU of the wave's
-// pair: acc[uu][t] = sum_k W[k] . B[k] (3 products per k-step into one accumulator, k-steps in
-// order).  The (k, t) loop runs flat with the B fragments of the next AON_WS_BPF (k, t) steps
-// already read from LDS (the sched_barrier keeps those reads above the current step's MFMAs:
-// left alone, hipcc sinks each ds_read to its use and waits lgkmcnt(0) in front of every sample
-// tile's MFMAs).
-template <typename Net, int L, int NT, int NU, typename AP>
-__device__ __forceinline__ void layer_mfma(AP& ap, const Planes& pl, int T0, f4 (&acc)[2][NT]) {
+// MFMAs of one layer for NT sample tiles from T0 and TU row tiles: acc[i][t] = sum_k W[k] . B[k]
+// (3 products per k-step into one accumulator, k-steps in order).  The (k, t) loop runs flat
+// with the B fragments of the next AON_WS_BPF (k, t) steps already read from LDS (the
+// sched_barrier keeps those reads above the current step's MFMAs: left alone, hipcc sinks each
+// ds_read to its use and waits lgkmcnt(0) in front of every sample tile's MFMAs).
+template <typename Net, typename G, int L, int NT, int TU, typename AP>
+__device__ __forceinline__ void layer_mfma(AP& ap, const Planes& pl, int T0, f4 (&acc)[TU][NT]) {
   constexpr LayerDesc d = Net::layer(L);
   constexpr int K = d.ka + d.kb;
   constexpr int NS = K * NT;
   constexpr int P = AON_WS_BPF < NS ? AON_WS_BPF : NS;
   constexpr int S0 = step0_of<Net>(L);
+  constexpr int kNb = G::kNb;
 #pragma unroll
-  for (int uu = 0; uu < NU; ++uu)
+  for (int i = 0; i < TU; ++i)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[uu][t] = f4{0.f, 0.f, 0.f, 0.f};
-  auto bsrc = [&](int i, f4& xh, f4& xl) {
-    const int k = i / NT, t = i % NT;
+    for (int t = 0; t < NT; ++t) acc[i][t] = f4{0.f, 0.f, 0.f, 0.f};
+  auto bsrc = [&](int s, f4& xh, f4& xl) {
+    const int k = s / NT, t = s % NT;
     const lds_f4w* bh = k < d.ka ? pl.act_hi + k * 4 * kNb : pl.enc_hi + (k - d.ka) * 4 * kNb;
     const lds_f4w* bl = k < d.ka ? pl.act_lo + k * 4 * kNb : pl.enc_lo + (k - d.ka) * 4 * kNb;
     xh = bh[16 * (T0 + t)];
@@ -169,105 +190,110 @@ __device__ __forceinline__ void layer_mfma(AP& ap, const Planes& pl, int T0, f4 
   };
   f4 qh[P], ql[P];
 #pragma unroll
-  for (int i = 0; i < P; ++i) bsrc(i, qh[i], ql[i]);
-  h8 wh[2], wl[2];
+  for (int s = 0; s < P; ++s) bsrc(s, qh[s], ql[s]);
+  h8 wh[AP::TM], wl[AP::TM];
 #pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    const int t = i % NT;
-    if (t == 0) ap.take(S0 + i / NT, wh, wl);
+  for (int s = 0; s < NS; ++s) {
+    const int t = s % NT;
+    if (t == 0) ap.take(S0 + s / NT, wh, wl);
     const h8 xh = as_h8(qh[0]), xl = as_h8(ql[0]);
 #pragma unroll
     for (int p = 0; p + 1 < P; ++p) {
       qh[p] = qh[p + 1];
       ql[p] = ql[p + 1];
     }
-    if (i + P < NS) bsrc(i + P, qh[P - 1], ql[P - 1]);
+    if (s + P < NS) bsrc(s + P, qh[P - 1], ql[P - 1]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int uu = 0; uu < NU; ++uu) {
-      acc[uu][t] = mfma16(wh[uu], xh, acc[uu][t]);
-      acc[uu][t] = mfma16(wh[uu], xl, acc[uu][t]);
-      acc[uu][t] = mfma16(wl[uu], xh, acc[uu][t]);
+    for (int i = 0; i < TU; ++i) {
+      acc[i][t] = mfma16(wh[i], xh, acc[i][t]);
+      acc[i][t] = mfma16(wh[i], xl, acc[i][t]);
+      acc[i][t] = mfma16(wl[i], xh, acc[i][t]);
     }
   }
 }
 
-// epilogue of a pair's tiles: bias at activation scale, ReLU, fp16 hi / lo split
-// (mlp_f16x3_core.hpp epi_part, V2 + fma_mix), written as the lane's k-step-pr B fragment of the
-// next layer; m16: the range guard's packed max of the hi bits
-template <bool RELU, int NT>
-__device__ __forceinline__ void pair_epilogue(const f4 (&acc)[2][NT], const f4 (&bias)[2],
-                                              const Planes& pl, int pr, int T0, uint32_t& m16) {
+// epilogue of the wave's row tiles: bias at activation scale, ReLU, fp16 hi / lo split
+// (mlp_f16x3_core.hpp epi_part, V2 + fma_mix), written as the lanes' B fragments of the next
+// layer (row tiles 2 pr, 2 pr + 1 = k-step pr); m16: the range guard's packed max of the hi bits
+template <typename G, bool RELU, int NT, int TU>
+__device__ __forceinline__ void pair_epilogue(const f4 (&acc)[TU][NT], const f4 (&bias)[TU],
+                                              const Planes& pl, int rt0, int T0, uint32_t& m16) {
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  constexpr int kNb = G::kNb;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    u4 hw, lw;
+  for (int p = 0; p < TU / 2; ++p)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int uu = q >> 1, r0 = (q & 1) * 2;
-      float vv[2];
+    for (int t = 0; t < NT; ++t) {
+      u4 hw, lw;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        float v = fmaf(acc[uu][t][r0 + e], 1.0f / kWS, bias[uu][r0 + e]);
-        // pinned: without an activation between them hipcc folds this fma and the fp16
-        // conversion of the hi part into one v_fma_mixlo_f16 -- ONE rounding of the exact fma
-        // to fp16 where the split (and k_mlp_fwd_f16x3) rounds to fp32 first: 1-ulp different
-        // hi / lo pairs in the bottleneck (tools/diag/ws_diff2.py)
-        asm("" : "+v"(v));
-        if (RELU) v = fmaxf(v, 0.0f);
-        vv[e] = v;
+      for (int q = 0; q < 4; ++q) {
+        const int uu = q >> 1, r0 = (q & 1) * 2;
+        float vv[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          float v = fmaf(acc[2 * p + uu][t][r0 + e], 1.0f / kWS, bias[2 * p + uu][r0 + e]);
+          // no activation: pinned, else hipcc folds this fma and the fp16 conversion of the hi
+          // part into one v_fma_mixlo_f16 -- ONE rounding of the exact fma to fp16 where the
+          // split (and k_mlp_fwd_f16x3) rounds to fp32 first: 1-ulp different hi / lo pairs in
+          // the bottleneck (tools/diag/ws_diff2.py).  (With ReLU the max stands between them;
+          // a pin there would also cost a canonicalising v_max per value.)
+          if (!RELU) asm("" : "+v"(v));
+          if (RELU) v = fmaxf(v, 0.0f);
+          vv[e] = v;
+        }
+        const h2 hp = {static_cast<_Float16>(vv[0]), static_cast<_Float16>(vv[1])};
+        const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
+        m16 = pk_max_i16(m16, RELU ? hu : (hu & 0x7FFF7FFFu));
+        asm("" : "+v"(m16));
+        float d0, d1;
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(vv[0]));
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(vv[1]));
+        const h2 lp = {static_cast<_Float16>(d0), static_cast<_Float16>(d1)};
+        hw[q] = hu;
+        lw[q] = __builtin_bit_cast(uint32_t, lp);
       }
-      const h2 hp = {static_cast<_Float16>(vv[0]), static_cast<_Float16>(vv[1])};
-      const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
-      m16 = pk_max_i16(m16, RELU ? hu : (hu & 0x7FFF7FFFu));
-      asm("" : "+v"(m16));
-      float d0, d1;
-      asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(vv[0]));
-      asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(vv[1]));
-      const h2 lp = {static_cast<_Float16>(d0), static_cast<_Float16>(d1)};
-      hw[q] = hu;
-      lw[q] = __builtin_bit_cast(uint32_t, lp);
+      const int pr = rt0 / 2 + p;
+      pl.act_hi[pr * 4 * kNb + 16 * (T0 + t)] = __builtin_bit_cast(f4, hw);
+      pl.act_lo[pr * 4 * kNb + 16 * (T0 + t)] = __builtin_bit_cast(f4, lw);
     }
-    pl.act_hi[pr * 4 * kNb + 16 * (T0 + t)] = __builtin_bit_cast(f4, hw);
-    pl.act_lo[pr * 4 * kNb + 16 * (T0 + t)] = __builtin_bit_cast(f4, lw);
-  }
 }
 
 __device__ __forceinline__ f4 ldg_f4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
-// One hidden layer (256 or 128 rows) of the wave's rows and sample tiles (pair_of), output in
+// One hidden layer (256 or 128 rows) of the wave's rows and sample tiles (Geo), output in
 // place: MFMAs; barrier (every wave past its reads of the input planes); epilogue; `mid` (work
 // that needs the input planes free, e.g. the next segment B into the enc planes); barrier.
 struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
-template <typename Net, int L, bool RELU, typename AP, typename MID = NoMid>
+template <typename Net, typename G, int L, bool RELU, typename AP, typename MID = NoMid>
 __device__ __forceinline__ void hidden_layer(AP& ap, const Planes& pl, const float* bias_g, int w,
                                              int g, uint32_t& m16, const MID& mid = MID{}) {
   constexpr LayerDesc d = Net::layer(L);
   static_assert(d.u == 16 || d.u == 8, "hidden layer of 256 or 128 rows");
-  constexpr int NT = d.u == 16 ? kTiles : kTiles / 2;
-  const int pr = pair_of(d.u, w), T0 = d.u == 16 ? 0 : NT * (w >> 2);
-  f4 bias[2];
+  constexpr int NT = G::nt(d.u), TU = G::tu(d.u);
+  const int r0 = G::rt0(d.u, w), T0 = G::t0(d.u, w);
+  f4 bias[TU];
 #pragma unroll
-  for (int uu = 0; uu < 2; ++uu) bias[uu] = ldg_f4(bias_g + d.bias0 + 16 * (2 * pr + uu) + 4 * g);
-  f4 acc[2][NT];
-  layer_mfma<Net, L, NT, 2>(ap, pl, T0, acc);
+  for (int i = 0; i < TU; ++i) bias[i] = ldg_f4(bias_g + d.bias0 + 16 * (r0 + i) + 4 * g);
+  f4 acc[TU][NT];
+  layer_mfma<Net, G, L, NT, TU>(ap, pl, T0, acc);
   lds_barrier();
-  pair_epilogue<RELU, NT>(acc, bias, pl, pr, T0, m16);
+  pair_epilogue<G, RELU, NT, TU>(acc, bias, pl, r0, T0, m16);
   mid();
   lds_barrier();
 }
 
 // a 1-tile head (density / rgb / deformation) on the wave's own sample tile: 4 rows at true scale
-template <typename Net, int L, typename AP>
+template <typename Net, typename G, int L, typename AP>
 __device__ __forceinline__ f4 head(AP& ap, const Planes& pl, const float* bias_g, int w, int g) {
   constexpr LayerDesc d = Net::layer(L);
   static_assert(d.u == 1 && d.kb == 0, "head");
   const f4 bias = ldg_f4(bias_g + d.bias0 + 4 * g);
-  f4 acc[2][1];
-  layer_mfma<Net, L, 1, 1>(ap, pl, w, acc);
+  f4 acc[1][1];
+  layer_mfma<Net, G, L, 1, 1>(ap, pl, w, acc);
   f4 res;
 #pragma unroll
   for (int r = 0; r < 4; ++r) res[r] = fmaf(acc[0][0][r], 1.0f / (kWS * kActS), bias[r]);
@@ -276,6 +302,7 @@ __device__ __forceinline__ f4 head(AP& ap, const Planes& pl, const float* bias_g
 
 // 8 fp32 features (true scale) of a segment-B k-step of this lane -> the enc planes (hi / lo at
 // activation scale, split8's range test into ovf)
+template <typename G>
 __device__ __forceinline__ void put_segb(const Planes& pl, int k, int w, const float (&v)[8],
                                          uint64_t& ovf) {
   float ev[8];
@@ -283,8 +310,8 @@ __device__ __forceinline__ void put_segb(const Planes& pl, int k, int w, const f
   for (int e = 0; e < 8; ++e) ev[e] = v[e] * kActS;
   h8 hi, lo;
   split8<false>(ev, hi, lo, ovf);
-  pl.enc_hi[k * 4 * kNb + 16 * w] = __builtin_bit_cast(f4, hi);
-  pl.enc_lo[k * 4 * kNb + 16 * w] = __builtin_bit_cast(f4, lo);
+  pl.enc_hi[k * 4 * G::kNb + 16 * w] = __builtin_bit_cast(f4, hi);
+  pl.enc_lo[k * 4 * G::kNb + 16 * w] = __builtin_bit_cast(f4, lo);
 }
 
 struct WsSetup {
@@ -292,6 +319,7 @@ struct WsSetup {
   int lane, w, g, j;
   int64_t row, rr, ray;
 };
+template <typename G>
 __device__ __forceinline__ WsSetup ws_setup(f4* smem, int64_t N, int S) {
   WsSetup c;
   const int tid = threadIdx.x;
@@ -299,29 +327,31 @@ __device__ __forceinline__ WsSetup ws_setup(f4* smem, int64_t N, int S) {
   c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
   c.g = c.lane >> 4;
   c.j = c.lane & 15;
-  const int gj = c.g * kNb + c.j;
+  const int gj = c.g * G::kNb + c.j;
   c.pl.act_hi = lds_base(smem + gj);
-  c.pl.act_lo = lds_base(smem + kActPlane + gj);
-  c.pl.enc_hi = lds_base(smem + 2 * kActPlane + gj);
-  c.pl.enc_lo = lds_base(smem + 2 * kActPlane + kEncPlane + gj);
-  c.row = (int64_t)blockIdx.x * kNb + 16 * c.w + c.j;  // this lane's sample (wave w's tile)
+  c.pl.act_lo = lds_base(smem + G::kActPlane + gj);
+  c.pl.enc_hi = lds_base(smem + 2 * G::kActPlane + gj);
+  c.pl.enc_lo = lds_base(smem + 2 * G::kActPlane + G::kEncPlane + gj);
+  c.row = (int64_t)blockIdx.x * G::kNb + 16 * c.w + c.j;  // this lane's sample (wave w's tile)
   c.rr = c.row < N ? c.row : N - 1;
   c.ray = c.rr / S;
   return c;
 }
 
 // ---- vanilla NeRFMLP (model.py:95-120), MODE 0 inputs: rays_o, rays_d, viewdirs, t
-__global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 2) void k_mlp_ws_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
     int64_t B, int S, int act, float* __restrict__ raw) {
   using Net = NetVanillaH;
-  __shared__ f4 smem[kLdsF4];
+  using G = Geo<WAVES>;
+  __shared__ f4 smem[G::kLdsF4];
   const int64_t N = B * S;
-  const WsSetup c = ws_setup(smem, N, S);
+  const WsSetup c = ws_setup<G>(smem, N, S);
   const int w = c.w, g = c.g;
   const Planes& pl = c.pl;
-  APipe<Net, AON_WS_PREFETCH> ap;
+  APipe<Net, G, G::kPrefetch> ap;
   ap.ws = wstream;
   ap.lane = c.lane;
   ap.w = w;
@@ -341,48 +371,33 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
       float ev[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) ev[e] = pos_enc_feature(x0, x1, x2, 32 * k + 8 * g + e, 0, 10);
-      put_segb(pl, k, w, ev, ovf);
+      put_segb<G>(pl, k, w, ev, ovf);
     }
   }
   lds_barrier();
 
   uint32_t m16 = 0;
-  hidden_layer<Net, L0, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, L1, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, L2, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, L3, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, L4, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, L0, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, L1, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, L2, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, L3, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, L4, true>(ap, pl, bias_g, w, g, m16);
   // skip layer cat[h4, enc]; once it has read the enc planes, pos_enc(viewdirs) of this wave's
   // tile goes to enc k-step 0 for the view layer
-#if AON_WS_VENC_EARLY  // A/B: pos_enc(viewdirs) computed at the start, parked in registers
-  h8 vhi, vlo;
-  {
-    const float* vd = in2 + 3 * c.ray;
-    float vv[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4) * kActS;
-    split8<false>(vv, vhi, vlo, ovf);
-  }
-  hidden_layer<Net, L5, true>(ap, pl, bias_g, w, g, m16, [&] {
-    pl.enc_hi[16 * w] = __builtin_bit_cast(f4, vhi);
-    pl.enc_lo[16 * w] = __builtin_bit_cast(f4, vlo);
-  });
-#else
-  hidden_layer<Net, L5, true>(ap, pl, bias_g, w, g, m16, [&] {
+  hidden_layer<Net, G, L5, true>(ap, pl, bias_g, w, g, m16, [&] {
     const float* vd = in2 + 3 * c.ray;
     float vv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
-    put_segb(pl, 0, w, vv, ovf);
+    put_segb<G>(pl, 0, w, vv, ovf);
   });
-#endif
-  hidden_layer<Net, L6, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, L7, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, L6, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, L7, true>(ap, pl, bias_g, w, g, m16);
   // density head on h7 (this wave's tile), then the bottleneck (no activation) on h7
-  const f4 dens = head<Net, LDEN>(ap, pl, bias_g, w, g);
-  hidden_layer<Net, LBOT, false>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, LVIEW, true>(ap, pl, bias_g, w, g, m16);  // cat[bottleneck, enc_dir] + ReLU
-  const f4 rgb = head<Net, LRGB>(ap, pl, bias_g, w, g);
+  const f4 dens = head<Net, G, LDEN>(ap, pl, bias_g, w, g);
+  hidden_layer<Net, G, LBOT, false>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, LVIEW, true>(ap, pl, bias_g, w, g, m16);  // cat[bottleneck, enc_dir] + ReLU
+  const f4 rgb = head<Net, G, LRGB>(ap, pl, bias_g, w, g);
   if (g == 0 && c.row < N) {
     const f4 o = {act_rgb(rgb[0], act), act_rgb(rgb[1], act), act_rgb(rgb[2], act), act_sigma(dens[0], act)};
     *reinterpret_cast<f4*>(raw + 4 * c.row) = o;
@@ -392,21 +407,22 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_ws_f16x3(
 }
 
 // ---- articulated NeRFMLP (model_autodecoder.py:168-239, latents folded into the biases as in
-// mlp_art.hip), MODE 0 inputs.  The deformation MLP's 128-row layers and the view branch run as
-// 4 pairs x 2 sample-tile halves; the deformation head gives each wave its tile's delta in lane
-// group 0, broadcast to the sample's lanes with ds_bpermute (as mlp_art.hip does), x' =
-// delta + xyz in fp32, pos_enc(x') into the enc planes.
-__global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_art_ws_f16x3(
+// mlp_art.hip), MODE 0 inputs.  The deformation head gives each wave its tile's delta in lane
+// group 0, broadcast to the sample's lanes (as mlp_art.hip does), x' = delta + xyz in fp32,
+// pos_enc(x') into the enc planes.
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 2) void k_mlp_art_ws_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
     const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
     int64_t B, int S, int act, float* __restrict__ raw) {
   using Net = NetArtH;
-  __shared__ f4 smem[kLdsF4];
+  using G = Geo<WAVES>;
+  __shared__ f4 smem[G::kLdsF4];
   const int64_t N = B * S;
-  const WsSetup c = ws_setup(smem, N, S);
+  const WsSetup c = ws_setup<G>(smem, N, S);
   const int w = c.w, g = c.g;
   const Planes& pl = c.pl;
-  APipe<Net, AON_WS_PREFETCH> ap;
+  APipe<Net, G, G::kPrefetch> ap;
   ap.ws = wstream;
   ap.lane = c.lane;
   ap.w = w;
@@ -424,17 +440,17 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_art_ws_f16x3(
     float dv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? px[e < 3 ? e : 0] : 0.f;
-    put_segb(pl, 0, w, dv, ovf);
+    put_segb<G>(pl, 0, w, dv, ovf);
   }
   lds_barrier();
 
   uint32_t m16 = 0;
-  hidden_layer<Net, A_D0, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_D1, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_D2, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_D3, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_D0, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_D1, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_D2, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_D3, true>(ap, pl, bias_g, w, g, m16);
   {
-    const f4 dlt = head<Net, A_DOUT>(ap, pl, bias_g, w, g);
+    const f4 dlt = head<Net, G, A_DOUT>(ap, pl, bias_g, w, g);
     // x' = deformation + xyz (:205), pos_enc(x') (:207-212) of this wave's tile -> enc planes
     // (the xyz segment there was last read by deformations_linear.0, long past its barriers)
     float q3[3];
@@ -445,31 +461,31 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_art_ws_f16x3(
       float ev[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) ev[e] = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10);
-      put_segb(pl, k, w, ev, ovf);
+      put_segb<G>(pl, k, w, ev, ovf);
     }
     lds_barrier();
   }
-  hidden_layer<Net, A_P0, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_P1, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_P2, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_P3, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_P4, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_P5, true>(ap, pl, bias_g, w, g, m16, [&] {
+  hidden_layer<Net, G, A_P0, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_P1, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_P2, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_P3, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_P4, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_P5, true>(ap, pl, bias_g, w, g, m16, [&] {
     const float* vd = in2 + 3 * c.ray;
     float vv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
-    put_segb(pl, 0, w, vv, ovf);
+    put_segb<G>(pl, 0, w, vv, ovf);
   });
-  hidden_layer<Net, A_P6, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_P7, true>(ap, pl, bias_g, w, g, m16);
-  const f4 dens = head<Net, A_DEN>(ap, pl, bias_g, w, g);
-  hidden_layer<Net, A_BOT, false>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_V0, true>(ap, pl, bias_g, w, g, m16);  // cat[bottleneck, enc_dir, app]
-  hidden_layer<Net, A_V1, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_V2, true>(ap, pl, bias_g, w, g, m16);
-  hidden_layer<Net, A_V3, true>(ap, pl, bias_g, w, g, m16);
-  const f4 rgb = head<Net, A_RGB>(ap, pl, bias_g, w, g);
+  hidden_layer<Net, G, A_P6, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_P7, true>(ap, pl, bias_g, w, g, m16);
+  const f4 dens = head<Net, G, A_DEN>(ap, pl, bias_g, w, g);
+  hidden_layer<Net, G, A_BOT, false>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_V0, true>(ap, pl, bias_g, w, g, m16);  // cat[bottleneck, enc_dir, app]
+  hidden_layer<Net, G, A_V1, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_V2, true>(ap, pl, bias_g, w, g, m16);
+  hidden_layer<Net, G, A_V3, true>(ap, pl, bias_g, w, g, m16);
+  const f4 rgb = head<Net, G, A_RGB>(ap, pl, bias_g, w, g);
   if (g == 0 && c.row < N) {
     const f4 o = {act_rgb(rgb[0], act), act_rgb(rgb[1], act), act_rgb(rgb[2], act), act_sigma(dens[0], act)};
     *reinterpret_cast<f4*>(raw + 4 * c.row) = o;
@@ -480,13 +496,26 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void k_mlp_art_ws_f16x3(
 
 }  // namespace ws
 
+// geometry of the weight-streamed kernels: AON_WS_WAVES=8 or 4 in the environment (A/B), else 4
+static int ws_waves() {
+  static int wv = [] {
+    const char* e = getenv("AON_WS_WAVES");
+    return (e && atoi(e) == 8) ? 8 : 4;
+  }();
+  return wv;
+}
+
 int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
                     const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream) {
   const int64_t N = B * S;
   const f4* wsp = static_cast<const f4*>(packed);
   const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + kStreamBytesF32);
-  hipLaunchKernelGGL(ws::k_mlp_ws_f16x3, static_cast<int>((N + ws::kNb - 1) / ws::kNb),
-                     ws::kThreads, 0, stream, wsp, bias, a0, a1, a2, a3, B, S, act, raw);
+  if (ws_waves() == 8)
+    hipLaunchKernelGGL(ws::k_mlp_ws_f16x3<8>, static_cast<int>((N + 127) / 128), 512, 0, stream,
+                       wsp, bias, a0, a1, a2, a3, B, S, act, raw);
+  else
+    hipLaunchKernelGGL(ws::k_mlp_ws_f16x3<4>, static_cast<int>((N + 63) / 64), 256, 0, stream,
+                       wsp, bias, a0, a1, a2, a3, B, S, act, raw);
   return launch_status("aon_mlp_fwd");
 }
 
@@ -495,8 +524,12 @@ int launch_art_ws_f16x3(const void* packed, const float* a0, const float* a1, co
   const int64_t N = B * S;
   const f4* wsp = static_cast<const f4*>(packed);
   const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
-  hipLaunchKernelGGL(ws::k_mlp_art_ws_f16x3, static_cast<int>((N + ws::kNb - 1) / ws::kNb),
-                     ws::kThreads, 0, stream, wsp, bias, a0, a1, a2, a3, B, S, act, raw);
+  if (ws_waves() == 8)
+    hipLaunchKernelGGL(ws::k_mlp_art_ws_f16x3<8>, static_cast<int>((N + 127) / 128), 512, 0, stream,
+                       wsp, bias, a0, a1, a2, a3, B, S, act, raw);
+  else
+    hipLaunchKernelGGL(ws::k_mlp_art_ws_f16x3<4>, static_cast<int>((N + 63) / 64), 256, 0, stream,
+                       wsp, bias, a0, a1, a2, a3, B, S, act, raw);
   return launch_status("aon_mlp_art_fwd");
 }
 
