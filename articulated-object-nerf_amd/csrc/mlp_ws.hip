@@ -24,6 +24,8 @@
 // the same epilogue arithmetic -- every raw value equals k_mlp_fwd_f16x3's bit for bit
 // (tests/test_gpu_parity.py::test_mlp_ws_equals_streamed).  MODE 0 (rays + t) inference only;
 // selected by AON_MLP_WS (env, mlp.hip) for the A/B.
+#include <utility>
+
 #include "mlp_f16x3_core.hpp"
 
 namespace aon {
@@ -494,9 +496,377 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_mlp_art_ws_f16x3(
   range_report(bias_g + Net::kBiasFloats, ovf | __builtin_amdgcn_ballot_w64(bad));
 }
 
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [0, N) -- the step indices that
+// select blocks and layers must be constants, or hipcc evaluates layer_of_step's loop at run
+// time in VGPRs (hundreds of spilled registers in the pipelined kernel)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---- pipelined schedule (AON_WS_PIPE): every hidden layer in two halves of the workgroup's
+// sample tiles (half h = tiles h kTiles / 2 ..), one barrier per half.  The epilogue of the half
+// just finished runs in small units between the MFMAs of the next half (MFMAs issue
+// asynchronously: the wave's VALU and LDS writes fill the matrix pipe's 16-cycle slots), instead
+// of after a barrier with every wave of the SIMD idle in it together.  Safe in place: the units
+// of half h of layer l write tiles of half h, which every wave finished reading before the
+// barrier that ends half h; the next half's MFMAs read the other half's tiles (or, across a
+// layer boundary, half 0 of layer l's output, completed by the previous phase's units).  The
+// weight fragments of a layer stream twice (once per half): 2x the L2 -> CU bytes.
+template <typename Net>
+__host__ __device__ constexpr bool hidden_of(int l) { return Net::layer(l).u > 1; }
+template <typename Net>
+__host__ __device__ constexpr int pstep0_of(int l) {
+  return l == 0 ? 0 : pstep0_of<Net>(l - 1) + (hidden_of<Net>(l - 1) ? 2 * layer_k<Net>(l - 1) : 0);
+}
+template <typename Net>
+__host__ __device__ constexpr int player_of_step(int s) {
+  int l = 0;
+  while (l + 1 < Net::kNumLayers && pstep0_of<Net>(l + 1) <= s) ++l;
+  return l;
+}
+template <typename Net>
+constexpr int kPStepsOf = pstep0_of<Net>(Net::kNumLayers);
+
+// APipe over the pipelined sequence (hidden layers twice, no heads)
+template <typename Net, typename G, int D>
+struct APipeP {
+  static constexpr int TM = G::tu(16);
+  const f4* __restrict__ ws;
+  int lane, w;
+  f4 qh[D][TM], ql[D][TM];
+  template <int S>
+  __device__ __forceinline__ void fetch(f4 (&h)[TM], f4 (&l)[TM]) {
+    if constexpr (S < kPStepsOf<Net>) {
+      constexpr int L = player_of_step<Net>(S);
+      constexpr LayerDesc d = Net::layer(L);
+      constexpr int K = d.ka + d.kb;
+      constexpr int k = (S - pstep0_of<Net>(L)) % K;
+      constexpr int TU = G::tu(d.u);
+      const int r0 = G::rt0(d.u, w);
+#pragma unroll
+      for (int i = 0; i < TU; ++i) {
+        const int u = r0 + i;
+        const int b = d.blk0 + 2 * (((u >> 1) * K + k) * 2 + (u & 1));
+        h[i] = ws[(size_t)b * 64 + lane];
+        l[i] = ws[(size_t)(b + 1) * 64 + lane];
+      }
+    }
+  }
+  __device__ __forceinline__ void start() {
+    static_for<D>([&](auto I) { fetch<decltype(I)::value>(qh[decltype(I)::value], ql[decltype(I)::value]); });
+  }
+  template <int S>
+  __device__ __forceinline__ void take(h8 (&wh)[TM], h8 (&wl)[TM]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      wh[i] = as_h8(qh[0][i]);
+      wl[i] = as_h8(ql[0][i]);
+    }
+#pragma unroll
+    for (int q = 0; q + 1 < D; ++q)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        qh[q][i] = qh[q + 1][i];
+        ql[q][i] = ql[q + 1][i];
+      }
+    fetch<S + D>(qh[D - 1], ql[D - 1]);
+  }
+};
+
+// the wave's part of half H of layer L: TU row tiles from rt0 over NTh sample tiles from T0
+template <typename Net, typename G, int L>
+struct LG {
+  static constexpr LayerDesc d = Net::layer(L);
+  static constexpr int K = d.ka + d.kb;
+  static constexpr int TU = G::tu(d.u), NTh = G::nt(d.u) / 2;
+  __device__ __forceinline__ static int rt0(int w) { return G::rt0(d.u, w); }
+  __device__ __forceinline__ static int T0(int w, int H) { return H * (G::kTiles / 2) + G::t0(d.u, w) / 2; }
+};
+
+// a finished half waiting for its epilogue: accumulators, biases, where the output goes
+template <typename Net, typename G, int L, bool RELU>
+struct Job {
+  using LGt = LG<Net, G, L>;
+  static constexpr int TU = LGt::TU, NTh = LGt::NTh;
+  static constexpr int kUnits = TU / 2 * NTh;  // (pair, sample tile) units
+  f4 acc[TU][NTh];
+  f4 bias[TU];
+  int rt0, T0;
+  __device__ __forceinline__ void load_bias(const float* bias_g, int g) {
+#pragma unroll
+    for (int i = 0; i < TU; ++i) bias[i] = ldg_f4(bias_g + LGt::d.bias0 + 16 * (rt0 + i) + 4 * g);
+  }
+  // epilogue unit I: pair I / NTh of the wave's rows, sample tile I % NTh (pair_epilogue's body)
+  template <int I>
+  __device__ __forceinline__ void unit(const Planes& pl, uint32_t& m16) const {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    constexpr int p = I / NTh, t = I % NTh;
+    u4 hw, lw;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int uu = q >> 1, r0 = (q & 1) * 2;
+      float vv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float v = fmaf(acc[2 * p + uu][t][r0 + e], 1.0f / kWS, bias[2 * p + uu][r0 + e]);
+        if (!RELU) asm("" : "+v"(v));  // (pair_epilogue: no fma + fp16-convert fold)
+        if (RELU) v = fmaxf(v, 0.0f);
+        vv[e] = v;
+      }
+      const h2 hp = {static_cast<_Float16>(vv[0]), static_cast<_Float16>(vv[1])};
+      const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
+      m16 = pk_max_i16(m16, RELU ? hu : (hu & 0x7FFF7FFFu));
+      asm("" : "+v"(m16));
+      float d0, d1;
+      asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(vv[0]));
+      asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(vv[1]));
+      const h2 lp = {static_cast<_Float16>(d0), static_cast<_Float16>(d1)};
+      hw[q] = hu;
+      lw[q] = __builtin_bit_cast(uint32_t, lp);
+    }
+    const int pr = rt0 / 2 + p;
+    pl.act_hi[pr * 4 * G::kNb + 16 * (T0 + t)] = __builtin_bit_cast(f4, hw);
+    pl.act_lo[pr * 4 * G::kNb + 16 * (T0 + t)] = __builtin_bit_cast(f4, lw);
+  }
+  __device__ __forceinline__ void all(const Planes& pl, uint32_t& m16) const {
+    static_for<kUnits>([&](auto I) { unit<decltype(I)::value>(pl, m16); });
+  }
+};
+struct NoJob {
+  static constexpr int kUnits = 0;
+  template <int I>
+  __device__ __forceinline__ void unit(const Planes&, uint32_t&) const {}
+};
+
+// MFMAs of half H of layer L (as layer_mfma, over the pipelined step sequence) with the
+// pending job's epilogue units after the MFMAs of every other (k, t) step; then the job's
+// remaining units
+template <typename Net, typename G, int L, int H, typename AP, typename J>
+__device__ __forceinline__ void half_mfma(AP& ap, const Planes& pl, int w,
+                                          f4 (&acc)[LG<Net, G, L>::TU][LG<Net, G, L>::NTh],
+                                          const J& job, uint32_t& m16) {
+  using LGt = LG<Net, G, L>;
+  constexpr LayerDesc d = LGt::d;
+  constexpr int K = LGt::K, NT = LGt::NTh, TU = LGt::TU;
+  constexpr int NS = K * NT;
+  constexpr int P = AON_WS_BPF < NS ? AON_WS_BPF : NS;
+  constexpr int S0 = pstep0_of<Net>(L) + H * K;
+  constexpr int kNb = G::kNb;
+  const int T0 = LGt::T0(w, H);
+#pragma unroll
+  for (int i = 0; i < TU; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[i][t] = f4{0.f, 0.f, 0.f, 0.f};
+  auto bsrc = [&](int s, f4& xh, f4& xl) {
+    const int k = s / NT, t = s % NT;
+    const lds_f4w* bh = k < d.ka ? pl.act_hi + k * 4 * kNb : pl.enc_hi + (k - d.ka) * 4 * kNb;
+    const lds_f4w* bl = k < d.ka ? pl.act_lo + k * 4 * kNb : pl.enc_lo + (k - d.ka) * 4 * kNb;
+    xh = bh[16 * (T0 + t)];
+    xl = bl[16 * (T0 + t)];
+  };
+  f4 qh[P], ql[P];
+#pragma unroll
+  for (int s = 0; s < P; ++s) bsrc(s, qh[s], ql[s]);
+  h8 wh[AP::TM], wl[AP::TM];
+  constexpr int kEvery = J::kUnits > 0 && NS / J::kUnits >= 2 ? NS / J::kUnits : 1;
+  static_for<NS>([&](auto I) {
+    constexpr int s = decltype(I)::value;
+    constexpr int t = s % NT;
+    if constexpr (t == 0) ap.template take<S0 + s / NT>(wh, wl);
+    const h8 xh = as_h8(qh[0]), xl = as_h8(ql[0]);
+#pragma unroll
+    for (int p = 0; p + 1 < P; ++p) {
+      qh[p] = qh[p + 1];
+      ql[p] = ql[p + 1];
+    }
+    if constexpr (s + P < NS) bsrc(s + P, qh[P - 1], ql[P - 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TU; ++i) {
+      acc[i][t] = mfma16(wh[i], xh, acc[i][t]);
+      acc[i][t] = mfma16(wh[i], xl, acc[i][t]);
+      acc[i][t] = mfma16(wl[i], xh, acc[i][t]);
+    }
+#ifndef AON_WS_DBG_NOUNITS
+    if constexpr (s % kEvery == kEvery - 1 && s / kEvery < J::kUnits)
+      job.template unit<s / kEvery>(pl, m16);
+#endif
+  });
+  static_for<(J::kUnits > NS / kEvery ? J::kUnits - NS / kEvery : 0)>([&](auto I) {
+    job.template unit<NS / kEvery + decltype(I)::value>(pl, m16);
+  });
+}
+
+// a finished half -> its job (biases loaded now: read by the units during the next half)
+template <typename Net, typename G, int L, bool RELU, int H>
+__device__ __forceinline__ Job<Net, G, L, RELU> make_job(
+    const f4 (&acc)[LG<Net, G, L>::TU][LG<Net, G, L>::NTh], const float* bias_g, int w, int g) {
+  Job<Net, G, L, RELU> j;
+#pragma unroll
+  for (int i = 0; i < LG<Net, G, L>::TU; ++i)
+#pragma unroll
+    for (int t = 0; t < LG<Net, G, L>::NTh; ++t) j.acc[i][t] = acc[i][t];
+  j.rt0 = LG<Net, G, L>::rt0(w);
+  j.T0 = LG<Net, G, L>::T0(w, H);
+  j.load_bias(bias_g, g);
+  return j;
+}
+
+// a 1-tile head on the wave's own sample tile, its weight fragments loaded straight from global
+// (two k-steps at a time; not in the prefetch sequence)
+template <typename Net, typename G, int L>
+__device__ __forceinline__ f4 head_direct(const Planes& pl, const f4* __restrict__ wstream,
+                                          const float* bias_g, int w, int g, int lane) {
+#ifdef AON_WS_DBG_NOHEADS
+  return f4{0.f, 0.f, 0.f, 0.f};
+#endif
+  constexpr LayerDesc d = Net::layer(L);
+  static_assert(d.u == 1 && d.kb == 0, "head");
+  const f4 bias = ldg_f4(bias_g + d.bias0 + 4 * g);
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k0 = 0; k0 < d.ka; k0 += 2) {
+    f4 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int b = d.blk0 + 2 * (k0 + k);
+      ah[k] = wstream[(size_t)b * 64 + lane];
+      al[k] = wstream[(size_t)(b + 1) * 64 + lane];
+      bh[k] = pl.act_hi[(k0 + k) * 4 * G::kNb + 16 * w];
+      bl[k] = pl.act_lo[(k0 + k) * 4 * G::kNb + 16 * w];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      acc = mfma16(as_h8(ah[k]), as_h8(bh[k]), acc);
+      acc = mfma16(as_h8(ah[k]), as_h8(bl[k]), acc);
+      acc = mfma16(as_h8(al[k]), as_h8(bh[k]), acc);
+    }
+  }
+  f4 res;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) res[r] = fmaf(acc[r], 1.0f / (kWS * kActS), bias[r]);
+  return res;
+}
+
+// one hidden layer, pipelined: half 0 (finishing `prev`), half 1 (finishing half 0); returns
+// the job of half 1, to be finished by the next layer's half 0
+#define AON_WS_HALVES(L_, RELU_, PREV, OUT)                                                  \
+  f4 OUT##_a0[LG<Net, G, L_>::TU][LG<Net, G, L_>::NTh];                                     \
+  half_mfma<Net, G, L_, 0>(ap, pl, w, OUT##_a0, PREV, m16);                                  \
+  lds_barrier();                                                                             \
+  const auto OUT##_j0 = make_job<Net, G, L_, RELU_, 0>(OUT##_a0, bias_g, w, g);              \
+  f4 OUT##_a1[LG<Net, G, L_>::TU][LG<Net, G, L_>::NTh];                                     \
+  half_mfma<Net, G, L_, 1>(ap, pl, w, OUT##_a1, OUT##_j0, m16);                              \
+  lds_barrier();                                                                             \
+  const auto OUT = make_job<Net, G, L_, RELU_, 1>(OUT##_a1, bias_g, w, g);
+
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 2) void k_mlp_ws_pipe_f16x3(
+    const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
+    const float* __restrict__ in1, const float* __restrict__ in2, const float* __restrict__ in3,
+    int64_t B, int S, int act, float* __restrict__ raw) {
+  using Net = NetVanillaH;
+  using G = Geo<WAVES>;
+  __shared__ f4 smem[G::kLdsF4];
+  const int64_t N = B * S;
+  const WsSetup c = ws_setup<G>(smem, N, S);
+  const int w = c.w, g = c.g;
+  const Planes& pl = c.pl;
+  APipeP<Net, G, G::kPrefetch> ap;
+  ap.ws = wstream;
+  ap.lane = c.lane;
+  ap.w = w;
+  ap.start();
+  const bool first_half = w < G::kTiles / 2;  // the wave's own sample tile (heads) is in half 0
+
+  uint64_t ovf = 0;
+  {
+    const float* ro = in0 + 3 * c.ray;
+    const float* rd = in1 + 3 * c.ray;
+    const float tt = in3[c.rr];
+    const float x0 = __fadd_rn(ro[0], __fmul_rn(tt, rd[0]));
+    const float x1 = __fadd_rn(ro[1], __fmul_rn(tt, rd[1]));
+    const float x2 = __fadd_rn(ro[2], __fmul_rn(tt, rd[2]));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float ev[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ev[e] = pos_enc_feature(x0, x1, x2, 32 * k + 8 * g + e, 0, 10);
+      put_segb<G>(pl, k, w, ev, ovf);
+    }
+  }
+  lds_barrier();
+
+  uint32_t m16 = 0;
+  const NoJob none;
+  AON_WS_HALVES(L0, true, none, j0)
+  AON_WS_HALVES(L1, true, j0, j1)
+  AON_WS_HALVES(L2, true, j1, j2)
+  AON_WS_HALVES(L3, true, j2, j3)
+  AON_WS_HALVES(L4, true, j3, j4)
+  AON_WS_HALVES(L5, true, j4, j5)  // the skip layer reads the enc planes (both halves)
+  // L6 half 0: every wave is past L5's reads of the enc planes -> pos_enc(viewdirs) of the
+  // wave's tile into enc k-step 0 for the view layer
+  {
+    const float* vd = in2 + 3 * c.ray;
+    float vv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
+    put_segb<G>(pl, 0, w, vv, ovf);
+  }
+  AON_WS_HALVES(L6, true, j5, j6)
+  AON_WS_HALVES(L7, true, j6, j7)
+  // the bottleneck's halves; the density head reads h7 of the wave's tile while it is complete
+  // and not yet overwritten: tiles of half 0 during the bottleneck's half 0 (j7 writes half 1),
+  // tiles of half 1 during its half 1 (its half-0 job writes half 0)
+  f4 dens = {0.f, 0.f, 0.f, 0.f};
+  if (first_half) dens = head_direct<Net, G, LDEN>(pl, wstream, bias_g, w, g, c.lane);
+  f4 jb_a0[LG<Net, G, LBOT>::TU][LG<Net, G, LBOT>::NTh];
+  half_mfma<Net, G, LBOT, 0>(ap, pl, w, jb_a0, j7, m16);
+  lds_barrier();
+  const auto jb_j0 = make_job<Net, G, LBOT, false, 0>(jb_a0, bias_g, w, g);
+  if (!first_half) dens = head_direct<Net, G, LDEN>(pl, wstream, bias_g, w, g, c.lane);
+  f4 jb_a1[LG<Net, G, LBOT>::TU][LG<Net, G, LBOT>::NTh];
+  half_mfma<Net, G, LBOT, 1>(ap, pl, w, jb_a1, jb_j0, m16);
+  lds_barrier();
+  const auto jb = make_job<Net, G, LBOT, false, 1>(jb_a1, bias_g, w, g);
+  AON_WS_HALVES(LVIEW, true, jb, jv)  // cat[bottleneck, enc_dir] + ReLU
+  // the view layer's half-1 epilogue; the rgb head of half-0 tiles meanwhile (hv complete there)
+  f4 rgb;
+  if (first_half) rgb = head_direct<Net, G, LRGB>(pl, wstream, bias_g, w, g, c.lane);
+  jv.all(pl, m16);
+  lds_barrier();
+  if (!first_half) rgb = head_direct<Net, G, LRGB>(pl, wstream, bias_g, w, g, c.lane);
+  if (g == 0 && c.row < N) {
+    const f4 o = {act_rgb(rgb[0], act), act_rgb(rgb[1], act), act_rgb(rgb[2], act), act_sigma(dens[0], act)};
+    *reinterpret_cast<f4*>(raw + 4 * c.row) = o;
+  }
+  const bool bad = (m16 & 0x7FFFu) >= 0x7C00u || ((m16 >> 16) & 0x7FFFu) >= 0x7C00u;
+  range_report(bias_g + Net::kBiasFloats, ovf | __builtin_amdgcn_ballot_w64(bad));
+}
+#undef AON_WS_HALVES
+
 }  // namespace ws
 
+// the pipelined schedule: AON_WS_PIPE=0 / 1 in the environment (A/B), else on
+static bool ws_pipe() {
+  static bool on = [] {
+    const char* e = getenv("AON_WS_PIPE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // geometry of the weight-streamed kernels: AON_WS_WAVES=8 or 4 in the environment (A/B), else 4
+// (the pipelined schedule is built for 8 waves only: at 4 its two accumulator sets and the
+// 4-tile A fragments spill)
 static int ws_waves() {
   static int wv = [] {
     const char* e = getenv("AON_WS_WAVES");
@@ -510,7 +880,10 @@ int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const 
   const int64_t N = B * S;
   const f4* wsp = static_cast<const f4*>(packed);
   const float* bias = reinterpret_cast<const float*>(static_cast<const char*>(packed) + kStreamBytesF32);
-  if (ws_waves() == 8)
+  if (ws_pipe() && ws_waves() == 8)
+    hipLaunchKernelGGL(ws::k_mlp_ws_pipe_f16x3<8>, static_cast<int>((N + 127) / 128), 512, 0,
+                       stream, wsp, bias, a0, a1, a2, a3, B, S, act, raw);
+  else if (ws_waves() == 8)
     hipLaunchKernelGGL(ws::k_mlp_ws_f16x3<8>, static_cast<int>((N + 127) / 128), 512, 0, stream,
                        wsp, bias, a0, a1, a2, a3, B, S, act, raw);
   else
