@@ -107,6 +107,8 @@ _SIGNATURES = {
     "aon_composite_bwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp, vp,
                                   vp, vp, vp, c_i64, vp]),
     "aon_mse": (c_int, [vp, vp, c_i64, c_float, vp, vp, vp]),
+    "aon_loss_pair": (c_int, [vp, vp, vp, c_i64, vp, vp, vp, vp, vp]),
+    "aon_loss_pair_bwd": (c_int, [vp, vp, c_i64, vp, vp, vp, vp, vp, vp]),
     "aon_colsum_workspace_bytes": (c_size, [c_i64, c_i64]),
     "aon_colsum": (c_int, [vp, c_i64, c_i64, c_i64, c_int, vp, vp, c_size, vp]),
     "aon_adam_step": (c_int, [ctypes.POINTER(AonAdamTensor), c_int, ctypes.c_double,

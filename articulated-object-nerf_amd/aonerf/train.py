@@ -375,6 +375,8 @@ class RenderLevel(torch.autograd.Function):
         ctx.h_tiled = FUSED_FORWARD  # the fused forward keeps its tensors tiled
         ctx.meta = (B, S, bool(white_bkgd))
         ctx.mark_non_differentiable(weights)
+        # unused outputs (acc, depth, weights in training_step) get no zero-filled gradients
+        ctx.set_materialize_grads(False)
         return comp, acc, depth, weights
 
     @staticmethod
@@ -387,7 +389,7 @@ class RenderLevel(torch.autograd.Function):
         dev = raw.device
         R = B * S
         draw = torch.empty((R, 4), device=dev)
-        g_rgb = L.contig(g_rgb)
+        g_rgb = L.contig(g_rgb) if g_rgb is not None else torch.zeros((B, 3), device=dev)
         L.call("aon_composite_bwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals),
                L.ptr(rays_d), B, S, int(white), L.ACT_VANILLA, L.ptr(g_rgb),
                L.ptr(L.contig(g_acc)) if g_acc is not None else None,
@@ -437,15 +439,52 @@ def mse2psnr(x):
     return -10.0 * torch.log(x) / np.log(10.0)
 
 
+class LossPair(torch.autograd.Function):
+    """The training step's loss terms (model.py:265-270; model_autodecoder.py:455-470) in one
+    aon_loss_pair launch: loss = (img2mse(fine) + img2mse(coarse)) [+ reg], both mses and
+    mse2psnr of each -- the same values as img2mse / `+` / mse2psnr, bit for bit, where those
+    took 9 launches.  Backward: one aon_loss_pair_bwd launch for both levels' rgb gradients."""
+
+    @staticmethod
+    def forward(ctx, pred0, pred1, target, reg):
+        L.require_gpu(pred0, pred1, target)
+        pred0, pred1, target = L.contig(pred0), L.contig(pred1), L.contig(target)
+        if pred0.shape != target.shape or pred1.shape != target.shape:
+            raise ValueError("LossPair: predictions and target must have one shape")
+        out = torch.empty((5,), device=pred0.device)
+        g0, g1 = torch.empty_like(pred0), torch.empty_like(pred1)
+        L.call("aon_loss_pair", L.ptr(pred0), L.ptr(pred1), L.ptr(target), pred0.numel(),
+               L.ptr(L.contig(reg)) if reg is not None else None, L.ptr(out), L.ptr(g0), L.ptr(g1),
+               L.stream(pred0.device))
+        ctx.save_for_backward(g0, g1)
+        ctx.has_reg = reg is not None
+        ctx.set_materialize_grads(False)
+        loss, loss0, loss1, psnr0, psnr1 = out.unbind(0)
+        ctx.mark_non_differentiable(psnr0, psnr1)
+        return loss, loss0, loss1, psnr0, psnr1
+
+    @staticmethod
+    def backward(ctx, g, g0, g1, _p0, _p1):
+        grad0, grad1 = ctx.saved_tensors
+        if g is None and g0 is None and g1 is None:
+            return None, None, None, None
+        d0, d1 = torch.empty_like(grad0), torch.empty_like(grad1)
+        L.call("aon_loss_pair_bwd", L.ptr(grad0), L.ptr(grad1), grad0.numel(),
+               *(L.ptr(L.contig(x)) if x is not None else None for x in (g, g0, g1)),
+               L.ptr(d0), L.ptr(d1), L.stream(grad0.device))
+        return d0, d1, None, (g if ctx.has_reg else None)
+
+
+def loss_pair(pred0, pred1, target, reg=None):
+    """(loss, loss0, loss1, psnr0, psnr1) of a training step (LossPair)."""
+    return LossPair.apply(pred0, pred1, target, reg)
+
+
 def training_step(model, batch, randomized, white_bkgd, near, far, *, u_coarse=None, u_fine=None):
     """LitNeRF.training_step (model.py:256-282): loss = mse(fine) + mse(coarse) and the psnrs."""
     ret = model(batch, randomized, white_bkgd, near, far, u_coarse=u_coarse, u_fine=u_fine)
-    target = batch["target"]
-    loss0 = img2mse(ret[0][0], target)
-    loss1 = img2mse(ret[1][0], target)
-    loss = loss1 + loss0
-    return loss, dict(loss0=loss0, loss1=loss1, psnr0=mse2psnr(loss0.detach()),
-                      psnr1=mse2psnr(loss1.detach()))
+    loss, loss0, loss1, psnr0, psnr1 = loss_pair(ret[0][0], ret[1][0], batch["target"])
+    return loss, dict(loss0=loss0, loss1=loss1, psnr0=psnr0, psnr1=psnr1)
 
 
 # ---------------------------------------------------------------------------- optimizer

@@ -34,7 +34,7 @@ from . import _lib as L
 from . import tiles
 from . import train as _train
 from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, batched, gemm
-from .train import Adam, _amax_word, img2mse, learning_rate, mse2psnr, relu_masks  # noqa: F401 (shared)
+from .train import Adam, _amax_word, img2mse, learning_rate, loss_pair, mse2psnr, relu_masks  # noqa: F401 (shared)
 
 # parameter layout of one articulated NeRFMLP in ArtRenderLevel: 20 layers x (weight, bias)
 DEF0, DL, PTS0, DENS, BOT, VIEW0, RGB = 0, 4, 5, 13, 14, 15, 19
@@ -492,6 +492,8 @@ class ArtRenderLevel(torch.autograd.Function):
         ctx.h_tiled = masks is not None  # the fused forward keeps its tensors tiled
         ctx.meta = (geo, B, S, bool(white_bkgd), tuple(x.shape for x in (shape, app, art)))
         ctx.mark_non_differentiable(weights)
+        # unused outputs (acc, depth, weights in training_step) get no zero-filled gradients
+        ctx.set_materialize_grads(False)
         return comp, acc, depth, weights
 
     @staticmethod
@@ -504,6 +506,8 @@ class ArtRenderLevel(torch.autograd.Function):
         dev = raw.device
         R = B * S
         draw = torch.empty((R, 4), device=dev)
+        if g_rgb is None:
+            g_rgb = torch.zeros((B, 3), device=dev)
         L.call("aon_composite_bwd", L.ptr(raw), 4, L.ptr(raw[:, 3:]), 4, L.ptr(t_vals),
                L.ptr(rays_d), B, S, int(white), L.ACT_ARTIC, L.ptr(L.contig(g_rgb)),
                L.ptr(L.contig(g_acc)) if g_acc is not None else None,
@@ -572,13 +576,10 @@ def training_step(model, code_library, batch, randomized, white_bkgd, near, far,
     latents = code_library(batch)
     ret = model(batch, randomized, white_bkgd, near, far, latents, u_coarse=u_coarse,
                 u_fine=u_fine)
-    target = batch["target"]
-    loss0 = img2mse(ret[0][0], target)
-    loss1 = img2mse(ret[1][0], target)
     reg = LatentReg.apply(latents["density"], latents["color"], latents["articulation"])
-    loss = loss1 + loss0 + reg
-    return loss, dict(loss0=loss0, loss1=loss1, reg=reg, psnr0=mse2psnr(loss0.detach()),
-                      psnr1=mse2psnr(loss1.detach()))
+    # loss1 + loss0 + reg and the psnrs in one launch (train.LossPair)
+    loss, loss0, loss1, psnr0, psnr1 = loss_pair(ret[0][0], ret[1][0], batch["target"], reg)
+    return loss, dict(loss0=loss0, loss1=loss1, reg=reg, psnr0=psnr0, psnr1=psnr1)
 
 
 def configure_optimizers(model, code_library, lr_init=5.0e-4):

@@ -1553,9 +1553,15 @@ __global__ __launch_bounds__(THREADS, 1) void k_gemm_f16x3_dma(Params p) {
 // (k_gemm_reduce sums the chunks in z order: deterministic).
 constexpr int kSkinnyRows = 16;
 #ifndef AON_GEMM_SKINNY_SK
-#define AON_GEMM_SKINNY_SK 4  // rows in flight per thread (skinny and segment-sum kernels); 1: A/B
+#define AON_GEMM_SKINNY_SK 4  // rows in flight per thread of the skinny kernel; 1: A/B
 #endif
-template <int M, typename TA, bool BT>
+#ifndef AON_GEMM_SEGSUM_SK
+#define AON_GEMM_SEGSUM_SK 16  // ... of the segment-sum kernel (one workgroup of 4 waves per CU)
+#endif
+#ifndef AON_GEMM_SKINNY_SK2
+#define AON_GEMM_SKINNY_SK2 8  // ... of the skinny kernel on B of <= 128 columns (A/B knob)
+#endif
+template <int M, typename TA, bool BT, int SK = AON_GEMM_SKINNY_SK>
 __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
   const int tid = threadIdx.x, r = tid & 15, cg = tid >> 4;
   const int64_t n0 = 8 * (int64_t)cg;
@@ -1589,8 +1595,8 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
   };
   // SK rows per thread in flight: their loads are issued before the first is consumed (one
   // dependent load per row left this kernel latency-bound: rgb's 0.27 GB at ~2.2 TB/s); the
-  // rows are still summed in k order (bit-identical)
-  constexpr int SK = AON_GEMM_SKINNY_SK;
+  // rows are still summed in k order (bit-identical); SK is doubled for B of <= 128 columns
+  // (half the waves per workgroup: the same bytes in flight per CU)
   int64_t k = kbeg + r;
   for (; k + (SK - 1) * kSkinnyRows < kend; k += SK * kSkinnyRows) {
     uint4 bv[SK];
@@ -1682,10 +1688,11 @@ __global__ __launch_bounds__(256) void k_gemm_segsum_bf16(Params p) {
   };
   int64_t k = kb;
   if (std::is_same<TA, __bf16>::value) {
-    // AON_GEMM_SKINNY_SK rows' 16-B loads in flight per thread before the first is summed (one
-    // dependent load per row left one workgroup of 4 waves per CU latency-bound); the rows are
-    // still summed in k order (bit-identical)
-    constexpr int SK = AON_GEMM_SKINNY_SK;
+    // AON_GEMM_SEGSUM_SK rows' 16-B loads in flight per thread before the first is summed (one
+    // dependent load per row left one workgroup of 4 waves per CU latency-bound; 4 rows still
+    // held the fine level's 0.2 GB at ~3.3 TB/s); the rows are still summed in k order
+    // (bit-identical)
+    constexpr int SK = AON_GEMM_SEGSUM_SK;
     for (; k + SK - 1 < ke; k += SK) {
       uint4 w[SK];
 #pragma unroll
@@ -1776,11 +1783,17 @@ __global__ __launch_bounds__(256) void k_gemm_small_f32_wave(Params p, int a_kc,
 template <typename TA, bool BT>
 static void launch_skinny(const Params& p, dim3 grid, hipStream_t st) {
   const dim3 block((unsigned)(2 * p.N));  // 16 row phases x N / 8 column groups
+  constexpr int SK = AON_GEMM_SKINNY_SK, SK2 = AON_GEMM_SKINNY_SK2;
+  const bool narrow = p.N <= 128;
   switch (p.M) {
-    case 1: hipLaunchKernelGGL((k_gemm_skinny_bf16<1, TA, BT>), grid, block, 0, st, p); break;
-    case 2: hipLaunchKernelGGL((k_gemm_skinny_bf16<2, TA, BT>), grid, block, 0, st, p); break;
-    case 3: hipLaunchKernelGGL((k_gemm_skinny_bf16<3, TA, BT>), grid, block, 0, st, p); break;
-    default: hipLaunchKernelGGL((k_gemm_skinny_bf16<4, TA, BT>), grid, block, 0, st, p); break;
+#define AON_SKINNY_L(M_)                                                                        \
+  if (narrow) hipLaunchKernelGGL((k_gemm_skinny_bf16<M_, TA, BT, SK2>), grid, block, 0, st, p); \
+  else hipLaunchKernelGGL((k_gemm_skinny_bf16<M_, TA, BT, SK>), grid, block, 0, st, p)
+    case 1: AON_SKINNY_L(1); break;
+    case 2: AON_SKINNY_L(2); break;
+    case 3: AON_SKINNY_L(3); break;
+    default: AON_SKINNY_L(4); break;
+#undef AON_SKINNY_L
   }
 }
 

@@ -233,6 +233,10 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
   const LayerDesc& last = a.layers[a.n_layers - 1];
   const int used_blocks = last.blk0 + (last.ka + last.kb) * last.u * 2;
   const StreamMap map{a.bf16, a.mx_lo, a.mx_hi};
+  // an all-bf16 stream never reports (no weight is range-tested): the status words are cleared
+  // here instead of by a memset launch ahead of the pack (pack_h)
+  if (a.bf16 == 1 && blockIdx.x == 0 && threadIdx.x < kStatusBytes / 4)
+    reinterpret_cast<uint32_t*>(bias_out + a.bias_floats)[threadIdx.x] = 0u;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e < nhalf) {
@@ -316,10 +320,13 @@ int pack_h(PackArgsH a, void* packed, hipStream_t stream) {
   const int64_t total = (int64_t)a.stream_blocks * 512 + a.bias_floats;
   // the range-status word behind the bias table: cleared (stream-ordered) before the pack, which
   // sets it for an unrepresentable weight; the kernels reading the stream set it on overflow
-  const hipError_t e = hipMemsetAsync(
-      static_cast<char*>(packed) + (size_t)a.stream_blocks * 1024 + (size_t)a.bias_floats * 4, 0,
-      kStatusBytes, stream);
-  if (e != hipSuccess) return static_cast<int>(e);
+  // (an all-bf16 stream: k_pack_h clears it itself, one launch fewer)
+  if (a.bf16 != 1) {
+    const hipError_t e = hipMemsetAsync(
+        static_cast<char*>(packed) + (size_t)a.stream_blocks * 1024 + (size_t)a.bias_floats * 4, 0,
+        kStatusBytes, stream);
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
   hipLaunchKernelGGL(k_pack_h, grid_for(total, 256, 4096), 256, 0, stream, a,
                      static_cast<float*>(packed));
   return launch_status("aon_mlp_pack");

@@ -176,6 +176,85 @@ __global__ __launch_bounds__(256) void k_mse(const float* __restrict__ pred,
   if (threadIdx.x == 0 && loss) *loss = (float)(part[0] / (double)n);
 }
 
+// The training step's loss terms in one launch (model.py:265-270 / model_autodecoder.py:455-470):
+// the two levels' img2mse against one target -- each with k_mse's arithmetic (the same per-thread
+// element order, fp64 accumulation, reduction tree and rounding), the loads of both levels in
+// flight together -- then loss = (loss1 + loss0) (+ extra), and mse2psnr of each as torch forms it
+// on the device (helper.py:21-22: log, * -10, then * fp32(1 / ln 10): torch's division by a
+// Python scalar multiplies by the scalar's fp32 reciprocal).  It replaces 2 k_mse launches, the
+// add and 3 elementwise kernels per psnr.
+__global__ __launch_bounds__(256) void k_loss_pair(const float* __restrict__ pred0,
+                                                   const float* __restrict__ pred1,
+                                                   const float* __restrict__ target, int64_t n,
+                                                   const float* __restrict__ extra,
+                                                   float* __restrict__ out, float* __restrict__ grad0,
+                                                   float* __restrict__ grad1) {
+  __shared__ double part[2][256];
+  double s0 = 0.0, s1 = 0.0;
+  const float gscale = __fdiv_rn(2.0f, (float)n);
+  constexpr int kU = 8;
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += 256 * kU) {
+    float p0[kU], p1[kU], q[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = i0 + 256 * u;
+      p0[u] = i < n ? pred0[i] : 0.f;
+      p1[u] = i < n ? pred1[i] : 0.f;
+      q[u] = i < n ? target[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = i0 + 256 * u;
+      if (i < n) {
+        const float d0 = __fsub_rn(p0[u], q[u]), d1 = __fsub_rn(p1[u], q[u]);
+        s0 += (double)d0 * (double)d0;
+        s1 += (double)d1 * (double)d1;
+        if (grad0) grad0[i] = __fmul_rn(gscale, d0);
+        if (grad1) grad1[i] = __fmul_rn(gscale, d1);
+      }
+    }
+  }
+  part[0][threadIdx.x] = s0;
+  part[1][threadIdx.x] = s1;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      part[0][threadIdx.x] += part[0][threadIdx.x + o];
+      part[1][threadIdx.x] += part[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float l0 = (float)(part[0][0] / (double)n), l1 = (float)(part[1][0] / (double)n);
+    float l = __fadd_rn(l1, l0);
+    if (extra) l = __fadd_rn(l, *extra);
+    const float inv_ln10 = __fdiv_rn(1.0f, (float)2.302585092994046);
+    out[0] = l;
+    out[1] = l0;
+    out[2] = l1;
+    out[3] = __fmul_rn(__fmul_rn(-10.0f, logf(l0)), inv_ln10);
+    out[4] = __fmul_rn(__fmul_rn(-10.0f, logf(l1)), inv_ln10);
+  }
+}
+
+// its backward: d_i = grad_i * (g_loss + g_loss_i), absent (NULL) scalars taken as 0 -- what
+// autograd forms for img2mse's `grad * g` after summing the two uses of loss_i
+__global__ __launch_bounds__(256) void k_loss_pair_bwd(const float* __restrict__ grad0,
+                                                       const float* __restrict__ grad1, int64_t n,
+                                                       const float* __restrict__ g_loss,
+                                                       const float* __restrict__ g_loss0,
+                                                       const float* __restrict__ g_loss1,
+                                                       float* __restrict__ d0, float* __restrict__ d1) {
+  const float g = g_loss ? *g_loss : 0.f;
+  const float a = g_loss0 ? (g_loss ? __fadd_rn(g, *g_loss0) : *g_loss0) : g;
+  const float b = g_loss1 ? (g_loss ? __fadd_rn(g, *g_loss1) : *g_loss1) : g;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    d0[i] = __fmul_rn(grad0[i], a);
+    d1[i] = __fmul_rn(grad1[i], b);
+  }
+}
+
 // column sums out[n] (+)= sum_m X[m*ldx + n]: partials over row chunks, then a fixed-order sum
 constexpr int kColRows = 1024;
 
@@ -280,6 +359,27 @@ extern "C" int aon_mse(const float* pred, const float* target, int64_t n, float 
   AON_REQUIRE(pred && target && (loss || grad), "null pointer");
   AON_REQUIRE(n >= 1, "empty input");
   hipLaunchKernelGGL(k_mse, 1, 256, 0, (hipStream_t)stream, pred, target, n, grad_scale, loss, grad);
+  return launch_status(__func__);
+}
+
+extern "C" int aon_loss_pair(const float* pred0, const float* pred1, const float* target,
+                             int64_t n, const float* extra, float* out, float* grad0, float* grad1,
+                             aon_stream_t stream) {
+  AON_REQUIRE(pred0 && pred1 && target && out, "null pointer");
+  AON_REQUIRE(n >= 1, "empty input");
+  hipLaunchKernelGGL(k_loss_pair, 1, 256, 0, (hipStream_t)stream, pred0, pred1, target, n, extra,
+                     out, grad0, grad1);
+  return launch_status(__func__);
+}
+
+extern "C" int aon_loss_pair_bwd(const float* grad0, const float* grad1, int64_t n,
+                                 const float* g_loss, const float* g_loss0, const float* g_loss1,
+                                 float* d0, float* d1, aon_stream_t stream) {
+  AON_REQUIRE(grad0 && grad1 && d0 && d1, "null pointer");
+  AON_REQUIRE(n >= 0, "bad size");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_loss_pair_bwd, grid_for(n, 256, 1024), 256, 0, (hipStream_t)stream, grad0,
+                     grad1, n, g_loss, g_loss0, g_loss1, d0, d1);
   return launch_status(__func__);
 }
 

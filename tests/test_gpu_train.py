@@ -311,6 +311,39 @@ def test_train_step_chain(golden, fwd_mode, loss_scale):
           f"(fp32 vs fp64 oracle: {worst32:.2e})")
 
 
+@pytest.mark.parametrize("n_rays,with_reg", [(4096, False), (1000, True), (1, False)])
+def test_loss_pair_equals_unfused(n_rays, with_reg):
+    """train.loss_pair (aon_loss_pair: both img2mse, their sum, the psnrs in one launch) gives
+    the unfused training_step's values bit for bit -- img2mse per level (aon_mse), loss1 + loss0
+    (+ reg) and mse2psnr as torch computes it on the device -- and its backward (one
+    aon_loss_pair_bwd launch) the same rgb gradients as img2mse's, for a non-unit dL/dloss and
+    with the per-level losses also used downstream."""
+    from aonerf import train
+
+    g = torch.Generator(device="cuda").manual_seed(n_rays)
+    p0 = torch.rand((n_rays, 3), device="cuda", generator=g)
+    p1 = torch.rand((n_rays, 3), device="cuda", generator=g)
+    tgt = torch.rand((n_rays, 3), device="cuda", generator=g)
+    reg = torch.rand((), device="cuda", generator=g) * 1e-3 if with_reg else None
+    a0, a1 = p0.clone().requires_grad_(True), p1.clone().requires_grad_(True)
+    b0, b1 = p0.clone().requires_grad_(True), p1.clone().requires_grad_(True)
+    ra = reg.clone().requires_grad_(True) if with_reg else None
+    rb = reg.clone().requires_grad_(True) if with_reg else None
+
+    loss, l0, l1, s0, s1 = train.loss_pair(a0, a1, tgt, ra)
+    u0, u1 = train.img2mse(b0, tgt), train.img2mse(b1, tgt)
+    uloss = u1 + u0 + rb if with_reg else u1 + u0
+    for got, want in ((loss, uloss), (l0, u0), (l1, u1), (s0, train.mse2psnr(u0.detach())),
+                      (s1, train.mse2psnr(u1.detach()))):
+        assert torch.equal(got.detach(), want.detach()), (got.item(), want.item())
+    assert not s0.requires_grad and not s1.requires_grad
+    (3.0 * loss + 0.5 * l0).backward()
+    (3.0 * uloss + 0.5 * u0).backward()
+    assert torch.equal(a0.grad, b0.grad) and torch.equal(a1.grad, b1.grad)
+    if with_reg:
+        assert torch.equal(ra.grad, rb.grad)
+
+
 def test_adam_matches_torch():
     """aon_adam_step against torch.optim.Adam (model.py:386-389) as the reference builds it on a
     GPU: foreach=None -> the multi-tensor path (_foreach_div_ by the Python-float sqrt(bc2) is a
