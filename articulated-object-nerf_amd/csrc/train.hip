@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_mse(const float* __restrict__ pred,
 // element order, fp64 accumulation, reduction tree and rounding), the loads of both levels in
 // flight together -- then loss = (loss1 + loss0) (+ extra), and mse2psnr of each as torch forms it
 // on the device (helper.py:21-22: log, * -10, then * fp32(1 / ln 10): torch's division by a
-// Python scalar multiplies by the scalar's fp32 reciprocal).  It replaces 2 k_mse launches, the
+// Python scalar multiplies by the scalar's fp32 reciprocal; the log itself to within 1 ulp).  It replaces 2 k_mse launches, the
 // add and 3 elementwise kernels per psnr.
 __global__ __launch_bounds__(256) void k_loss_pair(const float* __restrict__ pred0,
                                                    const float* __restrict__ pred1,
@@ -232,8 +232,10 @@ __global__ __launch_bounds__(256) void k_loss_pair(const float* __restrict__ pre
     out[0] = l;
     out[1] = l0;
     out[2] = l1;
-    out[3] = __fmul_rn(__fmul_rn(-10.0f, logf(l0)), inv_ln10);
-    out[4] = __fmul_rn(__fmul_rn(-10.0f, logf(l1)), inv_ln10);
+    // the log rounded from fp64 (correctly rounded but for the rarest ties); torch's fp32 log
+    // kernel may sit 1 ulp away: the psnrs are logged values, gated to 1 ulp of torch's
+    out[3] = __fmul_rn(__fmul_rn(-10.0f, (float)log((double)l0)), inv_ln10);
+    out[4] = __fmul_rn(__fmul_rn(-10.0f, (float)log((double)l1)), inv_ln10);
   }
 }
 
