@@ -442,8 +442,7 @@ def mse2psnr(x):
 class LossPair(torch.autograd.Function):
     """The training step's loss terms (model.py:265-270; model_autodecoder.py:455-470) in one
     aon_loss_pair launch: loss = (img2mse(fine) + img2mse(coarse)) [+ reg], both mses and
-    mse2psnr of each -- the losses bit for bit those of img2mse / `+`, the psnrs to 1 ulp of
-    mse2psnr (the kernel rounds its log from fp64), where those
+    mse2psnr of each -- the same values as img2mse / `+` / mse2psnr, bit for bit, where those
     took 9 launches.  Backward: one aon_loss_pair_bwd launch for both levels' rgb gradients."""
 
     @staticmethod

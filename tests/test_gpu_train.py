@@ -314,9 +314,8 @@ def test_train_step_chain(golden, fwd_mode, loss_scale):
 @pytest.mark.parametrize("n_rays,with_reg", [(4096, False), (1000, True), (1, False)])
 def test_loss_pair_equals_unfused(n_rays, with_reg):
     """train.loss_pair (aon_loss_pair: both img2mse, their sum, the psnrs in one launch) gives
-    the unfused training_step's losses bit for bit -- img2mse per level (aon_mse), loss1 + loss0
-    (+ reg) -- the psnrs to 1 ulp of mse2psnr as torch computes it on the device, and its
-    backward (one
+    the unfused training_step's values bit for bit -- img2mse per level (aon_mse), loss1 + loss0
+    (+ reg) and mse2psnr as torch computes it on the device -- and its backward (one
     aon_loss_pair_bwd launch) the same rgb gradients as img2mse's, for a non-unit dL/dloss and
     with the per-level losses also used downstream."""
     from aonerf import train
@@ -334,13 +333,9 @@ def test_loss_pair_equals_unfused(n_rays, with_reg):
     loss, l0, l1, s0, s1 = train.loss_pair(a0, a1, tgt, ra)
     u0, u1 = train.img2mse(b0, tgt), train.img2mse(b1, tgt)
     uloss = u1 + u0 + rb if with_reg else u1 + u0
-    for got, want in ((loss, uloss), (l0, u0), (l1, u1)):
+    for got, want in ((loss, uloss), (l0, u0), (l1, u1), (s0, train.mse2psnr(u0.detach())),
+                      (s1, train.mse2psnr(u1.detach()))):
         assert torch.equal(got.detach(), want.detach()), (got.item(), want.item())
-    # the psnrs (logged values, no gradient): within 1 ulp of torch's fp32 log formula -- the
-    # kernel's log is rounded from fp64, torch's fp32 log kernel is not always correctly rounded
-    for got, want in ((s0, train.mse2psnr(u0.detach())), (s1, train.mse2psnr(u1.detach()))):
-        ulp = (torch.nextafter(want, want + 1) - want).abs()
-        assert (got - want).abs() <= ulp, (got.item(), want.item())
     assert not s0.requires_grad and not s1.requires_grad
     (3.0 * loss + 0.5 * l0).backward()
     (3.0 * uloss + 0.5 * u0).backward()
