@@ -440,10 +440,12 @@ def mse2psnr(x):
 
 
 class LossPair(torch.autograd.Function):
-    """The training step's loss terms (model.py:265-270; model_autodecoder.py:455-470) in one
-    aon_loss_pair launch: loss = (img2mse(fine) + img2mse(coarse)) [+ reg], both mses and
-    mse2psnr of each -- the same values as img2mse / `+` / mse2psnr, bit for bit, where those
-    took 9 launches.  Backward: one aon_loss_pair_bwd launch for both levels' rgb gradients."""
+    """The training step's loss terms (model.py:265-270; model_autodecoder.py:455-470):
+    loss = (img2mse(fine) + img2mse(coarse)) [+ reg] and both mses in one aon_loss_pair launch,
+    mse2psnr of both in one pass of torch's own log / mul / div (torch's device log is not
+    correctly rounded: tools/diag/psnr_ulp.py) -- the same values as img2mse / `+` / mse2psnr,
+    bit for bit, in 4 launches where those took 9.  Backward: one aon_loss_pair_bwd launch for
+    both levels' rgb gradients."""
 
     @staticmethod
     def forward(ctx, pred0, pred1, target, reg):
@@ -451,7 +453,7 @@ class LossPair(torch.autograd.Function):
         pred0, pred1, target = L.contig(pred0), L.contig(pred1), L.contig(target)
         if pred0.shape != target.shape or pred1.shape != target.shape:
             raise ValueError("LossPair: predictions and target must have one shape")
-        out = torch.empty((5,), device=pred0.device)
+        out = torch.empty((3,), device=pred0.device)
         g0, g1 = torch.empty_like(pred0), torch.empty_like(pred1)
         L.call("aon_loss_pair", L.ptr(pred0), L.ptr(pred1), L.ptr(target), pred0.numel(),
                L.ptr(L.contig(reg)) if reg is not None else None, L.ptr(out), L.ptr(g0), L.ptr(g1),
@@ -459,7 +461,8 @@ class LossPair(torch.autograd.Function):
         ctx.save_for_backward(g0, g1)
         ctx.has_reg = reg is not None
         ctx.set_materialize_grads(False)
-        loss, loss0, loss1, psnr0, psnr1 = out.unbind(0)
+        psnr0, psnr1 = mse2psnr(out[1:]).unbind(0)
+        loss, loss0, loss1 = out.unbind(0)
         ctx.mark_non_differentiable(psnr0, psnr1)
         return loss, loss0, loss1, psnr0, psnr1
 

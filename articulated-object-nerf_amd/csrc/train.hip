@@ -179,9 +179,9 @@ __global__ __launch_bounds__(256) void k_mse(const float* __restrict__ pred,
 // The training step's loss terms in one launch (model.py:265-270 / model_autodecoder.py:455-470):
 // the two levels' img2mse against one target -- each with k_mse's arithmetic (the same per-thread
 // element order, fp64 accumulation, reduction tree and rounding), the loads of both levels in
-// flight together -- then loss = (loss1 + loss0) (+ extra), and mse2psnr of each as torch forms it
-// on the device (helper.py:21-22: fp32 log, * -10, / fp32(ln 10)).  It replaces 2 k_mse launches, the
-// add and 3 elementwise kernels per psnr.
+// flight together -- then loss = (loss1 + loss0) (+ extra): one launch for 2 k_mse launches and
+// the add.  (mse2psnr stays torch's own log / mul / div, on both losses at once: torch's device
+// log is not correctly rounded, tools/diag/psnr_ulp.py, so a restatement would sit 1 ulp off.)
 __global__ __launch_bounds__(256) void k_loss_pair(const float* __restrict__ pred0,
                                                    const float* __restrict__ pred1,
                                                    const float* __restrict__ target, int64_t n,
@@ -227,15 +227,9 @@ __global__ __launch_bounds__(256) void k_loss_pair(const float* __restrict__ pre
     const float l0 = (float)(part[0][0] / (double)n), l1 = (float)(part[1][0] / (double)n);
     float l = __fadd_rn(l1, l0);
     if (extra) l = __fadd_rn(l, *extra);
-    const float ln10 = (float)2.302585092994046;
     out[0] = l;
     out[1] = l0;
     out[2] = l1;
-    // logf is torch's device log (the same ocml function; not always correctly rounded, so
-    // not replaceable by an fp64 log); the division by ln 10 is a true fp32 division
-    // (tools/diag/psnr_ulp.py: the stages torch runs, measured)
-    out[3] = __fdiv_rn(__fmul_rn(-10.0f, logf(l0)), ln10);
-    out[4] = __fdiv_rn(__fmul_rn(-10.0f, logf(l1)), ln10);
   }
 }
 

@@ -458,9 +458,8 @@ int aon_mse(const float* pred, const float* target, int64_t n, float grad_scale,
 /* The training step's loss terms in one launch (LitNeRF.training_step, model.py:265-270;
  * LitNeRF_AutoDecoder.training_step, model_autodecoder.py:455-470): the coarse (pred0) and fine
  * (pred1) img2mse against one target, each with aon_mse's arithmetic; out[0] = loss1 + loss0
- * (+ *extra when extra != NULL: the latent regulariser), out[1] = loss0, out[2] = loss1,
- * out[3] = mse2psnr(loss0), out[4] = mse2psnr(loss1) (helper.py:21-22, as torch forms it on the
- * device); grad0 / grad1 (may be NULL) = 2 (pred - target) / n. */
+ * (+ *extra when extra != NULL: the latent regulariser), out[1] = loss0, out[2] = loss1;
+ * grad0 / grad1 (may be NULL) = 2 (pred - target) / n. */
 int aon_loss_pair(const float* pred0, const float* pred1, const float* target, int64_t n,
                   const float* extra, float* out, float* grad0, float* grad1, aon_stream_t stream);
 /* Its backward: d0 = grad0 * (g_loss + g_loss0), d1 = grad1 * (g_loss + g_loss1) for device
