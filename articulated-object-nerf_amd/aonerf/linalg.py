@@ -1,7 +1,7 @@
 """Layer products on aon_gemm (the f16x3 MFMA GEMM, gemm_f16x3.hip) shared by the
 layer-by-layer paths: the training forward/backward (train.py) and the articulated
 NeRF_AE_Art MLP (model_autodecoder.py).  Operands are tensor views passed as pointers +
-leading dimensions; workspace for split reductions is cached per device."""
+leading dimensions; workspace for split reductions is cached per device and stream."""
 import contextlib
 import ctypes
 import os
@@ -19,7 +19,8 @@ _ws = {}
 
 
 def _workspace(nbytes, device):
-    key = str(device)
+    # one per device AND stream: products on two streams (train.OVERLAP_DWEIGHT) run concurrently
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)

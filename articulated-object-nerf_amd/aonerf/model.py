@@ -258,6 +258,16 @@ class NeRF(nn.Module):
         rng = torch.cuda.get_rng_state(dev) if randomized and not training else None
         ret = []
         t_vals = weights = t_next = None
+        token, joined = None, {}
+        if training:
+            from . import train
+            if train.OVERLAP_DWEIGHT and train.FUSED_BACKWARD:
+                # both levels' parameters through one Join: its backward, after both levels',
+                # joins the fine level's weight-gradient stream (train.OVERLAP_DWEIGHT)
+                token = train.JoinToken()
+                ps = [p for m in (self.coarse_mlp, self.fine_mlp) for l in m._layers()
+                      for p in (l.weight, l.bias)]
+                joined = dict(zip(map(id, ps), train.Join.apply(token, *ps)))
         for level in range(2):
             with torch.no_grad():
                 t_vals = t_next if t_next is not None else self._level_t(
@@ -270,8 +280,9 @@ class NeRF(nn.Module):
                 if self.noise_std > 0 and randomized:  # model.py:183-184
                     noise = torch.rand((B * S,), device=dev) * self.noise_std
                 params = [p for m in mlp._layers() for p in (m.weight, m.bias)]
+                params = [joined.get(id(p), p) for p in params]
                 comp, acc, depth, weights = RenderLevel.apply(o, d, v, t_vals, bool(white_bkgd),
-                                                              noise, *params)
+                                                              noise, token, *params)
                 out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
                 if return_intermediates:
                     out = out + (dict(t_vals=t_vals, weights=weights),)

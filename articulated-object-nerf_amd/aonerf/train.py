@@ -20,6 +20,8 @@ torch.optim step pre-hook); ``Adam`` below is the fused replacement (aon_adam_st
 reference's learning-rate schedule.  All arithmetic is in the HIP kernels; torch only
 allocates buffers and routes autograd.
 """
+import contextlib
+
 import numpy as np
 import torch
 import torch.optim.optimizer as _torch_optim
@@ -149,6 +151,71 @@ def _rec(key, e0, rows):
         e1.record()
         TIMERS.setdefault(key, []).append((e0, e1, rows))
 
+# the fine level's weight-gradient GEMMs on a second stream, concurrent with the coarse level's
+# backward (compositing backward + input-gradient chain), when the two levels' parameters pass
+# through one Join (NeRF.forward's training path does this): Join's backward -- after both
+# levels' -- makes the caller's stream wait for them, so every gradient hook / AccumulateGrad /
+# optimizer sees finished gradients.  False: one stream, in autograd's order.
+OVERLAP_DWEIGHT = True
+
+
+class JoinToken:
+    """The side-stream work of one forward's render levels, joined by Join.backward."""
+
+    def __init__(self):
+        self.pending = []  # (stream the caller waits on, event on the side stream)
+
+
+class Join(torch.autograd.Function):
+    """Identity on the render levels' parameters (views), whose backward runs after every
+    level's: it joins the side stream (OVERLAP_DWEIGHT) before the gradients reach the
+    parameters."""
+
+    @staticmethod
+    def forward(ctx, token, *params):
+        ctx.token = token
+        ctx.set_materialize_grads(False)
+        return tuple(p.view_as(p) for p in params)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        for stream, ev in ctx.token.pending:
+            stream.wait_event(ev)
+        ctx.token.pending.clear()
+        return (None, *grads)
+
+
+_side = {}
+
+
+def _side_stream(dev):
+    s = _side.get(str(dev))
+    if s is None:
+        s = _side[str(dev)] = torch.cuda.Stream(device=dev)
+    return s
+
+
+@contextlib.contextmanager
+def _on_side(token, dev, tensors):
+    """Run the enclosed launches on the device's side stream after the current stream's work so
+    far; ``tensors`` (every tensor they touch) are kept from the caching allocator until the
+    side stream is done with them, and ``token`` records the join.  token None: in place."""
+    if token is None:
+        yield
+        return
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        yield
+    for t in tensors:
+        if t is not None:
+            t.record_stream(side)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    token.pending.append((main, ev))
+
+
 _packed = {}
 
 
@@ -241,12 +308,14 @@ def relu_masks(acts, R):
     return masks
 
 
-def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_tiled=True):
+def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_tiled=True,
+                          token=None):
     """_backward_level with every input-gradient product in one fused kernel (aon_mlp_bwd);
     the weight gradients dW = dZ^T X and db = sum_rows dZ stay split-K GEMMs.  ``masks``: the
     ReLU' bits of h0..h7, hv from the fused forward (built from the activations when None).
     h_tiled: h / bot / hv in the fused forward's tiled layout (tiles.py), else row-major (the
-    layer-by-layer forward).  The chain's dz / dzb / dzv are always tiled."""
+    layer-by-layer forward).  The chain's dz / dzb / dzv are always tiled.  ``token`` (a
+    JoinToken): the weight gradients run on the side stream (OVERLAP_DWEIGHT)."""
     R, dev = draw.shape[0], draw.device
     bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
@@ -257,7 +326,9 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
     dzv = torch.empty((NR, 128), device=dev, dtype=dt)
     dzb = torch.empty((NR, 256), device=dev, dtype=dt)
     dz = torch.empty((8, NR, 256), device=dev, dtype=dt)
-    work = _buffer("work", 4, dev)
+    # the chain's d raw scale word: the weight gradients read it, on the side stream while the
+    # next level's chain may already run -- its own word then
+    work = _buffer("work", 4, dev) if token is None else torch.empty((1,), device=dev)
     packed = _pack_bwd(P, dev, S, bf16)
     e0 = _ev()
     L.call("aon_mlp_bwd_bf16" if bf16 else "aon_mlp_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks),
@@ -284,7 +355,8 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
              n_store=n_store)
 
     # bf16: the eight 256 x 256 products (bottleneck, pts_linears.1-7) run as one aon_gemm_batch
-    with batched():
+    touched = [dzv, dzb, dz, draw, work, enc, venc, bot, hv, *h, *(t for wb in G for t in wb)]
+    with _on_side(token, dev, touched), batched():
         dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1], a_t=False)    # rgb_layer
         dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0
         dweight(G[10][0], dzv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
@@ -337,8 +409,9 @@ class RenderLevel(torch.autograd.Function):
     (model.py:175-197) with gradients for the level's 24 MLP parameters."""
 
     @staticmethod
-    def forward(ctx, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise, *params):
+    def forward(ctx, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise, token, *params):
         B, S = t_vals.shape
+        ctx.token = token  # a JoinToken: the weight gradients may run on the side stream
         R, dev = B * S, t_vals.device
         bf16 = FUSED_FORWARD and PRECISION == "bf16"
         if bf16:  # the bf16 training forward keeps pos_enc(x) itself (bf16, tiled, 128 columns)
@@ -398,7 +471,10 @@ class RenderLevel(torch.autograd.Function):
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
         if FUSED_BACKWARD:
-            _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, ctx.masks, ctx.h_tiled)
+            # (not while TIMERS time each level's kernels on the current stream)
+            token = ctx.token if OVERLAP_DWEIGHT and TIMERS is None else None
+            _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, ctx.masks, ctx.h_tiled,
+                                  token=token)
         else:
             if ctx.h_tiled:  # the all-GEMM backward reads row-major fp32 activations
                 h = [tiles.untile(x, R).float() for x in h]
@@ -407,7 +483,7 @@ class RenderLevel(torch.autograd.Function):
                 enc = tiles.untile(enc, R)[:, :63].float().contiguous()
             _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
-        return (None, None, None, None, None, None, *grads)
+        return (None, None, None, None, None, None, None, *grads)
 
 
 class Mse(torch.autograd.Function):
