@@ -155,8 +155,10 @@ def _rec(key, e0, rows):
 # backward (compositing backward + input-gradient chain), when the two levels' parameters pass
 # through one Join (NeRF.forward's training path does this): Join's backward -- after both
 # levels' -- makes the caller's stream wait for them, so every gradient hook / AccumulateGrad /
-# optimizer sees finished gradients.  False: one stream, in autograd's order.
-OVERLAP_DWEIGHT = True
+# optimizer sees finished gradients.  False (default): one stream, in autograd's order --
+# measured faster: the concurrent kernels contend for the CUs (bf16 C5 step 5.77-5.86 ms
+# overlapped against 5.67-5.71 ms, f16x3 17.34 against 17.12 ms; profiles/r04/overlap_ab.txt).
+OVERLAP_DWEIGHT = False
 
 
 class JoinToken:
