@@ -188,6 +188,12 @@ _STICKY = {}
 # unrelated model's optimizer neither pays the sync nor consumes (hides) this model's overflow
 PACK_PARAMS = {}
 _STICKY_PARAMS = {}
+# pending pack -> (pinned host copy of its status word, event after the copy): taken after the
+# last kernel that can set the word (snapshot_pack), so check_pending reads host memory once that
+# point has passed instead of draining the device queue with a sync on the device word -- the
+# step's later kernels (weight gradients) keep the GPU busy while the optimizer waits
+SNAPSHOTS = {}
+_PINNED = {}
 
 
 def status_word(buf):
@@ -201,6 +207,7 @@ def register_pack(key, buf, params=()):
     parameter tensors packed into ``buf`` (empty: the pack concerns every optimizer)."""
     dev = str(buf.device)
     k = (key[0], key[1], dev)
+    SNAPSHOTS.pop(k, None)  # a snapshot of the previous pack no longer covers the buffer
     if k in PENDING_PACKS:
         w = _STICKY.get(dev)
         if w is None:
@@ -209,6 +216,22 @@ def register_pack(key, buf, params=()):
         _STICKY_PARAMS.setdefault(dev, set()).update(PACK_PARAMS.get(k) or {None})
     PENDING_PACKS[k] = buf
     PACK_PARAMS[k] = frozenset(p.data_ptr() for p in params)
+
+
+def snapshot_pack(buf):
+    """Call after the LAST kernel that reads the pending pack ``buf`` (the only writers of its
+    status word) on the current stream: an asynchronous copy of the word to pinned host memory
+    and an event after it (no sync).  No-op for a buffer that is not pending."""
+    k = next((k for k, b in PENDING_PACKS.items() if b is buf), None)
+    if k is None:
+        return
+    h = _PINNED.get(k)
+    if h is None:
+        h = _PINNED[k] = torch.empty((1,), dtype=torch.int32, pin_memory=True)
+    h.copy_(status_word(buf).view(1), non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    SNAPSHOTS[k] = (h, ev)
 
 
 def _concerns(ids, param_ids):
@@ -235,18 +258,25 @@ def range_overflow(bufs):
 def check_pending(devices=None, param_ids=None):
     """Consume the pending training packs (and sticky words) of ``devices`` (str, None = all)
     that concern ``param_ids`` (data pointers of an optimizer's parameters; None = all):
-    True if any saw an overflow since the last check (one sync; False without a sync when
-    nothing is pending)."""
+    True if any saw an overflow since the last check.  A pack with a snapshot (snapshot_pack)
+    is read from host memory once its event has passed; the others (and sticky words) with one
+    device sync; none pending: no sync at all."""
     keys = [k for k in PENDING_PACKS if (devices is None or k[2] in devices)
             and _concerns(PACK_PARAMS.get(k), param_ids)]
-    words = []
+    words, bad = [], False
     for k in keys:
-        words.append(status_word(PENDING_PACKS.pop(k)))
+        buf = PENDING_PACKS.pop(k)
         PACK_PARAMS.pop(k, None)
+        snap = SNAPSHOTS.pop(k, None)
+        if snap is None:
+            words.append(status_word(buf))
+        else:
+            snap[1].synchronize()
+            bad |= int(snap[0][0]) != 0
     for dev in [d for d in _STICKY if (devices is None or d in devices)
                 and _concerns(_STICKY_PARAMS.get(d), param_ids)]:
         words.append(_STICKY.pop(dev))
         _STICKY_PARAMS.pop(dev, None)
     if not words:
-        return False
-    return bool(torch.stack(words).any().item())
+        return bad
+    return bool(torch.stack(words).any().item()) or bad

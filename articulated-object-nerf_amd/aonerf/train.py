@@ -335,6 +335,7 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
     e0 = _ev()
     L.call("aon_mlp_bwd_bf16" if bf16 else "aon_mlp_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks),
            R, L.ptr(dzv), L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
+    L.snapshot_pack(packed)  # the chain was the pack's last reader (range guard, _lib)
     _rec(f"bwd_chain{S}", e0, R)
     e0 = _ev()
     acts = ACT_SCALE
@@ -403,6 +404,7 @@ def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, m
                L.stream(dev))
     else:
         L.call("aon_mlp_fwd_train", *args, L.stream(dev))
+    L.snapshot_pack(packed)  # the forward was the pack's last reader (range guard, _lib)
     return list(hbuf.unbind(0)), bot, hv
 
 

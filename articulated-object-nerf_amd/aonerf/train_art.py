@@ -245,6 +245,7 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
                int(mixed), L.stream(dev))
     else:
         L.call("aon_mlp_art_fwd_train", *args, L.stream(dev))
+    L.snapshot_pack(packed)  # the forward was the pack's last reader (range guard, _lib)
     _train._rec(f"art_fwd_train{S}", e0, R)
     return xyz, hd, enc, h, bot, hv
 
@@ -384,6 +385,7 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     e0 = _train._ev()
     L.call("aon_mlp_art_bwd_bf16" if bf16 else "aon_mlp_art_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
            L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
+    L.snapshot_pack(packed)  # the chain was the pack's last reader
     _train._rec(f"art_bwd_chain{S}", e0, R)
     e0 = _train._ev()
     gs, acts = GRAD_SCALE, ACT_SCALE

@@ -16,11 +16,42 @@ def _buf(status=0):
 def L():
     from aonerf import _lib
 
-    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib._STICKY_PARAMS):
+    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib._STICKY_PARAMS, _lib.SNAPSHOTS):
         d.clear()
     yield _lib
-    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib._STICKY_PARAMS):
+    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib._STICKY_PARAMS, _lib.SNAPSHOTS):
         d.clear()
+
+
+class _Event:
+    def __init__(self):
+        self.waited = False
+
+    def synchronize(self):
+        self.waited = True
+
+
+def test_snapshot_read_from_host(L):
+    """A pack with a snapshot (snapshot_pack: the status word copied to host memory after its
+    last reader) is judged by the host copy once the snapshot's event has passed -- the device
+    word is not read (no device sync) -- and a re-pack drops the snapshot (the old status then
+    reaches the check through the sticky device word)."""
+    b = _buf(0)
+    L.register_pack(("train", "fwd65"), b)
+    ev = _Event()
+    L.SNAPSHOTS[("train", "fwd65", "cpu")] = (torch.tensor([1], dtype=torch.int32), ev)
+    assert L.check_pending({"cpu"}) is True and ev.waited
+    assert not L.SNAPSHOTS and not L.PENDING_PACKS
+    # a clean snapshot: False, though the (stand-in) device word says otherwise -- it is not read
+    L.register_pack(("train", "fwd65"), _buf(1))
+    L.SNAPSHOTS[("train", "fwd65", "cpu")] = (torch.tensor([0], dtype=torch.int32), _Event())
+    assert L.check_pending({"cpu"}) is False
+    # re-pack of a pending pack: its snapshot is dropped, its device word goes sticky
+    L.register_pack(("train", "fwd65"), _buf(1))
+    L.SNAPSHOTS[("train", "fwd65", "cpu")] = (torch.tensor([0], dtype=torch.int32), _Event())
+    L.register_pack(("train", "fwd65"), _buf(0))
+    assert not L.SNAPSHOTS
+    assert L.check_pending({"cpu"}) is True
 
 
 def test_pending_consumed_once(L):
