@@ -195,6 +195,7 @@ __device__ __forceinline__ uint64_t ovf_of(const Frag<N, NCOL>& f) {
 // (true scale) is stored for the weight-gradient GEMMs.
 struct NoStore {
   static constexpr bool kPkEpi = true;
+  static constexpr bool kPkFromF32 = false;
   __device__ __forceinline__ void begin_pair(int) const {}
   __device__ __forceinline__ float post(int, int, int, int, float v) const { return v; }
   __device__ __forceinline__ uint32_t post_pk(int, int, int, int, uint32_t pk) const { return pk; }
@@ -226,6 +227,16 @@ __device__ __forceinline__ uint32_t pk_nonzero(uint32_t a) {
 __device__ __forceinline__ uint32_t lshl_or(uint32_t m, int s, uint32_t a) {
   uint32_t r;
   asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "i"(s), "v"(a));
+  return r;
+}
+// bf16 pair at activation scale 2^3 (a ReLU output, >= 0) -> at true scale, exactly: one packed
+// max clears a -0 (negative as i16), one saturating packed subtract of 3 from each exponent
+// field divides by kActS -- exact for every normal bf16; a value whose exponent field is below 3
+// (true scale < 2^-124, fp32's denormal range) becomes 0 where v * 2^-3 would keep a subnormal
+__device__ __forceinline__ uint32_t pk_bf16_unscale(uint32_t pk) {
+  static_assert(kActS == 8.0f, "exponent shift of kActS");
+  uint32_t r;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(pk_max_i16(pk, 0u)), "s"(0x01800180u));
   return r;
 }
 // (bf16(lo), bf16(hi)) round to nearest even as one v_cvt_pk_bf16_f32: the empty asm pins the
@@ -322,6 +333,13 @@ __device__ __forceinline__ void store_enc_bf(__bf16* base, int64_t row, int g,
 #ifndef AON_BF_ST16
 #define AON_BF_ST16 1
 #endif
+#ifndef AON_PK_F16X3_BF
+#define AON_PK_F16X3_BF 1  // 0: A/B build -- fp32 ReLU' compares and per-value scaling (RowStore::put)
+#endif
+template <typename S, typename = void>
+struct pk_from_f32 : std::false_type {};
+template <typename S>
+struct pk_from_f32<S, std::void_t<decltype(S::kPkFromF32)>> : std::bool_constant<S::kPkFromF32> {};
 // pairs (r0 = 0, 2) of a tile meet in one 4-value store
 template <int NCOL, typename T>
 struct Store4 {
@@ -383,6 +401,9 @@ __device__ __forceinline__ int st16_off(int g) { return 256 * (g & 1) + 8 * (g >
 
 template <int NCOL, typename T = float>
 struct RowStore : Store4<NCOL, T> {
+  // fp16x3 layers keeping bf16 (the articulated bf16 mode's forward): a ReLU layer's pair is
+  // converted once at activation scale and stored / bit-tested packed (epi_part, put_pk)
+  static constexpr bool kPkFromF32 = std::is_same<T, __bf16>::value && AON_F16X3_V2 && AON_PK_F16X3_BF;
   T* rowp[NCOL];  // act_base(row) of each column's sample (stored when ok)
   float s;        // to true scale (a power of two: exact)
   __device__ __forceinline__ void begin_pair(int) const {}
@@ -594,7 +615,15 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
 #if !(AON_GUARD_PK && AON_F16X3_V2 && AON_FMA_MIX)
     or_ballot(out.ovf, fmaxf(fabsf(vv[0]), fabsf(vv[1])) > kF16Max);
 #endif
-    st.put(pr, uu, r0, c, vv[0], vv[1]);
+    if constexpr (RELU && pk_from_f32<Store>::value) {
+      // bf16 kept values of a fp16x3 ReLU layer: one conversion at activation scale, rescaled
+      // packed, then the bf16 layers' packed store and ReLU' bits from the packed pair (bit =
+      // stored value != 0: v > 0 but for fp32 denormals) -- where RowStore::put spent two
+      // multiplies, two fp32 compares and their selects, and an 8-B store per tile row
+      st.put_pk(pr, uu, r0, c, pk_bf16_unscale(cvt_pk_bf16(vv[0], vv[1])));
+    } else {
+      st.put(pr, uu, r0, c, vv[0], vv[1]);
+    }
 #if AON_F16X3_V2 && AON_FMA_MIX
     // hi pair by one v_cvt_pk_f16_f32; lo_e = v_e - hi_e by v_fma_mix_f32 reading the fp16 half
     // in place (exact in fp32), then one more cvt_pk
