@@ -250,22 +250,38 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
   return r;
 }
 
+// Stores of the kept tensors (activations, ReLU' bits, the chains' gradients): read once, by a
+// later kernel, long after -- AON_NT_STORE = 1 (A/B build) marks them non-temporal
+#ifndef AON_NT_STORE
+#define AON_NT_STORE 0
+#endif
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <typename V>
+__device__ __forceinline__ void kept_store(void* p, V v) {
+#if AON_NT_STORE
+  __builtin_nontemporal_store(v, static_cast<V*>(p));
+#else
+  *static_cast<V*>(p) = v;
+#endif
+}
+
 // two consecutive outputs at true scale: one 8-B fp32 store, or (bf16 mode) one 4-B bf16 store
 __device__ __forceinline__ void store2(float* p, float v0, float v1) {
-  *reinterpret_cast<float2*>(p) = float2{v0, v1};
+  kept_store(p, u32x2{__float_as_uint(v0), __float_as_uint(v1)});
 }
 __device__ __forceinline__ void store2(__bf16* p, float v0, float v1) {
-  *reinterpret_cast<bf2*>(p) = bf2{static_cast<__bf16>(v0), static_cast<__bf16>(v1)};
+  kept_store(p, __builtin_bit_cast(uint32_t, bf2{static_cast<__bf16>(v0), static_cast<__bf16>(v1)}));
 }
 
 // four consecutive outputs: one 16-B fp32 store, or one 8-B bf16 store
 __device__ __forceinline__ void store4(float* p, float v0, float v1, float v2, float v3) {
-  *reinterpret_cast<f4*>(p) = f4{v0, v1, v2, v3};
+  kept_store(p, f4{v0, v1, v2, v3});
 }
 __device__ __forceinline__ void store4(__bf16* p, float v0, float v1, float v2, float v3) {
   const bf2 a = {static_cast<__bf16>(v0), static_cast<__bf16>(v1)};
   const bf2 b = {static_cast<__bf16>(v2), static_cast<__bf16>(v3)};
-  *reinterpret_cast<uint2*>(p) = uint2{__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b)};
+  kept_store(p, u32x2{__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b)});
 }
 
 #ifndef AON_TILED
@@ -326,7 +342,7 @@ __device__ __forceinline__ void store_enc_bf(__bf16* base, int64_t row, int g,
         w[e] = __builtin_bit_cast(uint32_t, pr);
       }
     }
-    *reinterpret_cast<uint4*>(eb + 512 * k) = uint4{w[0], w[1], w[2], w[3]};
+    kept_store(eb + 512 * k, u32x4{w[0], w[1], w[2], w[3]});
   }
 }
 
@@ -388,10 +404,9 @@ struct Store4 {
     // every lane takes part in the swaps (EXEC full): only the store is predicated
     const auto s0 = __builtin_amdgcn_permlane16_swap(pend0[c].x, pendw[c], false, false);
     const auto s1 = __builtin_amdgcn_permlane16_swap(pend0[c].y, pk, false, false);
-    if (ok[c])
-      *reinterpret_cast<uint4*>(rowp + kTileStride * 2 * pr + off16) = uint4{s0[0], s1[0], s0[1], s1[1]};
+    if (ok[c]) kept_store(rowp + kTileStride * 2 * pr + off16, u32x4{s0[0], s1[0], s0[1], s1[1]});
 #else
-    if (ok[c]) *reinterpret_cast<uint2*>(rowp + kTileStride * (2 * pr + uu)) = uint2{pendw[c], pk};
+    if (ok[c]) kept_store(rowp + kTileStride * (2 * pr + uu), u32x2{pendw[c], pk});
 #endif
   }
 };
@@ -438,8 +453,8 @@ struct RowStoreBits : RowStore<NCOL, T> {
     const int q = 2 * uu + (r0 >> 1);  // compile-time after unrolling
     b[c] = q == 0 ? m : lshl_or(m, 2 * q, b[c]);
     if (q == 3 && this->ok[c]) {
-      mrow[c][pr] = static_cast<uint8_t>(b[c] | (b[c] >> 15));
-      if (narrow) mrow[c][pr + 4] = 0;
+      kept_store(mrow[c] + pr, static_cast<uint8_t>(b[c] | (b[c] >> 15)));
+      if (narrow) kept_store(mrow[c] + pr + 4, uint8_t{0});
     }
   }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
@@ -451,8 +466,8 @@ struct RowStoreBits : RowStore<NCOL, T> {
     const int bit = 4 * uu + r0;  // within the pair's byte (compile-time after unrolling)
     b[c] = bit == 0 ? m : (b[c] | (m << bit));
     if (uu == 1 && r0 == 2 && this->ok[c]) {
-      mrow[c][pr] = static_cast<uint8_t>(b[c]);
-      if (narrow) mrow[c][pr + 4] = 0;
+      kept_store(mrow[c] + pr, static_cast<uint8_t>(b[c]));
+      if (narrow) kept_store(mrow[c] + pr + 4, uint8_t{0});
     }
   }
 };
