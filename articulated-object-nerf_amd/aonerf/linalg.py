@@ -61,7 +61,11 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
         # tiles, or fp16x3
         cls = "f16" if f16 else 256 if M == 256 and N == 256 else 128
         if cls != 128 or BATCH128:
-            writes = [_span(C)] + ([_span(rowsum)] if rowsum is not None else [])
+            # what the product writes of C: its M x (n_store or N) corner, not the whole view (a
+            # dW passed whole while a K-concat segment fills its later columns must not count
+            # as overlapping that segment's product: a needless flush split the level's batch)
+            Cw = C[:M, :(n_store or N)] if C.dim() == 2 else C
+            writes = [_span(Cw)] + ([_span(rowsum)] if rowsum is not None else [])
             reads = [_span(A), _span(B)] + ([_span(a_amax)] if a_amax is not None else [])
             if any(_overlaps(w, it[4]) or _overlaps(w, it[5]) or _overlaps(r, it[4])
                    for it in _batch for w in writes for r in reads):

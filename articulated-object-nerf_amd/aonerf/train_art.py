@@ -418,27 +418,29 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
         gemm(dl, db, W[:, col0:], 1, n, n_out, lda=n_out, a_kc=True, ldb=W.stride(0), b_kc=False,
              ldc=n, accumulate=accumulate, a_scale=gs, b_scale=W_SCALE, exact_fp32=bf16)
 
-    dweight(RGB, draw, 4, hv[3], wc, wc, a_t=False)                       # rgb_layer
-    for i in range(3, 0, -1):                                             # views_linear.i
-        dweight(VIEW0 + i, dzv[i], wc, hv[i - 1], wc, wc)
-    dweight(VIEW0, dzv[0], wc, bot, nw, nw)                               # views_linear.0
-    dweight(VIEW0, dzv[0], wc, venc, nv, nv, col0=nw, rdiv=S, bias=False)
-    dlatent(VIEW0, nw + nv, app, dapp, False)
-    # bf16: the eight 256 x 256 products (bottleneck, pts_linears.1-7) as one aon_gemm_batch,
-    # flushed before dlatent reads pts_linears.5's bias gradient
+    # every whole-tile product of the level deferred to aon_gemm_batch launches (bf16: the eight
+    # 256 x 256 ones -- bottleneck, pts_linears.1-7 -- and the 128-wide view / deformation / enc
+    # column ones; fp16x3: all as the fp16x3 class), flushed before the latent terms read the
+    # bias gradients; the latent terms then run in the same order as before (bit-identical)
     with batched():
+        dweight(RGB, draw, 4, hv[3], wc, wc, a_t=False)                   # rgb_layer
+        for i in range(3, 0, -1):                                         # views_linear.i
+            dweight(VIEW0 + i, dzv[i], wc, hv[i - 1], wc, wc)
+        dweight(VIEW0, dzv[0], wc, bot, nw, nw)                           # views_linear.0
+        dweight(VIEW0, dzv[0], wc, venc, nv, nv, col0=nw, rdiv=S, bias=False)
         dweight(BOT, dbot, nw, h[7], nw, nw)                              # bottleneck
         dweight(DENS, draw[:, 3:], 4, h[7], nw, nw, a_t=False)            # density
         for i in range(7, 0, -1):                                         # pts_linears.i
             dweight(PTS0 + i, dz[i], nw, h[i - 1], nw, nw)
-    dweight(PTS0 + 5, dz[5], nw, enc, ne, ne, col0=nw, bias=False)
+        dweight(PTS0 + 5, dz[5], nw, enc, ne, ne, col0=nw, bias=False)
+        dweight(PTS0, dz[0], nw, enc, ne, ne)                             # pts_linears.0
+        dweight(DL, dxp, 3, hd[3], wd, wd, chain_scale=False, a_t=False)  # deformation_layer
+        for i in range(3, 0, -1):                                         # deformations_linear.i
+            dweight(DEF0 + i, dzd[i], wd, hd[i - 1], wd, wd, chain_scale=False)
+        dweight(DEF0, dzd[0], wd, xyz, 3, 3, chain_scale=False)           # deformations_linear.0
+    dlatent(VIEW0, nw + nv, app, dapp, False)
     dlatent(PTS0 + 5, nw + ne, shape, dshape, False)
-    dweight(PTS0, dz[0], nw, enc, ne, ne)                                 # pts_linears.0
     dlatent(PTS0, ne, shape, dshape, True)
-    dweight(DL, dxp, 3, hd[3], wd, wd, chain_scale=False, a_t=False)      # deformation_layer
-    for i in range(3, 0, -1):                                             # deformations_linear.i
-        dweight(DEF0 + i, dzd[i], wd, hd[i - 1], wd, wd, chain_scale=False)
-    dweight(DEF0, dzd[0], wd, xyz, 3, 3, chain_scale=False)               # deformations_linear.0
     dlatent(DEF0, 3, shape, dshape, True)
     dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
     _train._rec(f"art_dweight{S}", e0, R)

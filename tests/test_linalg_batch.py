@@ -72,3 +72,22 @@ def test_a_amax_kept_alive(monkeypatch):
         linalg.gemm(C, A, B, 256, 256, K, lda=256, a_kc=False, ldb=256, b_kc=False, ldc=256,
                     a_amax=amax)
     assert len(seen) == 1 and seen[0][3][4] is amax
+
+
+def test_whole_dw_view_with_concat_segment_one_flush(monkeypatch):
+    """The fused backward passes pts_linears.5's dW WHOLE (256 x 319) for its 256 main columns and
+    dW[:, 256:] for the skip segment's (63 stored of a 128-wide bf16 operand, n_store): the first
+    product writes only its M x N corner, so the two share one flush (a flush between them split
+    the level's 256 x 256 batch in two launches)."""
+    log = _rec(monkeypatch)
+    K = 8192
+    A = torch.zeros(K, 256, dtype=torch.bfloat16)
+    B = torch.zeros(K, 256, dtype=torch.bfloat16)
+    E = torch.zeros(K, 128, dtype=torch.bfloat16)
+    dW = torch.zeros(256, 319)
+    with linalg.batched():
+        linalg.gemm(dW, A, B, 256, 256, K, lda=256, a_kc=False, ldb=256, b_kc=False, ldc=319,
+                    mma_bf16=True)
+        linalg.gemm(dW[:, 256:], A, E, 256, 128, K, lda=256, a_kc=False, ldb=128, b_kc=False,
+                    ldc=319, mma_bf16=True, n_store=63)
+    assert len(log) == 1 and len(log[0]) == 2
