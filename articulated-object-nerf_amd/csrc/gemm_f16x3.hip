@@ -386,24 +386,47 @@ __device__ __forceinline__ float sum_z4(const float* src, int64_t stride, int sp
   return (q & 2) ? __fadd_rn(other, pair) : __fadd_rn(pair, other);
 }
 
+// Sixteen lanes per output (the small products -- heads, segment sums -- whose few hundred
+// outputs each sum 256-512 chunks: at 4 lanes they ran on ~6 workgroups in 16 dependent load
+// rounds, ~8-11 us): lane q sums the q-th sixteenth in z order, then a fixed xor tree combines
+// them, lower lane first at every level (deterministic).
+__device__ __forceinline__ float sum_z16(const float* src, int64_t stride, int splits, int q) {
+  const int zq = (splits + 15) / 16;
+  const int z0 = q * zq, z1 = z0 + zq < splits ? z0 + zq : splits;
+  float v = 0.f;
+  if (z0 < z1) v = sum_z(src + (int64_t)z0 * stride, stride, z1 - z0);
+#pragma unroll
+  for (int b = 1; b < 16; b <<= 1) {
+    const float w = __shfl_xor(v, b, 64);
+    v = (q & b) ? __fadd_rn(w, v) : __fadd_rn(v, w);
+  }
+  return v;
+}
+
+template <int L>
 __device__ __forceinline__ void reduce_body(const Params& p, int splits) {
+  static_assert(L == 4 || L == 16, "lanes per output");
+  constexpr int kSh = L == 4 ? 2 : 4;
   const int64_t total = p.M * p.N;
   const int64_t extra = p.rowsum ? p.M : 0;  // rowsum entries ride along as e >= total
-  const int q = threadIdx.x & 3;
+  const int q = threadIdx.x & (L - 1);
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  // every lane of a wave takes part in the shuffles: the loop bound is per group of 4 lanes and
-  // the grid stride a multiple of 4, so a group's lanes run the same iterations
-  for (int64_t e4 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (e4 >> 2) < total + extra;
-       e4 += nthreads) {
-    const int64_t e = e4 >> 2;
+  auto sum = [&](const float* src, int64_t stride) {
+    return L == 4 ? sum_z4(src, stride, splits, q) : sum_z16(src, stride, splits, q);
+  };
+  // every lane of a wave takes part in the shuffles: the loop bound is per group of L lanes and
+  // the grid stride a multiple of L, so a group's lanes run the same iterations
+  for (int64_t eL = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (eL >> kSh) < total + extra;
+       eL += nthreads) {
+    const int64_t e = eL >> kSh;
     if (e >= total) {
       const int64_t m = e - total;
-      const float v = sum_z4(p.rowsum_part + m, p.M, splits, q);
+      const float v = sum(p.rowsum_part + m, p.M);
       if (q == 0) p.rowsum[m] = v;
       continue;
     }
     const int64_t m = e / p.N, n = e - m * p.N;
-    float v = sum_z4(p.part + e, total, splits, q);
+    float v = sum(p.part + e, total);
     if (q != 0 || n >= p.nstore) continue;
     float* c = p.C + m * p.ldc + n;
     if (p.accumulate) v = __fadd_rn(*c, v);
@@ -414,7 +437,8 @@ __device__ __forceinline__ void reduce_body(const Params& p, int splits) {
   }
 }
 
-__global__ void k_gemm_reduce(Params p, int splits) { reduce_body(p, splits); }
+template <int L>
+__global__ void k_gemm_reduce(Params p, int splits) { reduce_body<L>(p, splits); }
 
 // aon_gemm_batch: up to AON_GEMM_BATCH_MAX products in one launch, selected by a wave-uniform
 // index into the kernel-argument table
@@ -425,7 +449,7 @@ struct ParamsBatch {
 };
 
 // the batch's split-K reduce: grid.y = product
-__global__ void k_gemm_reduce_batch(ParamsBatch pb) { reduce_body(pb.p[blockIdx.y], pb.zsplit); }
+__global__ void k_gemm_reduce_batch(ParamsBatch pb) { reduce_body<4>(pb.p[blockIdx.y], pb.zsplit); }
 
 // fp16x3 weight gradients of one level (aon_gemm_batch): every product's 128 x 128 tiles, chunk z
 // of all of them on one XCD (split_of's order), product b owning tiles tile0[b] .. tile0[b+1]-1
@@ -1556,10 +1580,12 @@ constexpr int kSkinnyRows = 16;
 #define AON_GEMM_SKINNY_SK 4  // rows in flight per thread of the skinny kernel; 1: A/B
 #endif
 #ifndef AON_GEMM_SEGSUM_SK
-#define AON_GEMM_SEGSUM_SK 16  // ... of the segment-sum kernel (one workgroup of 4 waves per CU)
+#define AON_GEMM_SEGSUM_SK 16  // ... of the segment-sum kernel (one workgroup of 4 waves per CU;
+                               // 16 vs 4: 60.4 vs 62.4 us fine level, neutral)
 #endif
 #ifndef AON_GEMM_SKINNY_SK2
-#define AON_GEMM_SKINNY_SK2 8  // ... of the skinny kernel on B of <= 128 columns (A/B knob)
+#define AON_GEMM_SKINNY_SK2 4  // ... of the skinny kernel on B of <= 128 columns (A/B knob: 8 measured
+                               // 81 -> 108 us on the fine level's rgb head, profiles/r04/final2)
 #endif
 template <int M, typename TA, bool BT, int SK = AON_GEMM_SKINNY_SK>
 __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
@@ -1595,8 +1621,8 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
   };
   // SK rows per thread in flight: their loads are issued before the first is consumed (one
   // dependent load per row left this kernel latency-bound: rgb's 0.27 GB at ~2.2 TB/s); the
-  // rows are still summed in k order (bit-identical); SK is doubled for B of <= 128 columns
-  // (half the waves per workgroup: the same bytes in flight per CU)
+  // rows are still summed in k order (bit-identical); SK2 for B of <= 128 columns (half the waves
+  // per workgroup)
   int64_t k = kbeg + r;
   for (; k + (SK - 1) * kSkinnyRows < kend; k += SK * kSkinnyRows) {
     uint4 bv[SK];
@@ -2035,7 +2061,11 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   if (zs > 1) {
     const int rc = launch_status(__func__);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_gemm_reduce, grid_for(4 * (a->M * a->N + a->M), 256, 16384), 256, 0, st, p, (int)zs);
+    const int64_t outs = a->M * a->N + a->M;
+    if (outs <= 4096)  // a few hundred outputs: 16 lanes each (sum_z16)
+      hipLaunchKernelGGL(k_gemm_reduce<16>, grid_for(16 * outs, 256, 16384), 256, 0, st, p, (int)zs);
+    else
+      hipLaunchKernelGGL(k_gemm_reduce<4>, grid_for(4 * outs, 256, 16384), 256, 0, st, p, (int)zs);
   }
   return launch_status(__func__);
 }
