@@ -439,6 +439,9 @@ __device__ __forceinline__ void reduce_body(const Params& p, int splits) {
 
 template <int L>
 __global__ void k_gemm_reduce(Params p, int splits) { reduce_body<L>(p, splits); }
+#ifndef AON_GEMM_REDUCE16
+#define AON_GEMM_REDUCE16 1  // 0: A/B build -- the small products' reduce at 4 lanes per output
+#endif
 
 // aon_gemm_batch: up to AON_GEMM_BATCH_MAX products in one launch, selected by a wave-uniform
 // index into the kernel-argument table
@@ -2062,7 +2065,7 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     const int rc = launch_status(__func__);
     if (rc) return rc;
     const int64_t outs = a->M * a->N + a->M;
-    if (outs <= 4096)  // a few hundred outputs: 16 lanes each (sum_z16)
+    if (AON_GEMM_REDUCE16 && outs <= 4096)  // a few hundred outputs: 16 lanes each (sum_z16)
       hipLaunchKernelGGL(k_gemm_reduce<16>, grid_for(16 * outs, 256, 16384), 256, 0, st, p, (int)zs);
     else
       hipLaunchKernelGGL(k_gemm_reduce<4>, grid_for(4 * outs, 256, 16384), 256, 0, st, p, (int)zs);

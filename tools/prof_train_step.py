@@ -20,14 +20,16 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--trunk", action="store_true", help="articulated bf16: BF16_TRUNK = True")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--no-overlap", action="store_true", help="train.OVERLAP_DWEIGHT = False")
+    ap.add_argument("--overlap", type=int, default=None,
+                    help="train.OVERLAP_DWEIGHT = 0 / 1 (default: the library's setting)")
     args = ap.parse_args()
     from test_gpu_train import _make_trainable, c5_batch
 
     from aonerf import train, train_art
     batch, _, _ = c5_batch(seed=12)
     train.PRECISION = args.precision
-    train.OVERLAP_DWEIGHT = not args.no_overlap
+    if args.overlap is not None:
+        train.OVERLAP_DWEIGHT = bool(args.overlap)
     if args.art:
         from test_gpu_art_train import _make
         train_art.PRECISION, train_art.BF16_TRUNK = args.precision, args.trunk
@@ -56,7 +58,7 @@ def main():
         step()
     torch.cuda.synchronize()
     print(f"{'art' if args.art else 'vanilla'} {args.precision}{' trunk' if args.trunk else ''}: "
-          f"{' no-overlap' if args.no_overlap else ''}: "
+          f"{' overlap' if train.OVERLAP_DWEIGHT else ''}: "
           f"{1e3 * (time.perf_counter() - t0) / args.steps:.3f} ms/step", flush=True)
 
 
