@@ -93,21 +93,83 @@ struct EncBwd {
   __device__ __forceinline__ void put_pk(int, int, int, int, uint32_t) const {}
 };
 
+// The bf16 chain at 32 samples per wave (NCOL = 2): the same two policies with the skip layer's
+// enc-column values parked in registers (16 floats per sample column) instead of LDS -- the
+// LDS-DMA ring and the bias table leave no room for twice the lane-private slots.  Same values,
+// same arithmetic per sample (bit-identical to NCOL = 1).
+template <int NCOL>
+struct EncStashReg {
+  static constexpr bool kPkEpi = false;
+  mutable float v[NCOL][4][4];  // [column][tile t = 2 pr + uu][reg r]
+  __device__ __forceinline__ void begin_pair(int) const {}
+  __device__ __forceinline__ float post(int pr, int uu, int r, int c, float x) const {
+    v[c][2 * pr + uu][r] = x;
+    return x;
+  }
+  __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
+  __device__ __forceinline__ void put_pk(int, int, int, int, uint32_t) const {}
+};
+template <int NCOL>
+struct EncBwdReg {
+  static constexpr bool kPkEpi = false;
+  const EncStashReg<NCOL>* park;
+  float x[NCOL][3];  // x' of each column's sample
+  int g;
+  mutable float dx[NCOL][3];
+  __device__ __forceinline__ void begin_pair(int) const {}
+  __device__ __forceinline__ float post(int pr, int uu, int r, int c, float v) const {
+    const int t = 2 * pr + uu;
+    const float tot = __fadd_rn(park->v[c][t][r], v);
+    const int f = 16 * t + 4 * g + r;
+    float a = 0.f;
+    int comp;
+    if (f < 3) {
+      a = tot;
+      comp = f;
+    } else if (f < 63) {
+      const bool cosine = f >= 33;
+      const int q = cosine ? f - 33 : f - 3;
+      const int d = q / 3;
+      comp = q - 3 * d;
+      const float sc = __builtin_ldexpf(1.0f, d);
+      const float xc = comp == 0 ? x[c][0] : (comp == 1 ? x[c][1] : x[c][2]);
+      const float xb = __fmul_rn(xc, sc);  // exact
+      a = __fmul_rn(__fmul_rn(tot, cosf(cosine ? __fadd_rn(xb, kHalfPi) : xb)), sc);
+    } else {
+      comp = 3;  // padding row
+    }
+    dx[c][0] = comp == 0 ? __fadd_rn(dx[c][0], a) : dx[c][0];
+    dx[c][1] = comp == 1 ? __fadd_rn(dx[c][1], a) : dx[c][1];
+    dx[c][2] = comp == 2 ? __fadd_rn(dx[c][2], a) : dx[c][2];
+    return v;
+  }
+  __device__ __forceinline__ void put(int, int, int, int, float, float) const {}
+  __device__ __forceinline__ void put_pk(int, int, int, int, uint32_t) const {}
+};
+
+#ifndef AON_BF_NCOL_ART_BWD
+#define AON_BF_NCOL_ART_BWD 2  // samples per wave / 16 of the bf16 articulated chain (1: A/B)
+#endif
+constexpr int kBfNcolArtBwd = AON_BF_NCOL_ART_BWD;
+template <bool BF>
+using ArtBwdGeom = GeomH<BF ? kBfNcolArtBwd : 1, BF>;
+
 // BF: the bf16 training mode -- the whole chain one bf16 MFMA per product on the compact stream
 // (the deformation branch too: only its forward needs fp16x3, for x'), every dZ stored as bf16
 // (ArtBwdArgs' dzv / dbot / dz / dzd then address bf16 arrays); dL/dx' stays fp32.
 template <bool BF = false>
-__global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
+__global__ __launch_bounds__(ArtBwdGeom<BF>::kThreads, 2) void k_mlp_art_bwd_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, ArtBwdArgs a) {
-  constexpr int NCOL = 1;
-  using G = GeomH<NCOL>;
+  constexpr int NCOL = BF ? kBfNcolArtBwd : 1;
+  constexpr bool kRegPark = NCOL > 1;  // enc-column values and d sigma kept in registers
+  using G = ArtBwdGeom<BF>;
   using Net = NetArtBwdH;
   using T = typename std::conditional<BF, __bf16, float>::type;
   T* const dzv = reinterpret_cast<T*>(a.dzv);
   T* const dz = reinterpret_cast<T*>(a.dz);
   T* const dzd = reinterpret_cast<T*>(a.dzd);
-  // per lane: d raw_sigma fragment (hi, lo) + 4 f4 of parked skip-enc gradients
-  constexpr int kSlots = 6;
+  // per lane: d raw_sigma fragment (hi, lo) + 4 f4 of parked skip-enc gradients (NCOL = 1)
+  constexpr int kSlots = kRegPark ? 0 : 6;
   __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + G::kWaves * 64 * kSlots];
   float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
   f4* stash = smem + kLdsWeights + Net::kBiasFloats / 4 + (threadIdx.x >> 6) * 64 * kSlots +
@@ -129,11 +191,13 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   const float inv = 1.0f / s;  // exact: a power of two
 
   Frag<1, NCOL> drgb, dsig;
-  int64_t rows[NCOL];
-  const int64_t row = (int64_t)blockIdx.x * G::kRowsPerBlock + wave * G::kRowsPerWave + j;
-  rows[0] = row;
-  const int64_t rr = row < N ? row : N - 1;
-  {
+  int64_t rows[NCOL], rrs[NCOL];
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    const int64_t row = (int64_t)blockIdx.x * G::kRowsPerBlock + wave * G::kRowsPerWave + 16 * c + j;
+    rows[c] = row;
+    const int64_t rr = row < N ? row : N - 1;
+    rrs[c] = rr;
     const f4 d = *reinterpret_cast<const f4*>(a.draw + 4 * rr);
     float dv[8], sv[8];
 #pragma unroll
@@ -141,8 +205,10 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
       dv[e] = (g == 0 && e < 3) ? d[e < 3 ? e : 0] * s : 0.f;
       sv[e] = (g == 0 && e == 0) ? d[3] * s : 0.f;
     }
-    split8<BF>(dv, drgb.hi[0][0], drgb.lo[0][0], drgb.ovf);
-    split8<BF>(sv, dsig.hi[0][0], dsig.lo[0][0], dsig.ovf);
+    split8<BF>(dv, drgb.hi[0][c], drgb.lo[0][c], drgb.ovf);
+    split8<BF>(sv, dsig.hi[0][c], dsig.lo[0][c], dsig.ovf);
+  }
+  if (!kRegPark) {
     stash[0] = __builtin_bit_cast(f4, dsig.hi[0][0]);
     stash[64] = __builtin_bit_cast(f4, dsig.lo[0][0]);
   }
@@ -167,14 +233,19 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   // d bottleneck = W_view0[:, :256]^T dZ_view0 (linear layer: no mask)
   {
     RowStore<NCOL, T> st;
-    st.ok[0] = keep_row(row, N);
-    st.rowp[0] = reinterpret_cast<T*>(a.dbot) + act_base(row, 256, g);
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+      st.ok[c] = keep_row(rows[c], N);
+      st.rowp[c] = reinterpret_cast<T*>(a.dbot) + act_base(rows[c], 256, g);
+    }
     st.off16 = st16_off(g);
     st.s = inv;
     layer_h<Net, AB_V0, false>(fp, y, none, x, bias_l, g, st);
   }
-  dsig.hi[0][0] = __builtin_bit_cast(h8, stash[0]);
-  dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
+  if (!kRegPark) {
+    dsig.hi[0][0] = __builtin_bit_cast(h8, stash[0]);
+    dsig.lo[0][0] = __builtin_bit_cast(h8, stash[64]);
+  }
   // d h7 = W_bot^T d bottleneck + W_den^T d sigma, * ReLU'(h7) -> dZ_7
   layer_h<Net, AB_BOTDEN, false>(fp, x, dsig, y, bias_l, g,
                                  mask_bits(a.masks + 11 * ms, dz + 7 * hs, 256, rows, N, g, inv));
@@ -187,7 +258,11 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   layer_h<Net, AB_P5, false>(fp, y, none, x, bias_l, g,
                              mask_bits(a.masks + 8 * ms, dz + 4 * hs, 256, rows, N, g, inv));
   float* slot = reinterpret_cast<float*>(stash + 2 * 64);
-  layer_h<Net, AB_P5E, false>(fp, y, none, junk, bias_l, g, EncStash{slot});
+  EncStashReg<NCOL> park;
+  if constexpr (kRegPark)
+    layer_h<Net, AB_P5E, false>(fp, y, none, junk, bias_l, g, park);
+  else
+    layer_h<Net, AB_P5E, false>(fp, y, none, junk, bias_l, g, EncStash{slot});
   layer_h<Net, AB_P4, false>(fp, x, none, y, bias_l, g,
                              mask_bits(a.masks + 7 * ms, dz + 3 * hs, 256, rows, N, g, inv));
   layer_h<Net, AB_P3, false>(fp, y, none, x, bias_l, g,
@@ -197,46 +272,71 @@ __global__ __launch_bounds__(GeomH<1>::kThreads, 2) void k_mlp_art_bwd_f16x3(
   layer_h<Net, AB_P1, false>(fp, y, none, x, bias_l, g,
                              mask_bits(a.masks + 4 * ms, dz, 256, rows, N, g, inv));
   // d enc = W_0[:, :63]^T dZ_0 + the parked skip part, and pos_enc's backward (:205-212)
-  EncBwd eb;
-  eb.slot = slot;
-  eb.x0 = a.enc[63 * rr];
-  eb.x1 = a.enc[63 * rr + 1];
-  eb.x2 = a.enc[63 * rr + 2];
-  eb.g = g;
-  layer_h<Net, AB_P0E, false>(fp, x, none, junk, bias_l, g, eb);
-  float dx[3] = {eb.dx0, eb.dx1, eb.dx2};
+  float dx[NCOL][3];
+  if constexpr (kRegPark) {
+    EncBwdReg<NCOL> eb;
+    eb.park = &park;
+    eb.g = g;
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    dx[q] = __fadd_rn(dx[q], __shfl_xor(dx[q], 16, 64));
-    dx[q] = __fadd_rn(dx[q], __shfl_xor(dx[q], 32, 64));
-    dx[q] *= inv;  // true dL/dx' (identical in the sample's four lane groups)
-  }
-  if (g == 0 && row < N) {
+    for (int c = 0; c < NCOL; ++c)
 #pragma unroll
-    for (int q = 0; q < 3; ++q) a.dxp[3 * row + q] = dx[q];
+      for (int q = 0; q < 3; ++q) {
+        eb.x[c][q] = a.enc[63 * rrs[c] + q];
+        eb.dx[c][q] = 0.f;
+      }
+    layer_h<Net, AB_P0E, false>(fp, x, none, junk, bias_l, g, eb);
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) dx[c][q] = eb.dx[c][q];
+  } else {
+    EncBwd eb;
+    eb.slot = slot;
+    eb.x0 = a.enc[63 * rrs[0]];
+    eb.x1 = a.enc[63 * rrs[0] + 1];
+    eb.x2 = a.enc[63 * rrs[0] + 2];
+    eb.g = g;
+    layer_h<Net, AB_P0E, false>(fp, x, none, junk, bias_l, g, eb);
+    dx[0][0] = eb.dx0;
+    dx[0][1] = eb.dx1;
+    dx[0][2] = eb.dx2;
   }
-  // dL/dx' carries pos_enc's 2^d factors: back into fp16 at this sample's own scale
-  const float sd = BF ? 1.0f : grad_scale(__float_as_uint(fmaxf(fabsf(dx[0]), fmaxf(fabsf(dx[1]), fabsf(dx[2])))));
-  const float invd = 1.0f / sd;
   Frag<1, NCOL> ddx;
-  {
+  float invd[NCOL];
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      dx[c][q] = __fadd_rn(dx[c][q], __shfl_xor(dx[c][q], 16, 64));
+      dx[c][q] = __fadd_rn(dx[c][q], __shfl_xor(dx[c][q], 32, 64));
+      dx[c][q] *= inv;  // true dL/dx' (identical in the sample's four lane groups)
+    }
+    if (g == 0 && rows[c] < N) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a.dxp[3 * rows[c] + q] = dx[c][q];
+    }
+    // dL/dx' carries pos_enc's 2^d factors: back into fp16 at this sample's own scale
+    const float sd = BF ? 1.0f : grad_scale(__float_as_uint(fmaxf(fabsf(dx[c][0]), fmaxf(fabsf(dx[c][1]), fabsf(dx[c][2])))));
+    invd[c] = 1.0f / sd;
     float dv[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? dx[e < 3 ? e : 0] * sd : 0.f;
-    split8<BF>(dv, ddx.hi[0][0], ddx.lo[0][0], ddx.ovf);
+    for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? dx[c][e < 3 ? e : 0] * sd : 0.f;
+    split8<BF>(dv, ddx.hi[0][c], ddx.lo[0][c], ddx.ovf);
   }
+  // (the fp16x3 chain's per-sample scale: one column; the bf16 chain runs unscaled, invd = 1)
+  const float invd0 = invd[0];
   // deformation head and MLP: d hd3 = W_dl^T dL/dx', then deformations_linear.3 .. 1
   layer_h<Net, AB_DL, false>(fp, none, ddx, y, bias_l, g,
-                             mask_bits(a.masks + 3 * ms, dzd + 3 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 3 * ms, dzd + 3 * ws, 128, rows, N, g, invd0));
   layer_h<Net, AB_D3, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 2 * ms, dzd + 2 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 2 * ms, dzd + 2 * ws, 128, rows, N, g, invd0));
   layer_h<Net, AB_D2, false>(fp, x, none, y, bias_l, g,
-                             mask_bits(a.masks + 1 * ms, dzd + 1 * ws, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 1 * ms, dzd + 1 * ws, 128, rows, N, g, invd0));
   // (the last layer's outputs are only stored, the enc-column layers' fragments are consumed in
   // their epilogues: neither fp16 split is used, so neither is range-checked)
   const uint64_t used_ovf = ovf_of(x) | ovf_of(y) | drgb.ovf | dsig.ovf | ddx.ovf;
   layer_h<Net, AB_D1, false>(fp, y, none, x, bias_l, g,
-                             mask_bits(a.masks + 0 * ms, dzd, 128, rows, N, g, invd));
+                             mask_bits(a.masks + 0 * ms, dzd, 128, rows, N, g, invd0));
   range_report(bias_g + Net::kBiasFloats, used_ovf);
 }
 
@@ -302,8 +402,8 @@ static int art_bwd(const void* packed, const float* draw, const uint32_t* masks,
                   aligned16(dbot) && aligned16(dz) && aligned16(dzd),
               "buffers must be 16-byte aligned");
   if (N == 0) return 0;
-  using G = GeomH<1>;
-  const int64_t grid = (N + G::kRowsPerBlock - 1) / G::kRowsPerBlock;
+  const int64_t rpb = bf16 ? ArtBwdGeom<true>::kRowsPerBlock : ArtBwdGeom<false>::kRowsPerBlock;
+  const int64_t grid = (N + rpb - 1) / rpb;
   AON_REQUIRE(grid < (1ll << 31), "too many rows");
   hipStream_t st = (hipStream_t)stream;
   uint32_t* amax = static_cast<uint32_t*>(work);
@@ -316,9 +416,11 @@ static int art_bwd(const void* packed, const float* draw, const uint32_t* masks,
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtBwdH::kStreamBytes);
   if (bf16)
-    hipLaunchKernelGGL(k_mlp_art_bwd_f16x3<true>, (unsigned)grid, G::kThreads, 0, st, wsp, bias, args);
+    hipLaunchKernelGGL(k_mlp_art_bwd_f16x3<true>, (unsigned)grid, ArtBwdGeom<true>::kThreads, 0, st,
+                       wsp, bias, args);
   else
-    hipLaunchKernelGGL(k_mlp_art_bwd_f16x3<false>, (unsigned)grid, G::kThreads, 0, st, wsp, bias, args);
+    hipLaunchKernelGGL(k_mlp_art_bwd_f16x3<false>, (unsigned)grid, ArtBwdGeom<false>::kThreads, 0,
+                       st, wsp, bias, args);
   return launch_status(bf16 ? "aon_mlp_art_bwd_bf16" : "aon_mlp_art_bwd");
 }
 
