@@ -291,26 +291,75 @@ struct AdamTable {
   const float* g[AON_ADAM_MAX_TENSORS];
   float* m[AON_ADAM_MAX_TENSORS];
   float* v[AON_ADAM_MAX_TENSORS];
-  int64_t start[AON_ADAM_MAX_TENSORS + 1];  // prefix offsets of numel
+  int64_t start[AON_ADAM_MAX_TENSORS + 1];  // prefix offsets of numel (k_adam4: of 4-element chunks)
+  int64_t numel[AON_ADAM_MAX_TENSORS];
   int count;
 };
 
-__global__ void k_adam(AdamTable t, float step_size, float one_minus_b1, float b2,
-                       float one_minus_b2, float eps, float bc2_sqrt) {
+struct AdamScalars {
+  float step_size, one_minus_b1, b2, one_minus_b2, eps, bc2_sqrt;
+};
+
+__device__ __forceinline__ void adam_update(const AdamScalars& c, float g, float& p, float& m,
+                                            float& v) {
+  m = __fadd_rn(m, __fmul_rn(c.one_minus_b1, __fsub_rn(g, m)));
+  v = __fadd_rn(__fmul_rn(v, c.b2), __fmul_rn(__fmul_rn(c.one_minus_b2, g), g));
+  const float denom = __fadd_rn(__fdiv_rn(sqrtf(v), c.bc2_sqrt), c.eps);
+  p = __fsub_rn(p, __fmul_rn(c.step_size, __fdiv_rn(m, denom)));
+}
+
+__global__ void k_adam(AdamTable t, AdamScalars c) {
   const int64_t total = t.start[t.count];
   int k = 0;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     while (e >= t.start[k + 1]) ++k;
     const int64_t i = e - t.start[k];
-    const float g = t.g[k][i];
-    float m = t.m[k][i], v = t.v[k][i];
-    m = __fadd_rn(m, __fmul_rn(one_minus_b1, __fsub_rn(g, m)));
-    v = __fadd_rn(__fmul_rn(v, b2), __fmul_rn(__fmul_rn(one_minus_b2, g), g));
-    const float denom = __fadd_rn(__fdiv_rn(sqrtf(v), bc2_sqrt), eps);
-    t.p[k][i] = __fsub_rn(t.p[k][i], __fmul_rn(step_size, __fdiv_rn(m, denom)));
+    float p = t.p[k][i], m = t.m[k][i], v = t.v[k][i];
+    adam_update(c, t.g[k][i], p, m, v);
+    t.p[k][i] = p;
     t.m[k][i] = m;
     t.v[k][i] = v;
+  }
+}
+
+// The same update 4 elements per thread with 16-B loads and stores (every pointer 16-B aligned):
+// t.start holds each tensor's first 4-element chunk, a tensor's last chunk runs its tail
+// element by element.  One launch over ~1.2 M parameters was 28 us at one scalar element per
+// thread (7 dependent 4-B accesses each, a linear search of the table per element).
+__global__ void k_adam4(AdamTable t, AdamScalars c) {
+  const int64_t chunks = t.start[t.count];
+  int k = 0;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < chunks;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    while (q >= t.start[k + 1]) ++k;
+    const int64_t i = 4 * (q - t.start[k]);
+    const int64_t n = t.numel[k];
+    if (i + 4 <= n) {
+      const f4 p4 = *reinterpret_cast<const f4*>(t.p[k] + i);
+      const f4 m4 = *reinterpret_cast<const f4*>(t.m[k] + i);
+      const f4 v4 = *reinterpret_cast<const f4*>(t.v[k] + i);
+      const f4 g4 = *reinterpret_cast<const f4*>(t.g[k] + i);
+      float p[4], m[4], v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        p[u] = p4[u];
+        m[u] = m4[u];
+        v[u] = v4[u];
+        adam_update(c, g4[u], p[u], m[u], v[u]);
+      }
+      *reinterpret_cast<f4*>(t.p[k] + i) = f4{p[0], p[1], p[2], p[3]};
+      *reinterpret_cast<f4*>(t.m[k] + i) = f4{m[0], m[1], m[2], m[3]};
+      *reinterpret_cast<f4*>(t.v[k] + i) = f4{v[0], v[1], v[2], v[3]};
+    } else {
+      for (int64_t e = i; e < n; ++e) {
+        float p = t.p[k][e], m = t.m[k][e], v = t.v[k][e];
+        adam_update(c, t.g[k][e], p, m, v);
+        t.p[k][e] = p;
+        t.m[k][e] = m;
+        t.v[k][e] = v;
+      }
+    }
   }
 }
 
@@ -423,15 +472,24 @@ extern "C" int aon_adam_step(const aon_adam_tensor* tensors, int count, double l
     t.m[i] = tensors[i].exp_avg;
     t.v[i] = tensors[i].exp_avg_sq;
     t.start[i + 1] = t.start[i] + tensors[i].numel;
+    t.numel[i] = tensors[i].numel;
   }
   if (t.start[count] == 0) return 0;
+  bool vec = true;  // every tensor 16-B aligned: k_adam4
+  for (int i = 0; i < count; ++i)
+    vec = vec && aligned16(t.p[i]) && aligned16(t.g[i]) && aligned16(t.m[i]) && aligned16(t.v[i]);
   // Every scalar is formed in double from the Python-float hyperparameters, as torch.optim.Adam
   // does (lerp weight 1 - beta1, addcmul value 1 - beta2, step size lr / bc1, sqrt(bc2)), and
   // only then rounded to fp32 where it meets the fp32 tensors.
   const double bc1 = 1.0 - std::pow(beta1, (double)step);
   const double bc2 = 1.0 - std::pow(beta2, (double)step);
-  hipLaunchKernelGGL(k_adam, grid_for(t.start[count], 256, 4096), 256, 0, (hipStream_t)stream, t,
-                     (float)(lr / bc1), (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
-                     (float)eps, (float)std::sqrt(bc2));
+  const AdamScalars c{(float)(lr / bc1), (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
+                      (float)eps, (float)std::sqrt(bc2)};
+  if (vec) {
+    for (int i = 0; i < count; ++i) t.start[i + 1] = t.start[i] + (t.numel[i] + 3) / 4;
+    hipLaunchKernelGGL(k_adam4, grid_for(t.start[count], 256, 4096), 256, 0, (hipStream_t)stream, t, c);
+  } else {
+    hipLaunchKernelGGL(k_adam, grid_for(t.start[count], 256, 4096), 256, 0, (hipStream_t)stream, t, c);
+  }
   return launch_status(__func__);
 }

@@ -380,6 +380,36 @@ def test_adam_matches_torch():
             assert d <= tol, (step, d, upd)
 
 
+def test_adam_vector_path_equals_scalar_path():
+    """aon_adam_step's 4-wide kernel (every tensor 16-B aligned) and its one-element kernel (any
+    misaligned tensor) give the same bits, ragged tails (numel % 4 != 0) included."""
+    from aonerf import train
+
+    g = torch.Generator(device="cuda").manual_seed(9)
+    shapes = ((256, 63), (3,), (1,), (7, 5), (128,))
+    base = [torch.randn(s, device="cuda", generator=g) for s in shapes]
+    grads = [torch.randn(s, device="cuda", generator=g) for s in shapes]
+    aligned = [b.clone().requires_grad_(True) for b in base]
+    # the same values at a 4-B offset inside a larger buffer: not 16-B aligned
+    store = [torch.empty(b.numel() + 1, device="cuda") for b in base]
+    shifted = []
+    for st, b in zip(store, base):
+        st[1:].copy_(b.reshape(-1))
+        shifted.append(st[1:].view(b.shape).requires_grad_(True))
+    assert shifted[0].data_ptr() % 16 != 0
+    oa, os_ = train.Adam(aligned, lr=1e-3), train.Adam(shifted, lr=1e-3)
+    for step in range(3):
+        for p, q, gr in zip(aligned, shifted, grads):
+            p.grad = gr * (step + 1)
+            q.grad = gr * (step + 1)
+        oa.step()
+        os_.step()
+        for p, q in zip(aligned, shifted):
+            assert torch.equal(p.detach(), q.detach())
+        for (m1, v1), (m2, v2) in zip(oa.state, os_.state):
+            assert torch.equal(m1, m2) and torch.equal(v1, v2)
+
+
 def test_render_after_adam_uses_new_weights():
     """A no_grad render packs the weights once and caches the pack by (pointer, version); the
     fused Adam updates parameters in place through raw pointers, so it must bump the versions or
