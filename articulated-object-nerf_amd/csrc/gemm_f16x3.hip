@@ -1944,8 +1944,9 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   AON_REQUIRE(a, "null args");
   AON_REQUIRE(a->A && a->B && a->C, "null operand");
   AON_REQUIRE(a->M >= 0 && a->N >= 0 && a->K >= 0, "bad shape");
-  AON_REQUIRE(a->lda >= 1 && a->ldb >= 1 && a->ldc >= (a->n_store > 0 ? a->n_store : a->N),
-              "bad leading dimension");
+  AON_REQUIRE(a->lda >= 1 && a->ldb >= 1 &&
+                  a->ldc >= (a->c_trans ? a->M : (a->n_store > 0 ? a->n_store : a->N)),
+              "bad leading dimension (c_trans: ldc >= M, C holds N rows)");
   AON_REQUIRE(!a->A2 || (a->a_kc && a->K1 >= 0 && a->K1 <= a->K && a->lda2 >= 1 && a->a2_rdiv >= 1),
               "A2 needs a_kc, 0 <= K1 <= K, lda2 >= 1, a2_rdiv >= 1");
   AON_REQUIRE(!a->mask || a->ldm >= a->N, "bad mask leading dimension");
