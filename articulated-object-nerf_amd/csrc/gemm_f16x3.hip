@@ -62,6 +62,7 @@ struct Params {
   int a_tiled, b_tiled;      // reduction-major operand in the fused training kernels' 16-row
                              // tiled layout (mlp_f16x3_core.hpp act_base; rdiv 1)
   int64_t nstore;            // columns of C written: n < nstore (a zero-padded B, bf16 mode)
+  int c_trans;               // C[n * ldc + m]; rowsum = column sums of B (skinny path, aon_gemm_args)
 };
 
 // start of the 4-element run (k, row .. row + 3) of a reduction-major operand (row % 4 == 0):
@@ -408,7 +409,8 @@ __device__ __forceinline__ void reduce_body(const Params& p, int splits) {
   static_assert(L == 4 || L == 16, "lanes per output");
   constexpr int kSh = L == 4 ? 2 : 4;
   const int64_t total = p.M * p.N;
-  const int64_t extra = p.rowsum ? p.M : 0;  // rowsum entries ride along as e >= total
+  const int64_t nrs = p.c_trans ? p.N : p.M;  // rowsum entries: row sums of A, or B's column sums
+  const int64_t extra = p.rowsum ? nrs : 0;   // they ride along as e >= total
   const int q = threadIdx.x & (L - 1);
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
   auto sum = [&](const float* src, int64_t stride) {
@@ -421,14 +423,14 @@ __device__ __forceinline__ void reduce_body(const Params& p, int splits) {
     const int64_t e = eL >> kSh;
     if (e >= total) {
       const int64_t m = e - total;
-      const float v = sum(p.rowsum_part + m, p.M);
+      const float v = sum(p.rowsum_part + m, nrs);
       if (q == 0) p.rowsum[m] = v;
       continue;
     }
     const int64_t m = e / p.N, n = e - m * p.N;
     float v = sum(p.part + e, total);
     if (q != 0 || n >= p.nstore) continue;
-    float* c = p.C + m * p.ldc + n;
+    float* c = p.C + (p.c_trans ? n * p.ldc + m : m * p.ldc + n);
     if (p.accumulate) v = __fadd_rn(*c, v);
     if (p.bias) v = __fadd_rn(v, p.bias[n]);
     if (p.relu) v = fmaxf(v, 0.0f);
@@ -1598,7 +1600,10 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
   const TA* A = reinterpret_cast<const TA*>(p.A);
   const __bf16* B = reinterpret_cast<const __bf16*>(p.B);
-  float acc[M][8], rs[M];
+  float acc[M][8], rs[M], cs[8];  // cs: B's column sums (c_trans)
+  const bool ct = p.c_trans != 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[j] = 0.f;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     rs[m] = 0.f;
@@ -1614,6 +1619,10 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
     float b[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) b[j] = __uint_as_float((j & 1) ? (bw[j >> 1] & 0xffff0000u) : (bw[j >> 1] << 16));
+    if (ct) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[j] = __fadd_rn(cs[j], b[j]);
+    }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const float a = static_cast<float>(static_cast<__bf16>(static_cast<float>(ar[m])));
@@ -1647,19 +1656,31 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
   }
   // the 16 row phases of a column group are lanes 16 q .. 16 q + 15 of one wave
 #pragma unroll
-  for (int sh = 1; sh < 16; sh <<= 1)
+  for (int sh = 1; sh < 16; sh <<= 1) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       rs[m] = __fadd_rn(rs[m], __shfl_xor(rs[m], sh, 64));
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[m][j] = __fadd_rn(acc[m][j], __shfl_xor(acc[m][j], sh, 64));
     }
+    if (ct) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[j] = __fadd_rn(cs[j], __shfl_xor(cs[j], sh, 64));
+    }
+  }
   if (r != 0) return;
   const bool split = p.zsplit > 1;
   const int z = blockIdx.x;
+  if (ct && p.rowsum) {  // B's column sums: columns n0 .. n0 + 7 of this column group
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (split) p.rowsum_part[(int64_t)z * p.N + n0 + j] = cs[j];
+      else p.rowsum[n0 + j] = cs[j];
+    }
+  }
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    if (p.rowsum && cg == 0) {
+    if (!ct && p.rowsum && cg == 0) {
       if (split) p.rowsum_part[(int64_t)z * p.M + m] = rs[m];
       else p.rowsum[m] = rs[m];
     }
@@ -1670,7 +1691,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
         p.part[((int64_t)z * p.M + m) * p.N + n0 + j] = v;
         continue;
       }
-      float* c = p.C + m * p.ldc + n0 + j;
+      float* c = p.C + (ct ? (n0 + j) * p.ldc + m : m * p.ldc + n0 + j);
       if (p.accumulate) v = __fadd_rn(*c, v);
       *c = v;
     }
@@ -1936,7 +1957,7 @@ static int64_t gemm_splits(const aon_gemm_args* a) {
 extern "C" size_t aon_gemm_workspace_bytes(const aon_gemm_args* a) {
   if (!a) return 0;
   const int64_t s = gemm_splits(a);
-  return s > 1 ? (size_t)s * (a->M * a->N + a->M) * sizeof(float) : 0;
+  return s > 1 ? (size_t)s * (a->M * a->N + (a->c_trans ? a->N : a->M)) * sizeof(float) : 0;
 }
 
 extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
@@ -1972,7 +1993,9 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
               "n_store < N: the bf16 LDS-DMA weight-gradient path only (both operands bf16, "
               "M and N multiples of 128)");
   if (a->M == 0 || a->N == 0) return 0;
+  AON_REQUIRE(!a->c_trans || skinny_path(a), "c_trans: the bf16 skinny path only (M <= 4, B bf16)");
   Params p;
+  p.c_trans = a->c_trans;
   p.a_tiled = a->a_tiled;
   p.b_tiled = a->b_tiled;
   p.nstore = a->n_store > 0 ? a->n_store : a->N;
@@ -1996,7 +2019,7 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   p.rowsum = a->rowsum;
   p.rowsum_part = nullptr;
   if (zs > 1) {
-    AON_REQUIRE(work && work_bytes >= (size_t)zs * (a->M * a->N + a->M) * sizeof(float),
+    AON_REQUIRE(work && work_bytes >= (size_t)zs * (a->M * a->N + (a->c_trans ? a->N : a->M)) * sizeof(float),
                 "split-K needs aon_gemm_workspace_bytes() of workspace");
     p.part = static_cast<float*>(work);
     p.rowsum_part = p.part + zs * a->M * a->N;
@@ -2065,7 +2088,7 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   if (zs > 1) {
     const int rc = launch_status(__func__);
     if (rc) return rc;
-    const int64_t outs = a->M * a->N + a->M;
+    const int64_t outs = a->M * a->N + (a->c_trans ? a->N : a->M);
     if (AON_GEMM_REDUCE16 && outs <= 4096)  // a few hundred outputs: 16 lanes each (sum_z16)
       hipLaunchKernelGGL(k_gemm_reduce<16>, grid_for(16 * outs, 256, 16384), 256, 0, st, p, (int)zs);
     else

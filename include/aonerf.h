@@ -420,6 +420,11 @@ typedef struct aon_gemm_args {
    * a_amax / tiled operands): the bf16 training mode's latent-code terms, which the 128 x 128
    * tiled kernel ran at 17-27 us each */
   int exact_fp32;
+  /* c_trans = 1: C is written transposed -- element (m, n) of the product at C[n * ldc + m] --
+   * and rowsum receives the column sums of B (N entries, in B's element type rounded as staged)
+   * instead of the row sums of A: dW of a layer whose input has <= 4 columns, computed as the
+   * skinny product (input)^T dZ.  The bf16 skinny path only (mma_bf16, M <= 4, B bf16). */
+  int c_trans;
 } aon_gemm_args;
 
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);

@@ -254,6 +254,33 @@ def test_bf16_skinny_weight_gradient(K, M, N, a_off, b_tiled):
                                atol=2e-5 * float(a64.abs().sum(0).max()))
 
 
+@pytest.mark.parametrize("K", [790528, 266240, 70001, 5])
+def test_bf16_skinny_transposed_weight_gradient(K):
+    """aon_gemm c_trans (the articulated bf16 step's deformations_linear.0 xyz columns): dW[:, 0:3]
+    = (xyz^T dZ)^T written transposed into the wider dW, and the bias = dZ's column sums, on the
+    tiled bf16 dZ -- against fp64 of the bf16-rounded operands; the other columns of dW untouched."""
+    from aonerf import tiles
+    from aonerf.linalg import gemm
+
+    g = torch.Generator(device="cuda").manual_seed(K)
+    xyz = torch.randn((K, 3), device="cuda", generator=g) * 2
+    dz = (torch.randn((K, 128), device="cuda", generator=g) * 1e-3).to(torch.bfloat16)
+    dW = torch.full((128, 40), 7.0, device="cuda")
+    db = torch.empty((128,), device="cuda")
+    gemm(dW, xyz, tiles.tile(dz), 3, 128, K, lda=3, a_kc=False, ldb=128, b_kc=False,
+         ldc=dW.stride(0), rowsum=db, mma_bf16=True, b_tiled=True, c_trans=True)
+    torch.cuda.synchronize()
+    a64 = bf16_round(xyz.cpu())
+    want = (a64.T @ dz.cpu().double()).T  # (128, 3)
+    err = rel_err(dW[:, :3].cpu().numpy(), want.numpy())
+    print(f"bf16 transposed skinny dW K={K}: max-rel err {err:.2e}")
+    assert err < 2e-5
+    assert bool((dW[:, 3:] == 7.0).all())
+    cs = dz.cpu().double().sum(0)
+    np.testing.assert_allclose(db.cpu().numpy(), cs.numpy(), rtol=0,
+                               atol=2e-5 * float(dz.cpu().double().abs().sum(0).max()))
+
+
 @pytest.mark.parametrize("K,rdiv,a_tiled,a_bf", [(4096 * 193, 193, True, True),
                                                   (2000, 33, False, True),
                                                   (29 * 65, 65, True, False)])
