@@ -22,15 +22,111 @@ ACT_NONE, ACT_VANILLA, ACT_ARTIC = 0, 1, 2
 class AonMlpParams(ctypes.Structure):
     _fields_ = [("pts_w", vp * 8), ("pts_b", vp * 8), ("density_w", vp), ("density_b", vp),
                 ("bottleneck_w", vp), ("bottleneck_b", vp), ("views_w", vp), ("views_b", vp),
-                ("rgb_w", vp), ("rgb_b", vp)]
+                ("rgb_w", vp), ("rgb_b", vp), ("w_rows", c_i64 * 12), ("w_cols", c_i64 * 12),
+                ("b_len", c_i64 * 12)]
 
 
 class AonMlpArtParams(ctypes.Structure):
     _fields_ = [("def_w", vp * 4), ("def_b", vp * 4), ("deformation_w", vp), ("deformation_b", vp),
                 ("pts_w", vp * 8), ("pts_b", vp * 8), ("density_w", vp), ("density_b", vp),
                 ("bottleneck_w", vp), ("bottleneck_b", vp), ("views_w", vp * 4),
-                ("views_b", vp * 4), ("rgb_w", vp), ("rgb_b", vp), ("ld_def0", c_i64),
-                ("ld_pts0", c_i64), ("ld_pts5", c_i64), ("ld_view0", c_i64)]
+                ("views_b", vp * 4), ("rgb_w", vp), ("rgb_b", vp), ("w_rows", c_i64 * 20),
+                ("w_cols", c_i64 * 20), ("b_len", c_i64 * 20)]
+
+
+# [out][in] of each layer in the kernels' layer order (= the order of the struct fields):
+# reference model.py:39-93 (vanilla) and model_autodecoder.py:60-166 (articulated, whose four
+# latent-carrying layers may be wider: their latent columns are folded into the bias)
+MLP_LAYERS = (["pts_linears.%d" % i for i in range(8)] +
+              ["density_layer", "bottleneck_layer", "views_linear.0", "rgb_layer"])
+MLP_SHAPES = [(256, 63)] + [(256, 256)] * 4 + [(256, 319)] + [(256, 256)] * 2 + \
+    [(1, 256), (256, 256), (128, 283), (3, 128)]
+ART_LAYERS = (["deformations_linear.%d" % i for i in range(4)] + ["deformation_layer"] +
+              ["pts_linears.%d" % i for i in range(8)] + ["density_layer", "bottleneck_layer"] +
+              ["views_linear.%d" % i for i in range(4)] + ["rgb_layer"])
+ART_SHAPES = [(128, 3)] + [(128, 128)] * 3 + [(3, 128), (256, 63)] + [(256, 256)] * 4 + \
+    [(256, 319)] + [(256, 256)] * 2 + [(1, 256), (256, 256), (128, 283)] + [(128, 128)] * 3 + \
+    [(3, 128)]
+ART_LATENT = {0, 5, 10, 15}  # deformations_linear.0, pts_linears.0 / .5, views_linear.0
+
+
+def _check_layers(pairs, names, shapes, latent=()):
+    """Raise ValueError unless ``pairs`` = [(weight, bias)] matches the layer table: count,
+    order (by shape), dtype, device and contiguity -- BEFORE any pointer reaches a kernel."""
+    if len(pairs) != len(names):
+        raise ValueError(f"expected {len(names)} (weight, bias) pairs in the kernels' layer order "
+                         f"({', '.join(names)}), got {len(pairs)}")
+    for i, ((w, b), name, (out, inp)) in enumerate(zip(pairs, names, shapes)):
+        if not (isinstance(w, torch.Tensor) and isinstance(b, torch.Tensor)):
+            raise ValueError(f"{name}: (weight, bias) must be tensors")
+        ok_w = (w.dim() == 2 and w.shape[0] == out and
+                (w.shape[1] >= inp if i in latent else w.shape[1] == inp))
+        if not ok_w or tuple(b.shape) != (out,):
+            raise ValueError(f"{name}: weight {tuple(w.shape)}, bias {tuple(b.shape)}; expected "
+                             f"weight ({out}, {'>=' if i in latent else ''}{inp}), bias ({out},) "
+                             "-- parameters must come in the kernels' layer order "
+                             f"({', '.join(names)}), not nn.Module registration order")
+    dev = pairs[0][0].device
+    for (w, b), name in zip(pairs, names):
+        for t, what in ((w, "weight"), (b, "bias")):
+            if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"{name}.{what}: needs a contiguous float32 GPU tensor, got "
+                                 f"{t.dtype} on {t.device}{'' if t.is_contiguous() else ' (strided)'}")
+            if t.device != dev:
+                raise ValueError(f"{name}.{what}: on {t.device}, the others on {dev}")
+
+
+def check_mlp_layers(pairs):
+    """ValueError unless ``pairs`` are one vanilla NeRFMLP's 12 (weight, bias) GPU tensors in the
+    kernels' layer order (as mlp_params checks them)."""
+    _check_layers([tuple(p) for p in pairs], MLP_LAYERS, MLP_SHAPES)
+
+
+def check_mlp_art_layers(pairs):
+    """The same for one articulated NeRFMLP's 20 pairs (mlp_art_params' order)."""
+    _check_layers([tuple(p) for p in pairs], ART_LAYERS, ART_SHAPES, ART_LATENT)
+
+
+def _fill_shapes(prm, pairs):
+    for i, (w, b) in enumerate(pairs):
+        prm.w_rows[i], prm.w_cols[i], prm.b_len[i] = w.shape[0], w.shape[1], b.numel()
+
+
+def mlp_params(pairs):
+    """AonMlpParams of one vanilla NeRFMLP: ``pairs`` = 12 (weight, bias) tensors in the order
+    pts_linears.0..7, density_layer, bottleneck_layer, views_linear.0, rgb_layer; validated
+    (ValueError) against the layer table before the struct exists."""
+    pairs = [tuple(p) for p in pairs]
+    _check_layers(pairs, MLP_LAYERS, MLP_SHAPES)
+    prm = AonMlpParams()
+    for i in range(8):
+        prm.pts_w[i], prm.pts_b[i] = pairs[i][0].data_ptr(), pairs[i][1].data_ptr()
+    for name, idx in (("density", 8), ("bottleneck", 9), ("views", 10), ("rgb", 11)):
+        setattr(prm, f"{name}_w", pairs[idx][0].data_ptr())
+        setattr(prm, f"{name}_b", pairs[idx][1].data_ptr())
+    _fill_shapes(prm, pairs)
+    return prm
+
+
+def mlp_art_params(pairs):
+    """AonMlpArtParams of one articulated NeRFMLP: ``pairs`` = 20 (weight, bias) tensors in the
+    order deformations_linear.0..3, deformation_layer, pts_linears.0..7, density_layer,
+    bottleneck_layer, views_linear.0..3, rgb_layer (the latent-carrying layers' biases folded by
+    the caller); validated (ValueError) against the layer table."""
+    pairs = [tuple(p) for p in pairs]
+    _check_layers(pairs, ART_LAYERS, ART_SHAPES, ART_LATENT)
+    prm = AonMlpArtParams()
+    for i in range(4):
+        prm.def_w[i], prm.def_b[i] = pairs[i][0].data_ptr(), pairs[i][1].data_ptr()
+        prm.views_w[i], prm.views_b[i] = pairs[15 + i][0].data_ptr(), pairs[15 + i][1].data_ptr()
+    for i in range(8):
+        prm.pts_w[i], prm.pts_b[i] = pairs[5 + i][0].data_ptr(), pairs[5 + i][1].data_ptr()
+    prm.deformation_w, prm.deformation_b = pairs[4][0].data_ptr(), pairs[4][1].data_ptr()
+    prm.density_w, prm.density_b = pairs[13][0].data_ptr(), pairs[13][1].data_ptr()
+    prm.bottleneck_w, prm.bottleneck_b = pairs[14][0].data_ptr(), pairs[14][1].data_ptr()
+    prm.rgb_w, prm.rgb_b = pairs[19][0].data_ptr(), pairs[19][1].data_ptr()
+    _fill_shapes(prm, pairs)
+    return prm
 
 
 class AonGemmArgs(ctypes.Structure):
@@ -70,7 +166,6 @@ _SIGNATURES = {
     "aon_mlp_read_status": (c_int, [vp, c_size, ctypes.POINTER(ctypes.c_uint32), vp]),
     "aon_mlp_pack": (c_int, [ctypes.POINTER(AonMlpParams), c_int, vp, vp]),
     "aon_mlp_fwd": (c_int, [vp, c_int, vp, vp, vp, vp, c_i64, c_int, c_int, vp, vp]),
-    "aon_mlp_set_dataflow": (c_int, [c_int]),
     "aon_mlp_fwd_encoded": (c_int, [vp, c_int, vp, vp, c_i64, c_int, c_int, vp, vp]),
     "aon_mlp_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp]),
     "aon_mlp_fwd_train_bf16": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp,
@@ -120,22 +215,42 @@ _SIGNATURES = {
 _lib = None
 
 
+ABI_VERSION = 9
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise ImportError(f"aonerf: HIP library not built: {path} "
+                          "(run `make -C articulated-object-nerf_amd/csrc` or __graft_entry__.build())")
+    handle = ctypes.CDLL(path)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    if handle.aon_abi_version() != ABI_VERSION:
+        raise ImportError(f"aonerf: ABI version mismatch ({path})")
+    return handle
+
+
 def lib():
     """Load libaonerf.so once; raise loudly if it is missing (no silent fallback)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"aonerf: HIP library not built: {LIB_PATH} "
-                              "(run `make -C articulated-object-nerf_amd/csrc` or __graft_entry__.build())")
-        handle = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in _SIGNATURES.items():
-            fn = getattr(handle, name)
-            fn.restype = res
-            fn.argtypes = args
-        if handle.aon_abi_version() != 8:
-            raise ImportError("aonerf: ABI version mismatch")
-        _lib = handle
+        _lib = _load(LIB_PATH)
     return _lib
+
+
+_variants = {}
+
+
+def variant(name):
+    """An A/B build of the library beside the release one (lib/variants/libaonerf_<name>.so,
+    e.g. ``make -C csrc variant-ws``): same ABI and packed formats, a different kernel behind
+    some entry points.  Test infrastructure only; the product path always uses lib()."""
+    if name not in _variants:
+        _variants[name] = _load(os.path.join(os.path.dirname(LIB_PATH), "variants",
+                                             f"libaonerf_{name}.so"))
+    return _variants[name]
 
 
 def call(name, *args):

@@ -89,13 +89,7 @@ class NeRFMLP(nn.Module):
         key = (self.precision,) + tuple((p.data_ptr(), p._version) for p in params)
         if key != self._packed_key:
             params = [L.contig(p.detach()) for p in params]
-            prm = L.AonMlpParams()
-            for i in range(8):
-                prm.pts_w[i] = params[2 * i].data_ptr()
-                prm.pts_b[i] = params[2 * i + 1].data_ptr()
-            for name, idx in (("density", 8), ("bottleneck", 9), ("views", 10), ("rgb", 11)):
-                setattr(prm, f"{name}_w", params[2 * idx].data_ptr())
-                setattr(prm, f"{name}_b", params[2 * idx + 1].data_ptr())
+            prm = L.mlp_params(zip(params[0::2], params[1::2]))  # shape-checked (ValueError)
             prec = L.PREC[self.precision]
             nbytes = L.lib().aon_mlp_packed_bytes(prec)
             if nbytes == 0:

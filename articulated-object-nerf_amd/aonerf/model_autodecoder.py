@@ -125,31 +125,17 @@ class NeRFMLP(nn.Module):
         fb = self.folded_biases(latents)
         W = lambda m: L.contig(m.weight.detach())  # noqa: E731
         b = lambda m: L.contig(m.bias.detach())  # noqa: E731
-        keep = []  # contiguous copies (if any) must live until the pack is enqueued
-
-        def ptr(t):
-            keep.append(t)
-            return t.data_ptr()
-
-        prm = L.AonMlpArtParams()
-        for i, m in enumerate(self.deformations_linear):
-            prm.def_w[i] = ptr(W(m))
-            prm.def_b[i] = ptr(fb["def0"] if i == 0 else b(m))
-        prm.deformation_w, prm.deformation_b = ptr(W(self.deformation_layer)), ptr(b(self.deformation_layer))
-        for i, m in enumerate(self.pts_linears):
-            prm.pts_w[i] = ptr(W(m))
-            prm.pts_b[i] = ptr(fb["pts0"] if i == 0 else fb["pts_skip"] if i == self.skip_layer + 1
-                               else b(m))
-        prm.density_w, prm.density_b = ptr(W(self.density_layer)), ptr(b(self.density_layer))
-        prm.bottleneck_w, prm.bottleneck_b = ptr(W(self.bottleneck_layer)), ptr(b(self.bottleneck_layer))
-        for i, m in enumerate(self.views_linear):
-            prm.views_w[i] = ptr(W(m))
-            prm.views_b[i] = ptr(fb["view0"] if i == 0 else b(m))
-        prm.rgb_w, prm.rgb_b = ptr(W(self.rgb_layer)), ptr(b(self.rgb_layer))
-        prm.ld_def0 = self.deformations_linear[0].weight.shape[1]
-        prm.ld_pts0 = self.pts_linears[0].weight.shape[1]
-        prm.ld_pts5 = self.pts_linears[self.skip_layer + 1].weight.shape[1]
-        prm.ld_view0 = self.views_linear[0].weight.shape[1]
+        # (weight, bias) in the kernels' layer order; contiguous copies (if any) live in `pairs`
+        # until the pack is enqueued
+        pairs = [(W(m), fb["def0"] if i == 0 else b(m)) for i, m in enumerate(self.deformations_linear)]
+        pairs.append((W(self.deformation_layer), b(self.deformation_layer)))
+        pairs += [(W(m), fb["pts0"] if i == 0 else fb["pts_skip"] if i == self.skip_layer + 1
+                   else b(m)) for i, m in enumerate(self.pts_linears)]
+        pairs += [(W(self.density_layer), b(self.density_layer)),
+                  (W(self.bottleneck_layer), b(self.bottleneck_layer))]
+        pairs += [(W(m), fb["view0"] if i == 0 else b(m)) for i, m in enumerate(self.views_linear)]
+        pairs.append((W(self.rgb_layer), b(self.rgb_layer)))
+        prm = L.mlp_art_params(pairs)  # shape-checked (ValueError) before the pack
         dev = self.rgb_layer.weight.device
         nbytes = L.lib().aon_mlp_art_packed_bytes()
         buf = getattr(self, "_art_packed", None)

@@ -222,13 +222,11 @@ _packed = {}
 
 
 def _params_struct(P):
-    prm = L.AonMlpParams()
-    for i in range(8):
-        prm.pts_w[i], prm.pts_b[i] = P[i][0].data_ptr(), P[i][1].data_ptr()
-    for name, idx in (("density", 8), ("bottleneck", 9), ("views", 10), ("rgb", 11)):
-        setattr(prm, f"{name}_w", P[idx][0].data_ptr())
-        setattr(prm, f"{name}_b", P[idx][1].data_ptr())
-    return prm
+    """AonMlpParams of one level's (weight, bias) pairs in the kernels' layer order (pts_linears.0
+    ..7, density, bottleneck, views_linear.0, rgb): shapes, dtype, device and contiguity are
+    checked against the layer table (ValueError) before any pointer reaches a pack kernel, and
+    the C side checks the shapes again (aon_mlp_params, ABI 9)."""
+    return L.mlp_params(P)
 
 
 def _buffer(key, nbytes, dev, guard=False, params=()):
@@ -428,6 +426,8 @@ class RenderLevel(torch.autograd.Function):
         venc = torch.empty((B, 27), device=dev)
         L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, 4, L.ptr(venc), L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
+        # the kernels' layer order, shapes, dtype and device (ValueError, before any launch)
+        L.check_mlp_layers(P)
         raw = torch.empty((R, 4), device=dev)
         masks = None  # ReLU' bits for the fused backward chain (built there when None)
         if FUSED_FORWARD:

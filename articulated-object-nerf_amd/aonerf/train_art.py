@@ -158,20 +158,11 @@ _packed = {}
 def _params_struct(P, fb=None):
     """AonMlpArtParams of one level's parameters (``fb``: folded biases by layer index)."""
     fb = fb or {}
-    b = lambda i: (fb.get(i, P[i][1])).data_ptr()  # noqa: E731
-    prm = L.AonMlpArtParams()
-    for i in range(4):
-        prm.def_w[i], prm.def_b[i] = P[DEF0 + i][0].data_ptr(), b(DEF0 + i)
-        prm.views_w[i], prm.views_b[i] = P[VIEW0 + i][0].data_ptr(), b(VIEW0 + i)
-    for i in range(8):
-        prm.pts_w[i], prm.pts_b[i] = P[PTS0 + i][0].data_ptr(), b(PTS0 + i)
-    prm.deformation_w, prm.deformation_b = P[DL][0].data_ptr(), b(DL)
-    prm.density_w, prm.density_b = P[DENS][0].data_ptr(), b(DENS)
-    prm.bottleneck_w, prm.bottleneck_b = P[BOT][0].data_ptr(), b(BOT)
-    prm.rgb_w, prm.rgb_b = P[RGB][0].data_ptr(), b(RGB)
-    prm.ld_def0, prm.ld_pts0 = P[DEF0][0].shape[1], P[PTS0][0].shape[1]
-    prm.ld_pts5, prm.ld_view0 = P[PTS0 + 5][0].shape[1], P[VIEW0][0].shape[1]
-    return prm
+    order = [DEF0 + i for i in range(4)] + [DL] + [PTS0 + i for i in range(8)] + [DENS, BOT] + \
+        [VIEW0 + i for i in range(4)] + [RGB]
+    # shape / dtype / device checked against the layer table (ValueError) before any pointer
+    # reaches a pack kernel; the C side checks the shapes again (aon_mlp_art_params, ABI 9)
+    return L.mlp_art_params([(P[i][0], fb.get(i, P[i][1])) for i in order])
 
 
 def _buffer(key, nbytes, dev, guard=False, params=()):
@@ -472,6 +463,8 @@ class ArtRenderLevel(torch.autograd.Function):
         venc = torch.empty((B, geo.nv), device=dev)
         L.call("aon_pos_enc", L.ptr(viewdirs), B, 0, geo.deg_view, L.ptr(venc), L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(20)]
+        # the kernels' layer order, shapes, dtype and device (ValueError, before any launch)
+        L.check_mlp_art_layers(P)
         raw = torch.empty((R, 4), device=dev)
         noise = L.contig(noise) if noise is not None else None
         masks = None  # ReLU' bits for the fused backward chain (built there when None)

@@ -14,6 +14,7 @@
 #include "aon_common.hpp"
 #include "mlp_layout.hpp"
 #include "mlp_pipe.hpp"
+#include "param_check.hpp"
 
 namespace aon {
 namespace mlp {
@@ -270,34 +271,12 @@ extern "C" int aon_mlp_read_status(const void* packed, size_t packed_bytes, uint
   return static_cast<int>(e);
 }
 
-static int f16x3_ncol() {
-  static int ncol = [] {
-    const char* e = getenv("AON_F16X3_NCOL");  // tuning knob: samples per wave = 16 * ncol
-    return (e && atoi(e) == 2) ? 2 : 1;
-  }();
-  return ncol;
-}
-
-// the render forward's dataflow (aon_mlp_set_dataflow; initial value from AON_MLP_WS)
-#ifndef AON_DATAFLOW_DEFAULT
-#define AON_DATAFLOW_DEFAULT AON_DATAFLOW_STREAMED
+// samples per wave of the fp16x3 render kernel = 16 x AON_F16X3_NCOL (compile-time A/B knob,
+// tools/build_variants.sh; 2 measured 3-5% slower: DESIGN.md §4)
+#ifndef AON_F16X3_NCOL
+#define AON_F16X3_NCOL 1
 #endif
-constexpr int kDefaultDataflow = AON_DATAFLOW_DEFAULT;
-static int g_dataflow = -1;
-bool aon::mlp::mlp_dataflow_ws() {
-  if (g_dataflow < 0) {
-    const char* e = getenv("AON_MLP_WS");
-    g_dataflow = e ? (atoi(e) == 1 ? AON_DATAFLOW_WS : AON_DATAFLOW_STREAMED) : kDefaultDataflow;
-  }
-  return g_dataflow == AON_DATAFLOW_WS;
-}
-
-extern "C" int aon_mlp_set_dataflow(int dataflow) {
-  AON_REQUIRE(dataflow == AON_DATAFLOW_STREAMED || dataflow == AON_DATAFLOW_WS, "bad dataflow");
-  const int prev = mlp_dataflow_ws() ? AON_DATAFLOW_WS : AON_DATAFLOW_STREAMED;
-  g_dataflow = dataflow;
-  return prev;
-}
+static_assert(AON_F16X3_NCOL == 1 || AON_F16X3_NCOL == 2, "AON_F16X3_NCOL is 1 or 2");
 
 extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* packed,
                             aon_stream_t stream) {
@@ -306,6 +285,7 @@ extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* pack
                   precision == AON_PREC_BF16,
               "unsupported precision");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
+  if (check_mlp_params(prm, __func__)) return -1;
   PackArgs a;
   for (int i = 0; i < 8; ++i) {
     a.w[i] = prm->pts_w[i];
@@ -343,10 +323,12 @@ static int mlp_launch(int mode, const void* packed, int precision, const float* 
   const int64_t N = B * S;
   if (N == 0) return 0;
   AON_REQUIRE((N + kRowsPerBlock - 1) / kRowsPerBlock < (1ll << 31), "too many rows");
-  if (precision == AON_PREC_F16X3 && mode == 0 && mlp_dataflow_ws())
+#if AON_DATAFLOW_WS_BUILD
+  if (precision == AON_PREC_F16X3 && mode == 0)
     return launch_ws_f16x3(packed, a0, a1, a2, a3, B, S, act, raw, (hipStream_t)stream);
+#endif
   if (precision == AON_PREC_F16X3)
-    return launch_f16x3(mode, f16x3_ncol(), packed, a0, a1, a2, a3, B, S, act, raw,
+    return launch_f16x3(mode, AON_F16X3_NCOL, packed, a0, a1, a2, a3, B, S, act, raw,
                         (hipStream_t)stream);
   const int grid = static_cast<int>((N + kRowsPerBlock - 1) / kRowsPerBlock);
   const f4* ws = static_cast<const f4*>(packed);

@@ -15,6 +15,7 @@
 // sample's other three lane groups with ds_bpermute, added to xyz in fp32 and encoded in
 // registers, so nothing leaves the chip between the deformation and the raw outputs.
 #include "mlp_f16x3_core.hpp"
+#include "param_check.hpp"
 
 namespace aon {
 namespace mlp {
@@ -208,6 +209,7 @@ extern "C" size_t aon_mlp_art_packed_bytes(void) { return NetArtH::kPackedBytes;
 static int art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream, bool mixed) {
   AON_REQUIRE(prm && packed, "null pointer");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
+  if (check_mlp_art_params(prm, mixed ? "aon_mlp_art_pack_bf16" : "aon_mlp_art_pack")) return -1;
   PackArgsH a{};
   for (int i = 0; i < 4; ++i) {
     a.w[A_D0 + i] = prm->def_w[i];
@@ -229,12 +231,10 @@ static int art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t st
     a.ldw[i] = kLayersArt[i].len_a + kLayersArt[i].len_b;
   }
   // weights whose rows carry folded latent columns after the per-sample ones
-  AON_REQUIRE(prm->ld_def0 >= 3 && prm->ld_pts0 >= 63 && prm->ld_pts5 >= 319 && prm->ld_view0 >= 283,
-              "latent-carrying weights are narrower than their per-sample columns");
-  a.ldw[A_D0] = prm->ld_def0;
-  a.ldw[A_P0] = prm->ld_pts0;
-  a.ldw[A_P5] = prm->ld_pts5;
-  a.ldw[A_V0] = prm->ld_view0;
+  a.ldw[A_D0] = (int)prm->w_cols[kArtDef0];
+  a.ldw[A_P0] = (int)prm->w_cols[kArtPts0];
+  a.ldw[A_P5] = (int)prm->w_cols[kArtPts5];
+  a.ldw[A_V0] = (int)prm->w_cols[kArtView0];
   a.n_layers = kNumLayersArt;
   a.stream_blocks = NetArtH::kStreamBlocks;
   a.bias_floats = NetArtH::kBiasFloats;
@@ -271,8 +271,10 @@ static int art_launch(int mode, const void* packed, const float* a0, const float
   const f4* ws = static_cast<const f4*>(packed);
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
-  if (mode == 0 && mlp_dataflow_ws())
+#if AON_DATAFLOW_WS_BUILD
+  if (mode == 0)
     return launch_art_ws_f16x3(packed, a0, a1, a2, a3, B, S, act, raw, (hipStream_t)stream);
+#endif
   if (mode == 0)
     hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1>), (unsigned)grid, G::kThreads, 0,
                        (hipStream_t)stream, ws, bias, a0, a1, a2, a3, B, S, act, raw);

@@ -21,6 +21,7 @@
 #define AON_GUARD_PK 0
 #endif
 #include "mlp_f16x3_core.hpp"
+#include "param_check.hpp"
 
 namespace aon {
 namespace mlp {
@@ -352,8 +353,10 @@ static int art_bwd_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_
                         bool bf16) {
   AON_REQUIRE(prm && packed, "null pointer");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
-  AON_REQUIRE(prm->ld_pts0 >= 63 && prm->ld_pts5 >= 319 && prm->ld_view0 >= 283,
-              "latent-carrying weights are narrower than their per-sample columns");
+  if (check_mlp_art_params(prm, bf16 ? "aon_mlp_art_bwd_pack_bf16" : "aon_mlp_art_bwd_pack"))
+    return -1;
+  const int ld_view0 = (int)prm->w_cols[kArtView0], ld_pts5 = (int)prm->w_cols[kArtPts5];
+  const int ld_pts0 = (int)prm->w_cols[kArtPts0];
   PackArgsH a{};
   const float* w[kNumLayersArtBwd] = {
       prm->rgb_w,     prm->views_w[3], prm->views_w[2], prm->views_w[1], prm->views_w[0],
@@ -362,9 +365,8 @@ static int art_bwd_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_
       prm->pts_w[4], prm->pts_w[3], prm->pts_w[2], prm->pts_w[1], prm->pts_w[0],
       prm->deformation_w, prm->def_w[3], prm->def_w[2], prm->def_w[1]};
   // row strides of the forward weights (their in-features, latent columns included)
-  const int ld[kNumLayersArtBwd] = {128, 128, 128, 128, (int)prm->ld_view0, 256, 256, 256,
-                                    (int)prm->ld_pts5, (int)prm->ld_pts5, 256, 256, 256, 256,
-                                    (int)prm->ld_pts0, 128, 128, 128, 128};
+  const int ld[kNumLayersArtBwd] = {128, 128, 128, 128, ld_view0, 256, 256, 256, ld_pts5,
+                                    ld_pts5, 256, 256, 256, 256, ld_pts0, 128, 128, 128, 128};
   for (int i = 0; i < kNumLayersArtBwd; ++i) {
     AON_REQUIRE(w[i], "null layer weight");
     a.w[i] = w[i];

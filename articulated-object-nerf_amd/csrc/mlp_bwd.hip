@@ -13,6 +13,7 @@
 // stores undo it exactly.  The ReLU' masks come from the stored forward activations (h > 0,
 // as torch's threshold_backward on the ReLU output), loaded one pair ahead.
 #include "mlp_f16x3_core.hpp"
+#include "param_check.hpp"
 
 namespace aon {
 namespace mlp {
@@ -177,6 +178,7 @@ extern "C" size_t aon_mlp_bwd_packed_bytes(void) { return NetBwdH::kPackedBytes;
 static int bwd_pack(const aon_mlp_params* prm, void* packed, aon_stream_t stream, bool bf16) {
   AON_REQUIRE(prm && packed, "null pointer");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
+  if (check_mlp_params(prm, bf16 ? "aon_mlp_bwd_pack_bf16" : "aon_mlp_bwd_pack")) return -1;
   PackArgsH a{};
   const float* w[kNumLayersBwd] = {prm->rgb_w,    prm->views_w,  prm->bottleneck_w,
                                    prm->pts_w[7], prm->pts_w[6], prm->pts_w[5],

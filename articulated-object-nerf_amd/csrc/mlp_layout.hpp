@@ -340,13 +340,17 @@ int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const 
                  const float* a2, const float* a3, int64_t B, int S, int act, float* raw,
                  hipStream_t stream, const TrainStore* ts = nullptr);
 // the weight-streamed fp16x3 render forward (mlp_ws.hip; MODE 0 inputs, bit-identical to
-// launch_f16x3 mode 0)
+// launch_f16x3 mode 0) -- an A/B variant, not in the release library: `make variant-ws` builds
+// lib/variants/libaonerf_ws.so with AON_DATAFLOW_WS_BUILD = 1, whose render forwards
+// (aon_mlp_fwd, aon_mlp_art_fwd) take this dataflow; the release build has no process-global
+// kernel selection and no environment knobs
+#ifndef AON_DATAFLOW_WS_BUILD
+#define AON_DATAFLOW_WS_BUILD 0
+#endif
 int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
                     const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream);
 int launch_art_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
                         const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream);
-// the render forward's dataflow (aon_mlp_set_dataflow, mlp.hip): true = weight-streamed
-bool mlp_dataflow_ws();
 
 }  // namespace mlp
 }  // namespace aon

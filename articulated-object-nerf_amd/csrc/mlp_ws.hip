@@ -855,27 +855,20 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_mlp_ws_pipe_f16x3(
 
 }  // namespace ws
 
-// the pipelined schedule: AON_WS_PIPE=1 in the environment (A/B), else off (measured 7% slower
+// the pipelined schedule: compile with -DAON_WS_PIPE=1 (A/B), else off (measured 7% slower
 // than the plain schedule: its halves stream the weights twice)
-static bool ws_pipe() {
-  static bool on = [] {
-    const char* e = getenv("AON_WS_PIPE");
-    return e && atoi(e) == 1;
-  }();
-  return on;
-}
+#ifndef AON_WS_PIPE
+#define AON_WS_PIPE 0
+#endif
+static constexpr bool ws_pipe() { return AON_WS_PIPE == 1; }
 
-// geometry of the weight-streamed kernels: AON_WS_WAVES=4 in the environment (A/B), else 8
-// (4 waves x 64 samples measured 2.5x slower: twice the A-fragment bytes per MFMA; the pipelined
-// schedule is built for 8 waves only: at 4 its two accumulator sets and the 4-tile A fragments
-// spill)
-static int ws_waves() {
-  static int wv = [] {
-    const char* e = getenv("AON_WS_WAVES");
-    return (e && atoi(e) == 4) ? 4 : 8;
-  }();
-  return wv;
-}
+// geometry of the weight-streamed kernels: -DAON_WS_WAVES=4 (A/B), else 8 (4 waves x 64 samples
+// measured 2.5x slower: twice the A-fragment bytes per MFMA; the pipelined schedule is built for
+// 8 waves only: at 4 its two accumulator sets and the 4-tile A fragments spill)
+#ifndef AON_WS_WAVES
+#define AON_WS_WAVES 8
+#endif
+static constexpr int ws_waves() { return AON_WS_WAVES == 4 ? 4 : 8; }
 
 int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
                     const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream) {

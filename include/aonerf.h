@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 8
+#define AON_ABI_VERSION 9
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -137,6 +137,14 @@ typedef struct aon_mlp_params {
   const float* views_b;
   const float* rgb_w;
   const float* rgb_b;
+  /* Shapes of the tensors above (ABI 9), in layer order pts_linears.0..7, density_layer,
+   * bottleneck_layer, views_linear.0, rgb_layer (the order of the fields): layer i's weight is
+   * w_rows[i] x w_cols[i] ([out][in], contiguous) and its bias b_len[i] floats.  Every pack
+   * (aon_mlp_pack, aon_mlp_bwd_pack[_bf16]) checks them against the default geometry --
+   * 256x63, 4 x 256x256, 256x319, 2 x 256x256, 1x256, 256x256, 128x283, 3x128 -- and returns
+   * < 0 before any launch on a mismatch (e.g. parameters passed in registration order), instead
+   * of reading past the end of a tensor. */
+  int64_t w_rows[12], w_cols[12], b_len[12];
 } aon_mlp_params;
 
 size_t aon_mlp_packed_bytes(int precision);
@@ -167,15 +175,10 @@ int aon_mlp_fwd(const void* packed, int precision, const float* rays_o, const fl
                 const float* viewdirs, const float* t, int64_t B, int S, int act, float* out,
                 aon_stream_t stream);
 
-/* Dataflow of aon_mlp_fwd's fp16x3 kernel (process-wide; returns the previous setting, or < 0
- * for an unknown value): AON_DATAFLOW_STREAMED -- each wave keeps 16 samples in registers and
- * the weights stream through an LDS ring (mlp_f16x3.hip); AON_DATAFLOW_WS -- a workgroup's 128
- * samples live in LDS and each wave reads its 32 output rows' weights from L2 (mlp_ws.hip).
- * Both give bit-identical outputs.  Initial value: AON_MLP_WS=1 / 0 in the environment, else the
- * build's default (AON_DATAFLOW_STREAMED). */
-#define AON_DATAFLOW_STREAMED 0
-#define AON_DATAFLOW_WS 1
-int aon_mlp_set_dataflow(int dataflow);
+/* (ABI 9: no process-global state and no environment knobs.  ABI 8's aon_mlp_set_dataflow is
+ * gone: the weight-streamed render dataflow, bit-identical and measured at parity, is an A/B
+ * variant library, `make -C csrc variant-ws` -> lib/variants/libaonerf_ws.so, whose aon_mlp_fwd
+ * and aon_mlp_art_fwd run it.) */
 
 /* NeRFMLP.forward on pre-encoded inputs: x (B*S, 63), condition (B, 27) -> out (B*S, 4). */
 int aon_mlp_fwd_encoded(const void* packed, int precision, const float* x,
@@ -267,7 +270,17 @@ typedef struct aon_mlp_art_params {
   const float* views_b[4];
   const float* rgb_w;
   const float* rgb_b;
-  int64_t ld_def0, ld_pts0, ld_pts5, ld_view0;
+  /* Shapes (ABI 9; replaces ABI 8's ld_def0 / ld_pts0 / ld_pts5 / ld_view0), in layer order
+   * deformations_linear.0..3, deformation_layer, pts_linears.0..7, density_layer,
+   * bottleneck_layer, views_linear.0..3, rgb_layer (the order of the fields): layer i's weight
+   * is w_rows[i] x w_cols[i] ([out][in], contiguous: w_cols is its row stride) and its (folded)
+   * bias b_len[i] floats (b_len = w_rows).  The packs check them against the default geometry
+   * and return < 0 before any launch on a mismatch: rows 4 x 128, 3, 8 x 256, 1, 256, 4 x 128,
+   * 3; columns exactly 128 (deformations_linear.1-3, deformation_layer, views_linear.1-3,
+   * rgb_layer) or 256 (pts_linears.1-4, 6-7, density, bottleneck) for the layers without latent
+   * columns, and at least the per-sample columns -- 3 (deformations_linear.0), 63
+   * (pts_linears.0), 319 (pts_linears.5), 283 (views_linear.0) -- for the four that carry them. */
+  int64_t w_rows[20], w_cols[20], b_len[20];
 } aon_mlp_art_params;
 
 size_t aon_mlp_art_packed_bytes(void);

@@ -35,7 +35,7 @@ def test_header_symbols_exported(L):
 
 def test_abi_version_and_sizes(L):
     lib = L.lib()
-    assert lib.aon_abi_version() == 8
+    assert lib.aon_abi_version() == L.ABI_VERSION == 9
     assert lib.aon_mlp_packed_bytes(0) == 2368 * 1024 + 2464 * 4 + 16  # + the status block
     assert lib.aon_mlp_packed_bytes(99) == 0
 
@@ -64,3 +64,91 @@ def test_cpu_tensors_rejected():
 
     with pytest.raises(ValueError, match="MI355X only"):
         helper.pos_enc(torch.zeros(4, 3), 0, 10)
+
+
+def _fake_pairs(shapes):
+    """(weight, bias) stand-ins with the given shapes: the C side only reads the shape fields
+    before it refuses, so the pointers are never dereferenced."""
+    import torch
+
+    return [(torch.empty(o, i), torch.empty(o)) for o, i in shapes]
+
+
+def _struct_with(L, cls, n, shapes):
+    prm = cls()
+    for i, (o, k) in enumerate(shapes):
+        prm.w_rows[i], prm.w_cols[i], prm.b_len[i] = o, k, o
+    # every pointer non-null: only the shape check stands between the struct and a launch
+    for name, typ in cls._fields_:
+        if name.endswith(("_w", "_b")):
+            v = getattr(prm, name)
+            if isinstance(v, int) or v is None:
+                setattr(prm, name, 16)
+            else:
+                for j in range(len(v)):
+                    v[j] = 16
+    return prm
+
+
+def _registration_order(mlp):
+    ps = list(mlp.parameters())
+    return [(ps[2 * i], ps[2 * i + 1]) for i in range(len(ps) // 2)]
+
+
+def test_registration_order_rejected_python(L):
+    """nn.Module.parameters() in registration order (pts_linears, views_linear,
+    bottleneck, density, rgb) is not the kernels' layer order.  The Python builders refuse it
+    with ValueError naming the layer -- before any pointer exists -- for both MLPs, and the
+    training path's _params_struct (train.py / train_art.py) goes through them."""
+    from aonerf import train, train_art
+    from aonerf.model import NeRFMLP
+    from aonerf.model_autodecoder import NeRFMLP as ArtMLP
+
+    mlp = NeRFMLP(0, 10, 4)
+    reg = _registration_order(mlp)
+    with pytest.raises(ValueError, match="density_layer.*layer order"):
+        L.mlp_params(reg)
+    with pytest.raises(ValueError, match="density_layer.*layer order"):
+        train._params_struct(reg)
+    # the kernels' order passes the shape check (and then needs GPU tensors)
+    good = [(m.weight, m.bias) for m in mlp._layers()]
+    with pytest.raises(ValueError, match="GPU tensor"):
+        L.mlp_params(good)
+    with pytest.raises(ValueError, match="12 \\(weight, bias\\) pairs"):
+        L.mlp_params(good[:11])
+    art = ArtMLP(0, 10, 4)
+    reg = _registration_order(art)
+    with pytest.raises(ValueError, match="density_layer.*layer order"):
+        L.mlp_art_params(reg)
+    with pytest.raises(ValueError, match="density_layer.*layer order"):
+        train_art._params_struct(reg)
+    good = [(m.weight, m.bias) for m in train_art.art_layers(art)]
+    with pytest.raises(ValueError, match="GPU tensor"):
+        L.mlp_art_params(good)
+
+
+def test_registration_order_rejected_c(L):
+    """The same refusal on the C side (aon_mlp_params / aon_mlp_art_params carry the shapes,
+    ABI 9): every pack returns < 0 naming the layer before any launch -- no GPU needed."""
+    reg = [(256, 63)] + [(256, 256)] * 4 + [(256, 319), (256, 256), (256, 256), (128, 283),
+                                             (256, 256), (1, 256), (3, 128)]
+    prm = _struct_with(L, L.AonMlpParams, 12, reg)
+    for fn, args in (("aon_mlp_pack", (1, ctypes.c_void_p(16), None)),
+                     ("aon_mlp_bwd_pack", (ctypes.c_void_p(16), None)),
+                     ("aon_mlp_bwd_pack_bf16", (ctypes.c_void_p(16), None))):
+        with pytest.raises(ValueError, match=f"{fn}: density_layer: weight 128 x 283"):
+            L.call(fn, ctypes.byref(prm), *args)
+    art_reg = ([(128, 163)] + [(128, 128)] * 3 + [(3, 128), (256, 191)] + [(256, 256)] * 4 +
+               [(256, 447), (256, 256), (256, 256), (128, 411)] + [(128, 128)] * 3 +
+               [(256, 256), (1, 256), (3, 128)])
+    prm = _struct_with(L, L.AonMlpArtParams, 20, art_reg)
+    for fn in ("aon_mlp_art_pack", "aon_mlp_art_pack_bf16", "aon_mlp_art_bwd_pack",
+               "aon_mlp_art_bwd_pack_bf16"):
+        with pytest.raises(ValueError, match=f"{fn}: density_layer: weight 128 x 411"):
+            L.call(fn, ctypes.byref(prm), ctypes.c_void_p(16), None)
+    # a latent-carrying layer narrower than its per-sample columns
+    ok = list(L.ART_SHAPES)
+    ok[10] = (256, 300)
+    prm = _struct_with(L, L.AonMlpArtParams, 20, ok)
+    with pytest.raises(ValueError, match="pts_linears.5: weight 256 x 300.*>= 319"):
+        L.call("aon_mlp_art_pack", ctypes.byref(prm), ctypes.c_void_p(16), None)

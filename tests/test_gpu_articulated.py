@@ -200,30 +200,3 @@ def test_full_frame_c3(art):
         attrib = att.rays(fine[jf].detach().numpy(), want)
         att.explain(f"C3 e2e fine {k}", err, attrib)
         assert_e2e(f"C3 e2e fine {k}", err, None, attrib)
-
-
-@pytest.mark.parametrize("B,S", [(517, 65), (300, 193), (1, 1)])
-def test_art_mlp_ws_equals_streamed(B, S):
-    """The articulated render MLP's two dataflows (aon_mlp_set_dataflow; mlp_art.hip's LDS-ring
-    weight stream and mlp_ws.hip's weight-streamed kernel) give the same raw outputs bit for bit,
-    ragged sample counts included."""
-    from aonerf import _lib as L
-    from aonerf.model_autodecoder import NeRF_AE_Art
-    from aonerf.synthetic import art_latents, init_like_reference
-
-    g = torch.Generator().manual_seed(B + S)
-    o = (torch.randn(B, 3, generator=g) * 0.1 + torch.tensor([0.0, -3.5, 2.0])).cuda()
-    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=g), dim=-1).cuda()
-    t = torch.sort(torch.rand(B, S, generator=g) * 4 + 2, dim=-1).values.cuda()
-    net = init_like_reference(NeRF_AE_Art()).cuda()
-    lat = art_latents(0, device="cuda")
-    lib = L.lib()
-    prev = lib.aon_mlp_set_dataflow(0)
-    try:
-        a = net.fine_mlp.forward_rays(o, d, d, t, lat)
-        lib.aon_mlp_set_dataflow(1)
-        b = net.fine_mlp.forward_rays(o, d, d, t, lat)
-    finally:
-        lib.aon_mlp_set_dataflow(prev)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b), (a - b).abs().max().item()

@@ -790,34 +790,3 @@ def test_render_fused_march_equals_unfused(golden, precision):
         for la, lb in zip(a, b):
             for x, y in zip(la, lb):
                 assert torch.equal(x, y)
-
-
-@pytest.mark.parametrize("B,S,act", [(1000, 65, 0), (1237, 193, 1), (3, 193, 2), (1, 1, 0)])
-def test_mlp_ws_equals_streamed(B, S, act):
-    """The render MLP's two dataflows (aon_mlp_set_dataflow: the LDS-ring weight stream,
-    mlp_f16x3.hip, and the weight-streamed kernel, mlp_ws.hip) give the same raw outputs bit for
-    bit -- same products, same accumulation order, same epilogue -- on ragged sample counts
-    (partial 128-sample workgroups, a single sample), every activation mode; and the weight-
-    streamed one sets the range-status word like the other (test_gpu_range covers the values)."""
-    from aonerf import _lib as L
-    from aonerf.model import NeRF
-    from aonerf.synthetic import init_like_reference
-
-    g = torch.Generator().manual_seed(B + S)
-    o = cuda(torch.randn(B, 3, generator=g) * 0.1 + torch.tensor([0.0, -3.5, 2.0]))
-    d = cuda(torch.nn.functional.normalize(torch.randn(B, 3, generator=g), dim=-1))
-    t = cuda(torch.sort(torch.rand(B, S, generator=g) * 4 + 2, dim=-1).values)
-    net = init_like_reference(NeRF()).cuda()
-    mlp = net.fine_mlp
-    lib = L.lib()
-    prev = lib.aon_mlp_set_dataflow(0)
-    try:
-        a = mlp.forward_rays(o, d, d, t, act)
-        lib.aon_mlp_set_dataflow(1)
-        b = mlp.forward_rays(o, d, d, t, act)
-    finally:
-        lib.aon_mlp_set_dataflow(prev)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b), (a - b).abs().max().item()
-    if B * S > 1:  # and the values are the oracle's (the stage-isolated MLP gate elsewhere)
-        assert torch.isfinite(b).all()

@@ -53,7 +53,26 @@ int main() {
   aon_mlp_params prm;
   std::memset(&prm, 0, sizeof(prm));
   expect_invalid(aon_mlp_pack(&prm, 7, p, nullptr), "mlp_pack bad precision");
+  expect_invalid(aon_mlp_pack(&prm, AON_PREC_F16X3, p, nullptr), "mlp_pack no shapes");
+  // the default geometry's shapes (ABI 9), null tensors: refused by the null check, no launch
+  const int64_t shp[12][2] = {{256, 63},  {256, 256}, {256, 256}, {256, 256}, {256, 256}, {256, 319},
+                              {256, 256}, {256, 256}, {1, 256},   {256, 256}, {128, 283}, {3, 128}};
+  for (int i = 0; i < 12; ++i) {
+    prm.w_rows[i] = shp[i][0];
+    prm.w_cols[i] = shp[i][1];
+    prm.b_len[i] = shp[i][0];
+  }
   expect_invalid(aon_mlp_pack(&prm, AON_PREC_F16X3, p, nullptr), "mlp_pack null layer");
+  // registration order (views_linear.0 in the density slot): refused by the shape check
+  prm.w_rows[8] = 128;
+  prm.w_cols[8] = 283;
+  prm.b_len[8] = 128;
+  expect_invalid(aon_mlp_pack(&prm, AON_PREC_F16X3, p, nullptr), "mlp_pack registration order");
+  expect_invalid(aon_mlp_bwd_pack(&prm, p, nullptr), "mlp_bwd_pack registration order");
+  aon_mlp_art_params aprm;
+  std::memset(&aprm, 0, sizeof(aprm));
+  expect_invalid(aon_mlp_art_pack(&aprm, p, nullptr), "mlp_art_pack no shapes");
+  expect_invalid(aon_mlp_art_bwd_pack(&aprm, p, nullptr), "mlp_art_bwd_pack no shapes");
   uint32_t st = 0;
   expect_invalid(aon_mlp_read_status(p, 3, &st, nullptr), "read_status bad size");
   aon_gemm_args g;
