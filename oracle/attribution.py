@@ -1,0 +1,230 @@
+"""End-to-end attribution and the reference's own implementation envelope.
+
+TEST INFRASTRUCTURE ONLY (oracle/__init__.py): used by tests/test_gpu_parity.py,
+tests/test_gpu_articulated.py, tests/golden/make_golden.py and bench.py's cpu_baseline leg to
+judge a GPU render against the reference's end-to-end output on identical rays and weights.
+
+Why attribution exists.  The fine level re-samples along the coarse CDF (reference
+helper.py:203-252, model.py:163-172): a fine sample sits at lo + (u - cdf_lo) / (cdf_hi -
+cdf_lo) * width, so a change of ~1e-7 in a coarse weight moves it by delta-cdf / pdf -- by a
+whole bin where the CDF has a plateau (coarse weights exactly 0 where ReLU clips density).  Any
+two fp32 implementations of the reference disagree at that level (different GEMM association,
+a sin or exp 1 ulp apart), so the north star's 1e-4 end-to-end gate cannot hold on every ray for
+ANY of them, the reference's own fp64 re-run included.  Every ray outside 1e-4 must therefore be
+explained, or the gate fails:
+
+  (a) plateau flip: the reference's own sample_pdf puts some fine-sample u in a different CDF
+      bin under our coarse weights than under its own, with our coarse weights within 1e-4;
+  (b) amplification: the reference's own fine level, fed our coarse weights' fine samples, moves
+      by >= AMPLIFICATION x the coarse-weight difference (a near-plateau bin), same 1e-4 bound;
+  (c) implementation envelope: the error is within ENV_FACTOR x the reference's own move on that
+      ray under equally valid fp32 implementations of itself (envelope() below: GEMMs
+      re-associated or in fp64, and torch.sin (pos_enc, helper.py:139) / torch.exp (alpha,
+      helper.py:168) correctly rounded or moved by a seeded +-1 ulp).
+
+A ray explained by none of them fails the test (or counts as `unattributed` in bench.py).
+"""
+import contextlib
+import math
+
+import numpy as np
+import torch
+
+from . import nerf_oracle as O
+
+E2E_ATOL = 1e-4
+AMPLIFICATION = 100.0
+ENV_FACTOR = 4.0
+
+
+# ----------------------------------------------------------------------------- envelope
+def _gemm(linear):
+    """oracle.mlp_forward with every nn.Linear product replaced by ``linear(x, w, b)``
+    (reference model.py:95-120 layer order and concatenations)."""
+    def mlp(p, x, cond, **_):
+        S, C = x.shape[1:]
+        x = x.reshape(-1, C)
+        inp = x
+        for i in range(8):
+            x = torch.relu(linear(x, p[f"pts_linears.{i}.weight"], p[f"pts_linears.{i}.bias"]))
+            if i == 4:
+                x = torch.cat([x, inp], -1)
+        dens = linear(x, p["density_layer.weight"], p["density_layer.bias"]).reshape(-1, S, 1)
+        bott = linear(x, p["bottleneck_layer.weight"], p["bottleneck_layer.bias"])
+        c = torch.tile(cond[:, None, :], (1, S, 1)).reshape(-1, cond.shape[-1])
+        x = torch.relu(linear(torch.cat([bott, c], -1), p["views_linear.0.weight"],
+                              p["views_linear.0.bias"]))
+        return linear(x, p["rgb_layer.weight"], p["rgb_layer.bias"]).reshape(-1, S, 3), dens
+    return mlp
+
+
+GEMM_VARIANTS = {
+    "fp64_gemm": lambda x, w, b: (x.double() @ w.double().T + b.double()).float(),
+    "k_split": lambda x, w, b: (x[:, : w.shape[1] // 2] @ w[:, : w.shape[1] // 2].T
+                                + x[:, w.shape[1] // 2:] @ w[:, w.shape[1] // 2:].T) + b,
+}
+
+
+def correctly_rounded(orig):
+    """fp32 inputs through the fp64 function, rounded once: a more accurate implementation."""
+    def f(x, *a, **k):
+        if x.dtype != torch.float32:
+            return orig(x, *a, **k)
+        return orig(x.double(), *a, **k).float()
+    return f
+
+
+def ulp_jitter(orig, seed):
+    """orig's result moved by -1, 0 or +1 ulp per element (seeded by the seed and the element
+    count, so a re-run draws the same pattern): any implementation accurate to 1 ulp may return
+    these values.  Exact cases stay exact: sin(0) = 0 and exp(0) = 1 in every implementation
+    (moving exp(0) would turn the reference's zero-density samples -- its CDF plateaus -- into
+    tiny weights, which no real exp does)."""
+    def f(x, *a, **k):
+        r = orig(x, *a, **k)
+        if r.dtype != torch.float32 or r.numel() == 0:
+            return r
+        g = torch.Generator().manual_seed(seed * 1_000_003 + r.numel())
+        s = torch.randint(-1, 2, r.shape, generator=g)
+        if torch.is_tensor(x) and x.shape == r.shape:
+            s = torch.where(x == 0, torch.zeros_like(s), s)
+        up = torch.nextafter(r, torch.full_like(r, math.inf))
+        dn = torch.nextafter(r, torch.full_like(r, -math.inf))
+        return torch.where(s > 0, up, torch.where(s < 0, dn, r))
+    return f
+
+
+@contextlib.contextmanager
+def patched_torch(name, make):
+    """torch.<name> replaced by make(original) for the duration (the reference and the oracle
+    both call torch.sin / torch.exp through the module attribute)."""
+    orig = getattr(torch, name)
+    setattr(torch, name, make(orig))
+    try:
+        yield
+    finally:
+        setattr(torch, name, orig)
+
+
+TRANSCENDENTAL_VARIANTS = {
+    "sin_cr": lambda: patched_torch("sin", correctly_rounded),
+    "sin_ulp": lambda: patched_torch("sin", lambda o: ulp_jitter(o, 1)),
+    "exp_cr": lambda: patched_torch("exp", correctly_rounded),
+    "exp_ulp": lambda: patched_torch("exp", lambda o: ulp_jitter(o, 2)),
+}
+
+
+@contextlib.contextmanager
+def _oracle_gemm(fn):
+    orig = O.mlp_forward
+    O.mlp_forward = _gemm(fn)
+    try:
+        yield
+    finally:
+        O.mlp_forward = orig
+
+
+def oracle_variants():
+    """name -> context manager: the oracle run as another valid fp32 implementation."""
+    out = {k: (lambda fn=fn: _oracle_gemm(fn)) for k, fn in GEMM_VARIANTS.items()}
+    out.update(TRANSCENDENTAL_VARIANTS)
+    return out
+
+
+def envelope(run, variants=None):
+    """Per output: max over the variants of |run() under the variant - run()| (numpy arrays);
+    ``run`` returns a dict or a sequence of tensors / arrays.  Also the per-variant maxima."""
+    variants = oracle_variants() if variants is None else variants
+
+    def as_np(out):
+        items = out.items() if isinstance(out, dict) else enumerate(out)
+        return {k: np.asarray(v.detach().numpy() if torch.is_tensor(v) else v, np.float64)
+                for k, v in items}
+
+    base = as_np(run())
+    env = {k: np.zeros_like(v) for k, v in base.items()}
+    worst = {}
+    for name, ctx in variants.items():
+        with ctx():
+            out = as_np(run())
+        for k in env:
+            d = np.abs(out[k] - base[k])
+            env[k] = np.maximum(env[k], d)
+            worst[(name, k)] = float(d.max()) if d.size else 0.0
+    return env, worst
+
+
+def fine_envelope(params, rays, white_bkgd=True, near=2.0, far=6.0, **kw):
+    """The reference's (oracle's) own per-ray envelope of its fine outputs (rgb (B,3), acc,
+    depth) on these rays, eval mode."""
+    def run():
+        return O.nerf_forward(params, rays, False, white_bkgd, near, far, **kw)[1]
+    env, worst = envelope(run)
+    return [env[0], env[1], env[2]], worst
+
+
+# ----------------------------------------------------------------------------- attribution
+def plateau_flips(w_ours, w_ref, num_fine, randomized=False, u=None):
+    """Per ray: True where the reference's inverse-CDF resampling (helper.py:203-243) puts some
+    fine-sample u in a different CDF bin under our coarse weights than under its own."""
+    wo = torch.as_tensor(np.asarray(w_ours, np.float32))
+    wr = torch.as_tensor(np.asarray(w_ref, np.float32))
+    uu = None if u is None else torch.as_tensor(np.asarray(u, np.float32))
+    io = O.pdf_bin_index(wo[..., 1:-1], num_fine, randomized, uu)
+    ir = O.pdf_bin_index(wr[..., 1:-1], num_fine, randomized, uu)
+    return (io != ir).any(-1).numpy()
+
+
+def _rowmax(a):
+    a = np.asarray(a, np.float64)
+    return a.reshape(len(a), -1).max(-1) if a.size else np.zeros(len(a))
+
+
+class Attribution:
+    """Per-ray evidence that an end-to-end outlier is the reference's own ill-conditioning (module
+    docstring): dw = max |our coarse weights - the reference's|, flips = plateau_flips, and per
+    quantity the reference's own move under our coarse weights (sens) and, when given, its
+    implementation envelope (env)."""
+
+    def __init__(self, w_ours, w_ref, num_fine, randomized=False, u=None):
+        self.dw = np.abs(np.asarray(w_ours, np.float64) - np.asarray(w_ref, np.float64)).max(-1)
+        self.flips = plateau_flips(w_ours, w_ref, num_fine, randomized, u)
+        self.sens = None
+        self.env = None
+        self.why = None
+
+    def rays(self, ref_on_ours, ref, err=None, env=None):
+        """Attributed rays for one quantity: ref_on_ours = the reference's fine output at our fine
+        samples, ref = its own end-to-end output; (B,) or (B, C).  err / env (optional): our
+        error and the reference's implementation envelope per ray -- criterion (c)."""
+        self.sens = _rowmax(np.abs(np.asarray(ref_on_ours, np.float64) - np.asarray(ref, np.float64)))
+        amplified = self.sens >= AMPLIFICATION * self.dw
+        small = self.dw <= E2E_ATOL
+        a = small & self.flips
+        b = small & amplified & ~a
+        ok = a | b
+        c = np.zeros_like(ok)
+        self.env = None
+        if err is not None and env is not None:
+            self.env = _rowmax(env)
+            c = (_rowmax(err) <= ENV_FACTOR * self.env) & ~ok
+            ok = ok | c
+        self.why = np.where(a, "plateau flip", np.where(b, "amplification",
+                            np.where(c, "implementation envelope", "")))
+        return ok
+
+    def explain(self, name, err, attrib, limit=8, out=print):
+        """Print (out) the evidence for the attributed outliers of the quantity last passed to
+        rays(); returns the lines."""
+        e = _rowmax(err)
+        lines = []
+        for r in np.nonzero((e > E2E_ATOL) & attrib)[0][:limit]:
+            ln = (f"    {name} ray {r}: |err| {e[r]:.2e}, coarse dw {self.dw[r]:.2e}, plateau flip "
+                  f"{bool(self.flips[r])}, reference's own move {self.sens[r]:.2e} "
+                  f"(= {self.sens[r] / max(self.dw[r], 1e-30):.1e} x dw)")
+            if self.env is not None:
+                ln += f", implementation envelope {self.env[r]:.2e}"
+            ln += f" -> {self.why[r]}"
+            lines.append(ln)
+            out(ln)
+        return lines

@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 
 import _refimport  # noqa: E402
 from oracle import weights as W  # noqa: E402
+from oracle.attribution import TRANSCENDENTAL_VARIANTS  # noqa: E402
 
 helper, model, ray_utils, sapien_multi = _refimport.load()
 torch.set_num_threads(8)
@@ -63,7 +64,10 @@ _LINEAR_VARIANTS = {
 
 
 def envelope(run):
-    """max over GEMM re-associations of |run() - run()_fp32| per output key."""
+    """max over equally valid fp32 implementations of the reference of |run() - run()| per output
+    key: its GEMMs re-associated or in fp64, and (round 5) its torch.sin (pos_enc, helper.py:139)
+    and torch.exp (alpha, helper.py:168) correctly rounded or moved by a seeded +-1 ulp
+    (oracle/attribution.py TRANSCENDENTAL_VARIANTS)."""
     base = run()
     env = {k: np.zeros_like(v) for k, v in base.items()}
     orig = torch.nn.Linear.forward
@@ -75,6 +79,11 @@ def envelope(run):
                 env[k] = np.maximum(env[k], np.abs(out[k] - base[k]))
     finally:
         torch.nn.Linear.forward = orig
+    for ctx in TRANSCENDENTAL_VARIANTS.values():
+        with ctx():
+            out = run()
+        for k in env:
+            env[k] = np.maximum(env[k], np.abs(out[k] - base[k]))
     keep = ("rgb", "acc", "depth", "weights")
     return {f"env_{k}": v for k, v in env.items() if k.endswith(keep) and "raw" not in k}
 

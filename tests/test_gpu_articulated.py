@@ -114,7 +114,8 @@ def test_forward_chain_and_golden(art, tag):
                       g[f"{tag}_u_fine"] if randomized else None)
     for j, k, jf in ((0, "rgb", 0), (1, "acc", 1), (2, "depth", 3)):
         err = report(f"art {tag} e2e fine {k}", npy(ret[1][j]), g[f"{tag}_fine_{k}"], ATOL)
-        attrib = att.rays(fine[jf].detach().numpy(), g[f"{tag}_fine_{k}"])
+        attrib = att.rays(fine[jf].detach().numpy(), g[f"{tag}_fine_{k}"], err,
+                          g[f"{tag}_env_fine_{k}"])
         att.explain(f"art {tag} e2e fine {k}", err, attrib)
         assert_e2e(f"art {tag} e2e fine {k}", err, g[f"{tag}_env_fine_{k}"], attrib)
     mse_gpu = float(np.mean((npy(ret[1][0]) - g[f"{tag}_fine_rgb"]) ** 2))
