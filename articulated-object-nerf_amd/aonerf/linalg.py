@@ -4,7 +4,6 @@ NeRF_AE_Art MLP (model_autodecoder.py).  Operands are tensor views passed as poi
 leading dimensions; workspace for split reductions is cached per device and stream."""
 import contextlib
 import ctypes
-import os
 
 import torch
 
@@ -84,10 +83,11 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
 
 
 _batch = None
-# AONERF_NO_GEMM_BATCH=1: batched() defers nothing (A/B of aon_gemm_batch against separate launches)
-BATCH = os.environ.get("AONERF_NO_GEMM_BATCH", "0") != "1"
-# AONERF_NO_GEMM_BATCH128=1: only the 256 x 256 products are deferred (A/B of the 128-tile class)
-BATCH128 = os.environ.get("AONERF_NO_GEMM_BATCH128", "0") != "1"
+# BATCH = False: batched() defers nothing (A/B of aon_gemm_batch against separate launches);
+# BATCH128 = False: only the 256 x 256 products are deferred (A/B of the 128-tile class).  Module
+# attributes an A/B driver sets explicitly -- no environment variable changes what a caller gets.
+BATCH = True
+BATCH128 = True
 
 
 @contextlib.contextmanager
