@@ -298,11 +298,12 @@ def contig(t):
 PENDING_PACKS = {}
 _STICKY = {}
 # data pointers of the parameters each pending pack was packed from (the tensor objects an
-# autograd Function sees are not always the optimizer's, their storage is), and per device those of the packs
-# OR-ed into its sticky word: an optimizer step checks only the packs of ITS parameters, so an
-# unrelated model's optimizer neither pays the sync nor consumes (hides) this model's overflow
+# autograd Function sees are not always the optimizer's, their storage is): an optimizer step
+# checks only the packs of ITS parameters, so an unrelated model's optimizer neither pays the
+# sync nor consumes (hides) this model's overflow.  The sticky words are kept per (device,
+# parameter set) for the same reason: two models that both re-pack before either
+# steps keep separate words, and each optimizer consumes only its own.
 PACK_PARAMS = {}
-_STICKY_PARAMS = {}
 # pending pack -> (pinned host copy of its status word, event after the copy): taken after the
 # last kernel that can set the word (snapshot_pack), so check_pending reads host memory once that
 # point has passed instead of draining the device queue with a sync on the device word -- the
@@ -324,11 +325,11 @@ def register_pack(key, buf, params=()):
     k = (key[0], key[1], dev)
     SNAPSHOTS.pop(k, None)  # a snapshot of the previous pack no longer covers the buffer
     if k in PENDING_PACKS:
-        w = _STICKY.get(dev)
+        sk = (dev, PACK_PARAMS.get(k) or frozenset({None}))
+        w = _STICKY.get(sk)
         if w is None:
-            w = _STICKY[dev] = torch.zeros((), dtype=torch.int32, device=buf.device)
+            w = _STICKY[sk] = torch.zeros((), dtype=torch.int32, device=buf.device)
         w.bitwise_or_(status_word(PENDING_PACKS[k]))
-        _STICKY_PARAMS.setdefault(dev, set()).update(PACK_PARAMS.get(k) or {None})
     PENDING_PACKS[k] = buf
     PACK_PARAMS[k] = frozenset(p.data_ptr() for p in params)
 
@@ -343,9 +344,12 @@ def snapshot_pack(buf):
     h = _PINNED.get(k)
     if h is None:
         h = _PINNED[k] = torch.empty((1,), dtype=torch.int32, pin_memory=True)
-    h.copy_(status_word(buf).view(1), non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
+    # the copy and its event on the current stream of the BUFFER's device (the
+    # current device may be another one; an event there would not order after the copy)
+    with torch.cuda.device(buf.device):
+        h.copy_(status_word(buf).view(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(buf.device))
     SNAPSHOTS[k] = (h, ev)
 
 
@@ -358,8 +362,8 @@ def has_pending(devices=None, param_ids=None):
     """Whether check_pending(devices, param_ids) would look at anything (no sync)."""
     return (any((devices is None or k[2] in devices) and _concerns(PACK_PARAMS.get(k), param_ids)
                 for k in PENDING_PACKS) or
-            any((devices is None or d in devices) and _concerns(_STICKY_PARAMS.get(d), param_ids)
-                for d in _STICKY))
+            any((devices is None or d in devices) and _concerns(ps, param_ids)
+                for d, ps in _STICKY))
 
 
 def range_overflow(bufs):
@@ -388,10 +392,9 @@ def check_pending(devices=None, param_ids=None):
         else:
             snap[1].synchronize()
             bad |= int(snap[0][0]) != 0
-    for dev in [d for d in _STICKY if (devices is None or d in devices)
-                and _concerns(_STICKY_PARAMS.get(d), param_ids)]:
-        words.append(_STICKY.pop(dev))
-        _STICKY_PARAMS.pop(dev, None)
+    for sk in [sk for sk in _STICKY if (devices is None or sk[0] in devices)
+               and _concerns(sk[1], param_ids)]:
+        words.append(_STICKY.pop(sk))
     if not words:
         return bad
     return bool(torch.stack(words).any().item()) or bad

@@ -77,6 +77,18 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
             # caching allocator before the flush) stays alive until the product runs
             _batch.append((a, C.device, cls, (A, B, C, rowsum, a_amax), writes, reads))
             return
+    if _batch:
+        # a product that runs at once inside batched(): it must not read what a
+        # deferred product writes, nor write what one reads or writes -- launch those first
+        Cw = C[:M, :(n_store or N)] if C.dim() == 2 else C
+        writes = [_span(Cw)] + ([_span(rowsum)] if rowsum is not None else [])
+        reads = [_span(A), _span(B)] + [_span(t) for t in (A2, bias, mask, a_amax) if t is not None]
+        if accumulate:
+            reads.append(_span(Cw))
+        if any(_overlaps(w, it[4]) or _overlaps(w, it[5]) or _overlaps(r, it[4])
+               for it in _batch for w in writes for r in reads):
+            _flush(_batch)
+            _batch.clear()
     nbytes = L.lib().aon_gemm_workspace_bytes(ctypes.byref(a))
     ws = _workspace(nbytes, C.device) if nbytes else None
     L.call("aon_gemm", ctypes.byref(a), L.ptr(ws), nbytes, L.stream(C.device))

@@ -229,10 +229,12 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t m, int s, uint32_t a) {
   asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "i"(s), "v"(a));
   return r;
 }
-// bf16 pair at activation scale 2^3 (a ReLU output, >= 0) -> at true scale, exactly: one packed
-// max clears a -0 (negative as i16), one saturating packed subtract of 3 from each exponent
-// field divides by kActS -- exact for every normal bf16; a value whose exponent field is below 3
-// (true scale < 2^-124, fp32's denormal range) becomes 0 where v * 2^-3 would keep a subnormal
+// bf16 pair at activation scale 2^3 (a ReLU output, >= 0) -> at true scale: one packed max clears
+// a -0 (negative as i16), one saturating packed subtract of 3 from each exponent field divides
+// by kActS -- exact for every bf16 whose exponent field is >= 4 (true scale >= 2^-126, fp32's
+// normal range).  Below that it is NOT v * 2^-3: a field of exactly 3 leaves exponent 0 with the
+// mantissa bits, the denormal m 2^-133 instead of (1 + m / 128) 2^-127 / 8, and a field below 3
+// saturates to 0 (fp32-denormal magnitudes only: no numerical effect at these activations)
 __device__ __forceinline__ uint32_t pk_bf16_unscale(uint32_t pk) {
   static_assert(kActS == 8.0f, "exponent shift of kActS");
   uint32_t r;

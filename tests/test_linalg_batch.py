@@ -91,3 +91,29 @@ def test_whole_dw_view_with_concat_segment_one_flush(monkeypatch):
         linalg.gemm(dW[:, 256:], A, E, 256, 128, K, lda=256, a_kc=False, ldb=128, b_kc=False,
                     ldc=319, mma_bf16=True, n_store=63)
     assert len(log) == 1 and len(log[0]) == 2
+
+
+def test_immediate_product_reading_pending_output_flushes_first(monkeypatch):
+    """a product that runs at once inside batched() (here K < 8192, as the latent
+    terms' tiny products) and reads a deferred product's bias gradient launches after it."""
+    events = []
+    monkeypatch.setattr(linalg, "_flush", lambda items: events.append(("flush", len(items))))
+    monkeypatch.setattr(linalg.L, "call", lambda name, *a: events.append((name,)))
+    monkeypatch.setattr(linalg.L, "stream", lambda device=None: None)  # (no GPU here)
+    monkeypatch.setattr(linalg, "_workspace", lambda nbytes, device: None)
+    K = 8192
+    A = torch.zeros(K, 256, dtype=torch.bfloat16)
+    B = torch.zeros(K, 256, dtype=torch.bfloat16)
+    C, db = torch.zeros(256, 256), torch.zeros(256)
+    lat = torch.zeros(1, 128)
+    with linalg.batched():
+        _dw(C, A, B, rowsum=db)
+        other = torch.zeros(1, 128)
+        linalg.gemm(other, lat, torch.zeros(256, 128), 1, 128, 16, lda=16, a_kc=True, ldb=128,
+                    b_kc=False, ldc=128)  # independent: no flush
+        assert events == [("aon_gemm",)]
+        dl = torch.zeros(1, 128)
+        linalg.gemm(dl, db[None, :], torch.zeros(256, 128), 1, 128, 256, lda=256, a_kc=True,
+                    ldb=128, b_kc=False, ldc=128)  # reads the pending db
+        assert events == [("aon_gemm",), ("flush", 1), ("aon_gemm",)]
+    assert events[-1] == ("flush", 0) or events[-1] == ("aon_gemm",)

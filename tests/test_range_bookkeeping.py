@@ -16,10 +16,10 @@ def _buf(status=0):
 def L():
     from aonerf import _lib
 
-    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib._STICKY_PARAMS, _lib.SNAPSHOTS):
+    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib.SNAPSHOTS):
         d.clear()
     yield _lib
-    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib._STICKY_PARAMS, _lib.SNAPSHOTS):
+    for d in (_lib.PENDING_PACKS, _lib._STICKY, _lib.PACK_PARAMS, _lib.SNAPSHOTS):
         d.clear()
 
 
@@ -67,7 +67,7 @@ def test_repack_keeps_status_sticky(L):
     L.register_pack(("train", "fwd65"), b)
     L.register_pack(("train", "fwd65"), b)  # called before the re-pack: the 1 is kept
     b.view(torch.int32)[-4] = 0          # what the re-pack then does to the status word
-    assert "cpu" in L._STICKY
+    assert any(sk[0] == "cpu" for sk in L._STICKY)
     assert L.check_pending({"cpu"}) is True
     assert not L._STICKY and not L.PENDING_PACKS
 
@@ -127,3 +127,27 @@ def test_sticky_keeps_its_parameters(L):
     with pytest.raises(FloatingPointError):
         torch.optim.SGD([mine], lr=0.1).step()
     assert not L._STICKY and not L.PENDING_PACKS
+
+
+def test_two_models_repack_before_either_steps(L):
+    """model A (no overflow) and model B (overflow) each re-pack before either steps.
+    Their status goes to separate sticky words (per parameter set): A's optimizer steps, B's
+    refuses -- a shared per-device word would have made A refuse and B go through."""
+    from aonerf import train  # noqa: F401
+
+    a = torch.nn.Parameter(torch.ones(3))
+    b = torch.nn.Parameter(torch.ones(3))
+    for p in (a, b):
+        p.grad = torch.ones(3)
+    ba, bb = _buf(0), _buf(1)
+    L.register_pack(("train", "fwdA"), ba, [a])
+    L.register_pack(("train", "fwdA"), ba, [a])   # re-pack: A's 0 goes sticky
+    L.register_pack(("train", "fwdB"), bb, [b])
+    L.register_pack(("train", "fwdB"), bb, [b])   # re-pack: B's 1 goes sticky
+    bb.view(torch.int32)[-4] = 0                  # what B's re-pack does to its word
+    assert len(L._STICKY) == 2
+    torch.optim.SGD([a], lr=0.1).step()           # A: no overflow of its own
+    assert torch.allclose(a.detach(), torch.full((3,), 0.9))
+    with pytest.raises(FloatingPointError):
+        torch.optim.SGD([b], lr=0.1).step()
+    assert torch.equal(b.detach(), torch.ones(3))
