@@ -615,7 +615,13 @@ def test_full_frame_properties(nerf):
     ref = ref_all[1]
     # every link gated at 1e-4 on the same rays, through the GPU's own rays (a1/a2 bit-exact)
     gr = frame_rays(c2w, H, Wd, f, p0=int(p0), n=FULL_FRAME_CHUNK)
-    np.testing.assert_array_equal(npy(gr["rays_d"]), rd[sel].numpy())
+    # a1/a2 are bit-exact against the reference's golden rays (test_ray_generation); the oracle
+    # re-run on this box's CPU may round a direction 1 ulp differently (its BLAS / vector path),
+    # which the end-to-end attribution below then sees as part of the input
+    dd = np.abs(npy(gr["rays_d"]).astype(np.float64) - rd[sel].numpy())
+    print(f"640x480 chunk rays_d: {int((dd > 0).any(-1).sum())} of {len(sel)} rays differ from "
+          f"this CPU's oracle, max {dd.max():.2e}")
+    assert dd.max() <= 1.2e-7
     got_sub, fine_ref = check_chain(nerf, gr, params, return_ref=True)
     np.testing.assert_array_equal(npy(got_sub[1][0]), o[sel][:, :3])
     att = Attribution(npy(got_sub[0][3]), inter[0]["weights"].numpy(), nerf.num_fine_samples)
