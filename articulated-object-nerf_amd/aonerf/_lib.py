@@ -145,7 +145,8 @@ class AonAdamTensor(ctypes.Structure):
 
 
 ADAM_MAX_TENSORS = 64
-GEMM_BATCH_MAX = 8  # AON_GEMM_BATCH_MAX
+GEMM_BATCH_MAX = 12  # AON_GEMM_BATCH_MAX
+GEMM_SMALL_BATCH_MAX = 16  # AON_GEMM_SMALL_BATCH_MAX
 
 _SIGNATURES = {
     "aon_abi_version": (c_int, []),
@@ -199,6 +200,7 @@ _SIGNATURES = {
     "aon_gemm": (c_int, [ctypes.POINTER(AonGemmArgs), vp, c_size, vp]),
     "aon_gemm_batch_workspace_bytes": (c_size, [ctypes.POINTER(AonGemmArgs), c_int]),
     "aon_gemm_batch": (c_int, [ctypes.POINTER(AonGemmArgs), c_int, vp, c_size, vp]),
+    "aon_gemm_small_batch": (c_int, [ctypes.POINTER(AonGemmArgs), c_int, vp]),
     "aon_composite_bwd": (c_int, [vp, c_i64, vp, c_i64, vp, vp, c_i64, c_int, c_int, c_int, vp, vp,
                                   vp, vp, vp, c_i64, vp]),
     "aon_mse": (c_int, [vp, vp, c_i64, c_float, vp, vp, vp]),

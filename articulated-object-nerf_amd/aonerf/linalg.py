@@ -51,6 +51,10 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
                       b_bf16=int(B.dtype == torch.bfloat16), a_tiled=int(bool(a_tiled)),
                       b_tiled=int(bool(b_tiled)), n_store=n_store,
                       exact_fp32=int(bool(exact_fp32)), c_trans=int(bool(c_trans)))
+    if _small is not None and exact_fp32:
+        # deferred to one aon_gemm_small_batch launch (small_batched); operands kept alive
+        _small.append((a, C.device, (A, B, C, bias)))
+        return
     bf = mma_bf16 and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16
     f16 = (not mma_bf16 and A.dtype == torch.float32 and B.dtype == torch.float32 and not a_kc
            and not b_kc and A2 is None and bias is None and mask is None and not relu
@@ -95,6 +99,26 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
 
 
 _batch = None
+_small = None
+
+
+@contextlib.contextmanager
+def small_batched():
+    """Defer the exact_fp32 tiny products issued inside (the articulated bf16 step's latent-code
+    terms and folded biases) to aon_gemm_small_batch launches at exit, in issue order --
+    GEMM_SMALL_BATCH_MAX per launch, bit-identical to launching them one by one (products on one
+    C chain in order; the library refuses any other dependency between them)."""
+    global _small
+    outer, _small = _small, []
+    try:
+        yield
+        items = _small
+    finally:
+        _small = outer
+    for i in range(0, len(items), L.GEMM_SMALL_BATCH_MAX):
+        chunk = items[i:i + L.GEMM_SMALL_BATCH_MAX]
+        arr = (L.AonGemmArgs * len(chunk))(*[it[0] for it in chunk])
+        L.call("aon_gemm_small_batch", arr, len(chunk), L.stream(chunk[0][1]))
 # BATCH = False: batched() defers nothing (A/B of aon_gemm_batch against separate launches);
 # BATCH128 = False: only the 256 x 256 products are deferred (A/B of the 128-tile class).  Module
 # attributes an A/B driver sets explicitly -- no environment variable changes what a caller gets.

@@ -33,7 +33,7 @@ import torch
 from . import _lib as L
 from . import tiles
 from . import train as _train
-from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, batched, gemm
+from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, batched, gemm, small_batched
 from .train import Adam, _amax_word, img2mse, learning_rate, loss_pair, mse2psnr, relu_masks  # noqa: F401 (shared)
 
 # parameter layout of one articulated NeRFMLP in ArtRenderLevel: 20 layers x (weight, bias)
@@ -185,10 +185,11 @@ def _pack(geo, P, lat, tag="", bf16=False):
     range-guarded: its deformation part is fp16x3)."""
     shape, app, art = lat
     dev = shape.device
-    fb = {DEF0: _fold(*P[DEF0], 3, torch.cat([shape, art], -1)),
-          PTS0: _fold(*P[PTS0], geo.ne, shape),
-          PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
-          VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
+    with small_batched():  # bf16: the four folds as one launch (exact-fp32 path, same bits)
+        fb = {DEF0: _fold(*P[DEF0], 3, torch.cat([shape, art], -1)),
+              PTS0: _fold(*P[PTS0], geo.ne, shape),
+              PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
+              VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
     buf = _buffer(f"fwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_art_packed_bytes(), dev,
                   guard=True, params=[t for wb in P for t in wb])
     L.call("aon_mlp_art_pack_bf16" if bf16 else "aon_mlp_art_pack",
@@ -435,11 +436,14 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
                  c_trans=True)
         else:
             dweight(DEF0, dzd[0], wd, xyz, 3, 3, chain_scale=False)       # deformations_linear.0
-    dlatent(VIEW0, nw + nv, app, dapp, False)
-    dlatent(PTS0 + 5, nw + ne, shape, dshape, False)
-    dlatent(PTS0, ne, shape, dshape, True)
-    dlatent(DEF0, 3, shape, dshape, True)
-    dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
+    # the latent terms read the bias gradients just flushed; bf16 (exact-fp32 tiny products): all
+    # ten as ONE aon_gemm_small_batch launch, bit-identical to ten launches in this order
+    with small_batched():
+        dlatent(VIEW0, nw + nv, app, dapp, False)
+        dlatent(PTS0 + 5, nw + ne, shape, dshape, False)
+        dlatent(PTS0, ne, shape, dshape, True)
+        dlatent(DEF0, 3, shape, dshape, True)
+        dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
     _train._rec(f"art_dweight{S}", e0, R)
 
 

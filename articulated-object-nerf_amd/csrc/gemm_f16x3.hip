@@ -453,6 +453,8 @@ struct ParamsBatch {
   int tile0[AON_GEMM_BATCH_MAX + 1];  // 128 x 128-tile batch: first tile of each product
 };
 
+static_assert(sizeof(ParamsBatch) <= 4096, "aon_gemm_batch's table must fit the kernel arguments");
+
 // the batch's split-K reduce: grid.y = product
 __global__ void k_gemm_reduce_batch(ParamsBatch pb) { reduce_body<4>(pb.p[blockIdx.y], pb.zsplit); }
 
@@ -1830,6 +1832,71 @@ __global__ __launch_bounds__(256) void k_gemm_small_f32_wave(Params p, int a_kc,
   if (lane == 0) small_store(p, m, n, v);
 }
 
+// aon_gemm_small_batch: up to AON_GEMM_SMALL_BATCH_MAX exact-fp32 tiny products in ONE launch,
+// each computed exactly as its own aon_gemm launch would (k_gemm_small_f32 for K <= 16: one
+// lane per output, a k-ordered fma chain; k_gemm_small_f32_wave above: one wave per output,
+// lane-strided chains and the same xor butterfly), and products writing the same C applied in
+// argument order in registers (c = accumulate ? c + v : v; + bias), so the result is bit for bit
+// that of the launches in sequence.  Work units: 64 outputs (lane kind) or 1 output (wave kind)
+// per wave; group g (one C) owns units unit0[g] .. unit0[g + 1] - 1.
+struct SmallItem {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  int64_t lda, ldb, ldc, M, N, K;
+  int a_kc, b_kc, accumulate, pad;
+};
+struct SmallBatch {
+  SmallItem it[AON_GEMM_SMALL_BATCH_MAX];   // in group order (a group's items consecutive)
+  int gfirst[AON_GEMM_SMALL_BATCH_MAX + 1];  // first item of each group
+  int64_t unit0[AON_GEMM_SMALL_BATCH_MAX + 1];
+  int ngroups;
+};
+static_assert(sizeof(SmallBatch) <= 4096, "aon_gemm_small_batch's table must fit the kernel arguments");
+
+__device__ __forceinline__ float small_dot_lane(const SmallItem& f, int64_t m, int64_t n) {
+  float v = 0.f;
+  for (int64_t k = 0; k < f.K; ++k) {
+    const float a = f.a_kc ? f.A[m * f.lda + k] : f.A[k * f.lda + m];
+    const float b = f.b_kc ? f.B[n * f.ldb + k] : f.B[k * f.ldb + n];
+    v = fmaf(a, b, v);
+  }
+  return v;
+}
+__device__ __forceinline__ float small_dot_wave(const SmallItem& f, int64_t m, int64_t n, int lane) {
+  float v = 0.f;
+  for (int64_t k = lane; k < f.K; k += 64) {
+    const float a = f.a_kc ? f.A[m * f.lda + k] : f.A[k * f.lda + m];
+    const float b = f.b_kc ? f.B[n * f.ldb + k] : f.B[k * f.ldb + n];
+    v = fmaf(a, b, v);
+  }
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) v = __fadd_rn(v, __shfl_xor(v, sh, 64));
+  return v;
+}
+__global__ __launch_bounds__(256) void k_gemm_small_batch(SmallBatch sb) {
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  if (u >= sb.unit0[sb.ngroups]) return;
+  int g = 0;
+  while (g + 1 < sb.ngroups && u >= sb.unit0[g + 1]) ++g;
+  const SmallItem& f0 = sb.it[sb.gfirst[g]];
+  const bool wave = f0.K > 16;
+  const int64_t e = wave ? u - sb.unit0[g] : (u - sb.unit0[g]) * 64 + lane;
+  if (e >= f0.M * f0.N) return;
+  const int64_t m = e / f0.N, n = e - m * f0.N;
+  float* c = f0.C + m * f0.ldc + n;
+  float acc = f0.accumulate ? *c : 0.f;
+  for (int i = sb.gfirst[g]; i < sb.gfirst[g + 1]; ++i) {
+    const SmallItem& f = sb.it[i];
+    const float v = wave ? small_dot_wave(f, m, n, lane) : small_dot_lane(f, m, n);
+    acc = f.accumulate ? __fadd_rn(acc, v) : v;
+    if (f.bias) acc = __fadd_rn(acc, f.bias[n]);
+  }
+  if (!wave || lane == 0) *c = acc;
+}
+
 template <typename TA, bool BT>
 static void launch_skinny(const Params& p, dim3 grid, hipStream_t st) {
   const dim3 block((unsigned)(2 * p.N));  // 16 row phases x N / 8 column groups
@@ -2271,4 +2338,95 @@ extern "C" int aon_gemm_batch(const aon_gemm_args* a, int count, void* work, siz
       if (rc) return rc;
     }
   return 0;
+}
+
+// whether two row-major views (rows x cols at row stride ld, cols <= ld) share an element:
+// views of one matrix with the same ld compare as row / column rectangles (column slices of one
+// dW -- the latent segments -- do not overlap), others by their byte extents
+static bool views_overlap(const float* p, int64_t rp, int64_t cp, int64_t lp, const float* q,
+                          int64_t rq, int64_t cq, int64_t lq) {
+  const intptr_t a = reinterpret_cast<intptr_t>(p), b = reinterpret_cast<intptr_t>(q);
+  const intptr_t ae = a + (intptr_t)(((rp - 1) * lp + cp) * 4), be = b + (intptr_t)(((rq - 1) * lq + cq) * 4);
+  if (ae <= b || be <= a) return false;
+  if (lp != lq || (b - a) % 4 != 0 || cp > lp || cq > lq) return true;
+  int64_t d = (b - a) / 4;  // q's first element relative to p's, in elements
+  int64_t row = d / lp, col = d % lp;
+  if (col < 0) {
+    col += lp;
+    row -= 1;
+  }
+  // q covers columns [col, col + cq) of rows row.., wrapping into the next row past ld
+  for (int w = 0; w < 2; ++w) {
+    const int64_t c0 = w == 0 ? col : 0, c1 = w == 0 ? (col + cq < lp ? col + cq : lp) : col + cq - lp;
+    const int64_t r0 = row + w;
+    if (c1 <= c0) continue;
+    if (r0 < rp && r0 + rq > 0 && c0 < cp && c1 > 0) return true;
+  }
+  return false;
+}
+
+extern "C" int aon_gemm_small_batch(const aon_gemm_args* a, int count, aon_stream_t stream) {
+  AON_REQUIRE(a && count >= 0 && count <= AON_GEMM_SMALL_BATCH_MAX, "bad batch");
+  if (count == 0) return 0;
+  SmallBatch sb{};
+  int group_of[AON_GEMM_SMALL_BATCH_MAX];
+  int ng = 0;
+  const aon_gemm_args* head[AON_GEMM_SMALL_BATCH_MAX];
+  for (int i = 0; i < count; ++i) {
+    const aon_gemm_args* g = &a[i];
+    AON_REQUIRE(small_path(g) && g->A && g->B && g->C && g->M > 0 && g->N > 0 && g->K > 0 &&
+                    g->ldc >= g->N,
+                "aon_gemm_small_batch: exact_fp32 tiny products only (as aon_gemm's exact_fp32)");
+    int gi = -1;
+    for (int j = 0; j < ng; ++j)
+      if (head[j]->C == g->C) gi = j;
+    if (gi < 0) {
+      head[ng] = g;
+      gi = ng++;
+    } else {
+      const aon_gemm_args* h = head[gi];
+      AON_REQUIRE(h->M == g->M && h->N == g->N && h->ldc == g->ldc && (h->K > 16) == (g->K > 16) &&
+                      g->accumulate,
+                  "aon_gemm_small_batch: products on one C must match in shape and accumulate");
+    }
+    group_of[i] = gi;
+  }
+  // no product may read or write what ANOTHER group writes (groups run concurrently), and no
+  // product may read its own group's C other than through `accumulate`
+  for (int x = 0; x < ng; ++x) {
+    const aon_gemm_args* h = head[x];
+    for (int i = 0; i < count; ++i) {
+      const aon_gemm_args* g = &a[i];
+      const int64_t ar = g->a_kc ? g->M : g->K, ac = g->a_kc ? g->K : g->M;
+      const int64_t br = g->b_kc ? g->N : g->K, bc = g->b_kc ? g->K : g->N;
+      AON_REQUIRE(group_of[i] == x || !views_overlap(h->C, h->M, h->N, h->ldc, g->C, g->M, g->N, g->ldc),
+                  "aon_gemm_small_batch: outputs overlap");
+      AON_REQUIRE(!views_overlap(h->C, h->M, h->N, h->ldc, g->A, ar, ac, g->lda) &&
+                      !views_overlap(h->C, h->M, h->N, h->ldc, g->B, br, bc, g->ldb) &&
+                      (!g->bias || !views_overlap(h->C, h->M, h->N, h->ldc, g->bias, 1, g->N, g->N)),
+                  "aon_gemm_small_batch: a product reads a batch output");
+    }
+  }
+  int k = 0;
+  sb.unit0[0] = 0;
+  for (int x = 0; x < ng; ++x) {
+    sb.gfirst[x] = k;
+    for (int i = 0; i < count; ++i) {
+      if (group_of[i] != x) continue;
+      const aon_gemm_args* g = &a[i];
+      SmallItem& f = sb.it[k++];
+      f.A = g->A; f.B = g->B; f.C = g->C; f.bias = g->bias;
+      f.lda = g->lda; f.ldb = g->ldb; f.ldc = g->ldc;
+      f.M = g->M; f.N = g->N; f.K = g->K;
+      f.a_kc = g->a_kc; f.b_kc = g->b_kc; f.accumulate = g->accumulate;
+    }
+    const int64_t outs = head[x]->M * head[x]->N;
+    sb.unit0[x + 1] = sb.unit0[x] + (head[x]->K > 16 ? outs : (outs + 63) / 64);
+  }
+  sb.gfirst[ng] = k;
+  sb.ngroups = ng;
+  const int64_t blocks = (sb.unit0[ng] + 3) / 4;
+  AON_REQUIRE(blocks < (1ll << 31), "too large");
+  hipLaunchKernelGGL(k_gemm_small_batch, (unsigned)blocks, 256, 0, (hipStream_t)stream, sb);
+  return launch_status(__func__);
 }

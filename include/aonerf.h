@@ -453,10 +453,20 @@ int aon_gemm(const aon_gemm_args* args, void* work, size_t work_bytes, aon_strea
  * reduction-major operands in whole 128 x 128 tiles, no A2 / bias / mask / relu) as one more;
  * the rest one by one as aon_gemm.
  * Deterministic; the chunking, and so the fp32 summation order, differs from aon_gemm's. */
-#define AON_GEMM_BATCH_MAX 8
+#define AON_GEMM_BATCH_MAX 12
 size_t aon_gemm_batch_workspace_bytes(const aon_gemm_args* args, int count);
 int aon_gemm_batch(const aon_gemm_args* args, int count, void* work, size_t work_bytes,
                    aon_stream_t stream);
+
+/* `count` (<= AON_GEMM_SMALL_BATCH_MAX) exact_fp32 tiny products (each valid for aon_gemm's
+ * exact_fp32 path) in ONE launch, bit for bit what the launches in argument order give: products
+ * writing the same C (same M, N, ldc, and accumulate = 1 after the first) are applied in argument
+ * order; any other two products must not touch each other's output (checked, < 0 otherwise).
+ * The articulated training step's latent-code terms (model_autodecoder.py:186-194: dW of the
+ * latent columns = db l^T, dl = db^T W_l, three terms summed into the shape code's gradient) and
+ * the per-call folded biases of its forward.  No workspace. */
+#define AON_GEMM_SMALL_BATCH_MAX 16
+int aon_gemm_small_batch(const aon_gemm_args* args, int count, aon_stream_t stream);
 
 /* Backward of volumetric_rendering (helper.py:157-195) and of the activations `act` applied to
  * the raw MLP outputs (model.py:186-187): given dL/dcomp_rgb (B,3) and optionally dL/dacc,

@@ -19,8 +19,11 @@ explained, or the gate fails:
       by >= AMPLIFICATION x the coarse-weight difference (a near-plateau bin), same 1e-4 bound;
   (c) implementation envelope: the error is within ENV_FACTOR x the reference's own move on that
       ray under equally valid fp32 implementations of itself (envelope() below: GEMMs
-      re-associated or in fp64, and torch.sin (pos_enc, helper.py:139) / torch.exp (alpha,
-      helper.py:168) correctly rounded or moved by a seeded +-1 ulp).
+      re-associated or in fp64, torch.sin (pos_enc, helper.py:139) / torch.exp (alpha,
+      helper.py:168) correctly rounded or moved by a seeded +-1 ulp, and -- for frames whose
+      rays the oracle regenerates on the machine at hand -- its ray generation as torch computes
+      it in the build container (nerf_oracle.get_rays_fma): torch's CPU matmul is
+      machine-dependent at one ulp).
 
 A ray explained by none of them fails the test (or counts as `unattributed` in bench.py).
 """
@@ -154,12 +157,27 @@ def envelope(run, variants=None):
     return env, worst
 
 
-def fine_envelope(params, rays, white_bkgd=True, near=2.0, far=6.0, **kw):
+def fine_envelope(params, rays, white_bkgd=True, near=2.0, far=6.0, alt_rays=None, **kw):
     """The reference's (oracle's) own per-ray envelope of its fine outputs (rgb (B,3), acc,
-    depth) on these rays, eval mode."""
+    depth) on these rays, eval mode.  alt_rays: the same rays as another valid implementation of
+    the reference's ray generation computes them (nerf_oracle.get_rays_fma: torch CPU in the
+    build container) -- one more variant ("rays_build_cpu")."""
+    cur = {"rays": rays}
+
     def run():
-        return O.nerf_forward(params, rays, False, white_bkgd, near, far, **kw)[1]
-    env, worst = envelope(run)
+        return O.nerf_forward(params, cur["rays"], False, white_bkgd, near, far, **kw)[1]
+
+    variants = oracle_variants()
+    if alt_rays is not None:
+        @contextlib.contextmanager
+        def swap():
+            cur["rays"] = alt_rays
+            try:
+                yield
+            finally:
+                cur["rays"] = rays
+        variants["rays_build_cpu"] = swap
+    env, worst = envelope(run, variants)
     return [env[0], env[1], env[2]], worst
 
 

@@ -79,6 +79,35 @@ def get_rays(directions, c2w, output_view_dirs=False, output_radii=False):
     return rays_o, rays_d
 
 
+def get_rays_fma(directions, c2w):
+    """get_rays(..., output_view_dirs=True) with the (n,3)@(3,3) product and the row norm as
+    forward fma chains -- what torch CPU computes for reference ray_utils.py:118-147 in the build
+    container (MKL on Intel AVX-512; measured equal element for element on the 640x480 frame and
+    on the golden frames), emulated exactly enough in fp64 (a*b is exact in fp64; one rounding of
+    the sum before the fp32 one).  The reference's ray generation is machine-dependent at one ulp:
+    torch on the GPU box's AMD CPU rounds ~3% of these elements differently (tools/diag/
+    parity_scale.py), so the attribution uses this as one more valid implementation of a2."""
+    M = c2w[:3, :3].double()
+    d = directions.reshape(-1, 3).double()
+
+    def r32(x):
+        return x.float().double()
+
+    cols = []
+    for k in range(3):
+        acc = r32(d[:, 0] * M[k, 0])
+        acc = r32(d[:, 1] * M[k, 1] + acc)
+        cols.append(r32(d[:, 2] * M[k, 2] + acc))
+    r = torch.stack(cols, -1)
+    s = r32(r[:, 0] * r[:, 0])
+    s = r32(r[:, 1] * r[:, 1] + s)
+    s = r32(r[:, 2] * r[:, 2] + s)
+    n = r32(torch.sqrt(s))
+    rays_d = (r / n[:, None]).float()
+    rays_o = c2w[:3, 3].float().expand(rays_d.shape).contiguous()
+    return rays_o, rays_d, rays_d.clone()
+
+
 def focal_from_fovy(H, fovy_deg=35.0):
     """SAPIEN camera (datagen/data_gen.py:60-67): fy = 0.5*H/tan(0.5*fovy)."""
     return 0.5 * H / math.tan(0.5 * math.radians(fovy_deg))

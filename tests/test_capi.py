@@ -152,3 +152,23 @@ def test_registration_order_rejected_c(L):
     prm = _struct_with(L, L.AonMlpArtParams, 20, ok)
     with pytest.raises(ValueError, match="pts_linears.5: weight 256 x 300.*>= 319"):
         L.call("aon_mlp_art_pack", ctypes.byref(prm), ctypes.c_void_p(16), None)
+
+
+def test_gemm_small_batch_validation(L):
+    """aon_gemm_small_batch refuses, before any launch: a product off the exact-fp32 tiny path,
+    two products on one C that differ in shape or do not accumulate, and overlapping outputs
+    (column slices of one matrix at the same row stride do not overlap)."""
+    def args(C, M, N, K, ldc, acc=0, exact=1):
+        return L.AonGemmArgs(M=M, N=N, K=K, A=16, lda=K, a_kc=1, B=16, ldb=K, b_kc=1, C=C,
+                             ldc=ldc, accumulate=acc, a_scale=1.0, b_scale=1.0, exact_fp32=exact)
+
+    def run(*items):
+        arr = (L.AonGemmArgs * len(items))(*items)
+        L.call("aon_gemm_small_batch", arr, len(items), None)
+
+    with pytest.raises(ValueError, match="exact_fp32 tiny products only"):
+        run(args(4096, 4, 4, 4, 4, exact=0))
+    with pytest.raises(ValueError, match="match in shape and accumulate"):
+        run(args(4096, 4, 4, 4, 4), args(4096, 4, 4, 4, 4, acc=0))
+    with pytest.raises(ValueError, match="outputs overlap"):
+        run(args(1 << 20, 8, 8, 4, 16), args((1 << 20) + 4 * 4, 8, 8, 4, 16))

@@ -634,7 +634,9 @@ def test_full_frame_properties(nerf):
     env = [None] * 3
     if bad.any():  # the reference's own implementation envelope, on the outlier rays only
         rows = np.nonzero(bad)[0]
-        part, worst = fine_envelope(params, {kk: v[rows] for kk, v in sub.items()})
+        rb = O.get_rays_fma(dirs, c2w[:3, :4])  # a2 as torch computes it in the build container
+        alt = {kk: v[sel][rows] for kk, v in zip(("rays_o", "rays_d", "viewdirs"), rb)}
+        part, worst = fine_envelope(params, {kk: v[rows] for kk, v in sub.items()}, alt_rays=alt)
         env = [np.zeros((len(sel),) + x.shape[1:]) for x in part]
         for full, x in zip(env, part):
             full[rows] = x

@@ -515,3 +515,61 @@ def test_f16x3_weight_gradient_batch():
         assert err < 2e-6 and err_own < 1e-6
         np.testing.assert_allclose(rb[i].cpu().numpy(), rs[i].cpu().numpy(), rtol=0,
                                    atol=1e-6 * float(As[i].abs().sum(0).max()))
+
+
+def test_gemm_small_batch_equals_sequential_launches():
+    """aon_gemm_small_batch (the articulated bf16 step's latent terms and folded biases in one
+    launch) gives exactly what the same exact_fp32 products give launched one by one in argument
+    order: outer products (K = 1, one lane per output), row products (K > 16, one wave per
+    output), a three-product accumulate chain on one C, a bias, column slices of one dW."""
+    from aonerf import _lib as L
+    from aonerf.linalg import gemm, small_batched
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    r = lambda *s: torch.randn(*s, device="cuda", generator=g)  # noqa: E731
+    db = [r(1, 256), r(1, 256), r(1, 128)]
+    lat = [r(1, 128), r(1, 32)]
+    Ws = [r(256, 447), r(256, 191), r(128, 163)]
+    bias = r(256)
+
+    def run():
+        dW = torch.full((128, 163), 7.0, device="cuda")
+        dW2 = torch.full((256, 447), 3.0, device="cuda")
+        dl = torch.full((1, 128), 2.0, device="cuda")
+        fold = torch.empty((1, 256), device="cuda")
+        # outer products into column slices of dW (K = 1)
+        gemm(dW[:, 3:], db[2], lat[0], 128, 128, 1, lda=1, a_kc=True, ldb=128, b_kc=False, ldc=163,
+             exact_fp32=True)
+        gemm(dW[:, 131:], db[2], lat[1], 128, 32, 1, lda=1, a_kc=True, ldb=32, b_kc=False, ldc=163,
+             exact_fp32=True)
+        gemm(dW2[:, 319:], db[0], lat[0], 256, 128, 1, lda=1, a_kc=True, ldb=128, b_kc=False,
+             ldc=447, exact_fp32=True)
+        # the shape code's gradient: three row products chained on one C
+        gemm(dl, db[0], Ws[0][:, 319:], 1, 128, 256, lda=256, a_kc=True, ldb=447, b_kc=False,
+             ldc=128, exact_fp32=True)
+        gemm(dl, db[1], Ws[1][:, 63:], 1, 128, 256, lda=256, a_kc=True, ldb=191, b_kc=False,
+             ldc=128, accumulate=True, exact_fp32=True)
+        gemm(dl, db[2], Ws[2][:, 3:131], 1, 128, 128, lda=128, a_kc=True, ldb=163, b_kc=False,
+             ldc=128, accumulate=True, exact_fp32=True)
+        # a folded bias: b + W[:, c0:] . lat (b_kc, bias)
+        gemm(fold, lat[0], Ws[0][:, 319:], 1, 256, 128, lda=128, a_kc=True, ldb=447, b_kc=True,
+             ldc=256, bias=bias, exact_fp32=True)
+        return dW, dW2, dl, fold
+
+    seq = run()
+    with small_batched():
+        bat = run()
+    torch.cuda.synchronize()
+    for a, b in zip(seq, bat):
+        assert torch.equal(a, b)
+    assert bool((seq[0][:, :3] == 7.0).all())  # columns no product writes are untouched
+    # a product reading another group's output is refused
+    x = torch.zeros((1, 128), device="cuda")
+    y = torch.zeros((1, 128), device="cuda")
+    with pytest.raises(ValueError, match="reads a batch output"):
+        with small_batched():
+            gemm(x, lat[0], Ws[0][:, 319:], 1, 128, 128, lda=128, a_kc=True, ldb=447, b_kc=True,
+                 ldc=128, exact_fp32=True)
+            gemm(y, x, Ws[0][:128, 319:], 1, 128, 128, lda=128, a_kc=True, ldb=447, b_kc=True,
+                 ldc=128, exact_fp32=True)
+    assert L.GEMM_SMALL_BATCH_MAX == 16

@@ -97,7 +97,10 @@ def main():
     on_ours = O.render_level(params, sub, t_fine[rows], 1, True)
     ours_rays = {k: v[rows].cpu() for k, v in rays.items()}
     on_ours_own = O.render_level(params, ours_rays, t_fine[rows], 1, True)
-    env, _ = A.fine_envelope(params, sub)
+    ro_b, rv_b, rd_b = O.get_rays_fma(dirs, c2w[:3, :4])
+    alt = {"rays_o": ro_b[p0:p0 + n][rows], "rays_d": rd_b[p0:p0 + n][rows],
+           "viewdirs": rv_b[p0:p0 + n][rows]}
+    env, _ = A.fine_envelope(params, sub, alt_rays=alt)
     att = A.Attribution(w_ours[rows], w_ref[rows], 128)
     ray_diff = (g_rd[p0:p0 + n][rows] != rd[p0:p0 + n][rows].double().numpy()).any(-1)
     detail = []
