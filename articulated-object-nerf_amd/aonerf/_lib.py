@@ -186,6 +186,7 @@ _SIGNATURES = {
     "aon_mlp_art_bwd_pack": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
     "aon_mlp_art_bwd": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp, vp, vp]),
     "aon_mlp_art_pack_bf16": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
+    "aon_mlp_art_pack_mixed": (c_int, [ctypes.POINTER(AonMlpArtParams), c_int, vp, vp]),
     "aon_mlp_art_bwd_pack_bf16": (c_int, [ctypes.POINTER(AonMlpArtParams), vp, vp]),
     "aon_mlp_art_bwd_bf16": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp, vp, vp, vp, vp]),
     "aon_mlp_art_fwd_train": (c_int, [vp, vp, vp, vp, vp, c_i64, c_int, vp, vp, vp, vp, vp, vp, vp,

@@ -151,6 +151,11 @@ PRECISION = "f16x3"
 # 2^-9 forward rounding alone leaves the deformation gradients at cosine 0.987 to the fp32
 # oracle (the bf16 backward itself, stage-isolated, is at >= 0.9999)
 BF16_TRUNK = False
+# bf16 mode, forward numerics (when BF16_TRUNK is False): True runs the view branch
+# (views_linear.0-3, rgb_layer: 12% of the MACs, the 128-wide layers whose epilogues cost the
+# most VALU per MFMA) one bf16 MFMA per product on the view-branch stream (aon_mlp_art_pack_mixed
+# mode 2); the deformation MLP, trunk, density and bottleneck stay fp16x3
+BF16_VIEW = False
 
 _packed = {}
 
@@ -178,11 +183,12 @@ def _buffer(key, nbytes, dev, guard=False, params=()):
     return buf
 
 
-def _pack(geo, P, lat, tag="", bf16=False):
+def _pack(geo, P, lat, tag="", mixed=0):
     """The fused kernel's fp16x3 weight stream (aon_mlp_art_pack) of one level's parameters with
     this call's latent codes folded into the biases; re-packed on every call (the optimizer
-    updates the parameters in place).  bf16: the bf16 mode's mixed stream (aon_mlp_art_pack_bf16,
-    range-guarded: its deformation part is fp16x3)."""
+    updates the parameters in place).  mixed: the bf16 mode's mixed streams
+    (aon_mlp_art_pack_mixed: 1 trunk bf16, 2 view branch bf16; range-guarded, their deformation
+    part is fp16x3)."""
     shape, app, art = lat
     dev = shape.device
     with small_batched():  # bf16: the four folds as one launch (exact-fp32 path, same bits)
@@ -190,10 +196,13 @@ def _pack(geo, P, lat, tag="", bf16=False):
               PTS0: _fold(*P[PTS0], geo.ne, shape),
               PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
               VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
-    buf = _buffer(f"fwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_art_packed_bytes(), dev,
+    buf = _buffer(f"fwd{'bf' if mixed else ''}{tag}", L.lib().aon_mlp_art_packed_bytes(), dev,
                   guard=True, params=[t for wb in P for t in wb])
-    L.call("aon_mlp_art_pack_bf16" if bf16 else "aon_mlp_art_pack",
-           L.ctypes.byref(_params_struct(P, fb)), L.ptr(buf), L.stream(dev))
+    if mixed:
+        L.call("aon_mlp_art_pack_mixed", L.ctypes.byref(_params_struct(P, fb)), mixed, L.ptr(buf),
+               L.stream(dev))
+    else:
+        L.call("aon_mlp_art_pack", L.ctypes.byref(_params_struct(P, fb)), L.ptr(buf), L.stream(dev))
     return buf
 
 
@@ -226,7 +235,7 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     hv = torch.empty((4, NR, geo.wc), device=dev, dtype=dt)
     enc = torch.empty((R, geo.ne), device=dev)
     xyz = torch.empty((R, 3), device=dev)
-    mixed = bf16 and BF16_TRUNK
+    mixed = (1 if BF16_TRUNK else 2 if BF16_VIEW else 0) if bf16 else 0
     packed = _pack(geo, P, lat, S, mixed)
     e0 = _train._ev()
     args = (L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs), L.ptr(t_vals), B, S,
@@ -234,7 +243,7 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
             L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks))
     if bf16:
         L.call("aon_mlp_art_fwd_train_bf16", *args, L.ptr(enc_bf) if enc_bf is not None else None,
-               int(mixed), L.stream(dev))
+               mixed, L.stream(dev))
     else:
         L.call("aon_mlp_art_fwd_train", *args, L.stream(dev))
     L.snapshot_pack(packed)  # the forward was the pack's last reader (range guard, _lib)

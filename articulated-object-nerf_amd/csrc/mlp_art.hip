@@ -25,9 +25,11 @@ namespace mlp {
 // sample points are kept for the backward (TrainStoreArt), raw_sigma gets the noise.
 // PREC (the training forward's numerics): 0 fp16x3, kept activations fp32; the bf16 training
 // mode keeps hd / h / bot / hv as bf16 (TrainStoreArt's pointers then address bf16 arrays;
-// pos_enc(x') and the points stay fp32) and computes 1: fp16x3 throughout, or 2: mixed (the
+// pos_enc(x') and the points stay fp32) and computes 1: fp16x3 throughout, 2: mixed (the
 // kArtMix stream, mlp_layout.hpp) -- the deformation MLP fp16x3 (x' = delta + xyz feeds
-// sin(2^9 x')), the trunk, heads and view branch one bf16 MFMA per product.
+// sin(2^9 x')), the trunk, heads and view branch one bf16 MFMA per product, or 3: the view
+// branch mixed (kArtMixV) -- everything through the bottleneck fp16x3, views_linear.0-3 and the
+// rgb head bf16 (the bottleneck's epilogue hands them bf16 fragments, layer_h OBF).
 template <int MODE, int NCOL, bool STORE = false, int PREC = 0>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_art_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
@@ -36,6 +38,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   using G = GeomH<NCOL>;
   using Net = NetArtH;
   constexpr bool BFM = PREC == 2;
+  constexpr bool BFV = PREC == 3;  // bf16 view branch (venc and the bottleneck's output in bf16)
   constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
   __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + kStash];
   float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
@@ -48,7 +51,9 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 
   using WP = typename std::conditional<
       BFM, DmaPipe<G::kThreads, kRing, kChunkH, kArtMixStream, kArtMixUsed, kRingLead>,
-      WeightPipe<Net, G::kThreads>>::type;
+      typename std::conditional<
+          BFV, DmaPipe<G::kThreads, kRing, kChunkH, kArtMixVStream, kArtMixVUsed, kRingLead>,
+          WeightPipe<Net, G::kThreads>>::type>::type;
   using T = typename std::conditional<PREC != 0, __bf16, float>::type;
   WP p;
   p.wbuf = smem;
@@ -98,13 +103,14 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     for (int e = 0; e < 8; ++e) dv[e] = (g == 0 && e < 3) ? px[c][e < 3 ? e : 0] * kActS : 0.f;
     split8(dv, din.hi[0][c], din.lo[0][c], din.ovf);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) vv[e] *= act_scale<BFM>();
-    split8<BFM>(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
+    for (int e = 0; e < 8; ++e) vv[e] *= act_scale<BFM || BFV>();
+    split8<BFM || BFV>(vv, venc.hi[0][c], venc.lo[0][c], venc.ovf);
     stash[64 * (6 * c + 4)] = __builtin_bit_cast(f4, venc.hi[0][c]);
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
 
-  FragPipe<WP, AON_PREFETCH, 0, false, kArtMix.lo, BFM ? kArtMix.hi : 0> fp(p);
+  FragPipe<WP, AON_PREFETCH, 0, false, 0, BFM ? kArtMix.hi : (BFV ? kArtMixV.hi : 0)> fp(p);
+  static_assert(kArtMix.lo == 0 && kArtMixV.lo == 0, "mixed streams start fp16x3");
   fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
 
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   f4 dens[NCOL], rgb[NCOL];
   head_h<Net, A_DEN>(fp, y, dens, bias_l, g);  // :221-223
   // bottleneck, no activation (:225)
-  layer_h<Net, A_BOT, false>(fp, y, none, x, bias_l, g, SP::make(reinterpret_cast<T*>(ts.bot), 256, rows, N, g));
+  layer_h<Net, A_BOT, false, BFV>(fp, y, none, x, bias_l, g, SP::make(reinterpret_cast<T*>(ts.bot), 256, rows, N, g));
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
     venc.hi[0][c] = __builtin_bit_cast(h8, stash[64 * (6 * c + 4)]);
@@ -206,10 +212,12 @@ using namespace aon::mlp;
 
 extern "C" size_t aon_mlp_art_packed_bytes(void) { return NetArtH::kPackedBytes; }
 
-static int art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream, bool mixed) {
+static int art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream, int mixed) {
   AON_REQUIRE(prm && packed, "null pointer");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
-  if (check_mlp_art_params(prm, mixed ? "aon_mlp_art_pack_bf16" : "aon_mlp_art_pack")) return -1;
+  if (check_mlp_art_params(prm, mixed == 1 ? "aon_mlp_art_pack_bf16"
+                                : mixed ? "aon_mlp_art_pack_mixed" : "aon_mlp_art_pack"))
+    return -1;
   PackArgsH a{};
   for (int i = 0; i < 4; ++i) {
     a.w[A_D0 + i] = prm->def_w[i];
@@ -239,21 +247,30 @@ static int art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t st
   a.stream_blocks = NetArtH::kStreamBlocks;
   a.bias_floats = NetArtH::kBiasFloats;
   if (mixed) {
-    a.bf16 = kArtMix.mode;
-    a.mx_lo = kArtMix.lo;
-    a.mx_hi = kArtMix.hi;
+    const StreamMap m = mixed == 1 ? kArtMix : kArtMixV;
+    a.bf16 = m.mode;
+    a.mx_lo = m.lo;
+    a.mx_hi = m.hi;
   }
   return pack_h(a, packed, (hipStream_t)stream);
 }
 
 extern "C" int aon_mlp_art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t stream) {
-  return art_pack(prm, packed, stream, false);
+  return art_pack(prm, packed, stream, 0);
+}
+
+// the articulated bf16 mode's mixed streams (same buffer size and bias table): mixed = 1 the
+// trunk-bf16 stream (= aon_mlp_art_pack_bf16), 2 the view-branch stream (kArtMixV)
+extern "C" int aon_mlp_art_pack_mixed(const aon_mlp_art_params* prm, int mixed, void* packed,
+                                      aon_stream_t stream) {
+  AON_REQUIRE(mixed == 1 || mixed == 2, "mixed: 1 trunk bf16, 2 view branch bf16");
+  return art_pack(prm, packed, stream, mixed);
 }
 
 // the bf16 training mode's mixed stream (kArtMix): same buffer size and bias table
 extern "C" int aon_mlp_art_pack_bf16(const aon_mlp_art_params* prm, void* packed,
                                      aon_stream_t stream) {
-  return art_pack(prm, packed, stream, true);
+  return art_pack(prm, packed, stream, 1);
 }
 
 static int art_launch(int mode, const void* packed, const float* a0, const float* a1,
@@ -313,7 +330,11 @@ static int art_fwd_train(const void* packed, const float* rays_o, const float* r
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
   const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise, reinterpret_cast<uint2*>(masks), enc_bf};
-  if (prec == 2)
+  if (prec == 3)
+    hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 3>), (unsigned)grid, G::kThreads, 0,
+                       (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
+                       (int)AON_ACT_NONE, raw, ts);
+  else if (prec == 2)
     hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 2>), (unsigned)grid, G::kThreads, 0,
                        (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
                        (int)AON_ACT_NONE, raw, ts);
@@ -344,9 +365,10 @@ extern "C" int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_
                                           float* xyz, float* raw, uint32_t* masks, void* enc_bf,
                                           int mixed, aon_stream_t stream) {
   AON_REQUIRE(aligned16(enc_bf), "enc_bf must be 16-byte aligned");
+  AON_REQUIRE(mixed >= 0 && mixed <= 2, "mixed: 0 fp16x3, 1 trunk bf16, 2 view branch bf16");
   return art_fwd_train(packed, rays_o, rays_d, viewdirs, t, B, S, noise, static_cast<float*>(hd),
                        static_cast<float*>(h), static_cast<float*>(bot), static_cast<float*>(hv),
-                       enc, xyz, raw, masks, stream, mixed ? 2 : 1, static_cast<__bf16*>(enc_bf));
+                       enc, xyz, raw, masks, stream, mixed + 1, static_cast<__bf16*>(enc_bf));
 }
 
 extern "C" int aon_mlp_art_fwd_points(const void* packed, const float* pos,

@@ -585,7 +585,11 @@ struct StorePick<true, NCOL, T> {
 // BF: a bf16 layer -- operands unscaled, the accumulator at true scale and already holding the
 // bias (layer_h seeds it): one v_cvt_pk_bf16_f32, then ReLU / mask / store on the packed pair
 // (kPkEpi policies, see NoStore).
-template <bool RELU, bool BF, int NCOL, int NO, typename Store = NoStore, bool ZB = false>
+// OBF: a fp16x3 layer whose consumer is a bf16 layer (the view-branch mixed stream's bottleneck):
+// its output fragment is bf16 at true scale -- one v_cvt_pk_bf16_f32 of v * 2^-3 (exact), the
+// same values the kept (bf16) store gets -- instead of the fp16 hi / lo split.
+template <bool RELU, bool BF, int NCOL, int NO, typename Store = NoStore, bool ZB = false,
+          bool OBF = false>
 __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f4 (&xx)[2][NCOL],
                                          const f4 (&bias)[2], Frag<NO, NCOL>& out, int pr,
                                          const Store& st = Store{}) {
@@ -624,6 +628,15 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
       const bf2 hb = {static_cast<__bf16>(vv[0]), static_cast<__bf16>(vv[1])};
       const uint32_t pk = __builtin_bit_cast(uint32_t, hb);
       st.put_pk(pr, uu, r0, c, pk);
+      u4 w = __builtin_bit_cast(u4, out.hi[pr][c]);
+      w[q] = pk;
+      out.hi[pr][c] = __builtin_bit_cast(h8, w);
+      continue;
+    }
+    if constexpr (OBF) {
+      static_assert(AON_F16X3_V2 && !RELU, "OBF: a V2 layer without ReLU (the bottleneck)");
+      st.put(pr, uu, r0, c, vv[0], vv[1]);
+      const uint32_t pk = cvt_pk_bf16(vv[0] * (1.0f / kActS), vv[1] * (1.0f / kActS));
       u4 w = __builtin_bit_cast(u4, out.hi[pr][c]);
       w[q] = pk;
       out.hi[pr][c] = __builtin_bit_cast(h8, w);
@@ -673,8 +686,8 @@ __device__ __forceinline__ void epi_part(int q, const f4 (&hh)[2][NCOL], const f
 
 // one layer with U >= 2 output tiles: out = act(W . [a ; b] + bias) as next-layer fragments.
 // Pair p's epilogue is spread over the first k-steps of pair p+1 (compute[cur] || finish[prev]).
-template <typename Net, int LAYER, bool RELU, typename P, int NCOL, int NA, int NB, int NO,
-          typename Store = NoStore>
+template <typename Net, int LAYER, bool RELU, bool OBF = false, typename P, int NCOL, int NA,
+          int NB, int NO, typename Store = NoStore>
 __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
                                         const Frag<NB, NCOL>& b, Frag<NO, NCOL>& out,
                                         lds_float* bias_l, int g, const Store& st = Store{}) {
@@ -753,12 +766,12 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
         }
       }
       if (pr > 0 && k >= EO && k - EO < 4)
-        epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias>(k - EO, phh, pxx, pbias, out, pr - 1, st);
+        epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias, OBF>(k - EO, phh, pxx, pbias, out, pr - 1, st);
     }
     if (pr > 0) {
 #pragma unroll
       for (int q = QIN; q < 4; ++q)
-        epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias>(q, phh, pxx, pbias, out, pr - 1, st);
+        epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias, OBF>(q, phh, pxx, pbias, out, pr - 1, st);
     }
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
@@ -772,7 +785,7 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q)
-    epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias>(q, phh, pxx, pbias, out, NP - 1, st);
+    epi_part<RELU, BF, NCOL, NO, Store, Net::kZeroBias, OBF>(q, phh, pxx, pbias, out, NP - 1, st);
 }
 
 // single-tile head (density / rgb): returns the 16-row tile at activation scale

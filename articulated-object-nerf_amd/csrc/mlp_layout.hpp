@@ -303,6 +303,17 @@ static_assert(kArtMixUsed == 1484 && kArtMixStream == 1536, "mixed articulated s
 static_assert(kArtMix.unmap(kArtMix.map(2750)) == 2750 && kArtMix.unmap(kArtMix.map(214)) == 214 &&
                   kArtMix.map(216) == 216 && kArtMix.map(218) == 217,
               "stream map round trip");
+// the articulated bf16 mode's view-branch stream (train_art.BF16_VIEW): the deformation MLP, the
+// trunk, density and bottleneck fp16x3 (blocks 0..2407 -- everything the deformation gradients
+// are ill-conditioned in), views_linear.0-3 and rgb_layer compact bf16: 2408 + 172 = 2580 blocks
+constexpr StreamMap kArtMixV{2, 0, 2408};
+constexpr int kArtMixVUsed = kArtMixV.used(2752);
+constexpr int kArtMixVStream = (kArtMixVUsed + 63) / 64 * 64;
+static_assert(kArtMixVUsed == 2580 && kArtMixVStream == 2624 && kArtMixVStream <= 2752,
+              "view-branch mixed articulated stream");
+static_assert(kLayersArt[A_V0].blk0 == kArtMixV.hi && kArtMixV.map(2408) == 2408 &&
+                  kArtMixV.unmap(kArtMixV.map(2750)) == 2750,
+              "view-branch stream map");
 
 // Training forward of the fused kernel (launch_f16x3 mode 2): every hidden activation goes to
 // HBM for the backward, as the layer-by-layer path keeps them: h (8, N, 256) post-ReLU

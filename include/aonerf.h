@@ -314,9 +314,14 @@ int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* 
  * the same buffer size: the deformation MLP stays fp16x3 -- x' feeds sin(2^9 x') -- the trunk,
  * heads and view branch are bf16), one bf16 MFMA per product past the deformation head;
  * mixed == 0: packed by aon_mlp_art_pack, fp16x3 numerics throughout (only the stores bf16).
+ * mixed == 2: packed by aon_mlp_art_pack_mixed(.., 2, ..) -- everything through the bottleneck
+ * fp16x3, the view branch (views_linear.0-3, rgb_layer) one bf16 MFMA per product.
  * enc_bf (optional, NULL: not kept): pos_enc(x') as bf16, tiled (NR, 128), columns 63..127 zero
  * (as aon_mlp_fwd_train_bf16's enc). */
 int aon_mlp_art_pack_bf16(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
+/* mixed = 1: as aon_mlp_art_pack_bf16; mixed = 2: the view-branch stream (ABI 9). */
+int aon_mlp_art_pack_mixed(const aon_mlp_art_params* params, int mixed, void* packed,
+                           aon_stream_t stream);
 int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_o, const float* rays_d,
                                const float* viewdirs, const float* t, int64_t B, int S,
                                const float* noise, void* hd, void* h, void* bot, void* hv,

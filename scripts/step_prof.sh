@@ -10,6 +10,7 @@ export TMPDIR=/tmp
 for m in $MODES; do
   case $m in
     art_bf16) a="--art --precision bf16" ;;
+    art_bf16_view) a="--art --precision bf16 --view" ;;
     art) a="--art --precision f16x3" ;;
     bf16) a="--precision bf16" ;;
     f16x3) a="--precision f16x3" ;;

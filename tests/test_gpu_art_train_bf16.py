@@ -34,10 +34,24 @@ pytestmark = pytest.mark.gpu
 def art_bf16():
     from aonerf import train_art
 
-    old = train_art.PRECISION, train_art.BF16_TRUNK
+    old = train_art.PRECISION, train_art.BF16_TRUNK, train_art.BF16_VIEW
     train_art.PRECISION = "bf16"
     yield train_art
-    train_art.PRECISION, train_art.BF16_TRUNK = old
+    train_art.PRECISION, train_art.BF16_TRUNK, train_art.BF16_VIEW = old
+
+
+# the bf16 mode's forward numerics: fp16x3 throughout (BF16_TRUNK = BF16_VIEW = False), the trunk
+# bf16 (BF16_TRUNK), or the view branch bf16 (BF16_VIEW)
+FWD_MODES = ["f16x3_fwd", "bf16_trunk", "bf16_view"]
+
+
+def _set_mode(train_art, mode, monkeypatch=None):
+    vals = {"BF16_TRUNK": mode == "bf16_trunk", "BF16_VIEW": mode == "bf16_view"}
+    for k, v in vals.items():
+        if monkeypatch is not None:
+            monkeypatch.setattr(train_art, k, v)
+        else:
+            setattr(train_art, k, v)
 
 
 def _level_inputs(seed=12, n=1024):
@@ -50,19 +64,22 @@ def _level_inputs(seed=12, n=1024):
     return net, lib, batch, u_c, u_f
 
 
-@pytest.mark.parametrize("trunk", [False, True], ids=["f16x3_fwd", "bf16_trunk"])
+@pytest.mark.parametrize("mode", FWD_MODES)
 @pytest.mark.parametrize("level", [0, 1], ids=["coarse", "fine"])
-def test_art_bf16_forward(level, trunk, monkeypatch):
+def test_art_bf16_forward(level, mode, monkeypatch):
     """One level's training forward, f16x3 mode vs bf16 mode at the same t.  The deformation MLP
     is the fp16x3 kernel's in both, so x', pos_enc(x'), the points and the deformation layers'
     ReLU' bits are bit-identical, hd is exactly bf16(f16x3 hd) and the tiled 128-column enc_bf
     exactly bf16(pos_enc(x')) with zero padding.  BF16_TRUNK False: everything
     is -- h / bot / hv exactly bf16 of the f16x3 values, raw and all ReLU' bits identical.
     True: the bf16 trunk's h / bot / hv and raw within bf16 distance of the fp64 oracle at our
-    x' (gate 2e-2 of each tensor's max)."""
+    x' (gate 2e-2 of each tensor's max).  BF16_VIEW: the trunk and bottleneck exactly as in the
+    fp16x3 forward (h / bot and their ReLU' bits), the view branch's hv and raw within bf16
+    distance of the fp64 oracle."""
     from aonerf import tiles, train_art
 
-    monkeypatch.setattr(train_art, "BF16_TRUNK", trunk)
+    _set_mode(train_art, mode, monkeypatch)
+    trunk = mode != "f16x3_fwd"
     net, lib, batch, u_c, u_f = _level_inputs()
     latents = lib(batch)
     with torch.no_grad():
@@ -99,6 +116,10 @@ def test_art_bf16_forward(level, trunk, monkeypatch):
         for a, b in ((hbf, h32), (botbf, bot32), (hvbf, hv32)):
             assert torch.equal(a, b.to(torch.bfloat16))
         return
+    if mode == "bf16_view":  # everything through the bottleneck is the fp16x3 forward's
+        assert torch.equal(mbf[:12], m32[:12])
+        for a, b in ((hbf, h32), (botbf, bot32)):
+            assert torch.equal(a, b.to(torch.bfloat16))
     # the bf16 part against the fp64 oracle at our x'
     rec = {}
     names = ("density", "color", "articulation")
@@ -126,8 +147,8 @@ def test_art_bf16_forward(level, trunk, monkeypatch):
     assert max(errs.values()) < 2e-2, errs
 
 
-@pytest.mark.parametrize("trunk", [False, True], ids=["f16x3_fwd", "bf16_trunk"])
-def test_art_bf16_train_step_c5(art_bf16, trunk):
+@pytest.mark.parametrize("mode", FWD_MODES)
+def test_art_bf16_train_step_c5(art_bf16, mode):
     """One C5 step of the articulated auto-decoder (4,096 rays, randomized, injected uniforms) in
     the bf16 mode: the loss against the fp32 oracle at our sample positions within 3e-3 relative,
     every MLP parameter's and latent code's gradient against the fp32 oracle (teacher-forced at
@@ -136,10 +157,10 @@ def test_art_bf16_train_step_c5(art_bf16, trunk):
     test_gpu_art_train.test_art_train_step_c5_4096_rays).  BF16_TRUNK = True (the bf16 trunk
     forward, not the default) is held to what its forward rounding allows: cosine >= 0.98,
     max-rel <= 0.3 (measured 0.987 / 0.21, the deformation gradients; the heads and view branch
-    0.9994 / 0.07)."""
+    0.9994 / 0.07).  BF16_VIEW (the view branch bf16) is held to the default gates."""
     train_art = art_bf16
-    train_art.BF16_TRUNK = trunk
-    min_cos, max_rel = (0.98, 0.3) if trunk else (0.999, 0.05)
+    _set_mode(train_art, mode)
+    min_cos, max_rel = (0.98, 0.3) if mode == "bf16_trunk" else (0.999, 0.05)
     net, lib, batch, u_c, u_f = _level_inputs(n=4096)
     latents = lib(batch)
     ret = net(batch, True, True, 2.0, 6.0, latents, u_coarse=u_c, u_fine=u_f,
@@ -182,11 +203,11 @@ def test_art_bf16_train_step_c5(art_bf16, trunk):
     assert not bad, bad
 
 
-def _art_trajectory_gpu(precision, batch, steps, lr, trunk=False):
+def _art_trajectory_gpu(precision, batch, steps, lr, trunk=False, view=False):
     from aonerf import train_art
 
-    old = train_art.PRECISION, train_art.BF16_TRUNK
-    train_art.PRECISION, train_art.BF16_TRUNK = precision, trunk
+    old = train_art.PRECISION, train_art.BF16_TRUNK, train_art.BF16_VIEW
+    train_art.PRECISION, train_art.BF16_TRUNK, train_art.BF16_VIEW = precision, trunk, view
     try:
         net, lib = _make(0)
         opt = train_art.configure_optimizers(net, lib, lr_init=lr)
@@ -199,7 +220,7 @@ def _art_trajectory_gpu(precision, batch, steps, lr, trunk=False):
             out.append(loss.item())
         return np.array(out)
     finally:
-        train_art.PRECISION, train_art.BF16_TRUNK = old
+        train_art.PRECISION, train_art.BF16_TRUNK, train_art.BF16_VIEW = old
 
 
 def _traj_batch():
@@ -266,6 +287,7 @@ def test_art_bf16_loss_trajectory():
     f16 = _art_trajectory_gpu("f16x3", batch, steps, lr)
     bf = _art_trajectory_gpu("bf16", batch, steps, lr)
     bft = _art_trajectory_gpu("bf16", batch, steps, lr, trunk=True)
+    bfv = _art_trajectory_gpu("bf16", batch, steps, lr, view=True)
     env = float(np.abs(ref64 / ref - 1).max())
     for i in range(0, steps, 4):
         print(f"step {i:2d}: oracle {ref[i]:.6f}  f16x3 {f16[i]:.6f}  bf16 {bf[i]:.6f}  "
@@ -273,11 +295,13 @@ def test_art_bf16_loss_trajectory():
     print(f"final: oracle {ref[-1]:.6f}  f16x3 {f16[-1]:.6f}  bf16 {bf[-1]:.6f}  bf16 trunk "
           f"{bft[-1]:.6f}; max rel to the fp32 oracle: fp64 oracle {env:.2e}  "
           f"f16x3 {np.abs(f16 / ref - 1).max():.2e} (gate {max(2 * env, 1e-3):.2e})  "
-          f"bf16 {np.abs(bf / ref - 1).max():.2e}  bf16 trunk {np.abs(bft / ref - 1).max():.2e}")
+          f"bf16 {np.abs(bf / ref - 1).max():.2e}  bf16 trunk {np.abs(bft / ref - 1).max():.2e}  "
+          f"bf16 view {np.abs(bfv / ref - 1).max():.2e}")
     assert ref[-1] < 0.8 * ref[0], "the oracle run must actually train"
     np.testing.assert_allclose(f16, ref, rtol=max(2 * env, 1e-3))
     np.testing.assert_allclose(bf, ref, rtol=2e-2)
     np.testing.assert_allclose(bft, ref, rtol=2e-2)
+    np.testing.assert_allclose(bfv, ref, rtol=2e-2)
 
 
 def test_art_trajectory_lr1e3_is_the_references_chaos():

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--art", action="store_true")
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--trunk", action="store_true", help="articulated bf16: BF16_TRUNK = True")
+    ap.add_argument("--view", action="store_true", help="articulated bf16: BF16_VIEW = True")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--overlap", type=int, default=None,
                     help="train.OVERLAP_DWEIGHT = 0 / 1 (default: the library's setting)")
@@ -33,6 +34,7 @@ def main():
     if args.art:
         from test_gpu_art_train import _make
         train_art.PRECISION, train_art.BF16_TRUNK = args.precision, args.trunk
+        train_art.BF16_VIEW = args.view
         batch["instance_id"] = torch.tensor([7], device="cuda")
         batch["articulation_id"] = torch.tensor([3], device="cuda")
         net, lib = _make(0)
