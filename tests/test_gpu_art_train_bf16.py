@@ -157,10 +157,13 @@ def test_art_bf16_train_step_c5(art_bf16, mode):
     test_gpu_art_train.test_art_train_step_c5_4096_rays).  BF16_TRUNK = True (the bf16 trunk
     forward, not the default) is held to what its forward rounding allows: cosine >= 0.98,
     max-rel <= 0.3 (measured 0.987 / 0.21, the deformation gradients; the heads and view branch
-    0.9994 / 0.07).  BF16_VIEW (the view branch bf16) is held to the default gates."""
+    0.9994 / 0.07).  BF16_VIEW = True (the view branch bf16, not the default either: it saves
+    0.23 ms of the 10.1 ms step) likewise: cosine >= 0.995, max-rel <= 0.15 (measured 0.9968 /
+    0.10, again the deformation gradients -- the view branch's bf16 rounding reaches them through
+    the bottleneck's gradient)."""
     train_art = art_bf16
     _set_mode(train_art, mode)
-    min_cos, max_rel = (0.98, 0.3) if mode == "bf16_trunk" else (0.999, 0.05)
+    min_cos, max_rel = {"bf16_trunk": (0.98, 0.3), "bf16_view": (0.995, 0.15)}.get(mode, (0.999, 0.05))
     net, lib, batch, u_c, u_f = _level_inputs(n=4096)
     latents = lib(batch)
     ret = net(batch, True, True, 2.0, 6.0, latents, u_coarse=u_c, u_fine=u_f,
