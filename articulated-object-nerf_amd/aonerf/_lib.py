@@ -137,7 +137,8 @@ class AonGemmArgs(ctypes.Structure):
                 ("relu", c_int), ("accumulate", c_int), ("a_scale", c_float), ("b_scale", c_float),
                 ("k_splits", c_i64), ("rowsum", vp), ("a_amax", vp), ("mma_bf16", c_int),
                 ("a_bf16", c_int), ("b_bf16", c_int), ("a_tiled", c_int), ("b_tiled", c_int),
-                ("n_store", c_i64), ("exact_fp32", c_int), ("c_trans", c_int)]
+                ("n_store", c_i64), ("exact_fp32", c_int), ("c_trans", c_int),
+                ("f16_single", c_int)]
 
 
 class AonAdamTensor(ctypes.Structure):
@@ -218,7 +219,7 @@ _SIGNATURES = {
 _lib = None
 
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 def _load(path):

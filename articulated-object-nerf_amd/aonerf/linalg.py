@@ -30,14 +30,16 @@ def _workspace(nbytes, device):
 def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, a2_rdiv=1,
          b_rdiv=1, bias=None, mask=None, ldm=0, relu=False, accumulate=False, a_scale=1.0,
          b_scale=1.0, k_splits=0, rowsum=None, a_amax=None, mma_bf16=False, a_tiled=False,
-         b_tiled=False, n_store=0, exact_fp32=False, c_trans=False):
+         b_tiled=False, n_store=0, exact_fp32=False, c_trans=False, f16_single=False):
     """aon_gemm on tensor views (each operand's data_ptr carries its own offset); a_amax: a
     device word with the bits of max |A| (per-call gradient scale, include/aonerf.h);
     mma_bf16: the bf16 mode (bf16 MFMA; torch.bfloat16 operands are read as bf16);
     a_tiled / b_tiled: a reduction-major operand in the fused training kernels' 16-row tiled
     layout (tiles.py); n_store: columns of C written (0: all N; a zero-padded bf16 B);
     exact_fp32: a tiny product in exact fp32 (include/aonerf.h); c_trans: C written transposed
-    and rowsum = B's column sums (the bf16 skinny path, include/aonerf.h)."""
+    and rowsum = B's column sums (the bf16 skinny path, include/aonerf.h); f16_single: the
+    caller's licence for the single-accumulator fp16x3 kernel (operands range-guarded at their
+    scales, include/aonerf.h)."""
     a = L.AonGemmArgs(M=M, N=N, K=K, A=A.data_ptr(), lda=lda, a_kc=int(a_kc),
                       A2=A2.data_ptr() if A2 is not None else None, lda2=lda2, K1=K1,
                       a2_rdiv=a2_rdiv, B=B.data_ptr(), ldb=ldb, b_kc=int(b_kc), b_rdiv=b_rdiv,
@@ -50,7 +52,8 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
                       mma_bf16=int(bool(mma_bf16)), a_bf16=int(A.dtype == torch.bfloat16),
                       b_bf16=int(B.dtype == torch.bfloat16), a_tiled=int(bool(a_tiled)),
                       b_tiled=int(bool(b_tiled)), n_store=n_store,
-                      exact_fp32=int(bool(exact_fp32)), c_trans=int(bool(c_trans)))
+                      exact_fp32=int(bool(exact_fp32)), c_trans=int(bool(c_trans)),
+                      f16_single=int(bool(f16_single)))
     if _small is not None and exact_fp32:
         # deferred to one aon_gemm_small_batch launch (small_batched); operands kept alive
         _small.append((a, C.device, (A, B, C, bias)))

@@ -350,10 +350,15 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
         n_store = 0
         if X is enc and enc_t:
             ldx, n_store, n_in = 128, n_in, 128
+        # f16x3, the 256 x 256 products of the fused kernels' tiled tensors: one accumulator
+        # (aon_gemm f16_single) with dY at the chain's scale and X at the forward's 2^3, the
+        # scales both kernels range-guard their own splits at
+        single = not bf16 and a_t and b_t and n_out == 256 and n_in == 256
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
-             b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=1.0, b_scale=1.0 if bf16 else acts,
-             rowsum=db, a_amax=None if bf16 else work, mma_bf16=bf16, a_tiled=a_t, b_tiled=b_t,
-             n_store=n_store)
+             b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=1.0,
+             b_scale=1.0 if bf16 else (8.0 if single else acts), rowsum=db,
+             a_amax=None if bf16 else work, mma_bf16=bf16, a_tiled=a_t, b_tiled=b_t,
+             n_store=n_store, f16_single=single)
 
     # bf16: the eight 256 x 256 products (bottleneck, pts_linears.1-7) run as one aon_gemm_batch
     touched = [dzv, dzb, dz, draw, work, enc, venc, bot, hv, *h, *(t for wb in G for t in wb)]

@@ -157,6 +157,21 @@ BF16_TRUNK = False
 # mode 2); the deformation MLP, trunk, density and bottleneck stay fp16x3.  Off: 2% of the step
 # (9.85 vs 10.08 ms) for deformation gradients at cosine 0.9968 (0.99983 with it off)
 BF16_VIEW = False
+# bf16 mode, forward numerics (when BF16_TRUNK and BF16_VIEW are False): True runs every layer
+# past the deformation MLP two fp16 MFMAs per product -- the weights rounded once to fp16 (2^-11
+# relative, 8x finer than bf16), the activations' exact fp16 hi / lo split kept (the kArtMix
+# stream with fp16 compact blocks, aon_mlp_art_pack_mixed mode 3); the deformation MLP stays
+# fp16x3
+F16_WEIGHTS = False
+# bf16 mode, forward numerics (when the flags above are False): True runs every layer past the
+# deformation MLP two fp16 MFMAs per product the other way round -- the weights' exact 22-bit
+# hi / lo split kept, the activations rounded once to fp16 per sample (2^-11 relative; the
+# plain fp16x3 stream, aon_mlp_art_fwd_train_bf16 mixed 4).  Per-sample rounding averages out
+# (Default: the backward already reads every kept activation rounded to bf16, 8x coarser than
+# this forward's fp16 rounding; C5 gradients cosine 0.99919 / max-rel 0.049 against the fp32
+# oracle at the unchanged 0.999 / 0.05 gates, step 9.5 ms against 10.0-10.5 fp16x3.  Weights
+# rounded instead, F16_WEIGHTS: 0.99886 / 0.074, outside them.)
+F16_ACTS = True
 
 _packed = {}
 
@@ -188,7 +203,7 @@ def _pack(geo, P, lat, tag="", mixed=0):
     """The fused kernel's fp16x3 weight stream (aon_mlp_art_pack) of one level's parameters with
     this call's latent codes folded into the biases; re-packed on every call (the optimizer
     updates the parameters in place).  mixed: the bf16 mode's mixed streams
-    (aon_mlp_art_pack_mixed: 1 trunk bf16, 2 view branch bf16; range-guarded, their deformation
+    (aon_mlp_art_pack_mixed: 1 trunk bf16, 2 view branch bf16, 3 fp16 weights; range-guarded, their deformation
     part is fp16x3)."""
     shape, app, art = lat
     dev = shape.device
@@ -236,8 +251,9 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     hv = torch.empty((4, NR, geo.wc), device=dev, dtype=dt)
     enc = torch.empty((R, geo.ne), device=dev)
     xyz = torch.empty((R, 3), device=dev)
-    mixed = (1 if BF16_TRUNK else 2 if BF16_VIEW else 0) if bf16 else 0
-    packed = _pack(geo, P, lat, S, mixed)
+    mixed = (1 if BF16_TRUNK else 2 if BF16_VIEW else 3 if F16_WEIGHTS else 4 if F16_ACTS else 0
+             ) if bf16 else 0
+    packed = _pack(geo, P, lat, S, mixed if mixed != 4 else 0)  # 4: the fp16x3 stream
     e0 = _train._ev()
     args = (L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs), L.ptr(t_vals), B, S,
             L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h), L.ptr(bot),
@@ -403,12 +419,17 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
         # bf16: one bf16 MFMA per product, no scales (bf16 has fp32's exponent range)
         dW = G[i][0]
         b_t = (h_tiled and X is not enc and X is not venc and X is not xyz) or X is enc_bf
+        # f16x3, the 256 x 256 products of the fused kernels' tiled tensors: one accumulator
+        # (aon_gemm f16_single), dY at the chain's scale, X at the forward's 2^3 (train.py)
+        single = (not bf16 and chain_scale and a_t and b_t and dW.shape[0] == 256
+                  and n_in == 256 and col0 == 0 and ldx == 256)
         gemm(dW[:, col0:] if col0 else dW, dY, X, dW.shape[0], n_in, R, lda=ldy, a_kc=False,
              ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0),
-             a_scale=1.0 if (chain_scale or bf16) else gs, b_scale=1.0 if bf16 else acts,
+             a_scale=1.0 if (chain_scale or bf16) else gs,
+             b_scale=1.0 if bf16 else (8.0 if single else acts),
              rowsum=G[i][1] if bias else None,
              a_amax=work if (chain_scale and not bf16) else None, mma_bf16=bf16, a_tiled=a_t,
-             b_tiled=b_t, n_store=n_store)
+             b_tiled=b_t, n_store=n_store, f16_single=single)
 
     def dlatent(i, col0, l, dl, accumulate):
         # (bf16 mode: the exact-fp32 tiny-product path)

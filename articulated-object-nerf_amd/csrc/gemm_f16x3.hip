@@ -1383,6 +1383,239 @@ __global__ __launch_bounds__(THREADS2, 2) void k_gemm_bf16_dma256_batch(ParamsBa
   dma256_body(pb.p[b], 0, 0, z, smem);
 }
 
+// ---- fp16x3 weight gradients in one 256 x 256 tile per workgroup, ONE fp32 accumulator
+// (aon_gemm_args.f16_single): the parity mode's 256 x 256 products dW = dY^T X of the fused
+// training kernels' tiled fp32 tensors (pts_linears, bottleneck).  k_gemm_f16x3 runs them as a
+// 2 x 2 grid of 128 x 128 tiles with two accumulators per tile (hi*hi and the 2^11-scaled cross
+// terms), each operand byte staged into two workgroups; at 0.57 ms per fine-level product it was
+// at 0.21 of the MFMA peak.  Here the operands carry the fused kernels' own scales -- A (dY) at
+// the backward chain's per-call gradient scale, B (the activations) at 2^3 -- where the lo parts
+// x s - fp16(x s) stay normal fp16 for |x s| >= 2^-3 (below it they keep an absolute 2^-25), so
+// hi*hi + hi*lo + lo*hi share one accumulator (the fused MLP kernels' V2 numerics) and a wave's
+// 64 x 128 sub-tile fits in 128 accumulator VGPRs.  The caller guarantees |x s| < 65504 for both
+// operands (the chain and the forward range-guard their own splits at exactly these scales).
+// 512 threads = 8 waves in 4 (m) x 2 (n), one workgroup per CU.  Per 32-row k-tile each thread
+// loads two 32-B runs of each operand (a wave reads 2 KB contiguous of the tiled layout), splits
+// them once into fp16 hi / lo and writes them (16-B stores) into [32 k][256 col] planes with
+// the bf16 kernels' XOR swizzle, from which the MFMA fragments come by ds_read_b64_tr_b16; two
+// LDS stages (128 KB), the split of tile kt + 1 and the loads of tile kt + 2 ride between the
+// MFMAs of tile kt, one barrier per k-tile.  rowsum: A's fp32 values in row order per thread,
+// then a fixed order over the 16 threads of a column run.
+#ifndef AON_F1_ROWS_LDS
+#define AON_F1_ROWS_LDS 0  // 1: A/B build -- the row sums in LDS instead of 8 VGPRs
+#endif
+#ifndef AON_F1_PUB0
+#define AON_F1_PUB0 0  // the j-steps of a k-tile's MFMAs after which the next tile's runs 0 / 1
+#endif                 // are published (and their registers refilled with the tile after)
+#ifndef AON_F1_PUB1
+#define AON_F1_PUB1 1
+#endif
+constexpr int F1_PLANE = BK * 512;  // bytes of one [32 k][256 col] fp16 plane
+constexpr int F1_STAGE = 4 * F1_PLANE;  // A hi, A lo, B hi, B lo
+
+__device__ __forceinline__ h8 f1_frag(const char* plane, int c0, int lane) {
+  return __builtin_bit_cast(h8, tt_frag2(plane, c0, lane));
+}
+
+// one thread's two 32-B runs of a k-tile of a tiled fp32 operand of width 256: k rows r and
+// 16 + r of the tile, columns cc .. cc + 7
+struct F1Run {
+  f4 v[2][2];
+  // run i (k row 16 i + r of the tile)
+  __device__ __forceinline__ void load(const float* base, int64_t k0, int64_t kend, int tid, int i) {
+    const int r = (tid & 31) >> 1;
+    const f4* src = reinterpret_cast<const f4*>(base + k0 * 256 + 8 * (tid + 512 * i));
+    if (k0 + 16 * i + r < kend) {
+      v[i][0] = src[0];
+      v[i][1] = src[1];
+    } else {
+      v[i][0] = f4{0.f, 0.f, 0.f, 0.f};
+      v[i][1] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  // split run i at scale s into the hi / lo planes (16-B stores)
+  __device__ __forceinline__ void store(char* hi, char* lo, float s, int tid, int i) const {
+    const int r = (tid & 31) >> 1, ch = 2 * (tid >> 5) + (tid & 1);
+    h8 h, l;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = v[i][e >> 2][e & 3] * s;  // power of two: exact
+      const _Float16 hh = static_cast<_Float16>(x);
+      h[e] = hh;
+      l[e] = static_cast<_Float16>(__fsub_rn(x, static_cast<float>(hh)));  // exact in fp32
+    }
+    const int off = tt_off2(16 * i + r, ch);
+    *reinterpret_cast<h8*>(hi + off) = h;
+    *reinterpret_cast<h8*>(lo + off) = l;
+  }
+  // run i added to the thread's 8 running column sums, in row order
+  __device__ __forceinline__ void add_rows(float (&rs)[8], int i) const {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rs[e] = __fadd_rn(rs[e], v[i][e >> 2][e & 3]);
+  }
+  __device__ __forceinline__ void add_rows(f4* rs, int i) const {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f4 a = rs[h];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = __fadd_rn(a[e], v[i][h][e]);
+      rs[h] = a;
+    }
+  }
+};
+
+// INTER: split-K by interleaved k-tiles (a lone product), else contiguous chunks (a batch)
+template <bool INTER>
+__device__ __forceinline__ void f1_256_body(const Params& p, int z, char* smem) {
+  float sa = p.sa, inv_s = p.inv_s;
+  if (p.sa_bits) {
+    const float gs = grad_scale(*p.sa_bits);
+    sa = __fmul_rn(sa, gs);
+    inv_s = __fdiv_rn(inv_s, gs);
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // INTER: workgroup z takes k-tiles z, z + zsplit, z + 2 zsplit, ... so a lone product's
+  // workgroups read one contiguous run of zsplit k-tiles at a time (its contiguous chunks put
+  // 256 read streams a fixed multiple of 3 MB apart: 0.51-0.54 ms against 0.45-0.48 interleaved;
+  // a batch's 8 products x 32 chunks measured the other way round, 3.08-3.17 ms contiguous
+  // against 3.57-3.71 interleaved, profiles/r05/f1_ab)
+  const int64_t ntiles = (p.K + BK - 1) / BK, zs = INTER ? p.zsplit : 1;
+  const int64_t kbeg = INTER ? 0 : (int64_t)z * p.kchunk;
+  const int64_t kend = INTER ? p.K : (kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K);
+  const int64_t t0 = INTER ? z : kbeg / BK;  // first k-tile; then every zs-th
+  const int nk = INTER ? (z < ntiles ? static_cast<int>((ntiles - 1 - z) / zs + 1) : 0)
+                       : static_cast<int>((kend - kbeg + BK - 1) / BK);
+  const bool want_rows = p.rowsum != nullptr;
+#if AON_F1_ROWS_LDS
+  f4* rs = reinterpret_cast<f4*>(smem + 2 * F1_STAGE) + 2 * tid;  // this thread's column sums
+  if (want_rows) rs[0] = rs[1] = f4{0.f, 0.f, 0.f, 0.f};
+#else
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#endif
+  F1Run ra, rb;
+  auto load = [&](int kt, int i) {
+    const int64_t k0 = (t0 + (int64_t)kt * zs) * BK;
+    ra.load(p.A, k0, kend, tid, i);
+    rb.load(p.B, k0, kend, tid, i);
+  };
+  // publish run i of both operands to stage st (and A's values to the row sums, in row order)
+  auto publish = [&](int st, int i) {
+    char* s = smem + st * F1_STAGE;
+    if (want_rows) ra.add_rows(rs, i);
+    ra.store(s, s + F1_PLANE, sa, tid, i);
+    rb.store(s + 2 * F1_PLANE, s + 3 * F1_PLANE, p.sb, tid, i);
+  };
+  f4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    load(0, 0);
+    load(0, 1);
+    publish(0, 0);
+    publish(0, 1);
+    if (nk > 1) {
+      load(1, 0);
+      load(1, 1);
+    }
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* s = smem + (kt & 1) * F1_STAGE;
+    const bool more = kt + 1 < nk;
+    h8 ah[4], al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = f1_frag(s, 8 * wm + 2 * i, lane);
+      al[i] = f1_frag(s + F1_PLANE, 8 * wm + 2 * i, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const h8 bh = f1_frag(s + 2 * F1_PLANE, 16 * wn + 2 * j, lane);
+      const h8 bl = f1_frag(s + 3 * F1_PLANE, 16 * wn + 2 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i][j] = mfma16(ah[i], bh, acc[i][j]);
+        acc[i][j] = mfma16(ah[i], bl, acc[i][j]);
+        acc[i][j] = mfma16(al[i], bh, acc[i][j]);
+      }
+      // tile kt + 1 (in registers) into the other stage between the MFMAs, each run's
+      // registers refilled with tile kt + 2's at once: its loads fly under a whole k-tile
+      if (more && (j == AON_F1_PUB0 || j == AON_F1_PUB1)) {
+        const int i = j == AON_F1_PUB0 ? 0 : 1;
+        publish((kt + 1) & 1, i);
+        if (kt + 2 < nk) load(kt + 2, i);
+      }
+    }
+    __syncthreads();
+  }
+  const bool split = p.zsplit > 1;
+  if (want_rows) {
+    // thread t holds columns 16 (t >> 5) + 8 (t & 1) .. + 7 of rows r = (t & 31) >> 1 (+ 16 j);
+    // combine the 16 r in order (LDS free after the last barrier)
+    float* red = reinterpret_cast<float*>(smem);  // [16 r][256]
+    const int r = (tid & 31) >> 1, c = 16 * (tid >> 5) + 8 * (tid & 1);
+#if AON_F1_ROWS_LDS
+    const f4 s0 = rs[0], s1 = rs[1];
+    __syncthreads();  // every thread has its sums before red overwrites stage 0
+#else
+    const f4 s0 = {rs[0], rs[1], rs[2], rs[3]}, s1 = {rs[4], rs[5], rs[6], rs[7]};
+#endif
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[r * 256 + c + e] = s0[e];
+      red[r * 256 + c + 4 + e] = s1[e];
+    }
+    __syncthreads();
+    if (tid < 256) {
+      float v = red[tid];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) v = __fadd_rn(v, red[q * 256 + tid]);
+      if (split) p.rowsum_part[(int64_t)z * p.M + tid] = v;
+      else p.rowsum[tid] = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t n = wn * 128 + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        float v = __fmul_rn(acc[i][j][r], inv_s);
+        if (split) {
+          p.part[((int64_t)z * p.M + m) * p.N + n] = v;
+          continue;
+        }
+        float* c = p.C + m * p.ldc + n;
+        if (p.accumulate) v = __fadd_rn(*c, v);
+        *c = v;
+      }
+    }
+}
+
+constexpr int F1_LDS = 2 * F1_STAGE + (AON_F1_ROWS_LDS ? THREADS2 * 32 : 0);  // + the row sums
+
+__global__ __launch_bounds__(THREADS2, 1) void k_gemm_f1_256(Params p) {
+  __shared__ __align__(16) char smem[F1_LDS];
+  int tile, z;
+  if (!split_of(p, tile, z)) return;
+  f1_256_body<true>(p, z, smem);
+}
+
+// a batch of them over the same K (one level's 256 x 256 weight gradients): chunk z of every
+// product on one XCD, as k_gemm_bf16_dma256_batch
+__global__ __launch_bounds__(THREADS2, 1) void k_gemm_f1_256_batch(ParamsBatch pb) {
+  __shared__ __align__(16) char smem[F1_LDS];
+  const int T = pb.count, L = blockIdx.x, x = L & 7, q = L >> 3;
+  const int z = 8 * (q / T) + x, b = q - (q / T) * T;
+  if (z >= pb.zsplit) return;  // padding block of the last chunk group (uniform exit)
+  f1_256_body<false>(pb.p[b], z, smem);
+}
+
 // ---- fp16x3 weight gradients on the LDS-DMA ring (fp32 operands, both reduction-major):
 // k_gemm_f16x3<false, false> staged each k-tile through registers (global loads -> transpose ->
 // split -> LDS), one tile ahead, and ran the fine level's 256 x 256 x 790k products at ~3 TB/s
@@ -1581,7 +1814,10 @@ __global__ __launch_bounds__(THREADS, 1) void k_gemm_f16x3_dma(Params p) {
 // a wave reads two whole 16 x 16 tiles, 1 KB contiguous, of the tiled layout); A's M values of
 // the row rounded to bf16 as the MFMA paths stage them, products exact in fp32, fp32 sums in
 // row order, then a fixed xor tree over the 16 row phases; one chunk's partial per workgroup
-// (k_gemm_reduce sums the chunks in z order: deterministic).
+// (k_gemm_reduce sums the chunks in z order: deterministic).  TB = float: the parity mode's
+// heads (fp32 A and B, the fused forward's tiled fp32 h7 / hv3), the same kernel with nothing
+// rounded -- fp32 products and sums, more accurate than the fp16x3 split it replaces for M <= 4
+// (a 128 x 128 tile 97-99% empty, 0.23-0.28 ms per fine-level head).
 constexpr int kSkinnyRows = 16;
 #ifndef AON_GEMM_SKINNY_SK
 #define AON_GEMM_SKINNY_SK 4  // rows in flight per thread of the skinny kernel; 1: A/B
@@ -1594,14 +1830,16 @@ constexpr int kSkinnyRows = 16;
 #define AON_GEMM_SKINNY_SK2 4  // ... of the skinny kernel on B of <= 128 columns (A/B knob: 8 measured
                                // 81 -> 108 us on the fine level's rgb head, profiles/r04/final2)
 #endif
-template <int M, typename TA, bool BT, int SK = AON_GEMM_SKINNY_SK>
+template <int M, typename TA, bool BT, int SK = AON_GEMM_SKINNY_SK, typename TB = __bf16>
 __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
+  constexpr bool RND = std::is_same<TB, __bf16>::value;  // the bf16 mode: A staged as bf16
+  constexpr int NB = sizeof(TB) / 2;                      // 16-B loads per 8-column run of B
   const int tid = threadIdx.x, r = tid & 15, cg = tid >> 4;
   const int64_t n0 = 8 * (int64_t)cg;
   const int64_t kbeg = (int64_t)blockIdx.x * p.kchunk;
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
   const TA* A = reinterpret_cast<const TA*>(p.A);
-  const __bf16* B = reinterpret_cast<const __bf16*>(p.B);
+  const TB* B = reinterpret_cast<const TB*>(p.B);
   float acc[M][8], rs[M], cs[8];  // cs: B's column sums (c_trans)
   const bool ct = p.c_trans != 0;
 #pragma unroll
@@ -1616,22 +1854,37 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
     return BT ? (k & ~int64_t(15)) * p.ldb + 256 * (n0 >> 4) + 16 * (k & 15) + (n0 & 15)
               : k * p.ldb + n0;
   };
-  auto row = [&](const uint4& bv, const TA* ar) {
-    const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
+  auto row = [&](const uint4 (&bv)[NB], const TA* ar) {
     float b[8];
+    if (RND) {
+      const uint32_t bw[4] = {bv[0].x, bv[0].y, bv[0].z, bv[0].w};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) b[j] = __uint_as_float((j & 1) ? (bw[j >> 1] & 0xffff0000u) : (bw[j >> 1] << 16));
+      for (int j = 0; j < 8; ++j) b[j] = __uint_as_float((j & 1) ? (bw[j >> 1] & 0xffff0000u) : (bw[j >> 1] << 16));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint4& q = bv[(j >> 2) & (NB - 1)];
+        const uint32_t w = (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
+        b[j] = __uint_as_float(w);
+      }
+    }
     if (ct) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) cs[j] = __fadd_rn(cs[j], b[j]);
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const float a = static_cast<float>(static_cast<__bf16>(static_cast<float>(ar[m])));
+      const float a = RND ? static_cast<float>(static_cast<__bf16>(static_cast<float>(ar[m])))
+                          : static_cast<float>(ar[m]);
       rs[m] = __fadd_rn(rs[m], a);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[m][j] = fmaf(a, b[j], acc[m][j]);  // a * b exact in fp32
+      for (int j = 0; j < 8; ++j) acc[m][j] = fmaf(a, b[j], acc[m][j]);  // bf16: a * b exact
     }
+  };
+  auto load_b = [&](int64_t kk, uint4 (&bv)[NB]) {
+    const uint4* src = reinterpret_cast<const uint4*>(B + boff(kk));
+#pragma unroll
+    for (int h = 0; h < NB; ++h) bv[h] = src[h];
   };
   // SK rows per thread in flight: their loads are issued before the first is consumed (one
   // dependent load per row left this kernel latency-bound: rgb's 0.27 GB at ~2.2 TB/s); the
@@ -1639,11 +1892,11 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
   // per workgroup)
   int64_t k = kbeg + r;
   for (; k + (SK - 1) * kSkinnyRows < kend; k += SK * kSkinnyRows) {
-    uint4 bv[SK];
+    uint4 bv[SK][NB];
     TA av[SK][M];
 #pragma unroll
     for (int u = 0; u < SK; ++u) {
-      bv[u] = *reinterpret_cast<const uint4*>(B + boff(k + u * kSkinnyRows));
+      load_b(k + u * kSkinnyRows, bv[u]);
 #pragma unroll
       for (int m = 0; m < M; ++m) av[u][m] = A[(k + u * kSkinnyRows) * p.lda + m];
     }
@@ -1654,7 +1907,9 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
     TA av[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) av[m] = A[k * p.lda + m];
-    row(*reinterpret_cast<const uint4*>(B + boff(k)), av);
+    uint4 bv[NB];
+    load_b(k, bv);
+    row(bv, av);
   }
   // the 16 row phases of a column group are lanes 16 q .. 16 q + 15 of one wave
 #pragma unroll
@@ -1708,7 +1963,8 @@ __global__ __launch_bounds__(512) void k_gemm_skinny_bf16(Params p) {
 // to LDS, and their outer products with bf16(B) make the chunk's partial of C (and of A's
 // column sums).  The km kernel read A with the reduction-major transposing loads at ~130 us for
 // the fine level's 0.2 GB; this reads A once, in 16-B runs, and does 1/rdiv of the products.
-template <typename TA, typename TB, bool AT>
+// RND = false: the parity mode's (fp32 A and B), nothing rounded -- fp32 sums and products.
+template <typename TA, typename TB, bool AT, bool RND = true>
 __global__ __launch_bounds__(256) void k_gemm_segsum_bf16(Params p) {
   __shared__ float seg[256 * 8];  // [RB rays][M]: RB * M = 8 * 256
   const int M = static_cast<int>(p.M), N = static_cast<int>(p.N);
@@ -1738,7 +1994,35 @@ __global__ __launch_bounds__(256) void k_gemm_segsum_bf16(Params p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = __fadd_rn(acc[j], v[j]);
   };
+  // fp32 A unrounded: one row's 8 columns as two 16-B loads
+  auto add_row32 = [&](const uint4 (&w)[2]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint4& q = w[j >> 2];
+      const uint32_t u = (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
+      acc[j] = __fadd_rn(acc[j], __uint_as_float(u));
+    }
+  };
   int64_t k = kb;
+  if (!RND && std::is_same<TA, float>::value) {
+    constexpr int SK = AON_GEMM_SEGSUM_SK / 2;
+    for (; k + SK - 1 < ke; k += SK) {
+      uint4 w[SK][2];
+#pragma unroll
+      for (int u = 0; u < SK; ++u) {
+        const uint4* src = reinterpret_cast<const uint4*>(A + aoff(k + u));
+        w[u][0] = src[0];
+        w[u][1] = src[1];
+      }
+#pragma unroll
+      for (int u = 0; u < SK; ++u) add_row32(w[u]);
+    }
+    for (; k < ke; ++k) {
+      const uint4* src = reinterpret_cast<const uint4*>(A + aoff(k));
+      const uint4 w[2] = {src[0], src[1]};
+      add_row32(w);
+    }
+  }
   if (std::is_same<TA, __bf16>::value) {
     // AON_GEMM_SEGSUM_SK rows' 16-B loads in flight per thread before the first is summed (one
     // dependent load per row left one workgroup of 4 waves per CU latency-bound; 4 rows still
@@ -1773,7 +2057,8 @@ __global__ __launch_bounds__(256) void k_gemm_segsum_bf16(Params p) {
     if (e < M * N) {
       const int m = e / N, n = e - m * N;
       for (int q = 0; q < nr; ++q) {
-        const float b = static_cast<float>(static_cast<__bf16>(static_cast<float>(Bm[(ray0 + q) * p.ldb + n])));
+        const float b = RND ? static_cast<float>(static_cast<__bf16>(static_cast<float>(Bm[(ray0 + q) * p.ldb + n])))
+                            : static_cast<float>(Bm[(ray0 + q) * p.ldb + n]);
         v = fmaf(seg[q * M + m], b, v);
       }
       if (split) {
@@ -1897,15 +2182,15 @@ __global__ __launch_bounds__(256) void k_gemm_small_batch(SmallBatch sb) {
   if (!wave || lane == 0) *c = acc;
 }
 
-template <typename TA, bool BT>
+template <typename TA, bool BT, typename TB = __bf16>
 static void launch_skinny(const Params& p, dim3 grid, hipStream_t st) {
   const dim3 block((unsigned)(2 * p.N));  // 16 row phases x N / 8 column groups
   constexpr int SK = AON_GEMM_SKINNY_SK, SK2 = AON_GEMM_SKINNY_SK2;
   const bool narrow = p.N <= 128;
   switch (p.M) {
-#define AON_SKINNY_L(M_)                                                                        \
-  if (narrow) hipLaunchKernelGGL((k_gemm_skinny_bf16<M_, TA, BT, SK2>), grid, block, 0, st, p); \
-  else hipLaunchKernelGGL((k_gemm_skinny_bf16<M_, TA, BT, SK>), grid, block, 0, st, p)
+#define AON_SKINNY_L(M_)                                                                            \
+  if (narrow) hipLaunchKernelGGL((k_gemm_skinny_bf16<M_, TA, BT, SK2, TB>), grid, block, 0, st, p); \
+  else hipLaunchKernelGGL((k_gemm_skinny_bf16<M_, TA, BT, SK, TB>), grid, block, 0, st, p)
     case 1: AON_SKINNY_L(1); break;
     case 2: AON_SKINNY_L(2); break;
     case 3: AON_SKINNY_L(3); break;
@@ -1945,12 +2230,17 @@ static bool bf16_copy256_path(const aon_gemm_args* a) {
          a->N % BM2 == 0;
 }
 
-// bf16 weight gradient of at most 4 rows on a bf16 B of up to 256 columns (k_gemm_skinny_bf16)
+// weight gradient of at most 4 rows on a B of up to 256 columns (k_gemm_skinny_bf16): the bf16
+// mode's (B bf16), or the parity mode's in exact fp32 (A and B fp32, no epilogue)
+static bool skinny32(const aon_gemm_args* a) {
+  return !a->mma_bf16 && !a->a_bf16 && !a->b_bf16 && !a->a_kc && !a->b_kc && !a->A2 &&
+         !a->bias && !a->mask && !a->relu && !a->exact_fp32;
+}
 static bool skinny_path(const aon_gemm_args* a) {
   const int64_t b_rdiv = a->b_kc ? 1 : a->b_rdiv;
-  return a->mma_bf16 && a->M >= 1 && a->M <= 4 && a->b_bf16 && !a->a_tiled && b_rdiv == 1 &&
-         a->N % 8 == 0 && a->N <= 256 && aligned16(a->B) && a->ldb % 8 == 0 && !a->k_splits &&
-         (a->n_store == 0 || a->n_store == a->N);
+  return ((a->mma_bf16 && a->b_bf16) || skinny32(a)) && a->M >= 1 && a->M <= 4 && !a->a_tiled &&
+         b_rdiv == 1 && a->N % 8 == 0 && a->N <= 256 && aligned16(a->B) && a->ldb % 8 == 0 &&
+         !a->k_splits && (a->n_store == 0 || a->n_store == a->N);
 }
 
 // tiny fp32 products (k_gemm_small_f32)
@@ -1960,11 +2250,12 @@ static bool small_path(const aon_gemm_args* a) {
          !a->k_splits && (a->n_store == 0 || a->n_store == a->N);
 }
 
-// bf16 weight gradient against a per-ray B (rdiv > 1): k_gemm_segsum_bf16
+// weight gradient against a per-ray B (rdiv > 1): k_gemm_segsum_bf16 -- the bf16 mode's, or
+// the parity mode's in exact fp32 (as skinny32)
 static bool segsum_path(const aon_gemm_args* a) {
-  return a->mma_bf16 && !a->a_kc && !a->b_kc && a->b_rdiv > 1 && !a->b_tiled && a->M % 8 == 0 &&
-         a->M >= 8 && a->M <= 256 && aligned16(a->A) && a->lda % 8 == 0 && !a->k_splits &&
-         (a->n_store == 0 || a->n_store == a->N);
+  return (a->mma_bf16 || skinny32(a)) && !a->a_kc && !a->b_kc && a->b_rdiv > 1 && !a->b_tiled &&
+         a->M % 8 == 0 && a->M >= 8 && a->M <= 256 && aligned16(a->A) && a->lda % 8 == 0 &&
+         !a->k_splits && (a->n_store == 0 || a->n_store == a->N);
 }
 
 // fp32 reduction-major x reduction-major weight gradients in whole 128 x 128 tiles with 16-B
@@ -1979,10 +2270,20 @@ static bool f16_copy_path(const aon_gemm_args* a) {
          b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) && a->lda % 4 == 0 && a->ldb % 4 == 0;
 }
 
+// fp32 reduction-major x reduction-major 256 x 256 weight gradients of the fused kernels' tiled
+// tensors with the caller's single-accumulator licence (f16_single): k_gemm_f1_256
+static bool f1_256_path(const aon_gemm_args* a) {
+  return a->f16_single && !a->mma_bf16 && !a->a_bf16 && !a->b_bf16 && !a->a_kc && !a->b_kc &&
+         !a->A2 && !a->bias && !a->mask && !a->relu && !a->exact_fp32 && !a->c_trans &&
+         a->a_tiled && a->b_tiled && a->M == BM2 && a->N == BM2 && a->lda == BM2 &&
+         a->ldb == BM2 && a->b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) &&
+         (a->n_store == 0 || a->n_store == a->N) && a->K >= 8 * 1024;
+}
+
 static int64_t gemm_splits(const aon_gemm_args* a) {
   const int64_t tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
   if (small_path(a)) return 1;
-  if (bf16_copy256_path(a) && a->k_splits <= 0) {
+  if ((bf16_copy256_path(a) || f1_256_path(a)) && a->k_splits <= 0) {
     // one workgroup per CU: 256 K chunks of a single 256 x 256 tile (chunks of >= 1024 rows;
     // the coarse level's 266k rows still fill the chip -- 2048-row chunks left half of it idle)
     const int64_t t2 = (a->M / BM2) * (a->N / BM2);
@@ -2060,7 +2361,7 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
               "n_store < N: the bf16 LDS-DMA weight-gradient path only (both operands bf16, "
               "M and N multiples of 128)");
   if (a->M == 0 || a->N == 0) return 0;
-  AON_REQUIRE(!a->c_trans || skinny_path(a), "c_trans: the bf16 skinny path only (M <= 4, B bf16)");
+  AON_REQUIRE(!a->c_trans || skinny_path(a), "c_trans: the skinny path only (M <= 4)");
   Params p;
   p.c_trans = a->c_trans;
   p.a_tiled = a->a_tiled;
@@ -2091,7 +2392,8 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     p.part = static_cast<float*>(work);
     p.rowsum_part = p.part + zs * a->M * a->N;
   }
-  const bool t256 = a->mma_bf16 && bf16_copy256_path(a);
+  const bool f1 = f1_256_path(a);
+  const bool t256 = (a->mma_bf16 && bf16_copy256_path(a)) || f1;
   const int64_t bmt = t256 ? BM2 : BM;  // C tile edge of the kernel that runs
   const int64_t tiles_m = (a->M + bmt - 1) / bmt, tiles_n = (a->N + bmt - 1) / bmt;
   const int64_t gm = tiles_m < 8 ? tiles_m : 8;
@@ -2146,6 +2448,16 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     else if (a->a_bf16) launch_bf<__bf16, float>(p, va16, vb16, grid, st);
     else if (a->b_bf16) launch_bf<float, __bf16>(p, va16, vb16, grid, st);
     else launch_bf<float, float>(p, va16, vb16, grid, st);
+  } else if (segsum_path(a)) {  // the parity mode's, exact fp32
+    const dim3 g((unsigned)zs, 1, 1);
+    if (a->a_tiled) hipLaunchKernelGGL((k_gemm_segsum_bf16<float, float, true, false>), g, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm_segsum_bf16<float, float, false, false>), g, dim3(256), 0, st, p);
+  } else if (skinny_path(a)) {  // the parity mode's, exact fp32
+    const dim3 g((unsigned)zs, 1, 1);
+    if (a->b_tiled) launch_skinny<float, true, float>(p, g, st);
+    else launch_skinny<float, false, float>(p, g, st);
+  } else if (f1) {
+    hipLaunchKernelGGL(k_gemm_f1_256, grid, dim3(THREADS2), 0, st, p);
   } else if (f16_copy_path(a)) {
     hipLaunchKernelGGL(k_gemm_f16x3_dma, grid, dim3(THREADS), 0, st, p);
   } else if (a->a_kc && a->b_kc) launch_v<true, true>(p, va, vb, grid, st);
@@ -2167,10 +2479,12 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
 // ---- aon_gemm_batch: one level's bf16 weight gradients in two launches (+ their reduces):
 // the one-tile 256 x 256 products on k_gemm_bf16_dma256_batch, the other whole-128 x 128-tile
 // products on k_gemm_bf16_dma_batch; any other product runs as aon_gemm.
-enum { kBatchNone = 0, kBatch256 = 1, kBatch128 = 2, kBatchF16 = 3 };
+enum { kBatchNone = 0, kBatch256 = 1, kBatch128 = 2, kBatchF16 = 3, kBatchF1 = 4 };
+constexpr int kBatchClasses[] = {kBatchF1, kBatchF16, kBatch256, kBatch128};
 
 static int batch_class(const aon_gemm_args* a) {
   if (a->k_splits > 0 || a->K < 8 * 1024) return kBatchNone;
+  if (f1_256_path(a)) return kBatchF1;
   if (!a->mma_bf16) {
     // fp16x3 weight gradients dW = dY^T X: fp32 reduction-major operands in 16-B runs, whole
     // 128 x 128 tiles, no epilogue beyond accumulate (k_gemm_f16x3<false, false, true, true>)
@@ -2204,12 +2518,13 @@ static BatchPlan plan_class(const aon_gemm_args* a, int count, int cls) {
   if (pl.n < 2) { pl.n = 0; return pl; }
   for (int j = 0; j < pl.n; ++j) {
     const aon_gemm_args* g = &a[pl.idx[j]];
-    pl.tiles += cls == kBatch256 ? 1 : (g->M / BM) * (g->N / BN);
+    pl.tiles += cls == kBatch256 || cls == kBatchF1 ? 1 : (g->M / BM) * (g->N / BN);
   }
   // 256 x 256 tiles: one workgroup per CU (256 in all), chunks >= 1024 rows; 128 x 128 tiles:
   // two per CU (512), chunks >= 2048 rows -- each product's chunks longer by the batch size;
   // fp16x3: whole rounds of 512 as aon_gemm's split (two when K is long enough)
-  const int64_t wgs = cls == kBatch256 ? 256 : 512, minrows = cls == kBatch256 ? 1024 : 2048;
+  const bool one = cls == kBatch256 || cls == kBatchF1;  // one 256 x 256 tile, one WG per CU
+  const int64_t wgs = one ? 256 : 512, minrows = one ? 1024 : 2048;
   const int64_t cap = pl.K / minrows < 256 ? pl.K / minrows : 256;
   int64_t s = wgs / pl.tiles < cap ? wgs / pl.tiles : cap;
   if (cls == kBatchF16 && cap * pl.tiles >= 1024) s = 1024 / pl.tiles;
@@ -2232,15 +2547,29 @@ static bool in_plan(const BatchPlan& pl, int i) {
   return false;
 }
 
+// the batch's plans, one per class (kBatchClasses order)
+struct BatchPlans {
+  BatchPlan pl[4];
+  bool planned(int i) const {
+    for (const BatchPlan& p : pl)
+      if (in_plan(p, i)) return true;
+    return false;
+  }
+};
+static BatchPlans plan_all(const aon_gemm_args* a, int count) {
+  BatchPlans b;
+  for (int c = 0; c < 4; ++c) b.pl[c] = plan_class(a, count, kBatchClasses[c]);
+  return b;
+}
+
 extern "C" size_t aon_gemm_batch_workspace_bytes(const aon_gemm_args* a, int count) {
   if (!a || count < 1 || count > AON_GEMM_BATCH_MAX) return 0;
-  const BatchPlan p2 = plan_class(a, count, kBatch256), p1 = plan_class(a, count, kBatch128),
-                  pf = plan_class(a, count, kBatchF16);
+  const BatchPlans bp = plan_all(a, count);
   // the launches are stream-ordered: one workspace serves each in turn
-  size_t m = plan_bytes(a, p2) > plan_bytes(a, p1) ? plan_bytes(a, p2) : plan_bytes(a, p1);
-  m = plan_bytes(a, pf) > m ? plan_bytes(a, pf) : m;
+  size_t m = 0;
+  for (const BatchPlan& p : bp.pl) m = plan_bytes(a, p) > m ? plan_bytes(a, p) : m;
   for (int i = 0; i < count; ++i)
-    if (!in_plan(p2, i) && !in_plan(p1, i) && !in_plan(pf, i)) {
+    if (!bp.planned(i)) {
       const size_t b = aon_gemm_workspace_bytes(&a[i]);
       m = b > m ? b : m;
     }
@@ -2276,7 +2605,7 @@ static int run_plan(const aon_gemm_args* a, const BatchPlan& pl, int cls, void* 
     p.C = g->C; p.ldc = g->ldc;
     p.accumulate = g->accumulate;
     p.sa = p.sb = p.inv_s = 1.0f;
-    if (cls == kBatchF16) {
+    if (cls == kBatchF16 || cls == kBatchF1) {
       AON_REQUIRE(g->a_scale > 0.f && g->b_scale > 0.f, "operand scales must be positive");
       p.sa = g->a_scale; p.sb = g->b_scale; p.inv_s = 1.0f / (g->a_scale * g->b_scale);
       p.sa_bits = g->a_amax;
@@ -2284,7 +2613,7 @@ static int run_plan(const aon_gemm_args* a, const BatchPlan& pl, int cls, void* 
     p.kchunk = pl.kchunk;
     p.rowsum = g->rowsum;
     p.zsplit = (int)pl.zs;
-    const int bmt = cls == kBatch256 ? BM2 : BM;
+    const int bmt = cls == kBatch256 || cls == kBatchF1 ? BM2 : BM;
     p.tiles_m = (int)(g->M / bmt);
     p.tiles_n = (int)(g->N / bmt);
     p.gm = p.tiles_m;
@@ -2298,6 +2627,7 @@ static int run_plan(const aon_gemm_args* a, const BatchPlan& pl, int cls, void* 
   }
   const dim3 grid((unsigned)(8 * pb.tile0[pl.n] * ((pl.zs + 7) / 8)), 1, 1);
   if (cls == kBatch256) hipLaunchKernelGGL(k_gemm_bf16_dma256_batch, grid, dim3(THREADS2), 0, st, pb);
+  else if (cls == kBatchF1) hipLaunchKernelGGL(k_gemm_f1_256_batch, grid, dim3(THREADS2), 0, st, pb);
   else if (cls == kBatch128) hipLaunchKernelGGL(k_gemm_bf16_dma_batch, grid, dim3(THREADS), 0, st, pb);
   else hipLaunchKernelGGL(k_gemm_f16x3_batch, grid, dim3(THREADS), 0, st, pb);
   if (pl.zs > 1) {
@@ -2318,22 +2648,14 @@ extern "C" int aon_gemm_batch(const aon_gemm_args* a, int count, void* work, siz
                               aon_stream_t stream) {
   AON_REQUIRE(a && count >= 0 && count <= AON_GEMM_BATCH_MAX, "bad batch");
   hipStream_t st = (hipStream_t)stream;
-  const BatchPlan p2 = plan_class(a, count, kBatch256), p1 = plan_class(a, count, kBatch128),
-                  pf = plan_class(a, count, kBatchF16);
-  if (pf.n) {
-    const int rc = run_plan(a, pf, kBatchF16, work, work_bytes, st);
-    if (rc) return rc;
-  }
-  if (p2.n) {
-    const int rc = run_plan(a, p2, kBatch256, work, work_bytes, st);
-    if (rc) return rc;
-  }
-  if (p1.n) {
-    const int rc = run_plan(a, p1, kBatch128, work, work_bytes, st);
-    if (rc) return rc;
-  }
+  const BatchPlans bp = plan_all(a, count);
+  for (int c = 0; c < 4; ++c)
+    if (bp.pl[c].n) {
+      const int rc = run_plan(a, bp.pl[c], kBatchClasses[c], work, work_bytes, st);
+      if (rc) return rc;
+    }
   for (int i = 0; i < count; ++i)
-    if (!in_plan(p2, i) && !in_plan(p1, i) && !in_plan(pf, i)) {
+    if (!bp.planned(i)) {
       const int rc = aon_gemm(&a[i], work, work_bytes, stream);
       if (rc) return rc;
     }

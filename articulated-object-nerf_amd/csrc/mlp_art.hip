@@ -29,7 +29,13 @@ namespace mlp {
 // kArtMix stream, mlp_layout.hpp) -- the deformation MLP fp16x3 (x' = delta + xyz feeds
 // sin(2^9 x')), the trunk, heads and view branch one bf16 MFMA per product, or 3: the view
 // branch mixed (kArtMixV) -- everything through the bottleneck fp16x3, views_linear.0-3 and the
-// rgb head bf16 (the bottleneck's epilogue hands them bf16 fragments, layer_h OBF).
+// rgb head bf16 (the bottleneck's epilogue hands them bf16 fragments, layer_h OBF), or 4: the
+// kArtMix stream with fp16 weights in its compact blocks (aon_mlp_art_pack_mixed 3) -- the
+// deformation MLP fp16x3, every later layer two fp16 MFMAs per product, hi(W) x (hi(x) + lo(x)),
+// with the fp16x3 activations and epilogue (FragPipe W1), or 5: the fp16x3 stream
+// (aon_mlp_art_pack) with every layer past the deformation MLP two fp16 MFMAs per product the
+// other way round, (hi(W) + lo(W)) x hi(x): the weights exact to 22 bits, the activations
+// rounded once to fp16 per sample (FragPipe X1F).
 template <int MODE, int NCOL, bool STORE = false, int PREC = 0>
 __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_mlp_art_f16x3(
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, const float* __restrict__ in0,
@@ -39,6 +45,8 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   using Net = NetArtH;
   constexpr bool BFM = PREC == 2;
   constexpr bool BFV = PREC == 3;  // bf16 view branch (venc and the bottleneck's output in bf16)
+  constexpr bool F16W = PREC == 4;  // fp16 weights past the deformation MLP
+  constexpr int X1F = PREC == 5 ? kArtMix.hi : -1;  // fp16 activations past it
   constexpr int kStash = G::kWaves * 64 * 6 * NCOL;  // f4: enc 2 k-steps + venc 1, hi & lo
   __shared__ f4 smem[kLdsWeights + Net::kBiasFloats / 4 + kStash];
   float* bias_s = reinterpret_cast<float*>(smem + kLdsWeights);
@@ -50,7 +58,7 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
   const int64_t N = B * S;
 
   using WP = typename std::conditional<
-      BFM, DmaPipe<G::kThreads, kRing, kChunkH, kArtMixStream, kArtMixUsed, kRingLead>,
+      BFM || F16W, DmaPipe<G::kThreads, kRing, kChunkH, kArtMixStream, kArtMixUsed, kRingLead>,
       typename std::conditional<
           BFV, DmaPipe<G::kThreads, kRing, kChunkH, kArtMixVStream, kArtMixVUsed, kRingLead>,
           WeightPipe<Net, G::kThreads>>::type>::type;
@@ -109,7 +117,9 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
     stash[64 * (6 * c + 5)] = __builtin_bit_cast(f4, venc.lo[0][c]);
   }
 
-  FragPipe<WP, AON_PREFETCH, 0, false, 0, BFM ? kArtMix.hi : (BFV ? kArtMixV.hi : 0)> fp(p);
+  FragPipe<WP, AON_PREFETCH, 0, false, 0, BFM || F16W ? kArtMix.hi : (BFV ? kArtMixV.hi : 0), F16W,
+           X1F>
+      fp(p);
   static_assert(kArtMix.lo == 0 && kArtMixV.lo == 0, "mixed streams start fp16x3");
   fp.start();  // begin(0): chunk 0 landed; the barrier also publishes bias_s
   lds_float* bias_l = opaque_lds(bias_s + 4 * g);
@@ -247,10 +257,11 @@ static int art_pack(const aon_mlp_art_params* prm, void* packed, aon_stream_t st
   a.stream_blocks = NetArtH::kStreamBlocks;
   a.bias_floats = NetArtH::kBiasFloats;
   if (mixed) {
-    const StreamMap m = mixed == 1 ? kArtMix : kArtMixV;
+    const StreamMap m = mixed == 2 ? kArtMixV : kArtMix;
     a.bf16 = m.mode;
     a.mx_lo = m.lo;
     a.mx_hi = m.hi;
+    a.f16w = mixed == 3;
   }
   return pack_h(a, packed, (hipStream_t)stream);
 }
@@ -260,10 +271,12 @@ extern "C" int aon_mlp_art_pack(const aon_mlp_art_params* prm, void* packed, aon
 }
 
 // the articulated bf16 mode's mixed streams (same buffer size and bias table): mixed = 1 the
-// trunk-bf16 stream (= aon_mlp_art_pack_bf16), 2 the view-branch stream (kArtMixV)
+// trunk-bf16 stream (= aon_mlp_art_pack_bf16), 2 the view-branch stream (kArtMixV), 3 the
+// kArtMix map with fp16 weights in the compact blocks
 extern "C" int aon_mlp_art_pack_mixed(const aon_mlp_art_params* prm, int mixed, void* packed,
                                       aon_stream_t stream) {
-  AON_REQUIRE(mixed == 1 || mixed == 2, "mixed: 1 trunk bf16, 2 view branch bf16");
+  AON_REQUIRE(mixed >= 1 && mixed <= 3,
+              "mixed: 1 trunk bf16, 2 view branch bf16, 3 fp16 weights past the deformation MLP");
   return art_pack(prm, packed, stream, mixed);
 }
 
@@ -330,7 +343,15 @@ static int art_fwd_train(const void* packed, const float* rays_o, const float* r
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
   const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise, reinterpret_cast<uint2*>(masks), enc_bf};
-  if (prec == 3)
+  if (prec == 5)
+    hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 5>), (unsigned)grid, G::kThreads, 0,
+                       (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
+                       (int)AON_ACT_NONE, raw, ts);
+  else if (prec == 4)
+    hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 4>), (unsigned)grid, G::kThreads, 0,
+                       (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
+                       (int)AON_ACT_NONE, raw, ts);
+  else if (prec == 3)
     hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 3>), (unsigned)grid, G::kThreads, 0,
                        (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
                        (int)AON_ACT_NONE, raw, ts);
@@ -365,7 +386,8 @@ extern "C" int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_
                                           float* xyz, float* raw, uint32_t* masks, void* enc_bf,
                                           int mixed, aon_stream_t stream) {
   AON_REQUIRE(aligned16(enc_bf), "enc_bf must be 16-byte aligned");
-  AON_REQUIRE(mixed >= 0 && mixed <= 2, "mixed: 0 fp16x3, 1 trunk bf16, 2 view branch bf16");
+  AON_REQUIRE(mixed >= 0 && mixed <= 4,
+              "mixed: 0 fp16x3, 1 trunk bf16, 2 view branch bf16, 3 fp16 weights, 4 fp16 activations");
   return art_fwd_train(packed, rays_o, rays_d, viewdirs, t, B, S, noise, static_cast<float*>(hd),
                        static_cast<float*>(h), static_cast<float*>(bot), static_cast<float*>(hv),
                        enc, xyz, raw, masks, stream, mixed + 1, static_cast<__bf16*>(enc_bf));

@@ -235,7 +235,7 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
   const StreamMap map{a.bf16, a.mx_lo, a.mx_hi};
   // an all-bf16 stream never reports (no weight is range-tested): the status words are cleared
   // here instead of by a memset launch ahead of the pack (pack_h)
-  if (a.bf16 == 1 && blockIdx.x == 0 && threadIdx.x < kStatusBytes / 4)
+  if (a.bf16 == 1 && !a.f16w && blockIdx.x == 0 && threadIdx.x < kStatusBytes / 4)
     reinterpret_cast<uint32_t*>(bias_out + a.bias_floats)[threadIdx.x] = 0u;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -282,7 +282,7 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
           w = a.tr[li] ? src[(int64_t)col * ld + o] : src[(int64_t)o * ld + col];
       }
 #if AON_F16X3_V2
-      if (bf) {  // bf16 layer: bf16(w), unscaled, in the compact (hi-only) stream
+      if (bf && !a.f16w) {  // bf16 layer: bf16(w), unscaled, in the compact (hi-only) stream
         out[e] = bf_bits(w);
         continue;
       }
@@ -307,7 +307,8 @@ __global__ void k_pack_h(PackArgsH a, float* __restrict__ out_f) {
       // hidden layers add the bias at activation scale; the 1-tile heads at true scale
       // (bf16 layers: at true scale, their activations are unscaled)
       const StreamMap map{a.bf16, a.mx_lo, a.mx_hi};
-      const float bs = a.layers[li].u == 1 || !map.f16(a.layers[li].blk0) ? 1.0f : kActS;
+      const float bs =
+          a.layers[li].u == 1 || !(map.f16(a.layers[li].blk0) || a.f16w) ? 1.0f : kActS;
 #else
       const float bs = kActScale;
 #endif
@@ -321,7 +322,7 @@ int pack_h(PackArgsH a, void* packed, hipStream_t stream) {
   // the range-status word behind the bias table: cleared (stream-ordered) before the pack, which
   // sets it for an unrepresentable weight; the kernels reading the stream set it on overflow
   // (an all-bf16 stream: k_pack_h clears it itself, one launch fewer)
-  if (a.bf16 != 1) {
+  if (a.bf16 != 1 || a.f16w) {
     const hipError_t e = hipMemsetAsync(
         static_cast<char*>(packed) + (size_t)a.stream_blocks * 1024 + (size_t)a.bias_floats * 4, 0,
         kStatusBytes, stream);

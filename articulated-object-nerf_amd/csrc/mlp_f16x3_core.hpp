@@ -126,9 +126,19 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, uint
 // BF: bf16 numerics -- the compact stream (WeightPipeP) of hi blocks only.  MXL < MXH: the
 // mixed stream (StreamMap mode 2): layers in the fp16x3 blocks [MXL, MXH) run fp16x3, the
 // others bf16 (layer_h / head_h ask f16_block(d.blk0)).
-template <typename P, int D = AON_PREFETCH, int EOFF = 0, bool BF = false, int MXL = 0, int MXH = 0>
+// W1: the compact blocks of a mixed stream hold fp16 weights at the 2^6 weight scale (k_pack_h
+// f16w), not bf16 -- their layers run two fp16 MFMAs per product (hi(W) x hi(x) + hi(W) x lo(x):
+// the activations keep their exact hi / lo split, the weights round once to fp16) with the
+// fp16x3 epilogue.
+// X1F >= 0: the layers from fp16x3 block X1F on run two fp16 MFMAs per product the other way
+// round, (hi(W) + lo(W)) x hi(x) -- the weights keep their exact split, the activations round
+// once to fp16 (per sample, 2^-11 relative; their lo parts are never formed).
+template <typename P, int D = AON_PREFETCH, int EOFF = 0, bool BF = false, int MXL = 0, int MXH = 0,
+          bool W1 = false, int X1F = -1>
 struct FragPipe {
   static constexpr int kEpiOff = EOFF;
+  static constexpr bool kW1 = W1;
+  static constexpr int kX1From = X1F;
   static constexpr int kMode = MXH > MXL ? 2 : (BF ? 1 : 0);
   __host__ __device__ static constexpr bool f16_block(int b) { return StreamMap{kMode, MXL, MXH}.f16(b); }
   __host__ __device__ static constexpr int map_block(int b) { return StreamMap{kMode, MXL, MXH}.map(b); }
@@ -695,7 +705,10 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
   constexpr int K = d.ka + d.kb;
   constexpr int NP = d.u / 2;
   constexpr int EO = P::kEpiOff;  // epilogue parts of pair p-1 at k-steps EO..EO+3 of pair p
-  constexpr bool BF = !P::f16_block(d.blk0);  // bf16 numerics: one MFMA per k-step and tile
+  constexpr bool CMP = !P::f16_block(d.blk0);  // a compact (hi-only) block of the stream
+  constexpr bool BF = CMP && !P::kW1;  // bf16 numerics: one MFMA per k-step and tile
+  constexpr bool W1 = CMP && P::kW1;   // fp16 weights: two MFMAs, the fp16x3 epilogue
+  constexpr bool X1 = !CMP && P::kX1From >= 0 && d.blk0 >= P::kX1From;  // fp16 activations
   constexpr int QIN = K - EO < 0 ? 0 : (K - EO > 4 ? 4 : K - EO);  // parts done inside the loop
   static_assert(d.u % 2 == 0 && NP <= NO && d.ka <= NA && d.kb <= NB, "layer shape");
   f4 phh[2][NCOL], pxx[2][NCOL];  // accumulators of the pair whose epilogue is pending
@@ -756,7 +769,16 @@ __device__ __forceinline__ void layer_h(P& p, const Frag<NA, NCOL>& a,
             continue;
           }
           hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
+          if (X1) {
+            (void)xl;
+            hh[uu][c] = mfma16(wl, xh, hh[uu][c]);
+            continue;
+          }
           hh[uu][c] = mfma16(wh, xl, hh[uu][c]);
+          if (W1) {
+            (void)wl;
+            continue;
+          }
           hh[uu][c] = mfma16(wl, xh, hh[uu][c]);
 #else
           hh[uu][c] = mfma16(wh, xh, hh[uu][c]);
@@ -793,7 +815,9 @@ template <typename Net, int LAYER, typename P, int NCOL, int NA>
 __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[NCOL],
                                        lds_float* bias_l, int g) {
   constexpr LayerDesc d = Net::layer(LAYER);
-  constexpr bool BF = !P::f16_block(d.blk0);
+  constexpr bool CMP = !P::f16_block(d.blk0);
+  constexpr bool BF = CMP && !P::kW1, W1 = CMP && P::kW1;
+  constexpr bool X1 = !CMP && P::kX1From >= 0 && d.blk0 >= P::kX1From;
   static_assert(d.u == 1 && d.kb == 0 && d.ka <= NA, "head shape");
   f4 hh[NCOL], xx[NCOL];
   const f4 bias = *reinterpret_cast<lds_f4*>(bias_l + d.bias0);
@@ -819,8 +843,8 @@ __device__ __forceinline__ void head_h(P& p, const Frag<NA, NCOL>& a, f4 (&res)[
         continue;
       }
       hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
-      hh[c] = mfma16(wh, a.lo[k][c], hh[c]);
-      hh[c] = mfma16(wl, a.hi[k][c], hh[c]);
+      if (!X1) hh[c] = mfma16(wh, a.lo[k][c], hh[c]);
+      if (!W1) hh[c] = mfma16(wl, a.hi[k][c], hh[c]);
 #else
       hh[c] = mfma16(wh, a.hi[k][c], hh[c]);
       xx[c] = mfma16(wh, a.lo[k][c], xx[c]);

@@ -261,6 +261,9 @@ struct PackArgsH {
   // training mode keeps the deformation MLP in fp16x3, StreamMap mode 2)
   int bf16;
   int mx_lo, mx_hi;
+  // compact blocks (modes 1, 2) hold fp16(w 2^6) instead of bf16(w), range-guarded like the
+  // fp16x3 hi blocks, and their layers' biases are at activation scale (FragPipe W1)
+  int f16w;
 };
 
 // Where the weight stream holds fp16x3 block b (even b: the hi block of a (hi, lo) pair, b + 1

@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 9
+#define AON_ABI_VERSION 10
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -316,10 +316,17 @@ int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* 
  * mixed == 0: packed by aon_mlp_art_pack, fp16x3 numerics throughout (only the stores bf16).
  * mixed == 2: packed by aon_mlp_art_pack_mixed(.., 2, ..) -- everything through the bottleneck
  * fp16x3, the view branch (views_linear.0-3, rgb_layer) one bf16 MFMA per product.
+ * mixed == 3: packed by aon_mlp_art_pack_mixed(.., 3, ..) -- the deformation MLP fp16x3, every
+ * later layer two fp16 MFMAs per product: the weights rounded once to fp16 (at 2^6), the
+ * activations split exactly into fp16 hi + lo as in fp16x3 (range-guarded likewise).
+ * mixed == 4: packed by aon_mlp_art_pack (the fp16x3 stream) -- the deformation MLP fp16x3,
+ * every later layer two fp16 MFMAs per product, (hi(W) + lo(W)) x hi(x): the weights' exact
+ * split kept, the activations rounded once to fp16 (range-guarded as the hi parts).
  * enc_bf (optional, NULL: not kept): pos_enc(x') as bf16, tiled (NR, 128), columns 63..127 zero
  * (as aon_mlp_fwd_train_bf16's enc). */
 int aon_mlp_art_pack_bf16(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
-/* mixed = 1: as aon_mlp_art_pack_bf16; mixed = 2: the view-branch stream (ABI 9). */
+/* mixed = 1: as aon_mlp_art_pack_bf16; mixed = 2: the view-branch stream; mixed = 3: the
+ * fp16-weight stream (ABI 9). */
 int aon_mlp_art_pack_mixed(const aon_mlp_art_params* params, int mixed, void* packed,
                            aon_stream_t stream);
 int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_o, const float* rays_d,
@@ -441,10 +448,24 @@ typedef struct aon_gemm_args {
   /* c_trans = 1: C is written transposed -- element (m, n) of the product at C[n * ldc + m] --
    * and rowsum receives the column sums of B (N entries, in B's element type rounded as staged)
    * instead of the row sums of A: dW of a layer whose input has <= 4 columns, computed as the
-   * skinny product (input)^T dZ.  The bf16 skinny path only (mma_bf16, M <= 4, B bf16). */
+   * skinny product (input)^T dZ.  The skinny path only (M <= 4, below). */
   int c_trans;
+  /* f16_single = 1 (ABI 10): licence for the single-accumulator fp16x3 kernel -- hi*hi + hi*lo +
+   * lo*hi in ONE fp32 accumulator, the lo parts unscaled (normal fp16 for |x s| >= 2^-3, an
+   * absolute 2^-25 at scale below) -- where the caller guarantees |A a_scale| (times a_amax's
+   * scale) and |B b_scale| below 65504: the parity-mode weight gradients dW = dY^T X of the fused
+   * kernels' tiled tensors, dY at the backward chain's own scale (a_amax) and X at b_scale 8 (the
+   * forward's activation scale: both kernels range-guard their splits at exactly these scales).
+   * Used for 256 x 256 products with both operands tiled, fp32, K >= 8192 (k_gemm_f1_256, one
+   * 256 x 256 tile per workgroup); any other product computes as with f16_single = 0. */
+  int f16_single;
 } aon_gemm_args;
 
+/* Weight gradients (a_kc = b_kc = 0, no A2 / bias / mask / relu) with M <= 4 rows (B of <= 256
+ * columns, 16-B aligned, a row-major A), or against a per-ray B (b_rdiv > 1, M a multiple of 8
+ * up to 256), compute without the fp16x3 split when mma_bf16 = 0: fp32 products and sums in a
+ * fixed order (the streaming skinny / segment-sum kernels; a_scale, b_scale and a_amax then
+ * only cancel). */
 size_t aon_gemm_workspace_bytes(const aon_gemm_args* args);
 int aon_gemm(const aon_gemm_args* args, void* work, size_t work_bytes, aon_stream_t stream);
 

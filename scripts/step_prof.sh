@@ -11,6 +11,9 @@ for m in $MODES; do
   case $m in
     art_bf16) a="--art --precision bf16" ;;
     art_bf16_view) a="--art --precision bf16 --view" ;;
+    art_bf16_f16w) a="--art --precision bf16 --f16w 1" ;;
+    art_bf16_f16x) a="--art --precision bf16 --f16w 0 --f16x 1" ;;
+    art_bf16_f16x3) a="--art --precision bf16 --f16w 0 --f16x 0" ;;
     art) a="--art --precision f16x3" ;;
     bf16) a="--precision bf16" ;;
     f16x3) a="--precision f16x3" ;;

@@ -35,7 +35,7 @@ def test_header_symbols_exported(L):
 
 def test_abi_version_and_sizes(L):
     lib = L.lib()
-    assert lib.aon_abi_version() == L.ABI_VERSION == 9
+    assert lib.aon_abi_version() == L.ABI_VERSION == 10
     assert lib.aon_mlp_packed_bytes(0) == 2368 * 1024 + 2464 * 4 + 16  # + the status block
     assert lib.aon_mlp_packed_bytes(99) == 0
 

@@ -109,6 +109,155 @@ def test_gemm_epilogues_segments_split():
     assert (db2.double() - ref_b2).abs().max().item() < 1e-5 * ref_b2.abs().max().item()
 
 
+def _single_operands(K, seed):
+    """dY-like A (rows spread over six decades, a per-call scale word) and activation-like B
+    (ReLU outputs from 1e-6 to ~100, under the forward's 8188 range guard), tiled."""
+    from aonerf import _lib as L
+    from aonerf import tiles
+
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    A = torch.randn((K, 256), device="cuda", generator=g) * 1e-3
+    A *= 10.0 ** (-6 * torch.rand((K, 1), device="cuda", generator=g))
+    B = torch.relu(torch.randn((K, 256), device="cuda", generator=g))
+    B *= 10.0 ** (2 - 8 * torch.rand((K, 256), device="cuda", generator=g))
+    word = torch.zeros((1,), dtype=torch.int32, device="cuda")
+    L.call("aon_absmax", L.ptr(A), A.numel(), L.ptr(word), L.stream())
+
+    def tile_nan(x):  # the padding rows of the last tile NaN: never read
+        p = torch.full((tiles.rows(K), 256), float("nan"), device="cuda")
+        p[:K] = x
+        return tiles.tile(p)
+    return A, B, tile_nan(A), tile_nan(B), word
+
+
+def _single_dw(At, Bt, word, K, single, C=None, accumulate=False, rowsum=None):
+    from aonerf.linalg import ACT_SCALE, gemm
+
+    C = torch.zeros((256, 256), device="cuda") if C is None else C
+    gemm(C, At, Bt, 256, 256, K, lda=256, a_kc=False, ldb=256, b_kc=False, ldc=256,
+         a_scale=1.0, b_scale=8.0 if single else ACT_SCALE, a_amax=word, rowsum=rowsum,
+         accumulate=accumulate, a_tiled=True, b_tiled=True, f16_single=single)
+    return C
+
+
+@pytest.mark.parametrize("K", [8192 + 5, 70003, 266240])
+def test_f16_single_weight_gradient(K):
+    """aon_gemm f16_single (k_gemm_f1_256: one 256 x 256 tile per workgroup, hi*hi + hi*lo +
+    lo*hi in ONE accumulator with dY at its per-call scale and X at 2^3): the parity mode's
+    256 x 256 weight gradients against fp64 at the GEMM gate (2e-6 of the magnitude), the bias
+    gradient (rowsum) within 1e-6, within 2e-6 of the two-accumulator kernel (f16_single = 0),
+    accumulate, ragged K (rows past K in the tiles' padding ignored), deterministic."""
+    A, B, At, Bt, word = _single_operands(K, K)
+    db, db0 = torch.empty((256,), device="cuda"), torch.empty((256,), device="cuda")
+    C1 = _single_dw(At, Bt, word, K, True, rowsum=db)
+    C1b = _single_dw(At, Bt, word, K, True)
+    C0 = _single_dw(At, Bt, word, K, False, rowsum=db0)
+    C_init = torch.randn((256, 256), device="cuda")
+    Cacc = _single_dw(At, Bt, word, K, True, C=C_init.clone(), accumulate=True)
+    torch.cuda.synchronize()
+    want = (A.double().T @ B.double()).cpu().numpy()
+    e1, e0 = rel_err(C1.cpu().numpy(), want), rel_err(C0.cpu().numpy(), want)
+    eb = rel_err(db.cpu().numpy(), A.double().sum(0).cpu().numpy())
+    e10 = rel_err(C1.cpu().numpy(), C0.cpu().numpy())
+    ea = rel_err(Cacc.cpu().numpy(), want + C_init.double().cpu().numpy())
+    print(f"f16_single dW K={K}: max-rel {e1:.2e} (two accumulators {e0:.2e}, between {e10:.2e}),"
+          f" rowsum {eb:.2e}, accumulate {ea:.2e}")
+    assert torch.equal(C1, C1b), "deterministic"
+    assert e1 < 2e-6 and e10 < 2e-6 and eb < 1e-6 and ea < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K,tiled", [(3, 128, 790528, True), (1, 256, 790528, True),
+                                         (4, 256, 70003, False), (2, 16, 5, False)])
+def test_f32_skinny_weight_gradient(M, N, K, tiled):
+    """The parity mode's head weight gradients (M <= 4: dW = d raw^T X with X = hv3 / h7, the
+    fused forward's tiled fp32 tensors) on the streaming skinny kernel without rounding: fp32
+    products and sums against fp64 within 1e-6 of the magnitude (the fp16x3 GEMM gate is 2e-6),
+    the bias gradient likewise; a_amax and the operand scales cancel; deterministic."""
+    from aonerf import _lib as L
+    from aonerf import tiles
+    from aonerf.linalg import gemm
+
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    draw = torch.randn((K, 4), device="cuda", generator=g) * 1e-3
+    X = torch.relu(torch.randn((K, N), device="cuda", generator=g)) * 3
+    Xs = tiles.tile(X) if tiled else X
+    word = torch.zeros((1,), dtype=torch.int32, device="cuda")
+    L.call("aon_absmax", L.ptr(draw), draw.numel(), L.ptr(word), L.stream())
+    out = []
+    for _ in range(2):
+        C, db = torch.empty((M, N), device="cuda"), torch.empty((M,), device="cuda")
+        gemm(C, draw, Xs, M, N, K, lda=4, a_kc=False, ldb=N, b_kc=False, ldc=N, rowsum=db,
+             a_scale=1.0, b_scale=2.0 ** -8, a_amax=word, b_tiled=tiled)
+        out.append((C, db))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    want = draw[:, :M].double().T @ X.double()
+    e = rel_err(out[0][0].cpu().numpy(), want.cpu().numpy())
+    eb = rel_err(out[0][1].cpu().numpy(), draw[:, :M].double().sum(0).cpu().numpy())
+    print(f"fp32 skinny dW M={M} N={N} K={K}: max-rel {e:.2e}, rowsum {eb:.2e}")
+    assert e < 1e-6 and eb < 1e-6
+
+
+@pytest.mark.parametrize("K,rdiv", [(790528, 193), (266240, 65), (1885, 65)])
+def test_f32_segsum_weight_gradient(K, rdiv):
+    """views_linear.0's enc_dir columns in the parity mode (dW = dZv^T venc[row / S], dZv the
+    chain's tiled fp32 gradient) on the segment-sum kernel without rounding: against fp64 within
+    1e-6, the bias gradient likewise, deterministic."""
+    from aonerf import tiles
+    from aonerf.linalg import gemm
+
+    g = torch.Generator(device="cuda").manual_seed(K)
+    dz = torch.randn((K, 128), device="cuda", generator=g) * 1e-3
+    V = torch.randn(((K + rdiv - 1) // rdiv, 27), device="cuda", generator=g)
+    dzt = tiles.tile(dz)
+    out = []
+    for _ in range(2):
+        C, db = torch.empty((128, 27), device="cuda"), torch.empty((128,), device="cuda")
+        gemm(C, dzt, V, 128, 27, K, lda=128, a_kc=False, ldb=27, b_kc=False, b_rdiv=rdiv, ldc=27,
+             rowsum=db, a_scale=1.0, b_scale=2.0 ** -8, a_tiled=True)
+        out.append((C, db))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    Vr = V.double()[torch.arange(K, device="cuda") // rdiv]
+    e = rel_err(out[0][0].cpu().numpy(), (dz.double().T @ Vr).cpu().numpy())
+    eb = rel_err(out[0][1].cpu().numpy(), dz.double().sum(0).cpu().numpy())
+    print(f"fp32 segsum dW K={K} rdiv={rdiv}: max-rel {e:.2e}, rowsum {eb:.2e}")
+    assert e < 1e-6 and eb < 1e-6
+
+
+def test_f16_single_weight_gradient_batch_full_level():
+    """The fine level's 790,528-row products as aon_gemm_batch's f16_single class
+    (k_gemm_f1_256_batch: chunk z of every product on one XCD) plus a two-accumulator product in
+    the same batch: each within 2e-6 of its own f16_single launch and of the two-accumulator
+    kernel (fp64 at this size is the single-size test above); deterministic."""
+    from aonerf.linalg import batched
+
+    K = 790528
+    A, B, At, Bt, word = _single_operands(K, 5)
+    del A, B
+
+    def run():
+        Cs = [torch.zeros((256, 256), device="cuda") for _ in range(3)]
+        rs = [torch.empty((256,), device="cuda") for _ in range(3)]
+        with batched():
+            for i in range(3):
+                _single_dw(At, Bt, word, K, i != 1, C=Cs[i], rowsum=rs[i])
+        torch.cuda.synchronize()
+        return Cs, rs
+
+    (Cb, rb), (Cb2, rb2) = run(), run()
+    own = _single_dw(At, Bt, word, K, True)
+    v1 = _single_dw(At, Bt, word, K, False)
+    torch.cuda.synchronize()
+    for i in range(3):
+        assert torch.equal(Cb[i], Cb2[i]) and torch.equal(rb[i], rb2[i])
+    e_own = rel_err(Cb[0].cpu().numpy(), own.cpu().numpy())
+    e_v1 = rel_err(Cb[0].cpu().numpy(), v1.cpu().numpy())
+    print(f"f16_single dW batch K={K}: vs own launch {e_own:.2e}, vs two accumulators {e_v1:.2e}")
+    assert torch.equal(Cb[0], Cb[2]) and e_own < 2e-6 and e_v1 < 2e-6
+    assert rel_err(Cb[1].cpu().numpy(), v1.cpu().numpy()) < 1e-6
+
+
 # ----------------------------------------------------------------------------- compositing bwd
 @pytest.mark.parametrize("S,white", [(65, True), (193, False), (7, True), (130, True)])
 def test_composite_backward(S, white):

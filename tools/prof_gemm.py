@@ -55,6 +55,35 @@ def main():
         sha = hashlib.sha256(C.cpu().numpy().tobytes() + rs.cpu().numpy().tobytes()).hexdigest()[:16]
         res[mode] = {"ms": ms, "hbm_frac": nbytes / (ms * 1e-3) / 8e12,
                      "mfma_frac": 2 * K * M * N / (ms * 1e-3) / 1e12 / peak, "sha": sha}
+    # the parity mode's 256 x 256 products with the single-accumulator licence (k_gemm_f1_256),
+    # alone and as one level's batch of 8 (distinct operands, as the step's products)
+    from aonerf.linalg import batched
+    A = [tiles.tile(torch.randn((K, M), device="cuda", generator=g) * 1e-3) for _ in range(8)]
+    B = [tiles.tile(torch.rand((K, N), device="cuda", generator=g)) for _ in range(8)]
+    Cs = [torch.empty((M, N), device="cuda") for _ in range(8)]
+    rss = [torch.empty((M,), device="cuda") for _ in range(8)]
+    word = torch.zeros((1,), dtype=torch.int32, device="cuda")
+    from aonerf import _lib as L
+    L.call("aon_absmax", L.ptr(A[0]), A[0].numel(), L.ptr(word), L.stream())
+
+    def one(i):
+        gemm(Cs[i], A[i], B[i], M, N, K, lda=M, a_kc=False, ldb=N, b_kc=False, ldc=N,
+             rowsum=rss[i], a_scale=1.0, b_scale=8.0, a_amax=word, a_tiled=True, b_tiled=True,
+             f16_single=True)
+
+    def level():
+        with batched():
+            for i in range(8):
+                one(i)
+
+    for name, fn, n in (("f16_single", lambda: one(0), 1), ("f16_single_b8", level, 8)):
+        ms = timed(fn, 10)
+        fn()
+        torch.cuda.synchronize()
+        sha = hashlib.sha256(b"".join(Cs[i].cpu().numpy().tobytes() + rss[i].cpu().numpy().tobytes()
+                                      for i in range(n))).hexdigest()[:16]
+        res[name] = {"ms": ms, "hbm_frac": n * K * (M + N) * 4 / (ms * 1e-3) / 8e12,
+                     "mfma_frac": n * 2 * K * M * N / (ms * 1e-3) / 1e12 / (2500.0 / 3), "sha": sha}
     print(json.dumps(res))
 
 

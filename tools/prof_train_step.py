@@ -20,6 +20,10 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--trunk", action="store_true", help="articulated bf16: BF16_TRUNK = True")
     ap.add_argument("--view", action="store_true", help="articulated bf16: BF16_VIEW = True")
+    ap.add_argument("--f16w", type=int, default=None,
+                    help="articulated bf16: F16_WEIGHTS = 0 / 1 (default: the library's setting)")
+    ap.add_argument("--f16x", type=int, default=None,
+                    help="articulated bf16: F16_ACTS = 0 / 1 (default: the library's setting)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--overlap", type=int, default=None,
                     help="train.OVERLAP_DWEIGHT = 0 / 1 (default: the library's setting)")
@@ -35,6 +39,10 @@ def main():
         from test_gpu_art_train import _make
         train_art.PRECISION, train_art.BF16_TRUNK = args.precision, args.trunk
         train_art.BF16_VIEW = args.view
+        if args.f16w is not None:
+            train_art.F16_WEIGHTS = bool(args.f16w)
+        if args.f16x is not None:
+            train_art.F16_ACTS = bool(args.f16x)
         batch["instance_id"] = torch.tensor([7], device="cuda")
         batch["articulation_id"] = torch.tensor([3], device="cuda")
         net, lib = _make(0)
