@@ -2232,8 +2232,11 @@ static bool bf16_copy256_path(const aon_gemm_args* a) {
 
 // weight gradient of at most 4 rows on a B of up to 256 columns (k_gemm_skinny_bf16): the bf16
 // mode's (B bf16), or the parity mode's in exact fp32 (A and B fp32, no epilogue)
+#ifndef AON_GEMM_F32_STREAM
+#define AON_GEMM_F32_STREAM 1  // 0: A/B build -- the parity mode's heads / per-ray columns on k_gemm_f16x3
+#endif
 static bool skinny32(const aon_gemm_args* a) {
-  return !a->mma_bf16 && !a->a_bf16 && !a->b_bf16 && !a->a_kc && !a->b_kc && !a->A2 &&
+  return AON_GEMM_F32_STREAM && !a->mma_bf16 && !a->a_bf16 && !a->b_bf16 && !a->a_kc && !a->b_kc && !a->A2 &&
          !a->bias && !a->mask && !a->relu && !a->exact_fp32;
 }
 static bool skinny_path(const aon_gemm_args* a) {

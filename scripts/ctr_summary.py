@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Counter-based utilisation of the fused MLP kernel from a scripts/prof_counters.sh session:
 
-    python scripts/ctr_summary.py gpurun_out/ctr4 profiles/r01_f16x3/counters.json
+    python scripts/ctr_summary.py gpurun_out/ctr4 profiles/r01_f16x3/counters.json [KERNEL]
+
+KERNEL: a substring of the kernel name (default "f16x3", the fused MLP); the last launch of it
+in each pass is summarised.
 
 MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x cycles), LDS busy = SQ_LDS_IDX_ACTIVE / (CUs x
 cycles), cycles = GRBM_GUI_ACTIVE / 8 XCDs (MI355X_MICROARCH.md), L2 hit rate, dynamic
@@ -27,14 +30,15 @@ def agg(path, kernel="f16x3"):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    a, grid, dur_a = agg(f"{src}/A")
-    b, _, dur_b = agg(f"{src}/B")
-    c, _, _ = agg(f"{src}/C")
+    kern = sys.argv[3] if len(sys.argv) > 3 else "f16x3"
+    a, grid, dur_a = agg(f"{src}/A", kern)
+    b, _, dur_b = agg(f"{src}/B", kern)
+    c, _, _ = agg(f"{src}/C", kern)
     cus, simds = 256, 1024
     cycles = b["GRBM_GUI_ACTIVE"] / 8
     waves = grid / 64
     res = {
-        "kernel": "k_mlp_fwd_f16x3<0, 1> (tools/prof_mlp.py launch)", "grid_threads": grid,
+        "kernel": kern, "grid_threads": grid,
         "duration_ms_profiled": dur_b * 1e3, "clock_ghz_profiled": cycles / dur_b / 1e9,
         "mfma_busy_frac": a["SQ_VALU_MFMA_BUSY_CYCLES"] / (simds * cycles),
         "lds_busy_frac": b["SQ_LDS_IDX_ACTIVE"] / (cus * cycles),
