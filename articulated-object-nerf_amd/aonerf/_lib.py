@@ -160,6 +160,7 @@ _SIGNATURES = {
     "aon_sample_rays": (c_int, [vp, vp, c_int, c_i64, c_int, c_int, c_float, vp, c_i64, c_int,
                                 c_float, vp, vp, vp, vp, vp]),
     "aon_cast_rays": (c_int, [vp, vp, vp, c_i64, c_int, vp, c_i64, vp, c_int, c_int, vp, vp]),
+    "aon_cast_rays_tiled": (c_int, [vp, vp, vp, c_i64, c_int, c_int, c_int, c_int, vp, vp]),
     "aon_sample_pdf": (c_int, [vp, c_i64, vp, c_i64, c_i64, c_int, c_int, vp, c_i64, vp, c_int,
                                vp, vp, vp, vp, vp]),
     "aon_composite_march": (c_int, [vp, vp, vp, c_i64, c_int, c_int, c_int, vp, c_i64, c_int, vp,

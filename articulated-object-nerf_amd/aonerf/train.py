@@ -338,7 +338,9 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
     e0 = _ev()
     acts = ACT_SCALE
 
-    enc_t = enc.dtype == torch.bfloat16  # the bf16 forward's own tiled, 128-column copy
+    # the tiled copy of pos_enc(x): the bf16 forward's (NR, 128) bf16 or the f16x3 mode's
+    # (NR, 64) fp32 (aon_cast_rays_tiled); else row-major (R, 63)
+    enc_t = enc.shape[1] != 63
 
     def dweight(dW, dY, ldy, n_out, X, ldx, n_in, rdiv=1, col0=0, db=None, a_t=True):
         # f16x3: dY rides at the chain's own per-call scale from max |d raw| (the word in
@@ -349,11 +351,13 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
         b_t = (h_tiled and X is not enc and X is not venc) or (X is enc and enc_t)
         n_store = 0
         if X is enc and enc_t:
-            ldx, n_store, n_in = 128, n_in, 128
-        # f16x3, the 256 x 256 products of the fused kernels' tiled tensors: one accumulator
-        # (aon_gemm f16_single) with dY at the chain's scale and X at the forward's 2^3, the
-        # scales both kernels range-guard their own splits at
-        single = not bf16 and a_t and b_t and n_out == 256 and n_in == 256
+            ldx, n_store, n_in = enc.shape[1], n_in, enc.shape[1]
+        # f16x3, the 256 x 256 / 128 x 256 / 256 x 64 products of the fused kernels' tiled
+        # tensors: one accumulator (aon_gemm f16_single) with dY at the chain's scale and X at
+        # the forward's 2^3, the scales both kernels range-guard their own splits at (pos_enc(x)
+        # and x itself: far inside the range)
+        single = (not bf16 and a_t and b_t
+                  and (n_out, n_in) in ((256, 256), (128, 256), (256, 64)))
         gemm(dW[:, col0:] if col0 else dW, dY, X, n_out, n_in, R, lda=ldy, a_kc=False, ldb=ldx,
              b_kc=False, b_rdiv=rdiv, ldc=dW.shape[1], a_scale=1.0,
              b_scale=1.0 if bf16 else (8.0 if single else acts), rowsum=db,
@@ -423,6 +427,12 @@ class RenderLevel(torch.autograd.Function):
         bf16 = FUSED_FORWARD and PRECISION == "bf16"
         if bf16:  # the bf16 training forward keeps pos_enc(x) itself (bf16, tiled, 128 columns)
             enc = torch.empty((tiles.rows(R), 128), device=dev, dtype=torch.bfloat16)
+        elif FUSED_FORWARD and FUSED_BACKWARD:
+            # xyz = o + t d straight into the encodings, tiled with 64 columns (column 63 zero):
+            # the fused backward's enc-column weight gradients read whole 16-column tiles
+            enc = torch.empty((tiles.rows(R), 64), device=dev)
+            L.call("aon_cast_rays_tiled", L.ptr(L.contig(rays_o)), L.ptr(L.contig(rays_d)),
+                   L.ptr(L.contig(t_vals)), B, S, 0, 10, 64, L.ptr(enc), L.stream(dev))
         else:
             # xyz = o + t d (helper.py:25-26) straight into the encodings (helper.py:136-140)
             enc = torch.empty((R, 63), device=dev)
@@ -488,7 +498,7 @@ class RenderLevel(torch.autograd.Function):
             if ctx.h_tiled:  # the all-GEMM backward reads row-major fp32 activations
                 h = [tiles.untile(x, R).float() for x in h]
                 bot, hv = tiles.untile(bot, R).float(), tiles.untile(hv, R).float()
-            if enc.dtype == torch.bfloat16:  # the bf16 forward's tiled copy
+            if enc.shape[1] != 63:  # a tiled copy (the bf16 forward's, or aon_cast_rays_tiled's)
                 enc = tiles.untile(enc, R)[:, :63].float().contiguous()
             _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]

@@ -419,10 +419,11 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
         # bf16: one bf16 MFMA per product, no scales (bf16 has fp32's exponent range)
         dW = G[i][0]
         b_t = (h_tiled and X is not enc and X is not venc and X is not xyz) or X is enc_bf
-        # f16x3, the 256 x 256 products of the fused kernels' tiled tensors: one accumulator
-        # (aon_gemm f16_single), dY at the chain's scale, X at the forward's 2^3 (train.py)
-        single = (not bf16 and chain_scale and a_t and b_t and dW.shape[0] == 256
-                  and n_in == 256 and col0 == 0 and ldx == 256)
+        # f16x3, the 256 x 256 / 128 x 256 products of the fused kernels' tiled tensors: one
+        # accumulator (aon_gemm f16_single), dY at the chain's scale, X at the forward's 2^3
+        # (train.py)
+        single = (not bf16 and chain_scale and a_t and b_t and col0 == 0 and ldx == n_in
+                  and (dW.shape[0], n_in) in ((256, 256), (128, 256)))
         gemm(dW[:, col0:] if col0 else dW, dY, X, dW.shape[0], n_in, R, lda=ldy, a_kc=False,
              ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0),
              a_scale=1.0 if (chain_scale or bf16) else gs,

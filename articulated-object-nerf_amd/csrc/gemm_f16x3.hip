@@ -336,6 +336,7 @@ __device__ __forceinline__ void f16x3_body(const Params& p, int tm, int tn, int 
           p.part[((int64_t)z * p.M + m) * p.N + n] = v;
           continue;
         }
+        if (n >= p.nstore) continue;
         float* c = p.C + m * p.ldc + n;
         if (p.accumulate) v = __fadd_rn(*c, v);
         if (p.bias) v = __fadd_rn(v, p.bias[n]);
@@ -1401,31 +1402,47 @@ __global__ __launch_bounds__(THREADS2, 2) void k_gemm_bf16_dma256_batch(ParamsBa
 // LDS stages (128 KB), the split of tile kt + 1 and the loads of tile kt + 2 ride between the
 // MFMAs of tile kt, one barrier per k-tile.  rowsum: A's fp32 values in row order per thread,
 // then a fixed order over the 16 threads of a column run.
-#ifndef AON_F1_ROWS_LDS
-#define AON_F1_ROWS_LDS 0  // 1: A/B build -- the row sums in LDS instead of 8 VGPRs
-#endif
-#ifndef AON_F1_PUB0
-#define AON_F1_PUB0 0  // the j-steps of a k-tile's MFMAs after which the next tile's runs 0 / 1
-#endif                 // are published (and their registers refilled with the tile after)
-#ifndef AON_F1_PUB1
-#define AON_F1_PUB1 1
-#endif
-constexpr int F1_PLANE = BK * 512;  // bytes of one [32 k][256 col] fp16 plane
-constexpr int F1_STAGE = 4 * F1_PLANE;  // A hi, A lo, B hi, B lo
+// Shapes (MW x NW, the operands' widths): 256 x 256 (pts_linears, bottleneck), 128 x 256
+// (views_linear.0's bottleneck columns) and 256 x 64 (pts_linears.0's and the skip layer's
+// pos_enc columns, B the tiled 64-column encodings of aon_cast_rays_tiled).  Waves in MW / 64
+// (m) x 8 / (MW / 64) (n): every wave 64 rows x NW / WN columns.  An operand of width W < 128
+// is staged into a 128-column image (the 128-column swizzle of the bf16 kernels).
+template <int W>
+struct F1Img {
+  static constexpr int kCols = W < 128 ? 128 : W;  // image columns
+  static constexpr int kPlane = BK * kCols * 2;    // bytes of one [32 k][kCols] fp16 plane
+  static constexpr int kRuns = (4 * W + THREADS2 - 1) / THREADS2;  // 8-float runs per thread
+  __device__ __forceinline__ static int off(int row, int ch) {
+    return kCols == 256 ? tt_off2(row, ch) : tt_off(row, ch);
+  }
+  __device__ __forceinline__ static h8 frag(const char* plane, int c0, int lane) {
+    return __builtin_bit_cast(h8, kCols == 256 ? tt_frag2(plane, c0, lane) : tt_frag(plane, c0, lane));
+  }
+};
 
-__device__ __forceinline__ h8 f1_frag(const char* plane, int c0, int lane) {
-  return __builtin_bit_cast(h8, tt_frag2(plane, c0, lane));
-}
-
-// one thread's two 32-B runs of a k-tile of a tiled fp32 operand of width 256: k rows r and
-// 16 + r of the tile, columns cc .. cc + 7
+// one thread's runs of a k-tile of a tiled fp32 operand of width W: run u = tid + 512 i (< 4 W)
+// is floats 8 u .. 8 u + 7 of the k-tile's contiguous 32 W floats -- k row 16 (8 u / 16 W) +
+// (8 u % 256) / 16, columns 16 ((8 u % 16 W) / 256) + (8 u % 16) .. + 7 (a wave reads 2 KB
+// contiguous)
+template <int W>
 struct F1Run {
-  f4 v[2][2];
-  // run i (k row 16 i + r of the tile)
+  static constexpr int NR = F1Img<W>::kRuns;
+  f4 v[NR][2];
+  __device__ __forceinline__ static bool valid(int tid, int i) {
+    return (4 * W) % THREADS2 == 0 || tid + THREADS2 * i < 4 * W;  // every thread's: no branch
+  }
+  __device__ __forceinline__ static int row(int tid, int i) {
+    const int u = tid + THREADS2 * i;
+    return 16 * (8 * u / (16 * W)) + (8 * u % 256) / 16;
+  }
+  __device__ __forceinline__ static int col(int tid, int i) {
+    const int u = tid + THREADS2 * i;
+    return 16 * ((8 * u % (16 * W)) / 256) + (8 * u % 16);
+  }
   __device__ __forceinline__ void load(const float* base, int64_t k0, int64_t kend, int tid, int i) {
-    const int r = (tid & 31) >> 1;
-    const f4* src = reinterpret_cast<const f4*>(base + k0 * 256 + 8 * (tid + 512 * i));
-    if (k0 + 16 * i + r < kend) {
+    if (!valid(tid, i)) return;
+    const f4* src = reinterpret_cast<const f4*>(base + k0 * W + 8 * (tid + THREADS2 * i));
+    if (k0 + row(tid, i) < kend) {
       v[i][0] = src[0];
       v[i][1] = src[1];
     } else {
@@ -1435,7 +1452,7 @@ struct F1Run {
   }
   // split run i at scale s into the hi / lo planes (16-B stores)
   __device__ __forceinline__ void store(char* hi, char* lo, float s, int tid, int i) const {
-    const int r = (tid & 31) >> 1, ch = 2 * (tid >> 5) + (tid & 1);
+    if (!valid(tid, i)) return;
     h8 h, l;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -1444,7 +1461,7 @@ struct F1Run {
       h[e] = hh;
       l[e] = static_cast<_Float16>(__fsub_rn(x, static_cast<float>(hh)));  // exact in fp32
     }
-    const int off = tt_off2(16 * i + r, ch);
+    const int off = F1Img<W>::off(row(tid, i), col(tid, i) >> 3);
     *reinterpret_cast<h8*>(hi + off) = h;
     *reinterpret_cast<h8*>(lo + off) = l;
   }
@@ -1453,20 +1470,27 @@ struct F1Run {
 #pragma unroll
     for (int e = 0; e < 8; ++e) rs[e] = __fadd_rn(rs[e], v[i][e >> 2][e & 3]);
   }
-  __device__ __forceinline__ void add_rows(f4* rs, int i) const {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      f4 a = rs[h];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] = __fadd_rn(a[e], v[i][h][e]);
-      rs[h] = a;
-    }
-  }
+};
+
+
+template <int MW, int NW>
+struct F1Shape {
+  static constexpr int kWM = MW / 64, kWN = 8 / kWM;  // waves in m / n
+  static constexpr int kTJ = NW / kWN / 16;           // 16-column tiles per wave
+  static constexpr int kStage = 2 * F1Img<MW>::kPlane + 2 * F1Img<NW>::kPlane;  // A hi, lo, B hi, lo
+  static constexpr int kLds = 2 * kStage;
+  // row sums: a thread's A runs share their columns when it has two (rows r, 16 + r: 16 slots
+  // per column), else its one run is row 16 h + r (32 slots)
+  static constexpr int kSlots = F1Img<MW>::kRuns == 2 ? 16 : 32;
+  static_assert(MW % 64 == 0 && 8 % kWM == 0 && kTJ >= 1 && kSlots * MW * 4 <= kLds, "f1 shape");
 };
 
 // INTER: split-K by interleaved k-tiles (a lone product), else contiguous chunks (a batch)
-template <bool INTER>
-__device__ __forceinline__ void f1_256_body(const Params& p, int z, char* smem) {
+template <int MW, int NW, bool INTER>
+__device__ __forceinline__ void f1_body(const Params& p, int z, char* smem) {
+  using S = F1Shape<MW, NW>;
+  using IA = F1Img<MW>;
+  using IB = F1Img<NW>;
   float sa = p.sa, inv_s = p.inv_s;
   if (p.sa_bits) {
     const float gs = grad_scale(*p.sa_bits);
@@ -1474,7 +1498,7 @@ __device__ __forceinline__ void f1_256_body(const Params& p, int z, char* smem) 
     inv_s = __fdiv_rn(inv_s, gs);
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / S::kWN, wn = wave % S::kWN;
   // INTER: workgroup z takes k-tiles z, z + zsplit, z + 2 zsplit, ... so a lone product's
   // workgroups read one contiguous run of zsplit k-tiles at a time (its contiguous chunks put
   // 256 read streams a fixed multiple of 3 MB apart: 0.51-0.54 ms against 0.45-0.48 interleaved;
@@ -1487,54 +1511,55 @@ __device__ __forceinline__ void f1_256_body(const Params& p, int z, char* smem) 
   const int nk = INTER ? (z < ntiles ? static_cast<int>((ntiles - 1 - z) / zs + 1) : 0)
                        : static_cast<int>((kend - kbeg + BK - 1) / BK);
   const bool want_rows = p.rowsum != nullptr;
-#if AON_F1_ROWS_LDS
-  f4* rs = reinterpret_cast<f4*>(smem + 2 * F1_STAGE) + 2 * tid;  // this thread's column sums
-  if (want_rows) rs[0] = rs[1] = f4{0.f, 0.f, 0.f, 0.f};
-#else
   float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#endif
-  F1Run ra, rb;
+  F1Run<MW> ra;
+  F1Run<NW> rb;
+  constexpr int NRUN = IA::kRuns > IB::kRuns ? IA::kRuns : IB::kRuns;
   auto load = [&](int kt, int i) {
     const int64_t k0 = (t0 + (int64_t)kt * zs) * BK;
-    ra.load(p.A, k0, kend, tid, i);
-    rb.load(p.B, k0, kend, tid, i);
+    if (i < IA::kRuns) ra.load(p.A, k0, kend, tid, i);
+    if (i < IB::kRuns) rb.load(p.B, k0, kend, tid, i);
   };
   // publish run i of both operands to stage st (and A's values to the row sums, in row order)
   auto publish = [&](int st, int i) {
-    char* s = smem + st * F1_STAGE;
-    if (want_rows) ra.add_rows(rs, i);
-    ra.store(s, s + F1_PLANE, sa, tid, i);
-    rb.store(s + 2 * F1_PLANE, s + 3 * F1_PLANE, p.sb, tid, i);
+    char* s = smem + st * S::kStage;
+    if (i < IA::kRuns) {
+      if (want_rows && ra.valid(tid, i)) ra.add_rows(rs, i);
+      ra.store(s, s + IA::kPlane, sa, tid, i);
+    }
+    if (i < IB::kRuns) rb.store(s + 2 * IA::kPlane, s + 2 * IA::kPlane + IB::kPlane, p.sb, tid, i);
   };
-  f4 acc[4][8];
+  f4 acc[4][S::kTJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < S::kTJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   if (nk > 0) {
-    load(0, 0);
-    load(0, 1);
-    publish(0, 0);
-    publish(0, 1);
+#pragma unroll
+    for (int i = 0; i < NRUN; ++i) load(0, i);
+#pragma unroll
+    for (int i = 0; i < NRUN; ++i) publish(0, i);
     if (nk > 1) {
-      load(1, 0);
-      load(1, 1);
+#pragma unroll
+      for (int i = 0; i < NRUN; ++i) load(1, i);
     }
   }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const char* s = smem + (kt & 1) * F1_STAGE;
+    const char* s = smem + (kt & 1) * S::kStage;
+    const char* sb = s + 2 * IA::kPlane;
     const bool more = kt + 1 < nk;
     h8 ah[4], al[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      ah[i] = f1_frag(s, 8 * wm + 2 * i, lane);
-      al[i] = f1_frag(s + F1_PLANE, 8 * wm + 2 * i, lane);
+      ah[i] = IA::frag(s, 8 * wm + 2 * i, lane);
+      al[i] = IA::frag(s + IA::kPlane, 8 * wm + 2 * i, lane);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const h8 bh = f1_frag(s + 2 * F1_PLANE, 16 * wn + 2 * j, lane);
-      const h8 bl = f1_frag(s + 3 * F1_PLANE, 16 * wn + 2 * j, lane);
+    for (int j = 0; j < S::kTJ; ++j) {
+      const int c0 = 2 * (S::kTJ * wn + j);
+      const h8 bh = IB::frag(sb, c0, lane);
+      const h8 bl = IB::frag(sb + IB::kPlane, c0, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         acc[i][j] = mfma16(ah[i], bh, acc[i][j]);
@@ -1543,8 +1568,14 @@ __device__ __forceinline__ void f1_256_body(const Params& p, int z, char* smem) 
       }
       // tile kt + 1 (in registers) into the other stage between the MFMAs, each run's
       // registers refilled with tile kt + 2's at once: its loads fly under a whole k-tile
-      if (more && (j == AON_F1_PUB0 || j == AON_F1_PUB1)) {
-        const int i = j == AON_F1_PUB0 ? 0 : 1;
+      if (more && j < NRUN) {
+        publish((kt + 1) & 1, j);
+        if (kt + 2 < nk) load(kt + 2, j);
+      }
+    }
+    if (more && S::kTJ < NRUN) {  // narrow B: the runs left after the MFMAs
+#pragma unroll
+      for (int i = S::kTJ; i < NRUN; ++i) {
         publish((kt + 1) & 1, i);
         if (kt + 2 < nk) load(kt + 2, i);
       }
@@ -1553,26 +1584,19 @@ __device__ __forceinline__ void f1_256_body(const Params& p, int z, char* smem) 
   }
   const bool split = p.zsplit > 1;
   if (want_rows) {
-    // thread t holds columns 16 (t >> 5) + 8 (t & 1) .. + 7 of rows r = (t & 31) >> 1 (+ 16 j);
-    // combine the 16 r in order (LDS free after the last barrier)
-    float* red = reinterpret_cast<float*>(smem);  // [16 r][256]
-    const int r = (tid & 31) >> 1, c = 16 * (tid >> 5) + 8 * (tid & 1);
-#if AON_F1_ROWS_LDS
-    const f4 s0 = rs[0], s1 = rs[1];
-    __syncthreads();  // every thread has its sums before red overwrites stage 0
-#else
-    const f4 s0 = {rs[0], rs[1], rs[2], rs[3]}, s1 = {rs[4], rs[5], rs[6], rs[7]};
-#endif
+    // combine the slots of every column in slot order (LDS free after the last barrier)
+    float* red = reinterpret_cast<float*>(smem);  // [kSlots][MW]
+    if (ra.valid(tid, 0)) {
+      const int slot = S::kSlots == 16 ? ra.row(tid, 0) : ra.row(tid, 0) & 31;
+      const int c = ra.col(tid, 0);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      red[r * 256 + c + e] = s0[e];
-      red[r * 256 + c + 4 + e] = s1[e];
+      for (int e = 0; e < 8; ++e) red[slot * MW + c + e] = rs[e];
     }
     __syncthreads();
-    if (tid < 256) {
+    if (tid < MW) {
       float v = red[tid];
 #pragma unroll
-      for (int q = 1; q < 16; ++q) v = __fadd_rn(v, red[q * 256 + tid]);
+      for (int q = 1; q < S::kSlots; ++q) v = __fadd_rn(v, red[q * MW + tid]);
       if (split) p.rowsum_part[(int64_t)z * p.M + tid] = v;
       else p.rowsum[tid] = v;
     }
@@ -1580,16 +1604,17 @@ __device__ __forceinline__ void f1_256_body(const Params& p, int z, char* smem) 
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t n = wn * 128 + 16 * j + (lane & 15);
+    for (int j = 0; j < S::kTJ; ++j) {
+      const int64_t n = (NW / S::kWN) * wn + 16 * j + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t m = wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        const int64_t m = 64 * wm + 16 * i + 4 * (lane >> 4) + r;
         float v = __fmul_rn(acc[i][j][r], inv_s);
         if (split) {
           p.part[((int64_t)z * p.M + m) * p.N + n] = v;
           continue;
         }
+        if (n >= p.nstore) continue;
         float* c = p.C + m * p.ldc + n;
         if (p.accumulate) v = __fadd_rn(*c, v);
         *c = v;
@@ -1597,23 +1622,22 @@ __device__ __forceinline__ void f1_256_body(const Params& p, int z, char* smem) 
     }
 }
 
-constexpr int F1_LDS = 2 * F1_STAGE + (AON_F1_ROWS_LDS ? THREADS2 * 32 : 0);  // + the row sums
-
-__global__ __launch_bounds__(THREADS2, 1) void k_gemm_f1_256(Params p) {
-  __shared__ __align__(16) char smem[F1_LDS];
+template <int MW, int NW>
+__global__ __launch_bounds__(THREADS2, 1) void k_gemm_f1(Params p) {
+  __shared__ __align__(16) char smem[F1Shape<MW, NW>::kLds];
   int tile, z;
   if (!split_of(p, tile, z)) return;
-  f1_256_body<true>(p, z, smem);
+  f1_body<MW, NW, true>(p, z, smem);
 }
 
-// a batch of them over the same K (one level's 256 x 256 weight gradients): chunk z of every
-// product on one XCD, as k_gemm_bf16_dma256_batch
+// a batch of 256 x 256 products over the same K (one level's): chunk z of every product on one
+// XCD, as k_gemm_bf16_dma256_batch
 __global__ __launch_bounds__(THREADS2, 1) void k_gemm_f1_256_batch(ParamsBatch pb) {
-  __shared__ __align__(16) char smem[F1_LDS];
+  __shared__ __align__(16) char smem[F1Shape<256, 256>::kLds];
   const int T = pb.count, L = blockIdx.x, x = L & 7, q = L >> 3;
   const int z = 8 * (q / T) + x, b = q - (q / T) * T;
   if (z >= pb.zsplit) return;  // padding block of the last chunk group (uniform exit)
-  f1_256_body<false>(pb.p[b], z, smem);
+  f1_body<256, 256, false>(pb.p[b], z, smem);
 }
 
 // ---- fp16x3 weight gradients on the LDS-DMA ring (fp32 operands, both reduction-major):
@@ -2273,23 +2297,25 @@ static bool f16_copy_path(const aon_gemm_args* a) {
          b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) && a->lda % 4 == 0 && a->ldb % 4 == 0;
 }
 
-// fp32 reduction-major x reduction-major 256 x 256 weight gradients of the fused kernels' tiled
-// tensors with the caller's single-accumulator licence (f16_single): k_gemm_f1_256
-static bool f1_256_path(const aon_gemm_args* a) {
+// fp32 reduction-major x reduction-major weight gradients of the fused kernels' tiled tensors
+// in one of k_gemm_f1's shapes (M x N = 256 x 256, 128 x 256, 256 x 64), with the caller's
+// single-accumulator licence (f16_single)
+static bool f1_path(const aon_gemm_args* a) {
+  const bool shape = (a->M == 256 && (a->N == 256 || a->N == 64)) || (a->M == 128 && a->N == 256);
   return a->f16_single && !a->mma_bf16 && !a->a_bf16 && !a->b_bf16 && !a->a_kc && !a->b_kc &&
          !a->A2 && !a->bias && !a->mask && !a->relu && !a->exact_fp32 && !a->c_trans &&
-         a->a_tiled && a->b_tiled && a->M == BM2 && a->N == BM2 && a->lda == BM2 &&
-         a->ldb == BM2 && a->b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) &&
-         (a->n_store == 0 || a->n_store == a->N) && a->K >= 8 * 1024;
+         a->a_tiled && a->b_tiled && shape && a->lda == a->M && a->ldb == a->N &&
+         a->b_rdiv == 1 && aligned16(a->A) && aligned16(a->B) && a->K >= 8 * 1024;
 }
+static bool f1_256_path(const aon_gemm_args* a) { return f1_path(a) && a->M == 256 && a->N == 256; }
 
 static int64_t gemm_splits(const aon_gemm_args* a) {
   const int64_t tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
   if (small_path(a)) return 1;
-  if ((bf16_copy256_path(a) || f1_256_path(a)) && a->k_splits <= 0) {
+  if ((bf16_copy256_path(a) || f1_path(a)) && a->k_splits <= 0) {
     // one workgroup per CU: 256 K chunks of a single 256 x 256 tile (chunks of >= 1024 rows;
     // the coarse level's 266k rows still fill the chip -- 2048-row chunks left half of it idle)
-    const int64_t t2 = (a->M / BM2) * (a->N / BM2);
+    const int64_t t2 = f1_path(a) ? 1 : (a->M / BM2) * (a->N / BM2);
     if (t2 >= 256 || a->K < 8 * 1024) return 1;
     const int64_t cap = a->K / 1024 < 256 ? a->K / 1024 : 256;
     const int64_t s = 256 / t2 < cap ? 256 / t2 : cap;
@@ -2360,9 +2386,10 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
   AON_REQUIRE(!a->exact_fp32 || small_path(a),
               "exact_fp32: tiny fp32 products only (M N <= 65536, K <= 1024, no A2 / mask / relu / "
               "rowsum / a_amax / tiled operands / k_splits / n_store)");
-  AON_REQUIRE(a->n_store == 0 || a->n_store == a->N || bf16_copy_path(a),
-              "n_store < N: the bf16 LDS-DMA weight-gradient path only (both operands bf16, "
-              "M and N multiples of 128)");
+  AON_REQUIRE(a->n_store == 0 || a->n_store == a->N || bf16_copy_path(a) ||
+                  (!a->mma_bf16 && !a->exact_fp32),
+              "n_store < N: the bf16 LDS-DMA weight-gradient path (both operands bf16, M and N "
+              "multiples of 128) or an fp32 product");
   if (a->M == 0 || a->N == 0) return 0;
   AON_REQUIRE(!a->c_trans || skinny_path(a), "c_trans: the skinny path only (M <= 4)");
   Params p;
@@ -2395,10 +2422,11 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     p.part = static_cast<float*>(work);
     p.rowsum_part = p.part + zs * a->M * a->N;
   }
-  const bool f1 = f1_256_path(a);
-  const bool t256 = (a->mma_bf16 && bf16_copy256_path(a)) || f1;
+  const bool f1 = f1_path(a);
+  const bool t256 = a->mma_bf16 && bf16_copy256_path(a);
   const int64_t bmt = t256 ? BM2 : BM;  // C tile edge of the kernel that runs
-  const int64_t tiles_m = (a->M + bmt - 1) / bmt, tiles_n = (a->N + bmt - 1) / bmt;
+  // (k_gemm_f1: the whole product is one tile)
+  const int64_t tiles_m = f1 ? 1 : (a->M + bmt - 1) / bmt, tiles_n = f1 ? 1 : (a->N + bmt - 1) / bmt;
   const int64_t gm = tiles_m < 8 ? tiles_m : 8;
   const int64_t blocks = (tiles_m + gm - 1) / gm * gm * tiles_n;
   AON_REQUIRE(blocks < (1ll << 31), "too large");
@@ -2460,7 +2488,9 @@ extern "C" int aon_gemm(const aon_gemm_args* a, void* work, size_t work_bytes,
     if (a->b_tiled) launch_skinny<float, true, float>(p, g, st);
     else launch_skinny<float, false, float>(p, g, st);
   } else if (f1) {
-    hipLaunchKernelGGL(k_gemm_f1_256, grid, dim3(THREADS2), 0, st, p);
+    if (a->M == 128) hipLaunchKernelGGL((k_gemm_f1<128, 256>), grid, dim3(THREADS2), 0, st, p);
+    else if (a->N == 64) hipLaunchKernelGGL((k_gemm_f1<256, 64>), grid, dim3(THREADS2), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm_f1<256, 256>), grid, dim3(THREADS2), 0, st, p);
   } else if (f16_copy_path(a)) {
     hipLaunchKernelGGL(k_gemm_f16x3_dma, grid, dim3(THREADS), 0, st, p);
   } else if (a->a_kc && a->b_kc) launch_v<true, true>(p, va, vb, grid, st);
@@ -2488,6 +2518,7 @@ constexpr int kBatchClasses[] = {kBatchF1, kBatchF16, kBatch256, kBatch128};
 static int batch_class(const aon_gemm_args* a) {
   if (a->k_splits > 0 || a->K < 8 * 1024) return kBatchNone;
   if (f1_256_path(a)) return kBatchF1;
+  if (f1_path(a)) return kBatchNone;  // k_gemm_f1's other shapes: their own launch
   if (!a->mma_bf16) {
     // fp16x3 weight gradients dW = dY^T X: fp32 reduction-major operands in 16-B runs, whole
     // 128 x 128 tiles, no epilogue beyond accumulate (k_gemm_f16x3<false, false, true, true>)

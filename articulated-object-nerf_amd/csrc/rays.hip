@@ -165,6 +165,34 @@ __global__ void k_cast_rays(const float* __restrict__ ro, const float* __restric
   }
 }
 
+// The same encodings in the fused training kernels' 16-row tiled layout (mlp_f16x3_core.hpp
+// act_base) with `width` columns, the ones past 3 + 6 L zero: the parity mode's copy of
+// pos_enc(x) for the enc-column weight gradients (aon_gemm's 256 x 64 f16_single kernel reads
+// whole 16-column tiles).  One thread per (sample, column).
+template <typename Idx>
+__global__ void k_cast_rays_tiled(const float* __restrict__ ro, const float* __restrict__ rd,
+                                  const float* __restrict__ t, int64_t B, int S, int min_deg,
+                                  int L, int width, float* __restrict__ enc) {
+  const int C = 3 + 6 * L;
+  const Idx total = static_cast<Idx>(B * S * width);
+  for (Idx i = blockIdx.x * (Idx)blockDim.x + threadIdx.x; i < total;
+       i += (Idx)gridDim.x * blockDim.x) {
+    const Idx r = i / static_cast<Idx>(width);
+    const int f = static_cast<int>(i - r * static_cast<Idx>(width));
+    float v = 0.0f;
+    if (f < C) {
+      const Idx b = r / static_cast<Idx>(S);
+      const float tv = t[r];
+      const float x0 = __fadd_rn(ro[3 * b], __fmul_rn(tv, rd[3 * b]));
+      const float x1 = __fadd_rn(ro[3 * b + 1], __fmul_rn(tv, rd[3 * b + 1]));
+      const float x2 = __fadd_rn(ro[3 * b + 2], __fmul_rn(tv, rd[3 * b + 2]));
+      v = pos_enc_feature(x0, x1, x2, f, min_deg, L);
+    }
+    const int64_t rr = static_cast<int64_t>(r);
+    enc[(rr & ~int64_t(15)) * width + 256 * (f >> 4) + 16 * (rr & 15) + (f & 15)] = v;
+  }
+}
+
 // Training-ray batches straight from the device-resident dataset (reference
 // datasets/sapien.py:84-113 / :131-154 and sapien_multi.py:196-238): for flat index
 // g = image * H * W + pixel, the camera ray of that pixel (as k_frame_rays) and its target:
@@ -292,6 +320,24 @@ extern "C" int aon_cast_rays(const float* rays_o, const float* rays_d, const flo
     hipLaunchKernelGGL(k_cast_rays<int64_t>, grid_for(B * S * C, 256, 65536), 256, 0,
                        (hipStream_t)stream, rays_o, rays_d, t, B, S, offset, offset_stride, xyz,
                        min_deg, L, enc);
+  return launch_status(__func__);
+}
+
+extern "C" int aon_cast_rays_tiled(const float* rays_o, const float* rays_d, const float* t,
+                                   int64_t B, int S, int min_deg, int max_deg, int width,
+                                   float* enc, aon_stream_t stream) {
+  AON_REQUIRE(rays_o && rays_d && t && enc && B >= 0 && S >= 1, "bad arguments");
+  AON_REQUIRE(max_deg >= min_deg && min_deg >= -126 && max_deg <= 127, "bad degrees");
+  AON_REQUIRE(width % 16 == 0 && width >= 3 + 6 * (max_deg - min_deg),
+              "width: a multiple of 16 holding every encoding");
+  if (B == 0) return 0;
+  const int L = max_deg - min_deg;
+  if (B * S * width < (int64_t(1) << 31))
+    hipLaunchKernelGGL(k_cast_rays_tiled<uint32_t>, grid_for(B * S * width, 256, 65536), 256, 0,
+                       (hipStream_t)stream, rays_o, rays_d, t, B, S, min_deg, L, width, enc);
+  else
+    hipLaunchKernelGGL(k_cast_rays_tiled<int64_t>, grid_for(B * S * width, 256, 65536), 256, 0,
+                       (hipStream_t)stream, rays_o, rays_d, t, B, S, min_deg, L, width, enc);
   return launch_status(__func__);
 }
 

@@ -89,6 +89,13 @@ int aon_cast_rays(const float* rays_o, const float* rays_d, const float* t, int6
                   const float* offset, int64_t offset_stride, float* xyz, int min_deg,
                   int max_deg, float* enc, aon_stream_t stream);
 
+/* cast_rays + pos_enc as above (no offset, no xyz), written in the fused training kernels'
+ * tiled layout (aon_mlp_fwd_train) with `width` columns (a multiple of 16), the ones past
+ * 3 + 6 (max - min) zero: enc holds B*S rounded up to 16 rows (rows past B*S not written).  The
+ * parity mode's pos_enc(x) copy for the enc-column weight gradients (ABI 10). */
+int aon_cast_rays_tiled(const float* rays_o, const float* rays_d, const float* t, int64_t B, int S,
+                        int min_deg, int max_deg, int width, float* enc, aon_stream_t stream);
+
 /* pos_enc (helper.py:136-140): out (n, 3 + 6*(max_deg-min_deg)). */
 int aon_pos_enc(const float* x, int64_t n, int min_deg, int max_deg, float* out,
                 aon_stream_t stream);
@@ -436,7 +443,8 @@ typedef struct aon_gemm_args {
   int a_tiled, b_tiled;
   /* columns of C written (0: all N): a B zero-padded to whole 128-column tiles (the bf16 mode's
    * pos_enc copy, 63 -> 128 columns) updates only the real columns of dW; n_store < N on the
-   * bf16 LDS-DMA path only (both operands bf16, M and N multiples of 128) */
+   * bf16 LDS-DMA path (both operands bf16, M and N multiples of 128) and on fp32 products
+   * (the parity mode's 64-column pos_enc copy, aon_cast_rays_tiled; ABI 10) */
   int64_t n_store;
   /* exact_fp32 = 1: compute in exact fp32 fmaf instead of the fp16x3 MFMA split, in a fixed
    * (deterministic) order: K <= 16 one fma chain in k order per output; K > 16 one wave per

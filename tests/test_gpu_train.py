@@ -166,6 +166,60 @@ def test_f16_single_weight_gradient(K):
     assert e1 < 2e-6 and e10 < 2e-6 and eb < 1e-6 and ea < 2e-6
 
 
+@pytest.mark.parametrize("M,N,n_store", [(128, 256, 256), (256, 64, 63)])
+def test_f16_single_other_shapes(M, N, n_store):
+    """k_gemm_f1's 128 x 256 (views_linear.0's bottleneck columns) and 256 x 64 (the pos_enc
+    columns against aon_cast_rays_tiled's 64-column copy, n_store 63) shapes: against fp64 at
+    the GEMM gate, rowsum, only n_store columns written, deterministic; and the tiled
+    encodings equal the row-major aon_cast_rays ones bit for bit."""
+    from aonerf import _lib as L
+    from aonerf import tiles
+    from aonerf.linalg import ACT_SCALE, gemm
+
+    K = 70003
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    A = torch.randn((K, M), device="cuda", generator=g) * 1e-3
+    if N == 64:  # pos_enc(o + t d) tiled, as the f16x3 training step keeps it
+        B_, S = 61, K // 61 + 1
+        ro = torch.randn((B_, 3), device="cuda", generator=g)
+        rd = torch.randn((B_, 3), device="cuda", generator=g)
+        t = torch.rand((B_, S), device="cuda", generator=g) * 4 + 2
+        Bt = torch.full((tiles.rows(B_ * S), 64), float("nan"), device="cuda")
+        L.call("aon_cast_rays_tiled", L.ptr(ro), L.ptr(rd), L.ptr(t), B_, S, 0, 10, 64, L.ptr(Bt),
+               L.stream())
+        enc = torch.empty((B_ * S, 63), device="cuda")
+        L.call("aon_cast_rays", L.ptr(ro), L.ptr(rd), L.ptr(t), B_, S, None, 0, None, 0, 10,
+               L.ptr(enc), L.stream())
+        un = tiles.untile(Bt, B_ * S)
+        assert torch.equal(un[:, :63], enc) and not un[:, 63].any()
+        B = un[:K]  # the product's K rows of the (longer) tiled copy
+    else:
+        B = torch.relu(torch.randn((K, N), device="cuda", generator=g)) * 3
+        Bt = tiles.tile(B)
+    At = tiles.tile(A)
+    word = torch.zeros((1,), dtype=torch.int32, device="cuda")
+    L.call("aon_absmax", L.ptr(A), A.numel(), L.ptr(word), L.stream())
+    outs = []
+    for single in (True, True, False):
+        C = torch.full((M, N), 7.0, device="cuda")
+        db = torch.empty((M,), device="cuda")
+        gemm(C, At, Bt, M, N, K, lda=M, a_kc=False, ldb=N, b_kc=False, ldc=N, rowsum=db,
+             a_scale=1.0, b_scale=8.0 if single else ACT_SCALE, a_amax=word, a_tiled=True,
+             b_tiled=True, n_store=n_store if single else 0, f16_single=single)
+        outs.append((C, db))
+    torch.cuda.synchronize()
+    (C1, db1), (C2, db2), (C0, _) = outs
+    assert torch.equal(C1, C2) and torch.equal(db1, db2)
+    want = (A.double().T @ B.double()).cpu().numpy()
+    e = rel_err(C1[:, :n_store].cpu().numpy(), want[:, :n_store])
+    e0 = rel_err(C1[:, :n_store].cpu().numpy(), C0[:, :n_store].cpu().numpy())
+    eb = rel_err(db1.cpu().numpy(), A.double().sum(0).cpu().numpy())
+    print(f"f16_single dW {M}x{N} K={K}: max-rel {e:.2e} (vs two accumulators {e0:.2e}), rowsum {eb:.2e}")
+    assert e < 2e-6 and e0 < 2e-6 and eb < 1e-6
+    if n_store < N:
+        assert (C1[:, n_store:] == 7.0).all()
+
+
 @pytest.mark.parametrize("M,N,K,tiled", [(3, 128, 790528, True), (1, 256, 790528, True),
                                          (4, 256, 70003, False), (2, 16, 5, False)])
 def test_f32_skinny_weight_gradient(M, N, K, tiled):
