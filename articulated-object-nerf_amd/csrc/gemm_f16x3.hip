@@ -1640,6 +1640,189 @@ __global__ __launch_bounds__(THREADS2, 1) void k_gemm_f1_256_batch(ParamsBatch p
   f1_body<256, 256, false>(pb.p[b], z, smem);
 }
 
+// The batch's 256 x 256 products as two 256 x 128 half tiles each (k_gemm_f1h_batch): a
+// workgroup keeps 64 accumulator VGPRs per wave instead of 128, which buys AON_F1H_SETS
+// register sets of staged runs -- that many k-tiles of loads in flight instead of one -- for
+// twice the A reads, the second from L2 (the two halves of a chunk are dispatched together on
+// one XCD: block ids 8 apart).
+#ifndef AON_F1H_SETS
+#define AON_F1H_SETS 2  // 3 spills (22 VGPRs): 5.13 ms against 3.62-3.71 for 2, 4.08-4.12 whole tiles
+#endif
+#ifndef AON_F1_HALF
+#define AON_F1_HALF 1  // 0: A/B build -- the batch on whole 256 x 256 tiles (k_gemm_f1_256_batch)
+#endif
+constexpr int F1H_SETS = AON_F1H_SETS;
+
+// one thread's run of a k-tile of the 128-column half h of a tiled fp32 operand of width 256:
+// run u = tid: k row 16 (u / 256) + (u % 32) / 2, columns 16 ((u % 256) / 32) + 8 (u % 2) of
+// the half (a wave reads two 1-KB runs of the tiled layout)
+struct F1HalfRun {
+  f4 v[2];
+  __device__ __forceinline__ static int row(int tid) { return 16 * (tid >> 8) + ((tid & 31) >> 1); }
+  __device__ __forceinline__ static int col(int tid) { return 16 * ((tid & 255) >> 5) + 8 * (tid & 1); }
+  __device__ __forceinline__ void load(const float* base, int h, int64_t k0, int64_t kend, int tid) {
+    const int rr = row(tid);
+    const f4* src = reinterpret_cast<const f4*>(base + (k0 + 16 * (tid >> 8)) * 256 +
+                                                256 * (8 * h + ((tid & 255) >> 5)) +
+                                                16 * ((tid & 31) >> 1) + 8 * (tid & 1));
+    if (k0 + rr < kend) {
+      v[0] = src[0];
+      v[1] = src[1];
+    } else {
+      v[0] = f4{0.f, 0.f, 0.f, 0.f};
+      v[1] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ __forceinline__ void store(char* hi, char* lo, float s, int tid) const {
+    h8 hh, ll;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = v[e >> 2][e & 3] * s;
+      const _Float16 q = static_cast<_Float16>(x);
+      hh[e] = q;
+      ll[e] = static_cast<_Float16>(__fsub_rn(x, static_cast<float>(q)));
+    }
+    const int off = tt_off(row(tid), col(tid) >> 3);
+    *reinterpret_cast<h8*>(hi + off) = hh;
+    *reinterpret_cast<h8*>(lo + off) = ll;
+  }
+};
+
+struct F1HSet {
+  F1Run<256> a;
+  F1HalfRun b;
+};
+
+constexpr int F1H_STAGE = 2 * F1Img<256>::kPlane + 2 * F1Img<128>::kPlane;  // 48 KB
+
+// product p's half h (columns 128 h ..) of K chunk z
+__device__ __forceinline__ void f1h_body(const Params& p, int h, int z, char* smem) {
+  float sa = p.sa, inv_s = p.inv_s;
+  if (p.sa_bits) {
+    const float gs = grad_scale(*p.sa_bits);
+    sa = __fmul_rn(sa, gs);
+    inv_s = __fdiv_rn(inv_s, gs);
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // 4 x 2 waves of 64 x 64
+  const int64_t kbeg = (int64_t)z * p.kchunk;
+  const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = static_cast<int>((kend - kbeg + BK - 1) / BK);
+  const bool want_rows = p.rowsum != nullptr && h == 0;
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  F1HSet set[F1H_SETS];
+  auto load = [&](F1HSet& st, int kt) {
+    const int64_t k0 = kbeg + (int64_t)kt * BK;
+    st.a.load(p.A, k0, kend, tid, 0);
+    st.a.load(p.A, k0, kend, tid, 1);
+    st.b.load(p.B, h, k0, kend, tid);
+  };
+  auto publish = [&](const F1HSet& st, int stage) {
+    char* s = smem + stage * F1H_STAGE;
+    if (want_rows) {
+      st.a.add_rows(rs, 0);
+      st.a.add_rows(rs, 1);
+    }
+    st.a.store(s, s + F1Img<256>::kPlane, sa, tid, 0);
+    st.a.store(s, s + F1Img<256>::kPlane, sa, tid, 1);
+    char* sb = s + 2 * F1Img<256>::kPlane;
+    st.b.store(sb, sb + F1Img<128>::kPlane, p.sb, tid);
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // tiles 0 .. SETS-1 into the sets, tile 0 to stage 0, its set refilled with tile SETS
+#pragma unroll
+  for (int q = 0; q < F1H_SETS; ++q)
+    if (q < nk) load(set[q], q);
+  if (nk > 0) {
+    publish(set[0], 0);
+    if (F1H_SETS < nk) load(set[0], F1H_SETS);
+  }
+  __syncthreads();
+  // step kt: tile kt in stage kt & 1; tile kt + 1 in set (kt + 1) % SETS, published between
+  // this step's MFMAs and that set refilled with tile kt + 1 + SETS (loaded SETS steps ahead)
+  auto step = [&](int kt, auto cur) {
+    constexpr int NXT = (decltype(cur)::value + 1) % F1H_SETS;
+    const char* s = smem + (kt & 1) * F1H_STAGE;
+    const char* sb = s + 2 * F1Img<256>::kPlane;
+    h8 ah[4], al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = F1Img<256>::frag(s, 8 * wm + 2 * i, lane);
+      al[i] = F1Img<256>::frag(s + F1Img<256>::kPlane, 8 * wm + 2 * i, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c0 = 2 * (4 * wn + j);
+      const h8 bh = F1Img<128>::frag(sb, c0, lane);
+      const h8 bl = F1Img<128>::frag(sb + F1Img<128>::kPlane, c0, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i][j] = mfma16(ah[i], bh, acc[i][j]);
+        acc[i][j] = mfma16(ah[i], bl, acc[i][j]);
+        acc[i][j] = mfma16(al[i], bh, acc[i][j]);
+      }
+      if (j == 0 && kt + 1 < nk) {
+        publish(set[NXT], (kt + 1) & 1);
+        if (kt + 1 + F1H_SETS < nk) load(set[NXT], kt + 1 + F1H_SETS);
+      }
+    }
+    __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += F1H_SETS) {
+    step(kt, std::integral_constant<int, 0>{});
+    if (F1H_SETS > 1 && kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1 % F1H_SETS>{});
+    if (F1H_SETS > 2 && kt + 2 < nk) step(kt + 2, std::integral_constant<int, 2 % F1H_SETS>{});
+    if (F1H_SETS > 3 && kt + 3 < nk) step(kt + 3, std::integral_constant<int, 3 % F1H_SETS>{});
+  }
+  const bool split = p.zsplit > 1;
+  if (want_rows) {
+    float* red = reinterpret_cast<float*>(smem);  // [16 r][256]
+    const int r = (tid & 31) >> 1, c = 16 * (tid >> 5) + 8 * (tid & 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[r * 256 + c + e] = rs[e];
+    __syncthreads();
+    if (tid < 256) {
+      float v = red[tid];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) v = __fadd_rn(v, red[q * 256 + tid]);
+      if (split) p.rowsum_part[(int64_t)z * p.M + tid] = v;
+      else p.rowsum[tid] = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = 128 * h + 64 * wn + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = 64 * wm + 16 * i + 4 * (lane >> 4) + r;
+        float v = __fmul_rn(acc[i][j][r], inv_s);
+        if (split) {
+          p.part[((int64_t)z * p.M + m) * p.N + n] = v;
+          continue;
+        }
+        float* c = p.C + m * p.ldc + n;
+        if (p.accumulate) v = __fadd_rn(*c, v);
+        *c = v;
+      }
+    }
+}
+
+// T = 2 count half tiles: chunk z of every half of every product on one XCD, the two halves of
+// a (product, chunk) 8 block ids apart
+__global__ __launch_bounds__(THREADS2, 1) void k_gemm_f1h_batch(ParamsBatch pb) {
+  __shared__ __align__(16) char smem[2 * F1H_STAGE];
+  const int T = 2 * pb.count, L = blockIdx.x, x = L & 7, q = L >> 3;
+  const int z = 8 * (q / T) + x, t = q - (q / T) * T;
+  if (z >= pb.zsplit) return;  // padding block of the last chunk group (uniform exit)
+  f1h_body(pb.p[t >> 1], t & 1, z, smem);
+}
+
 // ---- fp16x3 weight gradients on the LDS-DMA ring (fp32 operands, both reduction-major):
 // k_gemm_f16x3<false, false> staged each k-tile through registers (global loads -> transpose ->
 // split -> LDS), one tile ahead, and ran the fine level's 256 x 256 x 790k products at ~3 TB/s
@@ -2552,7 +2735,8 @@ static BatchPlan plan_class(const aon_gemm_args* a, int count, int cls) {
   if (pl.n < 2) { pl.n = 0; return pl; }
   for (int j = 0; j < pl.n; ++j) {
     const aon_gemm_args* g = &a[pl.idx[j]];
-    pl.tiles += cls == kBatch256 || cls == kBatchF1 ? 1 : (g->M / BM) * (g->N / BN);
+    pl.tiles += cls == kBatch256 ? 1 : cls == kBatchF1 ? (AON_F1_HALF ? 2 : 1)
+                                                   : (g->M / BM) * (g->N / BN);
   }
   // 256 x 256 tiles: one workgroup per CU (256 in all), chunks >= 1024 rows; 128 x 128 tiles:
   // two per CU (512), chunks >= 2048 rows -- each product's chunks longer by the batch size;
@@ -2659,8 +2843,11 @@ static int run_plan(const aon_gemm_args* a, const BatchPlan& pl, int cls, void* 
       part += pl.zs * (g->M * g->N + g->M);
     }
   }
-  const dim3 grid((unsigned)(8 * pb.tile0[pl.n] * ((pl.zs + 7) / 8)), 1, 1);
+  // (k_gemm_f1h_batch: two half tiles per product)
+  const int wtiles = cls == kBatchF1 && AON_F1_HALF ? 2 * pl.n : pb.tile0[pl.n];
+  const dim3 grid((unsigned)(8 * wtiles * ((pl.zs + 7) / 8)), 1, 1);
   if (cls == kBatch256) hipLaunchKernelGGL(k_gemm_bf16_dma256_batch, grid, dim3(THREADS2), 0, st, pb);
+  else if (cls == kBatchF1 && AON_F1_HALF) hipLaunchKernelGGL(k_gemm_f1h_batch, grid, dim3(THREADS2), 0, st, pb);
   else if (cls == kBatchF1) hipLaunchKernelGGL(k_gemm_f1_256_batch, grid, dim3(THREADS2), 0, st, pb);
   else if (cls == kBatch128) hipLaunchKernelGGL(k_gemm_bf16_dma_batch, grid, dim3(THREADS), 0, st, pb);
   else hipLaunchKernelGGL(k_gemm_f16x3_batch, grid, dim3(THREADS), 0, st, pb);
