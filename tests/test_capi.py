@@ -52,6 +52,28 @@ def test_invalid_arguments_raise(L, name, args):
         L.call(name, *args)
 
 
+def test_abi10_argument_checks(L):
+    """ABI 10's new entry points refuse bad arguments before any launch (no GPU needed):
+    aon_cast_rays_tiled's width (a multiple of 16 holding every encoding), the articulated bf16
+    forward's `mixed` range and aon_gemm's n_store on an exact-fp32 tiny product."""
+    p = ctypes.c_void_p(16)
+    with pytest.raises(ValueError, match="width"):
+        L.call("aon_cast_rays_tiled", p, p, p, 4, 8, 0, 10, 48, p, None)  # 63 encodings > 48
+    with pytest.raises(ValueError, match="width"):
+        L.call("aon_cast_rays_tiled", p, p, p, 4, 8, 0, 10, 72, p, None)  # not a multiple of 16
+    with pytest.raises(ValueError, match="bad arguments"):
+        L.call("aon_cast_rays_tiled", None, p, p, 4, 8, 0, 10, 64, p, None)
+    with pytest.raises(ValueError, match="mixed"):
+        L.call("aon_mlp_art_fwd_train_bf16", p, p, p, p, p, 1, 1, None, p, p, p, p, p, p, p, p, p,
+               5, None)
+    with pytest.raises(ValueError, match="mixed"):
+        L.call("aon_mlp_art_pack_mixed", None, 4, p, None)
+    a = L.AonGemmArgs(M=2, N=4, K=3, A=16, lda=3, a_kc=1, B=16, ldb=4, b_kc=0, b_rdiv=1, C=16,
+                      ldc=4, a_scale=1.0, b_scale=1.0, exact_fp32=1, n_store=2)
+    with pytest.raises(ValueError, match="n_store"):
+        L.call("aon_gemm", ctypes.byref(a), None, 0, None)
+
+
 def test_pdf_shape_limits(L):
     with pytest.raises(ValueError, match="bad shape"):
         L.call("aon_sample_pdf", ctypes.c_void_p(16), 0, ctypes.c_void_p(16), 0, 4, 1000, 128,
