@@ -279,23 +279,25 @@ def test_f32_segsum_weight_gradient(K, rdiv):
     assert e < 1e-6 and eb < 1e-6
 
 
-def test_f16_single_weight_gradient_batch_full_level():
-    """The fine level's 790,528-row products as aon_gemm_batch's f16_single class
-    (k_gemm_f1_256_batch: chunk z of every product on one XCD) plus a two-accumulator product in
-    the same batch: each within 2e-6 of its own f16_single launch and of the two-accumulator
-    kernel (fp64 at this size is the single-size test above); deterministic."""
+@pytest.mark.parametrize("K", [790528, 70003])
+def test_f16_single_weight_gradient_batch_full_level(K):
+    """The fine level's 790,528-row products (and a ragged 70,003-row level) as aon_gemm_batch's
+    f16_single class (k_gemm_f1h_batch: 256 x 128 half tiles, chunk z of every half on one XCD)
+    plus a two-accumulator product in the same batch, the third accumulating: each within 2e-6
+    of its own f16_single launch and of the two-accumulator kernel (fp64 at this size is the
+    single-size test above); deterministic."""
     from aonerf.linalg import batched
 
-    K = 790528
     A, B, At, Bt, word = _single_operands(K, 5)
     del A, B
+    C_init = torch.randn((256, 256), device="cuda")
 
     def run():
-        Cs = [torch.zeros((256, 256), device="cuda") for _ in range(3)]
+        Cs = [torch.zeros((256, 256), device="cuda") for _ in range(2)] + [C_init.clone()]
         rs = [torch.empty((256,), device="cuda") for _ in range(3)]
         with batched():
             for i in range(3):
-                _single_dw(At, Bt, word, K, i != 1, C=Cs[i], rowsum=rs[i])
+                _single_dw(At, Bt, word, K, i != 1, C=Cs[i], rowsum=rs[i], accumulate=i == 2)
         torch.cuda.synchronize()
         return Cs, rs
 
@@ -308,7 +310,8 @@ def test_f16_single_weight_gradient_batch_full_level():
     e_own = rel_err(Cb[0].cpu().numpy(), own.cpu().numpy())
     e_v1 = rel_err(Cb[0].cpu().numpy(), v1.cpu().numpy())
     print(f"f16_single dW batch K={K}: vs own launch {e_own:.2e}, vs two accumulators {e_v1:.2e}")
-    assert torch.equal(Cb[0], Cb[2]) and e_own < 2e-6 and e_v1 < 2e-6
+    assert torch.equal(Cb[0] + C_init, Cb[2])  # accumulate: C_init + the same product
+    assert torch.equal(rb[0], rb[2]) and e_own < 2e-6 and e_v1 < 2e-6
     assert rel_err(Cb[1].cpu().numpy(), v1.cpu().numpy()) < 1e-6
 
 
