@@ -220,7 +220,7 @@ _SIGNATURES = {
 _lib = None
 
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 def _load(path):

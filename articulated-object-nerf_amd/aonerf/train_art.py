@@ -232,13 +232,16 @@ def _pack_bwd(P, dev, tag="", bf16=False):
 
 
 def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None,
-                         masks=None, bf16=False, enc_bf=None):
+                         masks=None, bf16=False, enc_bf=None, return_enc_bf=False):
     """_forward_level on the fused kernel (aon_mlp_art_fwd_train): raw (R x 4) and the kept
-    activations (tiled, tiles.rows(R) rows each), plus the sample points and pos_enc(x')
-    (row-major); ``masks`` ((16, tiles.rows(R), 8) int32) receives the ReLU' bits of hd0..3,
-    h0..7, hv0..3 for the backward chain.  bf16: the bf16 mode (aon_mlp_art_fwd_train_bf16;
-    hd / h / bot / hv kept as torch.bfloat16; ``enc_bf``, optional, (tiles.rows(R), 128)
-    bfloat16, receives pos_enc(x') tiled, columns 63.. zero)."""
+    activations (tiled, tiles.rows(R) rows each), the sample points (row-major) and pos_enc(x')
+    (tiled, (tiles.rows(R), 64), column 63 zero); ``masks`` ((16, tiles.rows(R), 8) int32)
+    receives the ReLU' bits of hd0..3, h0..7, hv0..3 for the backward chain.  bf16: the bf16
+    mode (aon_mlp_art_fwd_train_bf16; hd / h / bot / hv kept as torch.bfloat16; enc keeps
+    columns 0..15 only, (tiles.rows(R), 16) -- the chain reads x' = columns 0..2 -- and
+    ``enc_bf`` ((tiles.rows(R), 128) bfloat16, allocated when None) receives pos_enc(x') tiled,
+    columns 63.. zero: the enc-column weight gradients' operand).  enc_rows() converts enc for
+    the all-GEMM backward."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
     NR = tiles.rows(R)
@@ -249,7 +252,9 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     h = torch.empty((8, NR, geo.nw), device=dev, dtype=dt)
     bot = torch.empty((NR, geo.nw), device=dev, dtype=dt)
     hv = torch.empty((4, NR, geo.wc), device=dev, dtype=dt)
-    enc = torch.empty((R, geo.ne), device=dev)
+    enc = torch.empty((NR, 16 if bf16 else 64), device=dev)
+    if bf16 and enc_bf is None:
+        enc_bf = torch.empty((NR, 128), device=dev, dtype=torch.bfloat16)
     xyz = torch.empty((R, 3), device=dev)
     mixed = (1 if BF16_TRUNK else 2 if BF16_VIEW else 3 if F16_WEIGHTS else 4 if F16_ACTS else 0
              ) if bf16 else 0
@@ -259,13 +264,37 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
             L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h), L.ptr(bot),
             L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks))
     if bf16:
-        L.call("aon_mlp_art_fwd_train_bf16", *args, L.ptr(enc_bf) if enc_bf is not None else None,
-               mixed, L.stream(dev))
+        L.call("aon_mlp_art_fwd_train_bf16", *args, L.ptr(enc_bf), mixed, L.stream(dev))
     else:
         L.call("aon_mlp_art_fwd_train", *args, L.stream(dev))
     L.snapshot_pack(packed)  # the forward was the pack's last reader (range guard, _lib)
     _train._rec(f"art_fwd_train{S}", e0, R)
-    return xyz, hd, enc, h, bot, hv
+    return (xyz, hd, enc, h, bot, hv) + ((enc_bf,) if return_enc_bf else ())
+
+
+def enc_rows(geo, enc, R):
+    """pos_enc(x') row-major (R, 63) fp32 from what a level's forward kept: as is (the
+    layer-by-layer forward), untiled (the fused fp16x3 forward's (NR, 64)), or recomputed from
+    x' (the fused bf16 forward keeps columns 0..15 only) by aon_pos_enc -- the kernel's own
+    pos_enc_feature, bit-identical."""
+    if enc.shape[1] == geo.ne:
+        return enc
+    if enc.shape[1] == 64:
+        return tiles.untile(enc, R)[:, :geo.ne].contiguous()
+    xp = tiles.untile(enc, R)[:, :3].contiguous()
+    out = torch.empty((R, geo.ne), device=enc.device)
+    L.call("aon_pos_enc", L.ptr(xp), R, geo.min_deg, geo.max_deg, L.ptr(out), L.stream(enc.device))
+    return out
+
+
+def _enc_tiled(enc, width):
+    """The chain's enc operand (tiled, ``width`` columns) from a row-major (R, 63) pos_enc(x')."""
+    if enc.shape[1] == width:
+        return enc
+    pad = torch.zeros((enc.shape[0], width), device=enc.device)
+    n = min(width, enc.shape[1])
+    pad[:, :n] = enc[:, :n]
+    return tiles.tile(pad)
 
 
 def _fused_ok(geo):
@@ -281,6 +310,7 @@ def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, dra
     density column of d raw, from all of d raw), as the fused chain scales its gradients."""
     R, dev = xyz.shape[0], xyz.device
     wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
+    enc = enc_rows(geo, enc, R)
     shape, app, art = lat
     dshape, dapp, dart = dlat
     gs, acts = GRAD_SCALE, ACT_SCALE
@@ -381,8 +411,10 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     kernel (aon_mlp_art_bwd); the weight gradients dW = dZ^T X, db = sum_rows dZ and the latent
     terms stay GEMMs.  ``masks``: the fused forward's ReLU' bits (built from the activations
     when None); h_tiled: hd / h / bot / hv in the fused forward's tiled layout (else
-    row-major); the chain's dzv / dbot / dz / dzd are tiled.  enc_bf: the bf16 forward's tiled
-    128-column pos_enc(x') (the enc-column weight gradients then run on the LDS-DMA kernel)."""
+    row-major); the chain's dzv / dbot / dz / dzd are tiled.  enc: the fused forward's tiled
+    pos_enc(x') ((NR, 64) fp16x3, (NR, 16) bf16) or the layer-by-layer forward's row-major
+    (R, 63).  enc_bf: the bf16 forward's tiled 128-column pos_enc(x') (the enc-column weight
+    gradients then run on the LDS-DMA kernel)."""
     R, dev = xyz.shape[0], xyz.device
     bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
@@ -400,8 +432,10 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     dzd = torch.empty((4, NR, wd), device=dev, dtype=dt)
     work = _buffer("work", 4, dev)
     packed = _pack_bwd(P, dev, S, bf16)
+    enc_t = enc.shape[1] != ne  # the fused forward's tiled copy
+    enc_chain = enc if enc_t else _enc_tiled(enc, 16 if bf16 else 64)
     e0 = _train._ev()
-    L.call("aon_mlp_art_bwd_bf16" if bf16 else "aon_mlp_art_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), L.ptr(enc), R,
+    L.call("aon_mlp_art_bwd_bf16" if bf16 else "aon_mlp_art_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), L.ptr(enc_chain), R,
            L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
     L.snapshot_pack(packed)  # the chain was the pack's last reader
     _train._rec(f"art_bwd_chain{S}", e0, R)
@@ -412,18 +446,23 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
         n_store = 0
         if X is enc and bf16 and enc_bf is not None:  # the tiled bf16 copy, 63 of 128 columns
             X, ldx, n_store, n_in = enc_bf, 128, n_in, 128
+        elif X is enc and enc_t:  # the fused fp16x3 forward's tiled fp32 copy, 63 of 64 columns
+            if enc.shape[1] != 64:
+                raise ValueError("the bf16 forward keeps 16 enc columns: pass its enc_bf")
+            ldx, n_store, n_in = 64, n_in, 64
         # chain_scale: dY is in the chain's d raw domain (draw, view/trunk outputs): A rides at
         # the chain's own per-call scale from max |d raw| (the word it left in `work`); the
         # deformation branch (dL/dx' carries pos_enc's 2^9, rescaled per sample) keeps 2^10.
         # a_t: dY is one of the chain's tiled gradients; X is tiled when it is a kept activation.
         # bf16: one bf16 MFMA per product, no scales (bf16 has fp32's exponent range)
         dW = G[i][0]
-        b_t = (h_tiled and X is not enc and X is not venc and X is not xyz) or X is enc_bf
-        # f16x3, the 256 x 256 / 128 x 256 products of the fused kernels' tiled tensors: one
-        # accumulator (aon_gemm f16_single), dY at the chain's scale, X at the forward's 2^3
-        # (train.py)
-        single = (not bf16 and chain_scale and a_t and b_t and col0 == 0 and ldx == n_in
-                  and (dW.shape[0], n_in) in ((256, 256), (128, 256)))
+        b_t = ((h_tiled and X is not enc and X is not venc and X is not xyz) or X is enc_bf
+               or (X is enc and enc_t))
+        # f16x3, the 256 x 256 / 128 x 256 / 256 x 64 products of the fused kernels' tiled
+        # tensors: one accumulator (aon_gemm f16_single), dY at the chain's scale, X at the
+        # forward's 2^3 (train.py; pos_enc(x') and x' far inside the range)
+        single = (not bf16 and chain_scale and a_t and b_t and ldx == n_in
+                  and (dW.shape[0], n_in) in ((256, 256), (128, 256), (256, 64)))
         gemm(dW[:, col0:] if col0 else dW, dY, X, dW.shape[0], n_in, R, lda=ldy, a_kc=False,
              ldb=ldx, b_kc=False, b_rdiv=rdiv, ldc=dW.stride(0),
              a_scale=1.0 if (chain_scale or bf16) else gs,
@@ -508,11 +547,9 @@ class ArtRenderLevel(torch.autograd.Function):
         if FUSED_FORWARD and _fused_ok(geo):
             masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device=dev)
             bf16 = PRECISION == "bf16"
-            enc_bf = (torch.empty((tiles.rows(R), 128), device=dev, dtype=torch.bfloat16)
-                      if bf16 else None)
-            xyz, hd, enc, h, bot, hv = _forward_level_fused(
+            xyz, hd, enc, h, bot, hv, enc_bf = _forward_level_fused(
                 geo, P, lat, L.contig(rays_o), L.contig(rays_d), L.contig(viewdirs),
-                L.contig(t_vals), raw, noise, masks, bf16=bf16, enc_bf=enc_bf)
+                L.contig(t_vals), raw, noise, masks, bf16=bf16, return_enc_bf=True)
         else:
             xyz = torch.empty((R, 3), device=dev)
             L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,

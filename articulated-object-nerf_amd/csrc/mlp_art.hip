@@ -153,11 +153,13 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float f = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10);
-        if (STORE && rows[c] < N && 32 * k + 8 * g + e < 63) ts.enc[63 * rows[c] + 32 * k + 8 * g + e] = f;
         fv[k][e] = f;
         ev[k][e] = f * act_scale<BFM>();
       }
-    if (STORE && PREC != 0 && ts.enc_bf && keep_row(rows[c], N)) store_enc_bf(ts.enc_bf, rows[c], g, fv);
+    if (STORE && keep_row(rows[c], N)) {
+      store_enc_f32<PREC == 0 ? 64 : 16>(ts.enc, rows[c], g, fv);
+      if (PREC != 0) store_enc_bf(ts.enc_bf, rows[c], g, fv);
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       split8<BFM>(ev[k], enc.hi[k][c], enc.lo[k][c], enc.ovf);
@@ -328,7 +330,8 @@ static int art_fwd_train(const void* packed, const float* rays_o, const float* r
                          int prec, __bf16* enc_bf = nullptr) {
   AON_REQUIRE(packed && rays_o && rays_d && viewdirs && t && raw, "null pointer");
   AON_REQUIRE(hd && h && bot && hv && enc && xyz && masks, "null activation buffer");
-  AON_REQUIRE(aligned16(masks), "masks must be 16-byte aligned");
+  AON_REQUIRE(aligned16(masks) && aligned16(enc), "masks / enc must be 16-byte aligned");
+  AON_REQUIRE(!prec || (enc_bf && aligned16(enc_bf)), "enc_bf: a 16-byte aligned buffer");
   AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
   AON_REQUIRE(aligned16(packed) && aligned16(raw), "packed / raw must be 16-byte aligned");
   AON_REQUIRE(((reinterpret_cast<uintptr_t>(hd) | reinterpret_cast<uintptr_t>(h) |
@@ -385,7 +388,6 @@ extern "C" int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_
                                           void* hd, void* h, void* bot, void* hv, float* enc,
                                           float* xyz, float* raw, uint32_t* masks, void* enc_bf,
                                           int mixed, aon_stream_t stream) {
-  AON_REQUIRE(aligned16(enc_bf), "enc_bf must be 16-byte aligned");
   AON_REQUIRE(mixed >= 0 && mixed <= 4,
               "mixed: 0 fp16x3, 1 trunk bf16, 2 view branch bf16, 3 fp16 weights, 4 fp16 activations");
   return art_fwd_train(packed, rays_o, rays_d, viewdirs, t, B, S, noise, static_cast<float*>(hd),

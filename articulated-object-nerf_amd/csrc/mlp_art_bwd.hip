@@ -29,7 +29,7 @@ namespace mlp {
 struct ArtBwdArgs {
   const float* draw;       // (N, 4): d raw_rgb (3), d raw_sigma
   const uint2* masks;      // (16, N, 4) ReLU' bits of hd0..3, h0..7, hv0..3
-  const float* enc;        // (N, 63) pos_enc(x'), enc[:, :3] = x'
+  const float* enc;        // the forward's tiled fp32 pos_enc(x') (store_enc_f32): x' = columns 0..2
   float* dzv;              // (4, N, 128): dL/d pre-activation of views_linear.i
   float* dbot;             // (N, 256): dL/d bottleneck output
   float* dz;               // (8, N, 256): dL/d pre-activation of pts_linears.i
@@ -163,6 +163,7 @@ __global__ __launch_bounds__(ArtBwdGeom<BF>::kThreads, 2) void k_mlp_art_bwd_f16
     const f4* __restrict__ wstream, const float* __restrict__ bias_g, ArtBwdArgs a) {
   constexpr int NCOL = BF ? kBfNcolArtBwd : 1;
   constexpr bool kRegPark = NCOL > 1;  // enc-column values and d sigma kept in registers
+  constexpr int kEncW = BF ? 16 : 64;  // the forward's store_enc_f32 width
   using G = ArtBwdGeom<BF>;
   using Net = NetArtBwdH;
   using T = typename std::conditional<BF, __bf16, float>::type;
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(ArtBwdGeom<BF>::kThreads, 2) void k_mlp_art_bwd_f16
     for (int c = 0; c < NCOL; ++c)
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        eb.x[c][q] = a.enc[63 * rrs[c] + q];
+        eb.x[c][q] = a.enc[enc_x_index(rrs[c], kEncW) + q];
         eb.dx[c][q] = 0.f;
       }
     layer_h<Net, AB_P0E, false>(fp, x, none, junk, bias_l, g, eb);
@@ -293,9 +294,9 @@ __global__ __launch_bounds__(ArtBwdGeom<BF>::kThreads, 2) void k_mlp_art_bwd_f16
   } else {
     EncBwd eb;
     eb.slot = slot;
-    eb.x0 = a.enc[63 * rrs[0]];
-    eb.x1 = a.enc[63 * rrs[0] + 1];
-    eb.x2 = a.enc[63 * rrs[0] + 2];
+    eb.x0 = a.enc[enc_x_index(rrs[0], kEncW)];
+    eb.x1 = a.enc[enc_x_index(rrs[0], kEncW) + 1];
+    eb.x2 = a.enc[enc_x_index(rrs[0], kEncW) + 2];
     eb.g = g;
     layer_h<Net, AB_P0E, false>(fp, x, none, junk, bias_l, g, eb);
     dx[0][0] = eb.dx0;
@@ -400,7 +401,7 @@ static int art_bwd(const void* packed, const float* draw, const uint32_t* masks,
   AON_REQUIRE(packed && draw && masks && enc && dzv && dbot && dz && dxp && dzd && work,
               "null pointer");
   AON_REQUIRE(N >= 0, "bad shape");
-  AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(masks) && aligned16(dzv) &&
+  AON_REQUIRE(aligned16(packed) && aligned16(draw) && aligned16(masks) && aligned16(enc) && aligned16(dzv) &&
                   aligned16(dbot) && aligned16(dz) && aligned16(dzd),
               "buffers must be 16-byte aligned");
   if (N == 0) return 0;

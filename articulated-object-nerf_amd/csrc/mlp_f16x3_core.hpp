@@ -358,6 +358,25 @@ __device__ __forceinline__ void store_enc_bf(__bf16* base, int64_t row, int g,
   }
 }
 
+// The articulated training forward's fp32 pos_enc(x'), tiled (act_base) with EW columns: EW = 64
+// keeps every feature (63 zero; the fp16x3 mode's enc-column weight gradients read it, and the
+// chain reads x' = columns 0..2); EW = 16 keeps columns 0..15 only (the bf16 modes: their
+// weight gradients read store_enc_bf's copy, so the chain's x' is all the fp32 copy serves).
+// Lane group g holds features 32 k + 8 g .. + 7: two 16-B stores into tile 2 k + g / 2.
+template <int EW>
+__device__ __forceinline__ void store_enc_f32(float* base, int64_t row, int g,
+                                              const float (&fv)[2][8]) {
+  float* e = base + act_base(row, EW, 0) + 8 * (g & 1) + 256 * (g >> 1);
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (32 * k + 16 * (g >> 1) < EW) {
+      kept_store(e + 512 * k, f4{fv[k][0], fv[k][1], fv[k][2], fv[k][3]});
+      kept_store(e + 512 * k + 4, f4{fv[k][4], fv[k][5], fv[k][6], fv[k][7]});
+    }
+}
+// x' (columns 0..2) of a store_enc_f32<EW> tensor
+__device__ __forceinline__ int64_t enc_x_index(int64_t row, int EW) { return act_base(row, EW, 0); }
+
 #ifndef AON_BF_ST16
 #define AON_BF_ST16 1
 #endif

@@ -332,15 +332,17 @@ TRAIN_BYTES_BF16 = {"fwd_train": 4 + 16 + 2 * 2432 + 288 + 2 * 128, "bwd_chain":
                     "dweight": 2 * (2432 + 2432) + 2 * 2 * 128 + 4 * 27}
 # articulated level (NeRF_AE_Art, model_autodecoder.py:168-239), bytes per sample: the fused
 # forward writes raw (16) + 3,328 activations (hd 4x128, h 8x256, bot 256, hv 4x128) + pos_enc(x')
-# (63) + the points (3) + ReLU' bits (16 x 32) and reads t; the chain reads d raw + bits + enc and
-# writes 3,328 gradients + dL/dx' (3); the weight GEMMs read every dZ (3,335) and every layer
-# input once (3,484: activations, enc twice, points, view encodings)
-ART_TRAIN_BYTES = {"art_fwd_train": 4 + 16 + 4 * (3328 + 63 + 3) + 512,
-                   "art_bwd_chain": 16 + 512 + 4 * 63 + 4 * (3328 + 3),
-                   "art_dweight": 4 * (3335 + 3484)}
-# bf16 mode: the kept activations and chain gradients 2 B (enc, points, d raw, dL/dx' fp32)
-ART_TRAIN_BYTES_BF16 = {"art_fwd_train": 4 + 16 + 2 * 3328 + 4 * (63 + 3) + 512 + 2 * 128,
-                        "art_bwd_chain": 16 + 512 + 4 * 63 + 2 * 3328 + 4 * 3,
+# (tiled, 64 columns; ABI 11) + the points (3) + ReLU' bits (16 x 32) and reads t; the chain reads
+# d raw + bits + x' (enc's columns 0..2) and writes 3,328 gradients + dL/dx' (3); the weight GEMMs
+# read every dZ (3,335) and every layer input once (3,486: activations, enc twice, points, view
+# encodings)
+ART_TRAIN_BYTES = {"art_fwd_train": 4 + 16 + 4 * (3328 + 64 + 3) + 512,
+                   "art_bwd_chain": 16 + 512 + 4 * 3 + 4 * (3328 + 3),
+                   "art_dweight": 4 * (3335 + 3486)}
+# bf16 mode: the kept activations and chain gradients 2 B (points, d raw, dL/dx' fp32; the fp32
+# enc keeps columns 0..15 -- x' for the chain -- beside the bf16 128-column copy)
+ART_TRAIN_BYTES_BF16 = {"art_fwd_train": 4 + 16 + 2 * 3328 + 4 * (16 + 3) + 512 + 2 * 128,
+                        "art_bwd_chain": 16 + 512 + 4 * 3 + 2 * 3328 + 4 * 3,
                         "art_dweight": 2 * (3328 + 3328) + 2 * 2 * 128 + 4 * (3 + 4 + 3 + 27)}
 ART_TRAIN_FLOP = {"art_fwd_train": 2 * 714_880, "art_bwd_chain": 2 * (714_880 - 3 * 128 - 128 * 27),
                   "art_dweight": 2 * 714_880}

@@ -24,7 +24,7 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 10
+#define AON_ABI_VERSION 11
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -305,19 +305,20 @@ int aon_mlp_art_fwd(const void* packed, const float* rays_o, const float* rays_d
 /* Training forward of one articulated level (reference model_autodecoder.py:168-239 under
  * autograd): aon_mlp_art_fwd (MODE 0 inputs, raw outputs, no activation) that also keeps what
  * the backward needs -- tiled (NR = B*S rounded up to 16): hd (4, NR, 128) deformation layers,
- * h (8, NR, 256) pts_linears, bot (NR, 256), hv (4, NR, 128) views_linear; row-major: enc (B*S,
- * 63) = pos_enc(x') and xyz (B*S, 3) the sample points; raw_sigma += noise[r] when noise !=
- * NULL (:318-319); masks (16, NR, 4) pairs
- * of uint32: the ReLU' bits of hd0..3, h0..7, hv0..3 (layout of aon_mlp_fwd_train's).  Activation
- * buffers 8-byte aligned, raw and masks 16-byte aligned. */
+ * h (8, NR, 256) pts_linears, bot (NR, 256), hv (4, NR, 128) views_linear, enc (NR, 64) =
+ * pos_enc(x') (column 63 zero; ABI 11 -- row-major (B*S, 63) before); row-major: xyz (B*S, 3)
+ * the sample points; raw_sigma += noise[r] when noise != NULL (:318-319); masks (16, NR, 4)
+ * pairs of uint32: the ReLU' bits of hd0..3, h0..7, hv0..3 (layout of aon_mlp_fwd_train's).
+ * Activation buffers 8-byte aligned, raw, enc and masks 16-byte aligned. */
 int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
                           const float* viewdirs, const float* t, int64_t B, int S,
                           const float* noise, float* hd, float* h, float* bot, float* hv,
                           float* enc, float* xyz, float* raw, uint32_t* masks,
                           aon_stream_t stream);
 /* The articulated bf16 training mode (train_art.PRECISION = "bf16"; BASELINE config C5's
- * "bf16" on the articulated model): hd, h, bot, hv are bf16 arrays of the shapes above, enc /
- * xyz / raw / masks as above.  mixed != 0: packed by aon_mlp_art_pack_bf16 (a mixed stream in
+ * "bf16" on the articulated model): hd, h, bot, hv are bf16 arrays of the shapes above, xyz /
+ * raw / masks as above, enc (NR, 16) fp32 tiled: pos_enc(x') columns 0..15 only (x' = columns
+ * 0..2, all the chain reads; ABI 11).  mixed != 0: packed by aon_mlp_art_pack_bf16 (a mixed stream in
  * the same buffer size: the deformation MLP stays fp16x3 -- x' feeds sin(2^9 x') -- the trunk,
  * heads and view branch are bf16), one bf16 MFMA per product past the deformation head;
  * mixed == 0: packed by aon_mlp_art_pack, fp16x3 numerics throughout (only the stores bf16).
@@ -329,8 +330,9 @@ int aon_mlp_art_fwd_train(const void* packed, const float* rays_o, const float* 
  * mixed == 4: packed by aon_mlp_art_pack (the fp16x3 stream) -- the deformation MLP fp16x3,
  * every later layer two fp16 MFMAs per product, (hi(W) + lo(W)) x hi(x): the weights' exact
  * split kept, the activations rounded once to fp16 (range-guarded as the hi parts).
- * enc_bf (optional, NULL: not kept): pos_enc(x') as bf16, tiled (NR, 128), columns 63..127 zero
- * (as aon_mlp_fwd_train_bf16's enc). */
+ * enc_bf (required since ABI 11, 16-byte aligned): pos_enc(x') as bf16, tiled (NR, 128),
+ * columns 63..127 zero (as aon_mlp_fwd_train_bf16's enc) -- the enc-column weight gradients'
+ * operand. */
 int aon_mlp_art_pack_bf16(const aon_mlp_art_params* params, void* packed, aon_stream_t stream);
 /* mixed = 1: as aon_mlp_art_pack_bf16; mixed = 2: the view-branch stream; mixed = 3: the
  * fp16-weight stream (ABI 9). */
@@ -343,8 +345,9 @@ int aon_mlp_art_fwd_train_bf16(const void* packed, const float* rays_o, const fl
                                void* enc_bf, int mixed, aon_stream_t stream);
 
 /* Backward chain of one articulated level (autograd of model_autodecoder.py:168-239): from
- * dL/d raw (N, 4), the ReLU' bits (16, N, 4) of hd0..3, h0..7, hv0..3 and pos_enc(x') (enc) kept
- * by aon_mlp_art_fwd_train, to
+ * dL/d raw (N, 4), the ReLU' bits (16, N, 4) of hd0..3, h0..7, hv0..3 and the tiled pos_enc(x')
+ * (enc, (NR, 64); the bf16 chain: aon_mlp_art_fwd_train_bf16's (NR, 16)) kept by
+ * aon_mlp_art_fwd_train, to
  * every layer's dL/d pre-activation -- tiled (NR rows): dzv (4, NR, 128) views_linear.i, dbot
  * (NR, 256) the bottleneck output, dz (8, NR, 256) pts_linears.i, dzd (4, NR, 128)
  * deformations_linear.i; row-major dxp (N, 3) = dL/dx' (the deformation head's output, through

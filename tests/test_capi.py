@@ -35,7 +35,7 @@ def test_header_symbols_exported(L):
 
 def test_abi_version_and_sizes(L):
     lib = L.lib()
-    assert lib.aon_abi_version() == L.ABI_VERSION == 10
+    assert lib.aon_abi_version() == L.ABI_VERSION == 11
     assert lib.aon_mlp_packed_bytes(0) == 2368 * 1024 + 2464 * 4 + 16  # + the status block
     assert lib.aon_mlp_packed_bytes(99) == 0
 
@@ -72,6 +72,19 @@ def test_abi10_argument_checks(L):
                       ldc=4, a_scale=1.0, b_scale=1.0, exact_fp32=1, n_store=2)
     with pytest.raises(ValueError, match="n_store"):
         L.call("aon_gemm", ctypes.byref(a), None, 0, None)
+
+
+def test_abi11_argument_checks(L):
+    """ABI 11: the articulated training forward keeps pos_enc(x') tiled with 16-byte stores, so
+    enc must be 16-byte aligned, and the bf16 entry requires enc_bf (its fp32 enc keeps x' only)."""
+    p, odd = ctypes.c_void_p(16), ctypes.c_void_p(20)
+    with pytest.raises(ValueError, match="enc_bf"):
+        L.call("aon_mlp_art_fwd_train_bf16", p, p, p, p, p, 1, 1, None, p, p, p, p, p, p, p, p,
+               None, 4, None)
+    with pytest.raises(ValueError, match="enc must be 16-byte aligned"):
+        L.call("aon_mlp_art_fwd_train", p, p, p, p, p, 1, 1, None, p, p, p, p, odd, p, p, p, None)
+    with pytest.raises(ValueError, match="16-byte aligned"):
+        L.call("aon_mlp_art_bwd", p, p, p, odd, 1, p, p, p, p, p, p, None)
 
 
 def test_pdf_shape_limits(L):

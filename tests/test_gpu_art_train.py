@@ -123,6 +123,7 @@ def test_fused_art_train_forward_activations():
     # kept tensors are tiled (aonerf/tiles.py; 2,405 rows: a partial last block)
     hd_f, h_f, hv_f = ([tiles.untile(x, R) for x in tt] for tt in (hd_t, h_t, hv_t))
     bot_f = tiles.untile(bot_t, R)
+    enc_f = train_art.enc_rows(geo, enc_f, R)  # tiled (NR, 64), column 63 zero
     # the ReLU' bits written by the forward == those built from its stored activations
     rebuilt = train_art.relu_masks(list(hd_f) + list(h_f) + list(hv_f), R)
     for i in range(16):
@@ -249,7 +250,7 @@ def test_art_backward_stage_isolated(B, S, level, scale, bwd):
            for k, v in sd.items() if k.startswith(pre)}
     names = ("density", "color", "articulation")
     l64 = {k: x.cpu().double().requires_grad_(True) for k, x in zip(names, lat)}
-    enc_c = enc.cpu()
+    enc_c = train_art.enc_rows(geo, enc, R).cpu()
     kept = {"xyz": xyz.cpu(), "hd": list(rm[0].cpu()), "xp": enc_c[:, :3].clone(), "enc": enc_c,
             "h": list(rm[1].cpu()), "bot": bot_rm.cpu(), "hv": list(rm[2].cpu())}
     r_rgb, r_sig = O.art_mlp_forward_kept(p64, kept, venc.cpu(), l64, S)
@@ -329,7 +330,7 @@ def test_art_c5_level_stage_isolated(level):
                                     masks, True)
     torch.cuda.synchronize()
     rm = [torch.stack([tiles.untile(x, R) for x in tt]).cpu() for tt in (hd, h, hv)]
-    enc_c = enc.cpu()
+    enc_c = train_art.enc_rows(geo, enc, R).cpu()
     kept = {"xyz": xyz.cpu(), "hd": list(rm[0]), "xp": enc_c[:, :3].clone(), "enc": enc_c,
             "h": list(rm[1]), "bot": tiles.untile(bot, R).cpu(), "hv": list(rm[2])}
     pre = "fine_mlp." if level else "coarse_mlp."
@@ -611,7 +612,7 @@ def test_art_train_step_c5_4096_rays():
             _, hd, enc, h, _, hv = train_art._forward_level_fused(
                 train_art._Geo(mlp), P, lat_t, batch["rays_o"], batch["rays_d"], batch["viewdirs"],
                 t, raw)
-            xp_ours.append(enc[:, :3].cpu())
+            xp_ours.append(tiles.untile(enc, R)[:, :3].cpu())
             # the ReLU' pattern our forward fed the backward: the sign of each kept activation
             relu_ours.append({grp: [tiles.untile(x, R).cpu() > 0 for x in tt]
                               for grp, tt in (("hd", hd), ("h", h), ("hv", hv))})

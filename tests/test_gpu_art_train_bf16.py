@@ -113,12 +113,15 @@ def test_art_bf16_forward(level, mode, monkeypatch):
     (xyz32, hd32, enc32, h32, bot32, hv32), raw32, m32 = out[False]
     (xyzbf, hdbf, encbf, hbf, botbf, hvbf), rawbf, mbf = out[True]
     assert hdbf.dtype == hbf.dtype == botbf.dtype == hvbf.dtype == torch.bfloat16
-    assert torch.equal(xyzbf, xyz32) and torch.equal(encbf, enc32)
+    # pos_enc(x'): the fp16x3 forward keeps it tiled (NR, 64), the bf16 one columns 0..15
+    e32 = tiles.untile(enc32, R)
+    assert encbf.shape == (tiles.rows(R), 16) and not e32[:, 63].any()
+    assert torch.equal(xyzbf, xyz32) and torch.equal(tiles.untile(encbf, R), e32[:, :16])
     assert torch.equal(hdbf, hd32.to(torch.bfloat16))
     assert torch.equal(mbf[:4], m32[:4])  # ReLU' bits of hd0..3
     # the tiled bf16 copy of pos_enc(x') for the enc-column weight gradients
     eb = tiles.untile(enc_bf, R)
-    assert torch.equal(eb[:, :63], enc32.to(torch.bfloat16)) and not eb[:, 63:].float().any()
+    assert torch.equal(eb[:, :63], e32[:, :63].to(torch.bfloat16)) and not eb[:, 63:].float().any()
     if not trunk:
         assert torch.equal(rawbf, raw32) and torch.equal(mbf, m32)
         for a, b in ((hbf, h32), (botbf, bot32), (hvbf, hv32)):
@@ -141,7 +144,7 @@ def test_art_bf16_forward(level, mode, monkeypatch):
         samples = O.cast_rays(t.cpu().double(), batch["rays_o"].cpu().double(), batch["rays_d"].cpu().double())
         rgb64, sig64 = O.art_mlp_forward(p64, samples, venc.cpu().double(),
                                          {k: x.cpu().double() for k, x in zip(names, lat)},
-                                         xp_fixed=encbf[:, :3].cpu(), record=rec)
+                                         xp_fixed=tiles.untile(encbf, R)[:, :3].cpu(), record=rec)
     errs = {}
     for i in range(8):
         errs[f"h{i}"] = rel_err(tiles.untile(hbf[i], R).float().cpu(), rec["h"][i])
@@ -400,9 +403,9 @@ def test_art_bf16_backward_stage_isolated(level, monkeypatch):
     P = [(m.weight.detach(), m.bias.detach()) for m in train_art.art_layers(mlp)]
     raw = torch.empty((R, 4), device="cuda")
     masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device="cuda")
-    xyz, hd, enc, h, bot, hv = train_art._forward_level_fused(
+    xyz, hd, enc, h, bot, hv, enc_bf = train_art._forward_level_fused(
         geo, P, lat_t, batch["rays_o"], batch["rays_d"], batch["viewdirs"], t, raw, None, masks,
-        bf16=True)
+        bf16=True, return_enc_bf=True)
     venc = torch.empty((B, 27), device="cuda")
     L.call("aon_pos_enc", L.ptr(batch["viewdirs"]), B, 0, 4, L.ptr(venc), L.stream())
     comp = torch.empty((B, 3), device="cuda")
@@ -419,11 +422,11 @@ def test_art_bf16_backward_stage_isolated(level, monkeypatch):
     G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
     dlat = tuple(torch.empty_like(x) for x in lat_t)
     train_art._backward_level_fused(geo, P, G, lat_t, dlat, xyz, enc, venc, S, hd, h, bot, hv,
-                                    draw, masks, True)
+                                    draw, masks, True, enc_bf)
     torch.cuda.synchronize()
     assert h[0].dtype == torch.bfloat16
     rm = [torch.stack([tiles.untile(x, R).float() for x in tt]).cpu() for tt in (hd, h, hv)]
-    enc_c = enc.cpu()
+    enc_c = train_art.enc_rows(geo, enc, R).cpu()
     kept = {"xyz": xyz.cpu(), "hd": list(rm[0]), "xp": enc_c[:, :3].clone(), "enc": enc_c,
             "h": list(rm[1]), "bot": tiles.untile(bot, R).float().cpu(), "hv": list(rm[2])}
     pre = "fine_mlp." if level else "coarse_mlp."

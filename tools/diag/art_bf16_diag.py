@@ -96,9 +96,9 @@ def main():
             P = [(m.weight.detach(), m.bias.detach()) for m in train_art.art_layers(mlp)]
             raw = torch.empty((R, 4), device="cuda")
             masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device="cuda")
-            xyz, hd, enc, h, bot, hv = train_art._forward_level_fused(
+            xyz, hd, enc, h, bot, hv, enc_bf = train_art._forward_level_fused(
                 geo, P, lat_t, batch["rays_o"], batch["rays_d"], batch["viewdirs"], t, raw, None,
-                masks, bf16=True)
+                masks, bf16=True, return_enc_bf=True)
             venc = torch.empty((B, 27), device="cuda")
             L.call("aon_pos_enc", L.ptr(batch["viewdirs"]), B, 0, 4, L.ptr(venc), L.stream())
             comp = torch.empty((B, 3), device="cuda")
@@ -116,10 +116,10 @@ def main():
             G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
             dlat = tuple(torch.empty_like(x) for x in lat_t)
             train_art._backward_level_fused(geo, P, G, lat_t, dlat, xyz, enc, venc, S, hd, h, bot,
-                                            hv, draw, masks, True)
+                                            hv, draw, masks, True, enc_bf)
             torch.cuda.synchronize()
             rm = [torch.stack([tiles.untile(x, R).float() for x in tt]).cpu() for tt in (hd, h, hv)]
-            enc_c = enc.cpu()
+            enc_c = train_art.enc_rows(geo, enc, R).cpu()
             kept = {"xyz": xyz.cpu(), "hd": list(rm[0]), "xp": enc_c[:, :3].clone(), "enc": enc_c,
                     "h": list(rm[1]), "bot": tiles.untile(bot, R).float().cpu(), "hv": list(rm[2])}
             pre = "fine_mlp." if level else "coarse_mlp."

@@ -69,7 +69,7 @@ def main():
                 geo, P, lat, batch["rays_o"], batch["rays_d"], batch["viewdirs"], t, raw)
         torch.cuda.synchronize()
         rm = [torch.stack([tiles.untile(x, R) for x in tt]).cpu() for tt in (hd, h, hv)]
-        enc_c = enc.cpu()
+        enc_c = train_art.enc_rows(geo, enc, R).cpu()
         ours = {"xyz": xyz.cpu().double(), "hd": [x.double() for x in rm[0]],
                 "xp": enc_c[:, :3].clone(), "enc": enc_c.double(),
                 "h": [x.double() for x in rm[1]], "bot": tiles.untile(bot, R).cpu().double(),

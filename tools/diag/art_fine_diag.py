@@ -70,7 +70,7 @@ def main():
     torch.cuda.synchronize()
     rm = [torch.stack([tiles.untile(x, R) for x in tt]).cpu() for tt in (hd, h, hv)]
     bot_rm = tiles.untile(bot, R).cpu()
-    enc_c = enc.cpu()
+    enc_c = train_art.enc_rows(geo, enc, R).cpu()
     kept = {"xyz": xyz.cpu(), "hd": list(rm[0]), "xp": enc_c[:, :3].clone(), "enc": enc_c,
             "h": list(rm[1]), "bot": bot_rm, "hv": list(rm[2])}
     pre = "fine_mlp." if level else "coarse_mlp."
