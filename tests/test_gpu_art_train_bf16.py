@@ -117,6 +117,9 @@ def test_art_bf16_forward(level, mode, monkeypatch):
     e32 = tiles.untile(enc32, R)
     assert encbf.shape == (tiles.rows(R), 16) and not e32[:, 63].any()
     assert torch.equal(xyzbf, xyz32) and torch.equal(tiles.untile(encbf, R), e32[:, :16])
+    # the all-GEMM backward's row-major pos_enc(x') recomputed from the bf16 forward's x'
+    # (aon_pos_enc, the kernel's own pos_enc_feature): bit-identical to what fp16x3 keeps
+    assert torch.equal(train_art.enc_rows(geo, encbf, R), e32[:, :63])
     assert torch.equal(hdbf, hd32.to(torch.bfloat16))
     assert torch.equal(mbf[:4], m32[:4])  # ReLU' bits of hd0..3
     # the tiled bf16 copy of pos_enc(x') for the enc-column weight gradients
