@@ -323,6 +323,9 @@ extern "C" int aon_mlp_art_fwd(const void* packed, const float* rays_o, const fl
   return art_launch(0, packed, rays_o, rays_d, viewdirs, t, B, S, act, out, stream);
 }
 
+#ifndef AON_ART_X1_NCOL
+#define AON_ART_X1_NCOL 1  // A/B knob (compile-time): samples per wave / 16 of the mixed-4 forward
+#endif
 static int art_fwd_train(const void* packed, const float* rays_o, const float* rays_d,
                          const float* viewdirs, const float* t, int64_t B, int S,
                          const float* noise, float* hd, float* h, float* bot, float* hv,
@@ -346,11 +349,13 @@ static int art_fwd_train(const void* packed, const float* rays_o, const float* r
   const float* bias =
       reinterpret_cast<const float*>(static_cast<const char*>(packed) + NetArtH::kStreamBytes);
   const TrainStoreArt ts{hd, h, bot, hv, enc, xyz, noise, reinterpret_cast<uint2*>(masks), enc_bf};
-  if (prec == 5)
-    hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 5>), (unsigned)grid, G::kThreads, 0,
+  if (prec == 5) {
+    using G5 = GeomH<AON_ART_X1_NCOL>;
+    hipLaunchKernelGGL((k_mlp_art_f16x3<0, AON_ART_X1_NCOL, true, 5>),
+                       (unsigned)((N + G5::kRowsPerBlock - 1) / G5::kRowsPerBlock), G5::kThreads, 0,
                        (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
                        (int)AON_ACT_NONE, raw, ts);
-  else if (prec == 4)
+  } else if (prec == 4)
     hipLaunchKernelGGL((k_mlp_art_f16x3<0, 1, true, 4>), (unsigned)grid, G::kThreads, 0,
                        (hipStream_t)stream, ws, bias, rays_o, rays_d, viewdirs, t, B, S,
                        (int)AON_ACT_NONE, raw, ts);
