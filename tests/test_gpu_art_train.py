@@ -82,12 +82,14 @@ def test_latent_reg():
         np.testing.assert_allclose(c.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-6, atol=0)
 
 
-@pytest.fixture(params=[(True, True), (False, False), (True, False)],
-                ids=["fused", "gemm", "fused_fwd_gemm_bwd"])
+@pytest.fixture(params=[(True, True), (False, False), (True, False), (False, True)],
+                ids=["fused", "gemm", "fused_fwd_gemm_bwd", "gemm_fwd_fused_bwd"])
 def art_fwd_mode(request):
     """Articulated training forward on the fused kernel with activation stores
     (aon_mlp_art_fwd_train) or layer by layer on aon_gemm; input gradients in the fused chain
-    (aon_mlp_art_bwd) or as GEMMs + aon_pos_enc_bwd."""
+    (aon_mlp_art_bwd) or as GEMMs + aon_pos_enc_bwd.  The mixed pairs convert pos_enc(x')
+    between the fused kernels' tiled copy and the GEMMs' row-major one (train_art.enc_rows /
+    _enc_tiled)."""
     from aonerf import train_art
 
     old = train_art.FUSED_FORWARD, train_art.FUSED_BACKWARD
