@@ -65,52 +65,122 @@ class GradAllReduce:
     """Data-parallel gradient averaging for the training step (run.py:109/151 trains with
     Lightning DDP: every rank draws its own ray batch, gradients are averaged).
 
-    The gradients of all parameters are packed into ONE flat bucket (vanilla NeRF: 1,191,688
-    values = 4.77 MB in fp32) and averaged with a single all-reduce (RCCL over xGMI; one bucket
-    amortises the per-collective latency, and at this size the ring is latency-, not
-    link-bound), then unpacked into each ``.grad``.
+    The gradients are packed into ONE flat buffer (vanilla NeRF: 1,191,688 values = 4.77 MB in
+    fp32) and averaged by all-reduce (RCCL over xGMI), then unpacked into each ``.grad``.
 
-    ``dtype=torch.bfloat16`` (for C5's bf16 mode) halves the bucket (2.38 MB):
+    ``buckets`` (optional): a partition of ``params`` into groups, in the order their gradients
+    complete in the backward -- e.g. ``[fine_mlp params, coarse_mlp params]``: autograd runs the
+    fine level's backward first (its node was created last), so the fine bucket's all-reduce is
+    issued from a post-accumulate-grad hook as soon as its last gradient lands and runs on RCCL's
+    stream while the coarse level's backward runs; the LAST bucket is always reduced in
+    ``__call__``.  Autograd sums a parameter's contributions from several uses (latent codes
+    both levels read) before its gradient lands, once per backward, so such a parameter simply
+    completes its bucket late; a gradient landing again in a bucket already in flight (a second
+    backward before ``__call__``: gradient accumulation) raises.
+    One bucket (the default) is one collective at ``__call__``: at 2-5 MB the ring is latency-,
+    not link-bound, so more buckets only pay where they overlap compute.
+
+    ``dtype=torch.bfloat16`` (for C5's bf16 mode) halves the bytes (2.38 MB):
     each rank's gradients are rounded to bf16, summed by the collective in bf16 (RCCL's ring
     rounds every partial sum to bf16: world - 1 roundings), then widened to fp32 and divided by
     the world size.  Relative error per value <= ~world x 2^-8 of the largest magnitude summed
-    into it; the fp32 master weights and Adam state are unchanged.  On a gloo group (CPU
-    transport) a device bucket is staged through the host.
+    into it; the fp32 master weights and Adam state are unchanged.  On a gloo group a device
+    buffer is staged through the host (no early launch there).
     """
 
-    def __init__(self, params, group=None, dtype=torch.float32):
+    def __init__(self, params, group=None, dtype=torch.float32, buckets=None):
         if dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("GradAllReduce: dtype must be torch.float32 or torch.bfloat16")
         self.params = [p for p in params if p.requires_grad]
+        if buckets is None:
+            buckets = [self.params]
+        buckets = [[p for p in b if p.requires_grad] for b in buckets]
+        order = [p for b in buckets for p in b]
+        if sorted(map(id, order)) != sorted(map(id, self.params)):
+            raise ValueError("GradAllReduce: buckets must partition the parameters")
+        self.params = order  # bucket order: each bucket one contiguous slice of the buffer
         self.group = group
         self.dtype = dtype
         self.sizes = [p.numel() for p in self.params]
+        spans, off = [], 0
+        for b in buckets:
+            n = sum(p.numel() for p in b)
+            spans.append((off, off + n, len(b)))
+            off += n
+        self.spans = spans  # (start, end, parameter count) per bucket
+        self.bucket_of = {}
+        k = 0
+        for bi, b in enumerate(buckets):
+            for p in b:
+                self.bucket_of[id(p)] = (bi, k)
+                k += 1
         self.flat = None
         self.flat32 = None
-        self.calls = 0  # collectives issued (bench.py records it with the DDP step)
+        self.calls = 0  # collectives issued (bench.py records them with the DDP step)
+        self._seen = [set() for _ in buckets]
+        self._works = [None] * len(buckets)
+        self._hooks = []
+        if len(buckets) > 1:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._landed))
 
-    def __call__(self):
-        if not dist.is_initialized():  # (a process group of one still runs the all-reduce)
-            return
-        self.calls += 1
-        world = dist.get_world_size(self.group)
-        dev = self.params[0].device
+    def _ensure(self, dev):
         if self.flat is None or self.flat.device != dev:
             n = sum(self.sizes)
             self.flat = torch.empty(n, dtype=self.dtype, device=dev)
             self.flat32 = self.flat if self.dtype == torch.float32 else torch.empty(n, device=dev)
-        off = 0
+
+    def _staged(self):
+        return self.flat.is_cuda and dist.get_backend(self.group) == "gloo"
+
+    def _landed(self, p):
+        # post-accumulate-grad hook: launch a bucket (not the last) once all its gradients landed
+        if not dist.is_initialized():
+            return
+        bi, _ = self.bucket_of[id(p)]
+        if self._works[bi] is not None:
+            raise RuntimeError("GradAllReduce: a gradient landed in a bucket already in flight "
+                               "(a second backward before the all-reduce; call it per backward)")
+        self._seen[bi].add(id(p))
+        if bi < len(self.spans) - 1 and len(self._seen[bi]) == self.spans[bi][2]:
+            self._ensure(p.device)
+            if not self._staged():
+                self._launch(bi)
+
+    def _launch(self, bi):
+        a, b, _ = self.spans[bi]
+        off = a
         for p, n in zip(self.params, self.sizes):
+            if self.bucket_of[id(p)][0] != bi:
+                continue
             if p.grad is None:
                 raise RuntimeError("GradAllReduce: a parameter has no gradient")
             self.flat[off:off + n].copy_(p.grad.reshape(-1))  # (rounds to bf16 in that mode)
             off += n
-        if self.flat.is_cuda and dist.get_backend(self.group) == "gloo":
-            host = self.flat.cpu()
+        self.calls += 1
+        seg = self.flat[a:b]
+        if self._staged():
+            host = seg.cpu()
             dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
-            self.flat.copy_(host)
+            seg.copy_(host)
+            self._works[bi] = True
         else:
-            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+            self._works[bi] = dist.all_reduce(seg, op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True)
+
+    def __call__(self):
+        if not dist.is_initialized():  # (a process group of one still runs the all-reduce)
+            return
+        world = dist.get_world_size(self.group)
+        self._ensure(self.params[0].device)
+        for bi in range(len(self.spans)):
+            if self._works[bi] is None:
+                self._launch(bi)
+        for w in self._works:
+            if w is not True:
+                w.wait()  # (RCCL: the current stream waits for the collective's)
+        self._works = [None] * len(self.spans)
+        self._seen = [set() for _ in self.spans]
         if self.flat32 is not self.flat:
             self.flat32.copy_(self.flat)
         self.flat32.div_(world)

@@ -117,6 +117,79 @@ def test_grad_allreduce_gloo_world2():
             assert torch.equal(gr, torch.full(gr.shape, 1.5 * (i + 1)))
 
 
+def _ddp_bucket_worker(rank, world, port, q):
+    """Two 'levels' (fine built last, so autograd runs its backward first) and a code shared by
+    both: buckets [fine, coarse + shared] launch the fine all-reduce from the gradient hooks
+    before __call__, and average exactly as one bucket does; a second backward before __call__
+    (its gradients would land in a bucket already in flight) raises."""
+    from aonerf.parallel import GradAllReduce
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(7)  # same weights on both ranks, different inputs
+        coarse = torch.nn.Linear(6, 4)
+        fine = torch.nn.Linear(6, 4)
+        shared = torch.nn.Parameter(torch.randn(4, generator=g))
+        for m in (coarse, fine):
+            for t in m.parameters():
+                t.data.copy_(torch.randn(t.shape, generator=g))
+        x = torch.randn(5, 6, generator=torch.Generator().manual_seed(100 + rank))
+
+        def backward():
+            for t in [*coarse.parameters(), *fine.parameters(), shared]:
+                t.grad = None
+            yc = coarse(x) * shared
+            yf = fine(x) * shared  # created last: its backward runs first
+            ((yc ** 2).sum() + (yf ** 3).sum()).backward()
+
+        params = [*coarse.parameters(), *fine.parameters(), shared]
+        one = GradAllReduce(params)
+        backward()
+        one()
+        ref = [t.grad.clone() for t in params]
+        two = GradAllReduce(params, buckets=[list(fine.parameters()),
+                                             [*coarse.parameters(), shared]])
+        backward()
+        early = two._works[0] is not None and two._works[1] is None and two.calls == 1
+        two()
+        same = all(torch.equal(t.grad, r) for t, r in zip(params, ref))
+        for h in two._hooks:
+            h.remove()
+        bad = GradAllReduce(params, buckets=[list(fine.parameters()), [*coarse.parameters(), shared]])
+        backward()
+        try:
+            backward()  # gradient accumulation without the all-reduce in between
+            raised = False
+        except RuntimeError as e:
+            raised = "already in flight" in str(e)
+        bad._works[0].wait()
+        q.put((rank, early, same, two.calls, raised))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_buckets_overlap_gloo_world2():
+    """GradAllReduce buckets: the first bucket's all-reduce is issued from the gradient hooks
+    (before __call__, i.e. overlapping the rest of the backward); results bit-equal to the one
+    bucket; a parameter accumulating after its bucket launched is refused."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, early, same, calls, raised in got:
+        assert early, rank
+        assert same, rank
+        assert calls == 2 and raised, rank
+
+
 def _ddp_bf16_worker(rank, world, port, q):
     from aonerf.parallel import GradAllReduce
 

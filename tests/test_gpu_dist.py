@@ -302,7 +302,7 @@ def test_bench_spawns_two_ranks_gloo(tmp_path):
     for key in ("train_step", "train_step_bf16", "train_step_art", "train_step_art_bf16"):
         d = rec[key]["ddp"]
         assert rec[key]["n_gpus"] == 2 and d["world"] == 2 and d["backend"] == "gloo", key
-        assert d["calls"] == 3, (key, d)  # warm-up + timed steps, one collective each
+        assert d["calls"] == 3 * d["buckets"] == 6, (key, d)  # warm-up + timed steps, 2 buckets
         assert d["params_identical_across_ranks"], (key, d)
         assert d["bucket_dtype"] == ("bf16" if key.endswith("bf16") else "fp32")
 
@@ -351,6 +351,50 @@ def _worker_c5_bf16(rank, world, port, q):
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def _worker_rccl_buckets(port, q):
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        from aonerf.parallel import GradAllReduce
+
+        net = _net()
+        ref = _c5_bf16_grads(net, 0)  # no collective
+        fine = list(net.fine_mlp.parameters())
+        coarse = list(net.coarse_mlp.parameters())
+        sync = GradAllReduce(net.parameters(), dtype=torch.bfloat16, buckets=[fine, coarse])
+        got = _c5_bf16_grads(net, 0)  # the hooks issue the fine bucket inside the backward
+        early = sync._works[0] is not None and sync._works[1] is None and sync.calls == 1
+        sync()
+        torch.cuda.synchronize()
+        q.put((early, sync.calls, [g.cpu().numpy() for g in ref], [g.cpu().numpy() for g in got],
+               [p.grad.cpu().numpy() for p in net.parameters()]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_bucketed_allreduce_overlaps_backward_world1():
+    """GradAllReduce's buckets on RCCL (world 1): C5's bf16 step with [fine, coarse] buckets --
+    the fine MLP's all-reduce is issued from the gradient hooks on autograd's device thread,
+    before the backward returns (it then runs beside the coarse level's backward), and the
+    gradients come back as bf16(g) exactly (one rank: the sum is the value), the same as
+    without buckets."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl_buckets, args=(_free_port(), q))
+    p.start()
+    early, calls, ref, got, after = q.get(timeout=240)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert early and calls == 2
+    for r, g, a in zip(ref, got, after):
+        np.testing.assert_array_equal(g, r)  # the backward itself is unchanged by the hooks
+        rb = torch.from_numpy(r).to(torch.bfloat16).float().numpy()
+        np.testing.assert_array_equal(a, rb)
 
 
 def test_c5_bf16_ddp_step_two_ranks():
