@@ -149,6 +149,9 @@ class GradAllReduce:
 
     def _launch(self, bi):
         a, b, _ = self.spans[bi]
+        if a == b:  # an empty bucket: nothing to reduce
+            self._works[bi] = True
+            return
         off = a
         for p, n in zip(self.params, self.sizes):
             if self.bucket_of[id(p)][0] != bi:
