@@ -388,15 +388,23 @@ struct pk_from_f32 : std::false_type {};
 template <typename S>
 struct pk_from_f32<S, std::void_t<decltype(S::kPkFromF32)>> : std::bool_constant<S::kPkFromF32> {};
 // pairs (r0 = 0, 2) of a tile meet in one 4-value store
+// fp32 kept values (the parity mode's activations and the chains' gradients): parts r0 = 0, 2 of
+// a tile row meet in ONE 16-B store per lane (the wave writes a whole 1-KB tile) instead of two
+// 8-B stores -- the kept stores are issue-bound (profiles/r05/vmcnt_ab/), and the 16-B form cut
+// the C5 f16x3 step 14.06 -> 13.38 ms (forward -7%, chain -9%; articulated forward -10%,
+// profiles/r05/st16_ab/).  0: the 8-B form (A/B).
+#ifndef AON_F32_ST16
+#define AON_F32_ST16 1
+#endif
 template <int NCOL, typename T>
 struct Store4 {
   bool ok[NCOL];  // keep_row of each column's sample (wave-uniform when tiled)
   mutable float pend[NCOL][2];
   __device__ __forceinline__ void emit(T* rowp, int pr, int uu, int r0, int c, float v0,
                                        float v1) const {
-    // fp32: one 8-B store per part (a lane's 16-B pair store measured slower); bf16: the two
-    // parts of a tile row meet in one 8-B store (4-B stores: 1.73 -> 1.51 ms forward)
-    if (std::is_same<T, float>::value) {
+    // fp32: one 16-B store per tile row (AON_F32_ST16; 0: one 8-B store per part); bf16: the
+    // two parts of a tile row meet in one 8-B store (4-B stores: 1.73 -> 1.51 ms forward)
+    if (std::is_same<T, float>::value && !AON_F32_ST16) {
       if (ok[c]) store2(rowp + kTileStride * (2 * pr + uu) + r0, v0, v1);
       return;
     }
