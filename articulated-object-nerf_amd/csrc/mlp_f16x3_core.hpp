@@ -475,11 +475,36 @@ struct RowStore : Store4<NCOL, T> {
 // layout [layer][N][4] of uint2), so the backward chains read 1/32 of the bytes of the fp32
 // activations for their masks.  Written a byte per output pair (the pair's 2 tiles x 4 rows),
 // so nothing is carried across pairs.
+// bf16 kept values: a layer's ReLU' word (row, g) gathered in registers byte by byte and stored
+// ONCE (8 B) at its last pair, instead of a byte store per pair (+ a zero byte per pair of a
+// 128-wide layer): bf16 forward 1.239 -> 1.219 ms, articulated 2.706 -> 2.666 ms
+// (profiles/r05/maskword_ab/).  fp32 forwards keep the byte stores (the gathered word spills
+// them: 182-207 VGPRs).  0: byte stores everywhere (A/B).
+#ifndef AON_MASK_WORD
+#define AON_MASK_WORD 1
+#endif
 template <int NCOL, typename T = float>
 struct RowStoreBits : RowStore<NCOL, T> {
   uint8_t* mrow[NCOL];  // bytes of word (row, g) (stored when ok)
   bool narrow;          // 4-pair (128-wide) layer: bytes 4..7 of the word are written as 0
   mutable uint32_t b[NCOL];  // the current pair's 8 bits (byte pr of the word)
+  mutable uint32_t wlo[NCOL], whi[NCOL];  // AON_MASK_WORD: bytes 0..3 / 4..7 gathered so far
+  // the finished byte of pair pr: kept and, at the layer's last pair, the whole word stored
+  __device__ __forceinline__ void byte_done(int pr, int c, uint32_t byte) const {
+    if constexpr (AON_MASK_WORD && std::is_same<T, __bf16>::value) {  // (fp32 forwards: spills)
+    if (pr < 4) wlo[c] = pr == 0 ? byte : (wlo[c] | (byte << (8 * pr)));
+    else whi[c] = pr == 4 ? byte : (whi[c] | (byte << (8 * (pr - 4))));
+    if (this->ok[c]) {
+      if (pr == 3 && narrow) kept_store(mrow[c], u32x2{wlo[c], 0u});
+      if (pr == 7) kept_store(mrow[c], u32x2{wlo[c], whi[c]});
+    }
+    } else {
+    if (this->ok[c]) {
+      kept_store(mrow[c] + pr, static_cast<uint8_t>(byte));
+      if (narrow) kept_store(mrow[c] + pr + 4, uint8_t{0});
+    }
+    }
+  }
   // bf16 layers: the bits from the packed ReLU output -- part q = 2 uu + r0 / 2 of the pair has
   // its two values' bits at 2q (element 0) and 2q + 1 (element 1): one v_pk_min_u16 gives them at
   // 0 and 16, one v_lshl_or_b32 per part gathers them at 2q and 16 + 2q, and the byte folds the
@@ -491,10 +516,7 @@ struct RowStoreBits : RowStore<NCOL, T> {
     const uint32_t m = pk_nonzero(pk);
     const int q = 2 * uu + (r0 >> 1);  // compile-time after unrolling
     b[c] = q == 0 ? m : lshl_or(m, 2 * q, b[c]);
-    if (q == 3 && this->ok[c]) {
-      kept_store(mrow[c] + pr, static_cast<uint8_t>(b[c] | (b[c] >> 15)));
-      if (narrow) kept_store(mrow[c] + pr + 4, uint8_t{0});
-    }
+    if (q == 3) byte_done(pr, c, (b[c] | (b[c] >> 15)) & 0xFFu);
   }
   __device__ __forceinline__ void put(int pr, int uu, int r0, int c, float v0, float v1) const {
     RowStore<NCOL, T>::put(pr, uu, r0, c, v0, v1);
@@ -504,10 +526,7 @@ struct RowStoreBits : RowStore<NCOL, T> {
     const uint32_t m = (v0 > 0.0f ? 1u : 0u) | (v1 > 0.0f ? 2u : 0u);  // v: post-ReLU, s > 0
     const int bit = 4 * uu + r0;  // within the pair's byte (compile-time after unrolling)
     b[c] = bit == 0 ? m : (b[c] | (m << bit));
-    if (uu == 1 && r0 == 2 && this->ok[c]) {
-      kept_store(mrow[c] + pr, static_cast<uint8_t>(b[c]));
-      if (narrow) kept_store(mrow[c] + pr + 4, uint8_t{0});
-    }
+    if (uu == 1 && r0 == 2) byte_done(pr, c, b[c] & 0xFFu);
   }
 };
 
