@@ -10,7 +10,9 @@ import os
 import torch  # load torch's HIP runtime first: libaonerf.so binds to the same libamdhip64.so.7
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("AONERF_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libaonerf.so"))
+# the release library; an A/B driver under tools/ may name another build with use_library()
+# before the first call (the product path reads no environment variable)
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libaonerf.so")
 
 c_i64, c_int, c_float, c_size, vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 
@@ -243,6 +245,15 @@ def lib():
     if _lib is None:
         _lib = _load(LIB_PATH)
     return _lib
+
+
+def use_library(path):
+    """Bind ``path`` (an A/B build of the library, same ABI) instead of the release library --
+    before anything has loaded one (tools/ A/B drivers; never the product path)."""
+    global LIB_PATH
+    if _lib is not None and os.path.abspath(path) != os.path.abspath(LIB_PATH):
+        raise RuntimeError(f"aonerf: {LIB_PATH} is already loaded")
+    LIB_PATH = path
 
 
 _variants = {}

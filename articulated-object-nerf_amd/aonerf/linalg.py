@@ -18,7 +18,8 @@ _ws = {}
 
 
 def _workspace(nbytes, device):
-    # one per device AND stream: products on two streams (train.OVERLAP_DWEIGHT) run concurrently
+    # one per device AND stream: products on two streams (TrainNumerics.overlap_dweight) run
+    # concurrently
     key = (str(device), torch.cuda.current_stream(device).cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
@@ -54,10 +55,25 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
                       b_tiled=int(bool(b_tiled)), n_store=n_store,
                       exact_fp32=int(bool(exact_fp32)), c_trans=int(bool(c_trans)),
                       f16_single=int(bool(f16_single)))
-    if _small is not None and exact_fp32:
-        # deferred to one aon_gemm_small_batch launch (small_batched); operands kept alive
-        _small.append((a, C.device, (A, B, C, bias)))
-        return
+    if _small is not None:
+        Cw = C[:M, :(n_store or N)] if C.dim() == 2 else C
+        writes = [_span(Cw)]
+        reads = [_span(A), _span(B)] + [_span(t) for t in (A2, bias, mask, a_amax) if t is not None]
+        if accumulate:
+            reads.append(_span(Cw))
+        if exact_fp32:
+            # deferred to one aon_gemm_small_batch launch (small_batched); operands kept alive.
+            # The library itself orders products on one C chain and refuses any other
+            # dependency between the items of one launch
+            _small.append((a, C.device, (A, B, C, bias), writes, reads))
+            return
+        if _small and any(_overlaps(w, it[3]) or _overlaps(w, it[4]) or _overlaps(r, it[3])
+                          for it in _small for w in writes for r in reads):
+            # a product that runs at once inside small_batched(): it must not read
+            # what a deferred tiny product writes, nor write what one reads or writes -- launch
+            # the deferred ones first, in issue order
+            _flush_small(_small)
+            _small.clear()
     bf = mma_bf16 and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16
     f16 = (not mma_bf16 and A.dtype == torch.float32 and B.dtype == torch.float32 and not a_kc
            and not b_kc and A2 is None and bias is None and mask is None and not relu
@@ -67,7 +83,7 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
         # operands kept alive until the flush; class: bf16 one 256 x 256 tile, bf16 128 x 128
         # tiles, or fp16x3
         cls = "f16" if f16 else 256 if M == 256 and N == 256 else 128
-        if cls != 128 or BATCH128:
+        if cls != 128 or _batch128:
             # what the product writes of C: its M x (n_store or N) corner, not the whole view (a
             # dW passed whole while a K-concat segment fills its later columns must not count
             # as overlapping that segment's product: a needless flush split the level's batch)
@@ -101,7 +117,9 @@ def gemm(C, A, B, M, N, K, *, lda, a_kc, ldb, b_kc, ldc, A2=None, lda2=0, K1=0, 
     L.call("aon_gemm", ctypes.byref(a), L.ptr(ws), nbytes, L.stream(C.device))
 
 
+# the deferral state of the innermost batched() / small_batched() context (None: outside one)
 _batch = None
+_batch128 = True
 _small = None
 
 
@@ -110,7 +128,10 @@ def small_batched():
     """Defer the exact_fp32 tiny products issued inside (the articulated bf16 step's latent-code
     terms and folded biases) to aon_gemm_small_batch launches at exit, in issue order --
     GEMM_SMALL_BATCH_MAX per launch, bit-identical to launching them one by one (products on one
-    C chain in order; the library refuses any other dependency between them)."""
+    C chain in order; the library refuses any other dependency between them).  An aon_gemm that
+    runs at once inside the context and touches a deferred product's output (or writes its
+    inputs) first launches the deferred ones; torch ops inside the context see no such check, so
+    callers read a deferred output only after the context exits."""
     global _small
     outer, _small = _small, []
     try:
@@ -118,35 +139,36 @@ def small_batched():
         items = _small
     finally:
         _small = outer
+    _flush_small(items)
+
+
+def _flush_small(items):
     for i in range(0, len(items), L.GEMM_SMALL_BATCH_MAX):
         chunk = items[i:i + L.GEMM_SMALL_BATCH_MAX]
         arr = (L.AonGemmArgs * len(chunk))(*[it[0] for it in chunk])
         L.call("aon_gemm_small_batch", arr, len(chunk), L.stream(chunk[0][1]))
-# BATCH = False: batched() defers nothing (A/B of aon_gemm_batch against separate launches);
-# BATCH128 = False: only the 256 x 256 products are deferred (A/B of the 128-tile class).  Module
-# attributes an A/B driver sets explicitly -- no environment variable changes what a caller gets.
-BATCH = True
-BATCH128 = True
-
-
 @contextlib.contextmanager
-def batched():
+def batched(enabled=True, tiles128=True):
     """Defer the weight-gradient products in whole 128-column tiles issued inside (dW = dZ^T X
     of pts_linears / bottleneck / views_linear.0, the bf16 enc-column products) to
     aon_gemm_batch launches -- bf16 256 x 256, other bf16, and fp16x3 ones, up to
     GEMM_BATCH_MAX products of equal K per launch -- flushed at exit; every other product runs
     at once.  The deferred products only read kept tensors and write their own dW / db (callers
-    flush before reading a deferred db), so the reordering is safe."""
-    global _batch
-    if not BATCH:
+    flush before reading a deferred db), so the reordering is safe.  enabled False: nothing is
+    deferred (A/B of aon_gemm_batch against separate launches, same bits); tiles128 False: only
+    the 256 x 256 products are (A/B of the 128-tile class) -- the caller's TrainNumerics
+    (batch_dweights / batch_128) passes both."""
+    global _batch, _batch128
+    if not enabled:
         yield
         return
     outer, _batch = _batch, []
+    outer128, _batch128 = _batch128, bool(tiles128)
     try:
         yield
         items = _batch
     finally:
-        _batch = outer
+        _batch, _batch128 = outer, outer128
     _flush(items)
 
 

@@ -6,9 +6,13 @@ loads unchanged.  The forward pass runs on the fused HIP kernels:
 
     level 0: aon_sample_along_rays (t only) -> aon_mlp_fwd (xyz + pos_enc + MLP + sigmoid/relu
              fused) -> aon_composite_march (alpha compositing fused with the fine level's
-             sample_pdf: the coarse weights stay on chip; FUSED_MARCH / march_ok)
+             sample_pdf: the coarse weights stay on chip; NeRF.fused_march / march_ok)
     level 1: aon_mlp_fwd on the merged t -> aon_composite_fwd
-    (FUSED_MARCH = False, or N_importance > 256: aon_composite_fwd + aon_sample_pdf, bit-identical)
+    (fused_march False, or N_importance > 256: aon_composite_fwd + aon_sample_pdf, bit-identical)
+
+Per-model configuration only (no mutable globals): the render precision
+(``precision``), the training numerics (``train_precision`` / ``train_numerics``,
+aonerf/numerics.py), ``fused_march`` and ``range_check`` are attributes of each NeRF.
 
 Intermediates live in HBM (a 640x480 frame needs ~1.6 GB), so a whole frame is one launch
 per stage instead of the reference's 80 chunk iterations.
@@ -21,6 +25,7 @@ import torch.nn.init as init
 
 from . import _lib as L
 from . import helper
+from .numerics import resolve as _resolve_numerics
 
 _DEFAULT_GEOMETRY = dict(min_deg_point=0, max_deg_point=10, deg_view=4, netdepth=8, netwidth=256,
                          netdepth_condition=1, netwidth_condition=128, skip_layer=4, input_ch=3,
@@ -124,11 +129,6 @@ class NeRFMLP(nn.Module):
         return raw[..., :3], raw[..., 3:]
 
 
-# render path: after a f16x3 render, read the packs' range-status words (one sync per forward;
-# skipped while a HIP graph is being captured) and fall back to the fp32 kernels on overflow
-RANGE_CHECK = True
-
-
 def _events(timers):
     """HIP events bracketing one launch on the current stream (the stream the C ABI uses)."""
     if timers is None:
@@ -171,15 +171,11 @@ def composite_march(raw, t_vals, d, white_bkgd, act, u, u_stride, num_fine_sampl
     return (comp, acc, depth, weights), t_fine
 
 
-# render path: the coarse compositor and the fine level's resampling as one kernel
-# (aon_composite_march); False: aon_composite_fwd + aon_sample_pdf (bit-identical outputs)
-FUSED_MARCH = True
-
-
-def march_ok(S, num_fine_samples):
+def march_ok(S, num_fine_samples, fused=True):
     """The fused march kernel's limits (include/aonerf.h: 3 <= S <= 256, 1 <= Ns <= 256); larger
-    N_importance (up to aon_sample_pdf's 512) takes the two-kernel path."""
-    return FUSED_MARCH and 3 <= S <= 256 and 1 <= num_fine_samples <= 256
+    N_importance (up to aon_sample_pdf's 512) takes the two-kernel path, as does a model whose
+    ``fused_march`` is False (aon_composite_fwd + aon_sample_pdf, bit-identical outputs)."""
+    return fused and 3 <= S <= 256 and 1 <= num_fine_samples <= 256
 
 
 def level_t_vals(level, o, d, t_prev, w_prev, randomized, near, far, num_coarse_samples,
@@ -208,10 +204,19 @@ class NeRF(nn.Module):
     def __init__(self, num_levels: int = 2, min_deg_point: int = 0, max_deg_point: int = 10,
                  deg_view: int = 4, num_coarse_samples: int = 64, num_fine_samples: int = 128,
                  use_viewdirs: bool = True, noise_std: float = 0.0, lindisp: bool = False,
-                 precision: str = "f16x3"):
+                 precision: str = "f16x3", train_precision: str = "f16x3", train_numerics=None,
+                 fused_march: bool = True, range_check: bool = True):
+        """The reference's kwargs (model.py:124-145) plus, per model: ``precision`` (render MLP:
+        "f16x3" or exact "fp32"), ``train_precision`` / ``train_numerics`` (the training step's
+        kernels, aonerf/numerics.py), ``fused_march`` (the coarse compositor fused with the fine
+        level's resampling) and ``range_check`` (after a f16x3 render, read the packs'
+        range-status words -- one sync per forward, skipped under HIP-graph capture -- and
+        re-render on the fp32 kernels on overflow)."""
         super().__init__()
         if num_levels != 2:
             raise ValueError("the reference NeRF is two-level (coarse + fine)")
+        self.train_numerics = _resolve_numerics(train_precision, train_numerics)
+        self.fused_march, self.range_check = bool(fused_march), bool(range_check)
         self.num_levels, self.min_deg_point, self.max_deg_point = num_levels, min_deg_point, max_deg_point
         self.deg_view, self.num_coarse_samples, self.num_fine_samples = deg_view, num_coarse_samples, num_fine_samples
         self.use_viewdirs, self.noise_std, self.lindisp = use_viewdirs, noise_std, lindisp
@@ -234,7 +239,8 @@ class NeRF(nn.Module):
         ``return_intermediates`` adds a dict(t_vals, weights[, rgb_sigma]) as the last element
         (rgb_sigma (B*S, 4), inference path only: the activated MLP outputs the compositor
         consumed);
-        ``timers`` (dict) records hip events around each level's MLP / composite launches.
+        ``timers`` (dict) records hip events around each level's MLP / composite launches (the
+        training path: around its fused training kernels).
 
         With autograd enabled and trainable parameters, each level runs the training path
         (train.RenderLevel: the fused training forward aon_mlp_fwd_train, which also stores the
@@ -253,11 +259,12 @@ class NeRF(nn.Module):
         ret = []
         t_vals = weights = t_next = None
         token, joined = None, {}
+        cfg = self.train_numerics
         if training:
             from . import train
-            if train.OVERLAP_DWEIGHT and train.FUSED_BACKWARD:
+            if cfg.overlap_dweight and cfg.fused_backward and timers is None:
                 # both levels' parameters through one Join: its backward, after both levels',
-                # joins the fine level's weight-gradient stream (train.OVERLAP_DWEIGHT)
+                # joins the fine level's weight-gradient stream (overlap_dweight)
                 token = train.JoinToken()
                 ps = [p for m in (self.coarse_mlp, self.fine_mlp) for l in m._layers()
                       for p in (l.weight, l.bias)]
@@ -276,7 +283,7 @@ class NeRF(nn.Module):
                 params = [p for m in mlp._layers() for p in (m.weight, m.bias)]
                 params = [joined.get(id(p), p) for p in params]
                 comp, acc, depth, weights = RenderLevel.apply(o, d, v, t_vals, bool(white_bkgd),
-                                                              noise, token, *params)
+                                                              noise, token, cfg, timers, *params)
                 out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
                 if return_intermediates:
                     out = out + (dict(t_vals=t_vals, weights=weights),)
@@ -285,7 +292,7 @@ class NeRF(nn.Module):
             # the last level's weights are an output only when asked for: otherwise the
             # compositor skips writing them (4 B of its 24 B per sample)
             keep_w = level == 0 or return_weights or return_intermediates
-            march = level == 0 and march_ok(S, self.num_fine_samples)
+            march = level == 0 and march_ok(S, self.num_fine_samples, self.fused_march)
             if march:  # the coarse weights are needed on chip only
                 keep_w = return_weights or return_intermediates
             with torch.no_grad():
@@ -299,7 +306,7 @@ class NeRF(nn.Module):
             if not return_intermediates:
                 out = out[:4] if return_weights else out[:3]
             ret.append(out)
-        if (not training and RANGE_CHECK and self.coarse_mlp.precision == "f16x3"
+        if (not training and self.range_check and self.coarse_mlp.precision == "f16x3"
                 and not torch.cuda.is_current_stream_capturing()
                 and L.range_overflow([self.coarse_mlp._packed, self.fine_mlp._packed])):
             # an activation left the fp16x3 split's range (|x| > 8188): these outputs are

@@ -30,8 +30,9 @@ import torch.nn.init as init
 
 from . import _lib as L
 from .linalg import ACT_SCALE, W_SCALE, gemm, linear_fwd
-from . import model as _vanilla
 from .model import _events, _record, composite_march, fine_uniforms, level_t_vals, march_ok
+from .numerics import resolve as _resolve_numerics
+
 
 class NeRFMLP(nn.Module):
     """reference model_autodecoder.py:60-166 (same nn.Linear layout and init)."""
@@ -259,8 +260,14 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
                  deg_view: int = 4, num_coarse_samples: int = 64, num_fine_samples: int = 128,
                  use_viewdirs: bool = True, noise_std: float = 0.0, lindisp: bool = False,
                  rgb_padding: float = 0.001, density_bias: float = -1.0, enc_after=True,
-                 embed_deg=False):
+                 embed_deg=False, train_precision: str = "f16x3", train_numerics=None,
+                 fused_march: bool = True, range_check: bool = True):
+        """The reference's kwargs (model_autodecoder.py:243-276) plus the per-model settings of
+        aonerf.model.NeRF: ``train_precision`` / ``train_numerics`` (aonerf/numerics.py),
+        ``fused_march`` and ``range_check``."""
         super().__init__()
+        self.train_numerics = _resolve_numerics(train_precision, train_numerics)
+        self.fused_march, self.range_check = bool(fused_march), bool(range_check)
         if num_levels != 2:
             raise ValueError("the reference NeRF_AE_Art is two-level (coarse + fine)")
         if rgb_padding != 0.001 or density_bias != -1.0:
@@ -294,14 +301,15 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
             or any(x.requires_grad for x in latents.values()))
         if training:
             return self._forward_train(o, d, v, randomized, white_bkgd, near, far, latents,
-                                       u_coarse, u_fine, return_weights, return_intermediates)
+                                       u_coarse, u_fine, return_weights, return_intermediates,
+                                       timers)
         with torch.no_grad():
             return self._forward_render(o, d, v, randomized, white_bkgd, near, far, latents,
                                         u_coarse, u_fine, return_weights, return_intermediates,
                                         timers)
 
     def _forward_train(self, o, d, v, randomized, white_bkgd, near, far, latents, u_coarse,
-                       u_fine, return_weights, return_intermediates):
+                       u_fine, return_weights, return_intermediates, timers=None):
         from .train_art import render_level
 
         B, dev = o.shape[0], o.device
@@ -317,7 +325,7 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
             if self.noise_std > 0 and randomized:  # model_autodecoder.py:318-319
                 noise = torch.rand((B * t_vals.shape[1],), device=dev) * self.noise_std
             comp, acc, depth, weights = render_level(mlp, o, d, v, t_vals, white_bkgd, latents,
-                                                     noise)
+                                                     noise, self.train_numerics, timers)
             out = (comp, acc, depth, weights) if return_weights else (comp, acc, depth)
             if return_intermediates:
                 out = out + (dict(t_vals=t_vals, weights=weights),)
@@ -343,7 +351,7 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
             if self.noise_std > 0 and randomized:  # model_autodecoder.py:318-319
                 raw[:, 3].copy_(raw[:, 3] + torch.rand_like(raw[:, 3]) * self.noise_std)
             ev = _events(timers)
-            if level == 0 and march_ok(S, self.num_fine_samples):
+            if level == 0 and march_ok(S, self.num_fine_samples, self.fused_march):
                 # coarse compositing + the fine level's resampling in one kernel; the coarse
                 # weights reach HBM only when asked for
                 u, u_stride = fine_uniforms(B, self.num_fine_samples, randomized, dev, u_fine)
@@ -365,7 +373,7 @@ class NeRF_AE_Art(nn.Module):  # noqa: N801 (reference name)
                 out = out + (dict(t_vals=t_vals, weights=weights, raw=raw),)
             ret.append(out)
         mlps = (self.coarse_mlp, self.fine_mlp)
-        if (_vanilla.RANGE_CHECK and all(m._fused_ok() for m in mlps)
+        if (self.range_check and all(m._fused_ok() for m in mlps)
                 and not torch.cuda.is_current_stream_capturing()
                 and L.range_overflow([getattr(m, "_art_packed", None) for m in mlps])):
             # an activation left the fp16x3 split's range (|x| > 8188) in the fused kernel:

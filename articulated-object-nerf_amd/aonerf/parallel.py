@@ -5,6 +5,8 @@ independent and the reference has no early termination, so equal row bands balan
 the only exchange is the final gather of [rgb, depth, acc] (20 B/ray) to the destination rank
 -- at 640x480 over 8 GPUs 768 KB per rank.
 """
+import weakref
+
 import torch
 import torch.distributed as dist
 
@@ -86,6 +88,11 @@ class GradAllReduce:
     the world size.  Relative error per value <= ~world x 2^-8 of the largest magnitude summed
     into it; the fp32 master weights and Adam state are unchanged.  On a gloo group a device
     buffer is staged through the host (no early launch there).
+
+    The early-launch hooks belong to this object: ``close()`` (or leaving a ``with`` block, or
+    garbage collection) removes them, and a hook only holds a weak reference, so a second
+    GradAllReduce over the same parameters (one per epoch or per bench leg) never sees the first
+    one's hooks fire.
     """
 
     def __init__(self, params, group=None, dtype=torch.float32, buckets=None):
@@ -120,9 +127,44 @@ class GradAllReduce:
         self._seen = [set() for _ in buckets]
         self._works = [None] * len(buckets)
         self._hooks = []
+        self._closed = False
         if len(buckets) > 1:
+            ref = weakref.ref(self)
+
+            def hook(p):
+                me = ref()
+                if me is not None and not me._closed:
+                    me._landed(p)
+
             for p in self.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._landed))
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+
+    def close(self):
+        """Remove the gradient hooks and drain a collective still in flight (idempotent)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        if not self._closed:
+            for w in self._works:
+                if w is not None and w is not True:
+                    w.wait()
+        self._closed = True
+        self._works = [None] * len(self.spans)
+        self._seen = [set() for _ in self.spans]
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):
+        try:
+            for h in self._hooks:
+                h.remove()
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
+            pass
 
     def _ensure(self, dev):
         if self.flat is None or self.flat.device != dev:
@@ -172,6 +214,8 @@ class GradAllReduce:
                                               async_op=True)
 
     def __call__(self):
+        if self._closed:
+            raise RuntimeError("GradAllReduce: closed")
         if not dist.is_initialized():  # (a process group of one still runs the all-reduce)
             return
         world = dist.get_world_size(self.group)

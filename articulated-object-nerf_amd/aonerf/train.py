@@ -11,8 +11,9 @@ One render level under autograd is ``RenderLevel`` (a torch.autograd.Function):
             dW = dY^T X and db = sum_rows dY from the same pass (aon_gemm, split-K,
             deterministic)
 
-(``FUSED_FORWARD`` / ``FUSED_BACKWARD`` = False select the layer-by-layer aon_gemm forward and
-backward that the fused kernels replaced; both are gated identically in tests/test_gpu_train.py.)
+(The model's TrainNumerics -- aonerf/numerics.py, per model -- with fused_forward /
+fused_backward False selects the layer-by-layer aon_gemm forward and backward that the fused
+kernels replaced; both are gated identically in tests/test_gpu_train.py.)
 
 Gradients land in each parameter's ``.grad`` through autograd, so the reference's own
 optimizer code runs unchanged (the fp16x3 range guard reaches it through a global
@@ -30,6 +31,7 @@ from . import _lib as L
 from . import tiles
 
 from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, batched, colsum, gemm, linear_fwd  # noqa: F401
+from .numerics import DEFAULT, TrainNumerics  # noqa: F401
 
 # ---------------------------------------------------------------------------- one render level
 def _mlp_params(mlp):
@@ -121,44 +123,25 @@ def _backward_level(P, G, enc, venc, S, h, bot, hv, draw):
             dx, dy = dy, dx
 
 
-# forward of a level under autograd: one fused kernel that also stores the activations
-# (aon_mlp_fwd_train) when True, else the layer-by-layer GEMMs of _forward_level
-FUSED_FORWARD = True
-# backward of a level: input gradients in one fused kernel (aon_mlp_bwd) + weight-gradient GEMMs
-# when True, else every product as a GEMM (_backward_level)
-FUSED_BACKWARD = True
-# numerics of the fused training kernels: "f16x3" (fp32-class, the parity mode) or "bf16"
-# (BASELINE config C5's bf16 training step: one bf16 MFMA per product in the forward, the
-# backward chain and the weight-gradient GEMMs, activations and gradients kept as bf16; the
-# compositing, loss, its backward and Adam stay fp32 on fp32 master weights)
-PRECISION = "f16x3"
-# a dict -> hip events around each level's training kernels, keyed by name and sample count
-# (bench.py's train_step roofline): "fwd_train<S>", "bwd_chain<S>", "dweight<S>"
-TIMERS = None
+# Which kernels and precision a level trains with is the MODEL's TrainNumerics
+# (aonerf/numerics.py; NeRF(train_precision=...)), passed into RenderLevel per call -- no
+# module-level switch.  ``timers`` (a dict, optional, per call) -> hip events around each level's
+# training kernels (bench.py's train_step roofline): "fwd_train<S>", "bwd_chain<S>", "dweight<S>".
 
 
-def _ev():
-    if TIMERS is None:
+def _ev(timers):
+    if timers is None:
         return None
     e = torch.cuda.Event(enable_timing=True)
     e.record()
     return e
 
 
-def _rec(key, e0, rows):
+def _rec(timers, key, e0, rows):
     if e0 is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        TIMERS.setdefault(key, []).append((e0, e1, rows))
-
-# the fine level's weight-gradient GEMMs on a second stream, concurrent with the coarse level's
-# backward (compositing backward + input-gradient chain), when the two levels' parameters pass
-# through one Join (NeRF.forward's training path does this): Join's backward -- after both
-# levels' -- makes the caller's stream wait for them, so every gradient hook / AccumulateGrad /
-# optimizer sees finished gradients.  False (default): one stream, in autograd's order --
-# measured faster: the concurrent kernels contend for the CUs (bf16 C5 step 5.77-5.86 ms
-# overlapped against 5.67-5.71 ms, f16x3 17.34 against 17.12 ms; profiles/r04/overlap_ab.txt).
-OVERLAP_DWEIGHT = False
+        timers.setdefault(key, []).append((e0, e1, rows))
 
 
 class JoinToken:
@@ -170,7 +153,7 @@ class JoinToken:
 
 class Join(torch.autograd.Function):
     """Identity on the render levels' parameters (views), whose backward runs after every
-    level's: it joins the side stream (OVERLAP_DWEIGHT) before the gradients reach the
+    level's: it joins the side stream (TrainNumerics.overlap_dweight) before the gradients reach the
     parameters."""
 
     @staticmethod
@@ -244,20 +227,18 @@ def _buffer(key, nbytes, dev, guard=False, params=()):
 
 # an optimizer step refuses gradients whose kernels met a fp16x3 range overflow (one sync per
 # step): aonerf's Adam.step, and every other torch.optim optimizer through a global step pre-hook
-RANGE_CHECK = True
-
 _RANGE_MSG = ("a fp16x3 training kernel met a value beyond its fp16 hi/lo range (|activation| > "
               "8188 or an overflowing gradient): the gradients of this step are invalid and were "
               "not applied.  Train this model on the layer-by-layer GEMM path "
-              "(train.FUSED_FORWARD = train.FUSED_BACKWARD = False; train_art likewise), whose "
-              "operands carry a 2^-8 scale (range 1.6e7), or in train.PRECISION = 'bf16'.")
+              "(train_numerics=TrainNumerics(fused_forward=False, fused_backward=False)), whose "
+              "operands carry a 2^-8 scale (range 1.6e7), or with train_precision='bf16'.")
 
 
 def check_range(devices=None, params=None):
     """Raise FloatingPointError if a fused fp16x3 training kernel on ``devices`` that packed any
     of ``params`` (None: any) overflowed since the last check (consumes those pending packs)."""
     ids = None if params is None else {p.data_ptr() for p in params}
-    if RANGE_CHECK and L.check_pending(devices, ids):
+    if L.check_pending(devices, ids):
         raise FloatingPointError(_RANGE_MSG)
 
 
@@ -309,13 +290,15 @@ def relu_masks(acts, R):
 
 
 def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_tiled=True,
-                          token=None):
+                          token=None, timers=None, cfg=DEFAULT):
     """_backward_level with every input-gradient product in one fused kernel (aon_mlp_bwd);
     the weight gradients dW = dZ^T X and db = sum_rows dZ stay split-K GEMMs.  ``masks``: the
     ReLU' bits of h0..h7, hv from the fused forward (built from the activations when None).
     h_tiled: h / bot / hv in the fused forward's tiled layout (tiles.py), else row-major (the
     layer-by-layer forward).  The chain's dz / dzb / dzv are always tiled.  ``token`` (a
-    JoinToken): the weight gradients run on the side stream (OVERLAP_DWEIGHT)."""
+    JoinToken): the weight gradients run on the side stream (TrainNumerics.overlap_dweight);
+    ``timers``: hip events per kernel class (bench.py); ``cfg``: the model's TrainNumerics (the
+    weight-gradient batching)."""
     R, dev = draw.shape[0], draw.device
     bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
@@ -330,12 +313,12 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
     # next level's chain may already run -- its own word then
     work = _buffer("work", 4, dev) if token is None else torch.empty((1,), device=dev)
     packed = _pack_bwd(P, dev, S, bf16)
-    e0 = _ev()
+    e0 = _ev(timers)
     L.call("aon_mlp_bwd_bf16" if bf16 else "aon_mlp_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks),
            R, L.ptr(dzv), L.ptr(dzb), L.ptr(dz), L.ptr(work), L.stream(dev))
     L.snapshot_pack(packed)  # the chain was the pack's last reader (range guard, _lib)
-    _rec(f"bwd_chain{S}", e0, R)
-    e0 = _ev()
+    _rec(timers, f"bwd_chain{S}", e0, R)
+    e0 = _ev(timers)
     acts = ACT_SCALE
 
     # the tiled copy of pos_enc(x): the bf16 forward's (NR, 128) bf16 or the f16x3 mode's
@@ -366,7 +349,7 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
 
     # bf16: the eight 256 x 256 products (bottleneck, pts_linears.1-7) run as one aon_gemm_batch
     touched = [dzv, dzb, dz, draw, work, enc, venc, bot, hv, *h, *(t for wb in G for t in wb)]
-    with _on_side(token, dev, touched), batched():
+    with _on_side(token, dev, touched), batched(cfg.batch_dweights, cfg.batch_128):
         dweight(G[11][0], draw, 4, 3, hv, 128, 128, db=G[11][1], a_t=False)    # rgb_layer
         dweight(G[10][0], dzv, 128, 128, bot, 256, 256, db=G[10][1])           # views_linear.0
         dweight(G[10][0], dzv, 128, 128, venc, 27, 27, rdiv=S, col0=256)
@@ -380,7 +363,7 @@ def _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, masks=None, h_ti
                 dweight(G[0][0], dz[0], 256, 256, enc, 63, 63, db=G[0][1])
             else:
                 dweight(G[i][0], dz[i], 256, 256, h[i - 1], 256, 256, db=G[i][1])
-    _rec(f"dweight{S}", e0, R)
+    _rec(timers, f"dweight{S}", e0, R)
 
 
 def _forward_level_fused(P, rays_o, rays_d, viewdirs, t_vals, raw, noise=None, masks=None,
@@ -420,14 +403,17 @@ class RenderLevel(torch.autograd.Function):
     (model.py:175-197) with gradients for the level's 24 MLP parameters."""
 
     @staticmethod
-    def forward(ctx, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise, token, *params):
+    def forward(ctx, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise, token, cfg, timers,
+                *params):
+        # cfg: the model's TrainNumerics; timers: a dict of hip events (bench.py) or None
         B, S = t_vals.shape
         ctx.token = token  # a JoinToken: the weight gradients may run on the side stream
+        ctx.cfg, ctx.timers = cfg, timers
         R, dev = B * S, t_vals.device
-        bf16 = FUSED_FORWARD and PRECISION == "bf16"
+        bf16 = cfg.fused_forward and cfg.bf16
         if bf16:  # the bf16 training forward keeps pos_enc(x) itself (bf16, tiled, 128 columns)
             enc = torch.empty((tiles.rows(R), 128), device=dev, dtype=torch.bfloat16)
-        elif FUSED_FORWARD and FUSED_BACKWARD:
+        elif cfg.fused_forward and cfg.fused_backward:
             # xyz = o + t d straight into the encodings, tiled with 64 columns (column 63 zero):
             # the fused backward's enc-column weight gradients read whole 16-column tiles
             enc = torch.empty((tiles.rows(R), 64), device=dev)
@@ -445,14 +431,14 @@ class RenderLevel(torch.autograd.Function):
         L.check_mlp_layers(P)
         raw = torch.empty((R, 4), device=dev)
         masks = None  # ReLU' bits for the fused backward chain (built there when None)
-        if FUSED_FORWARD:
+        if cfg.fused_forward:
             noise = L.contig(noise) if noise is not None else None
             masks = torch.empty((9, tiles.rows(R), 8), dtype=torch.int32, device=dev)
-            e0 = _ev()
+            e0 = _ev(timers)
             h, bot, hv = _forward_level_fused(P, L.contig(rays_o), L.contig(rays_d),
                                               L.contig(viewdirs), L.contig(t_vals), raw, noise,
                                               masks, bf16=bf16, enc=enc if bf16 else None)
-            _rec(f"fwd_train{S}", e0, R)
+            _rec(timers, f"fwd_train{S}", e0, R)
         else:
             h, bot, hv = _forward_level(P, enc, venc, S, raw, noise)
         comp = torch.empty((B, 3), device=dev)
@@ -464,7 +450,7 @@ class RenderLevel(torch.autograd.Function):
                L.ptr(weights), L.ptr(depth), L.stream(dev))
         ctx.save_for_backward(rays_d, t_vals, enc, venc, raw, bot, hv, *h, *params)
         ctx.masks = masks
-        ctx.h_tiled = FUSED_FORWARD  # the fused forward keeps its tensors tiled
+        ctx.h_tiled = cfg.fused_forward  # the fused forward keeps its tensors tiled
         ctx.meta = (B, S, bool(white_bkgd))
         ctx.mark_non_differentiable(weights)
         # unused outputs (acc, depth, weights in training_step) get no zero-filled gradients
@@ -489,11 +475,12 @@ class RenderLevel(torch.autograd.Function):
                L.ptr(draw), L.ptr(draw[:, 3:]), 4, L.stream(dev))
         P = [(params[2 * i], params[2 * i + 1]) for i in range(12)]
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
-        if FUSED_BACKWARD:
-            # (not while TIMERS time each level's kernels on the current stream)
-            token = ctx.token if OVERLAP_DWEIGHT and TIMERS is None else None
+        cfg, timers = ctx.cfg, ctx.timers
+        if cfg.fused_backward:
+            # (not while timers time each level's kernels on the current stream)
+            token = ctx.token if cfg.overlap_dweight and timers is None else None
             _backward_level_fused(P, G, enc, venc, S, h, bot, hv, draw, ctx.masks, ctx.h_tiled,
-                                  token=token)
+                                  token=token, timers=timers, cfg=cfg)
         else:
             if ctx.h_tiled:  # the all-GEMM backward reads row-major fp32 activations
                 h = [tiles.untile(x, R).float() for x in h]
@@ -502,7 +489,7 @@ class RenderLevel(torch.autograd.Function):
                 enc = tiles.untile(enc, R)[:, :63].float().contiguous()
             _backward_level(P, G, enc, venc, S, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
-        return (None, None, None, None, None, None, None, *grads)
+        return (None, None, None, None, None, None, None, None, None, *grads)
 
 
 class Mse(torch.autograd.Function):
@@ -578,9 +565,12 @@ def loss_pair(pred0, pred1, target, reg=None):
     return LossPair.apply(pred0, pred1, target, reg)
 
 
-def training_step(model, batch, randomized, white_bkgd, near, far, *, u_coarse=None, u_fine=None):
-    """LitNeRF.training_step (model.py:256-282): loss = mse(fine) + mse(coarse) and the psnrs."""
-    ret = model(batch, randomized, white_bkgd, near, far, u_coarse=u_coarse, u_fine=u_fine)
+def training_step(model, batch, randomized, white_bkgd, near, far, *, u_coarse=None, u_fine=None,
+                  timers=None):
+    """LitNeRF.training_step (model.py:256-282): loss = mse(fine) + mse(coarse) and the psnrs.
+    The kernels and precision are the model's own (model.train_numerics)."""
+    ret = model(batch, randomized, white_bkgd, near, far, u_coarse=u_coarse, u_fine=u_fine,
+                timers=timers)
     loss, loss0, loss1, psnr0, psnr1 = loss_pair(ret[0][0], ret[1][0], batch["target"])
     return loss, dict(loss0=loss0, loss1=loss1, psnr0=psnr0, psnr1=psnr1)
 

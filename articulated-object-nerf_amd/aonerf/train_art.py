@@ -11,13 +11,13 @@ gradients for the level's 40 MLP parameters AND the three latent codes:
             concat -> density, bottleneck -> view branch on cat[bottleneck, enc_dir tiled over
             samples, appearance] -> rgb, every activation, pos_enc(x') and the points kept
             (model_autodecoder.py:168-239); or the same layer by layer on aon_gemm
-            (FUSED_FORWARD = False) -> compositing with the padded sigmoid / softplus
+            (TrainNumerics.fused_forward False) -> compositing with the padded sigmoid / softplus
             (aon_composite_fwd, AON_ACT_ARTIC; :321-333)
   backward  aon_composite_bwd -> every input gradient dX = (dZ W) * relu'(X) in one fused
             kernel (aon_mlp_art_bwd): view branch, heads, trunk, the gradient w.r.t.
             pos_enc(x') (skip + first layer) through pos_enc's backward into the deformation
             head and MLP -> per layer dW = dZ^T X with db = sum_rows dZ from the same pass
-            (aon_gemm); or the whole chain as GEMMs + aon_pos_enc_bwd (FUSED_BACKWARD = False).
+            (aon_gemm); or the whole chain as GEMMs + aon_pos_enc_bwd (fused_backward False).
 
 The latent codes are the same row for every sample (repeated over B*S rows,
 model_autodecoder.py:186-194), so their columns are folded into per-call biases in the
@@ -34,6 +34,7 @@ from . import _lib as L
 from . import tiles
 from . import train as _train
 from .linalg import ACT_SCALE, GRAD_SCALE, W_SCALE, batched, gemm, small_batched
+from .numerics import ART_FORWARD, DEFAULT
 from .train import Adam, _amax_word, img2mse, learning_rate, loss_pair, mse2psnr, relu_masks  # noqa: F401 (shared)
 
 # parameter layout of one articulated NeRFMLP in ArtRenderLevel: 20 layers x (weight, bias)
@@ -68,13 +69,13 @@ class _Geo:
         self.n_art = mlp.articulation_latent_dim
 
 
-def _fold(W, b, c0, lat):
-    """b + W[:, c0:c0+n] . lat (the latent columns of a layer as a per-call bias); in the bf16
-    mode on aon_gemm's exact-fp32 tiny-product path."""
+def _fold(W, b, c0, lat, exact=False):
+    """b + W[:, c0:c0+n] . lat (the latent columns of a layer as a per-call bias); exact (the
+    bf16 mode): on aon_gemm's exact-fp32 tiny-product path."""
     N, n = W.shape[0], lat.shape[1]
     out = torch.empty((1, N), device=W.device)
     gemm(out, lat, W[:, c0:], 1, N, n, lda=n, a_kc=True, ldb=W.stride(0), b_kc=True, ldc=N,
-         bias=b, a_scale=1.0, b_scale=W_SCALE, exact_fp32=PRECISION == "bf16")
+         bias=b, a_scale=1.0, b_scale=W_SCALE, exact_fp32=exact)
     return out.reshape(-1)
 
 
@@ -87,15 +88,16 @@ def _linear(out, X, ldx, W, bias, K, *, relu=False, X2=None, K2=0, ld2=0, rdiv2=
          bias=bias, relu=relu, accumulate=accumulate, a_scale=ACT_SCALE, b_scale=W_SCALE)
 
 
-def _forward_level(geo, P, lat, xyz, venc, S, raw, noise=None):
-    """NeRFMLP.forward (model_autodecoder.py:168-239) layer by layer, keeping activations."""
+def _forward_level(geo, P, lat, xyz, venc, S, raw, noise=None, exact_folds=False):
+    """NeRFMLP.forward (model_autodecoder.py:168-239) layer by layer, keeping activations
+    (exact_folds: the latent folds on the exact-fp32 path, as the bf16 mode computes them)."""
     R, dev = xyz.shape[0], xyz.device
     shape, app, art = lat
     wd, nw, wc, ne, nv = geo.wd, geo.nw, geo.wc, geo.ne, geo.nv
     # deformation MLP on cat[xyz, shape, art] (:196-203), the latent columns folded
     hd = torch.empty((4, R, wd), device=dev)
-    _linear(hd[0], xyz, 3, P[DEF0][0], _fold(*P[DEF0], 3, torch.cat([shape, art], -1)), 3,
-            relu=True)
+    _linear(hd[0], xyz, 3, P[DEF0][0],
+            _fold(*P[DEF0], 3, torch.cat([shape, art], -1), exact_folds), 3, relu=True)
     for i in range(1, 4):
         _linear(hd[i], hd[i - 1], wd, *P[DEF0 + i], wd, relu=True)
     delta = torch.empty((R, 3), device=dev)
@@ -107,12 +109,12 @@ def _forward_level(geo, P, lat, xyz, venc, S, raw, noise=None):
     # trunk on cat[enc, shape] with the skip concat cat[h4, enc, shape] (:214-220)
     h = torch.empty((8, R, nw), device=dev)
     W0 = P[PTS0][0]
-    _linear(h[0], enc, ne, W0, _fold(W0, P[PTS0][1], ne, shape), ne, relu=True)
+    _linear(h[0], enc, ne, W0, _fold(W0, P[PTS0][1], ne, shape, exact_folds), ne, relu=True)
     for i in range(1, 8):
         W_, b_ = P[PTS0 + i]
         if i == 5:
-            _linear(h[5], h[4], nw, W_, _fold(W_, b_, nw + ne, shape), nw, relu=True, X2=enc,
-                    K2=ne, ld2=ne)
+            _linear(h[5], h[4], nw, W_, _fold(W_, b_, nw + ne, shape, exact_folds), nw,
+                    relu=True, X2=enc, K2=ne, ld2=ne)
         else:
             _linear(h[i], h[i - 1], nw, W_, b_, nw, relu=True)
     if noise is not None:  # raw_sigma + noise (:318-319), added in the GEMM epilogue
@@ -123,55 +125,28 @@ def _forward_level(geo, P, lat, xyz, venc, S, raw, noise=None):
     # view branch on cat[bottleneck, enc_dir tiled over samples, appearance] (:226-235)
     hv = torch.empty((4, R, wc), device=dev)
     Wv = P[VIEW0][0]
-    _linear(hv[0], bot, nw, Wv, _fold(Wv, P[VIEW0][1], nw + nv, app), nw, relu=True, X2=venc,
-            K2=nv, ld2=nv, rdiv2=S)
+    _linear(hv[0], bot, nw, Wv, _fold(Wv, P[VIEW0][1], nw + nv, app, exact_folds), nw,
+            relu=True, X2=venc, K2=nv, ld2=nv, rdiv2=S)
     for i in range(1, 4):
         _linear(hv[i], hv[i - 1], wc, *P[VIEW0 + i], wc, relu=True)
     _linear(raw, hv[3], wc, *P[RGB], wc, ldo=4)  # rgb_layer (:237)
     return hd, enc, h, bot, hv
 
 
-# forward of a level under autograd: one fused kernel that also stores the activations
-# (aon_mlp_art_fwd_train) when True, else the layer-by-layer GEMMs of _forward_level
-FUSED_FORWARD = True
-# backward of a level: every input gradient in one fused kernel (aon_mlp_art_bwd) + the
-# weight-gradient GEMMs when True, else every product as a GEMM (_backward_level)
-FUSED_BACKWARD = True
-# numerics of the fused training kernels: "f16x3" (fp32-class, the parity mode) or "bf16"
-# (BASELINE config C5's bf16 on the articulated model): the whole backward chain and the
-# weight-gradient GEMMs bf16 (aon_mlp_art_bwd_bf16, aon_gemm mma_bf16), kept activations and
+# Which kernels, precision and (bf16 mode) forward numerics a level trains with is the MODEL's
+# TrainNumerics (aonerf/numerics.py; NeRF_AE_Art(train_precision=...)), passed into
+# ArtRenderLevel per call -- no module-level switch.  The bf16 mode: the whole backward chain and
+# the weight-gradient GEMMs bf16 (aon_mlp_art_bwd_bf16, aon_gemm mma_bf16), kept activations and
 # gradients bf16 (aon_mlp_art_fwd_train_bf16); compositing, the loss, their backward, the latent
-# terms and Adam stay fp32 on fp32 master weights (tests/test_gpu_art_train_bf16.py).
-PRECISION = "f16x3"
-# bf16 mode, forward numerics.  False (default): fp16x3 throughout, only the stores bf16.  True:
-# the trunk, heads and view branch one bf16 MFMA per product on the mixed stream of
-# aon_mlp_art_pack_bf16 (the deformation MLP stays fp16x3: x' = delta + xyz feeds pos_enc's
-# sin(2^9 x'), where bf16's 8 bits would move the top degree's phase by radians) -- 13% faster
-# per step, but the articulated gradients are ill-conditioned in the forward values and its
-# 2^-9 forward rounding alone leaves the deformation gradients at cosine 0.987 to the fp32
-# oracle (the bf16 backward itself, stage-isolated, is at >= 0.9999)
-BF16_TRUNK = False
-# bf16 mode, forward numerics (when BF16_TRUNK is False): True runs the view branch
-# (views_linear.0-3, rgb_layer: 12% of the MACs, the 128-wide layers whose epilogues cost the
-# most VALU per MFMA) one bf16 MFMA per product on the view-branch stream (aon_mlp_art_pack_mixed
-# mode 2); the deformation MLP, trunk, density and bottleneck stay fp16x3.  Off: 2% of the step
-# (9.85 vs 10.08 ms) for deformation gradients at cosine 0.9968 (0.99983 with it off)
-BF16_VIEW = False
-# bf16 mode, forward numerics (when BF16_TRUNK and BF16_VIEW are False): True runs every layer
-# past the deformation MLP two fp16 MFMAs per product -- the weights rounded once to fp16 (2^-11
-# relative, 8x finer than bf16), the activations' exact fp16 hi / lo split kept (the kArtMix
-# stream with fp16 compact blocks, aon_mlp_art_pack_mixed mode 3); the deformation MLP stays
-# fp16x3
-F16_WEIGHTS = False
-# bf16 mode, forward numerics (when the flags above are False): True runs every layer past the
-# deformation MLP two fp16 MFMAs per product the other way round -- the weights' exact 22-bit
-# hi / lo split kept, the activations rounded once to fp16 per sample (2^-11 relative; the
-# plain fp16x3 stream, aon_mlp_art_fwd_train_bf16 mixed 4).  Per-sample rounding averages out
-# (Default: the backward already reads every kept activation rounded to bf16, 8x coarser than
-# this forward's fp16 rounding; C5 gradients cosine 0.99919 / max-rel 0.049 against the fp32
-# oracle at the unchanged 0.999 / 0.05 gates, step 9.5 ms against 10.0-10.5 fp16x3.  Weights
-# rounded instead, F16_WEIGHTS: 0.99886 / 0.074, outside them.)
-F16_ACTS = True
+# terms and Adam fp32 on fp32 master weights (tests/test_gpu_art_train_bf16.py).  Its forward
+# past the deformation MLP (TrainNumerics.art_forward): "f16_acts" (default) two fp16 MFMAs per
+# product, the weights' exact hi / lo split kept, the activations rounded once to fp16 per sample
+# (the backward already reads bf16 copies, 8x coarser; C5 gradients cosine 0.99919 / max-rel
+# 0.049 against the fp32 oracle at the 0.999 / 0.05 gates); "f16x3" fp16x3 throughout, only the
+# stores bf16; held off by their measured gates: "f16_weights" (weights rounded to fp16: 0.99886
+# / 0.074), "bf16_view" (view branch bf16: deformation gradients cosine 0.9968 for 2% of the
+# step) and "bf16_trunk" (trunk, heads and view branch bf16: 0.987 -- the articulated gradients
+# are ill-conditioned in the forward values).
 
 _packed = {}
 
@@ -199,19 +174,20 @@ def _buffer(key, nbytes, dev, guard=False, params=()):
     return buf
 
 
-def _pack(geo, P, lat, tag="", mixed=0):
+def _pack(geo, P, lat, tag="", mixed=0, exact_folds=False):
     """The fused kernel's fp16x3 weight stream (aon_mlp_art_pack) of one level's parameters with
     this call's latent codes folded into the biases; re-packed on every call (the optimizer
     updates the parameters in place).  mixed: the bf16 mode's mixed streams
-    (aon_mlp_art_pack_mixed: 1 trunk bf16, 2 view branch bf16, 3 fp16 weights; range-guarded, their deformation
-    part is fp16x3)."""
+    (aon_mlp_art_pack_mixed: 1 trunk bf16, 2 view branch bf16, 3 fp16 weights; range-guarded,
+    their deformation part is fp16x3).  exact_folds (the bf16 mode): the folds on the exact-fp32
+    path."""
     shape, app, art = lat
     dev = shape.device
     with small_batched():  # bf16: the four folds as one launch (exact-fp32 path, same bits)
-        fb = {DEF0: _fold(*P[DEF0], 3, torch.cat([shape, art], -1)),
-              PTS0: _fold(*P[PTS0], geo.ne, shape),
-              PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape),
-              VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app)}
+        fb = {DEF0: _fold(*P[DEF0], 3, torch.cat([shape, art], -1), exact_folds),
+              PTS0: _fold(*P[PTS0], geo.ne, shape, exact_folds),
+              PTS0 + 5: _fold(*P[PTS0 + 5], geo.nw + geo.ne, shape, exact_folds),
+              VIEW0: _fold(*P[VIEW0], geo.nw + geo.nv, app, exact_folds)}
     buf = _buffer(f"fwd{'bf' if mixed else ''}{tag}", L.lib().aon_mlp_art_packed_bytes(), dev,
                   guard=True, params=[t for wb in P for t in wb])
     if mixed:
@@ -232,7 +208,8 @@ def _pack_bwd(P, dev, tag="", bf16=False):
 
 
 def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None,
-                         masks=None, bf16=False, enc_bf=None, return_enc_bf=False):
+                         masks=None, bf16=False, enc_bf=None, return_enc_bf=False,
+                         art_forward="f16_acts", timers=None):
     """_forward_level on the fused kernel (aon_mlp_art_fwd_train): raw (R x 4) and the kept
     activations (tiled, tiles.rows(R) rows each), the sample points (row-major) and pos_enc(x')
     (tiled, (tiles.rows(R), 64), column 63 zero); ``masks`` ((16, tiles.rows(R), 8) int32)
@@ -240,8 +217,9 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     mode (aon_mlp_art_fwd_train_bf16; hd / h / bot / hv kept as torch.bfloat16; enc keeps
     columns 0..15 only, (tiles.rows(R), 16) -- the chain reads x' = columns 0..2 -- and
     ``enc_bf`` ((tiles.rows(R), 128) bfloat16, allocated when None) receives pos_enc(x') tiled,
-    columns 63.. zero: the enc-column weight gradients' operand).  enc_rows() converts enc for
-    the all-GEMM backward."""
+    columns 63.. zero: the enc-column weight gradients' operand; ``art_forward``: its forward numerics past
+    the deformation MLP, TrainNumerics.art_forward).  enc_rows() converts enc for the all-GEMM
+    backward.  ``timers``: hip events (bench.py)."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
     NR = tiles.rows(R)
@@ -256,10 +234,10 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     if bf16 and enc_bf is None:
         enc_bf = torch.empty((NR, 128), device=dev, dtype=torch.bfloat16)
     xyz = torch.empty((R, 3), device=dev)
-    mixed = (1 if BF16_TRUNK else 2 if BF16_VIEW else 3 if F16_WEIGHTS else 4 if F16_ACTS else 0
-             ) if bf16 else 0
-    packed = _pack(geo, P, lat, S, mixed if mixed != 4 else 0)  # 4: the fp16x3 stream
-    e0 = _train._ev()
+    mixed, mixed_stream = ART_FORWARD[art_forward] if bf16 else (0, False)
+    # (f16_acts, 4, and f16x3, 0, read the plain fp16x3 stream)
+    packed = _pack(geo, P, lat, S, mixed if mixed_stream else 0, exact_folds=bf16)
+    e0 = _train._ev(timers)
     args = (L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs), L.ptr(t_vals), B, S,
             L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h), L.ptr(bot),
             L.ptr(hv), L.ptr(enc), L.ptr(xyz), L.ptr(raw), L.ptr(masks))
@@ -268,7 +246,7 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     else:
         L.call("aon_mlp_art_fwd_train", *args, L.stream(dev))
     L.snapshot_pack(packed)  # the forward was the pack's last reader (range guard, _lib)
-    _train._rec(f"art_fwd_train{S}", e0, R)
+    _train._rec(timers, f"art_fwd_train{S}", e0, R)
     return (xyz, hd, enc, h, bot, hv) + ((enc_bf,) if return_enc_bf else ())
 
 
@@ -406,7 +384,7 @@ def _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, dra
 
 
 def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
-                          masks=None, h_tiled=True, enc_bf=None):
+                          masks=None, h_tiled=True, enc_bf=None, timers=None, cfg=DEFAULT):
     """_backward_level with every input-gradient product (and pos_enc's backward) in one fused
     kernel (aon_mlp_art_bwd); the weight gradients dW = dZ^T X, db = sum_rows dZ and the latent
     terms stay GEMMs.  ``masks``: the fused forward's ReLU' bits (built from the activations
@@ -414,7 +392,8 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     row-major); the chain's dzv / dbot / dz / dzd are tiled.  enc: the fused forward's tiled
     pos_enc(x') ((NR, 64) fp16x3, (NR, 16) bf16) or the layer-by-layer forward's row-major
     (R, 63).  enc_bf: the bf16 forward's tiled 128-column pos_enc(x') (the enc-column weight
-    gradients then run on the LDS-DMA kernel)."""
+    gradients then run on the LDS-DMA kernel).  ``timers``: hip events (bench.py); ``cfg``: the
+    model's TrainNumerics (the weight-gradient batching)."""
     R, dev = xyz.shape[0], xyz.device
     bf16 = h[0].dtype == torch.bfloat16  # activations kept by the bf16 training forward
     if masks is None:
@@ -434,12 +413,12 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     packed = _pack_bwd(P, dev, S, bf16)
     enc_t = enc.shape[1] != ne  # the fused forward's tiled copy
     enc_chain = enc if enc_t else _enc_tiled(enc, 16 if bf16 else 64)
-    e0 = _train._ev()
+    e0 = _train._ev(timers)
     L.call("aon_mlp_art_bwd_bf16" if bf16 else "aon_mlp_art_bwd", L.ptr(packed), L.ptr(draw), L.ptr(masks), L.ptr(enc_chain), R,
            L.ptr(dzv), L.ptr(dbot), L.ptr(dz), L.ptr(dxp), L.ptr(dzd), L.ptr(work), L.stream(dev))
     L.snapshot_pack(packed)  # the chain was the pack's last reader
-    _train._rec(f"art_bwd_chain{S}", e0, R)
-    e0 = _train._ev()
+    _train._rec(timers, f"art_bwd_chain{S}", e0, R)
+    e0 = _train._ev(timers)
     gs, acts = GRAD_SCALE, ACT_SCALE
 
     def dweight(i, dY, ldy, X, ldx, n_in, col0=0, rdiv=1, bias=True, chain_scale=True, a_t=True):
@@ -485,7 +464,7 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
     # 256 x 256 ones -- bottleneck, pts_linears.1-7 -- and the 128-wide view / deformation / enc
     # column ones; fp16x3: all as the fp16x3 class), flushed before the latent terms read the
     # bias gradients; the latent terms then run in the same order as before (bit-identical)
-    with batched():
+    with batched(cfg.batch_dweights, cfg.batch_128):
         dweight(RGB, draw, 4, hv[3], wc, wc, a_t=False)                   # rgb_layer
         for i in range(3, 0, -1):                                         # views_linear.i
             dweight(VIEW0 + i, dzv[i], wc, hv[i - 1], wc, wc)
@@ -515,7 +494,7 @@ def _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, h
         dlatent(PTS0, ne, shape, dshape, True)
         dlatent(DEF0, 3, shape, dshape, True)
         dlatent(DEF0, 3 + geo.n_shape, art, dart, False)
-    _train._rec(f"art_dweight{S}", e0, R)
+    _train._rec(timers, f"art_dweight{S}", e0, R)
 
 
 class ArtRenderLevel(torch.autograd.Function):
@@ -524,8 +503,9 @@ class ArtRenderLevel(torch.autograd.Function):
     three latent codes (density = shape, color = appearance, articulation)."""
 
     @staticmethod
-    def forward(ctx, geo, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise, shape, app, art,
-                *params):
+    def forward(ctx, geo, cfg, timers, rays_o, rays_d, viewdirs, t_vals, white_bkgd, noise,
+                shape, app, art, *params):
+        # cfg: the model's TrainNumerics; timers: a dict of hip events (bench.py) or None
         B, S = t_vals.shape
         R, dev = B * S, t_vals.device
         lat = tuple(L.contig(x.detach().reshape(1, -1)) for x in (shape, app, art))
@@ -544,17 +524,18 @@ class ArtRenderLevel(torch.autograd.Function):
         noise = L.contig(noise) if noise is not None else None
         masks = None  # ReLU' bits for the fused backward chain (built there when None)
         enc_bf = None  # the bf16 forward's tiled pos_enc(x') copy
-        if FUSED_FORWARD and _fused_ok(geo):
+        if cfg.fused_forward and _fused_ok(geo):
             masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device=dev)
-            bf16 = PRECISION == "bf16"
             xyz, hd, enc, h, bot, hv, enc_bf = _forward_level_fused(
                 geo, P, lat, L.contig(rays_o), L.contig(rays_d), L.contig(viewdirs),
-                L.contig(t_vals), raw, noise, masks, bf16=bf16, return_enc_bf=True)
+                L.contig(t_vals), raw, noise, masks, bf16=cfg.bf16, return_enc_bf=True,
+                art_forward=cfg.art_forward, timers=timers)
         else:
             xyz = torch.empty((R, 3), device=dev)
             L.call("aon_cast_rays", L.ptr(rays_o), L.ptr(rays_d), L.ptr(t_vals), B, S, None, 0,
                    L.ptr(xyz), 0, 0, None, L.stream(dev))
-            hd, enc, h, bot, hv = _forward_level(geo, P, lat, xyz, venc, S, raw, noise)
+            hd, enc, h, bot, hv = _forward_level(geo, P, lat, xyz, venc, S, raw, noise,
+                                                 exact_folds=cfg.bf16)
         comp = torch.empty((B, 3), device=dev)
         acc = torch.empty((B,), device=dev)
         weights = torch.empty((B, S), device=dev)
@@ -567,6 +548,7 @@ class ArtRenderLevel(torch.autograd.Function):
         ctx.enc_bf = enc_bf if masks is not None else None
         ctx.h_tiled = masks is not None  # the fused forward keeps its tensors tiled
         ctx.meta = (geo, B, S, bool(white_bkgd), tuple(x.shape for x in (shape, app, art)))
+        ctx.cfg, ctx.timers = cfg, timers
         ctx.mark_non_differentiable(weights)
         # unused outputs (acc, depth, weights in training_step) get no zero-filled gradients
         ctx.set_materialize_grads(False)
@@ -592,9 +574,10 @@ class ArtRenderLevel(torch.autograd.Function):
         P = [(params[2 * i], params[2 * i + 1]) for i in range(20)]
         G = [(torch.empty_like(w), torch.empty_like(b)) for w, b in P]
         dlat = tuple(torch.empty_like(x) for x in lat)
-        if FUSED_BACKWARD and _fused_ok(geo):
+        if ctx.cfg.fused_backward and _fused_ok(geo):
             _backward_level_fused(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw,
-                                  ctx.masks, ctx.h_tiled, ctx.enc_bf)
+                                  ctx.masks, ctx.h_tiled, ctx.enc_bf, timers=ctx.timers,
+                                  cfg=ctx.cfg)
         else:
             if ctx.h_tiled:  # the all-GEMM backward reads row-major fp32 activations
                 hd, h, hv = (torch.stack([tiles.untile(x, R).float() for x in t]) for t in (hd, h, hv))
@@ -602,16 +585,19 @@ class ArtRenderLevel(torch.autograd.Function):
             _backward_level(geo, P, G, lat, dlat, xyz, enc, venc, S, hd, h, bot, hv, draw)
         grads = [g for pair in G for g in pair]
         dlat = [d.reshape(s) for d, s in zip(dlat, lat_shapes)]
-        return (None, None, None, None, None, None, None, *dlat, *grads)
+        return (None, None, None, None, None, None, None, None, None, *dlat, *grads)
 
 
-def render_level(mlp, rays_o, rays_d, viewdirs, t_vals, white_bkgd, latents, noise=None):
-    """One NeRF_AE_Art level under autograd -> (comp_rgb, acc, depth, weights)."""
+def render_level(mlp, rays_o, rays_d, viewdirs, t_vals, white_bkgd, latents, noise=None,
+                 cfg=DEFAULT, timers=None):
+    """One NeRF_AE_Art level under autograd -> (comp_rgb, acc, depth, weights); ``cfg``: the
+    model's TrainNumerics."""
     params = [p for m in art_layers(mlp) for p in (m.weight, m.bias)]
     geo = getattr(mlp, "_geo", None)
     if geo is None:
         geo = mlp._geo = _Geo(mlp)
-    return ArtRenderLevel.apply(geo, rays_o, rays_d, viewdirs, t_vals, bool(white_bkgd), noise,
+    return ArtRenderLevel.apply(geo, cfg, timers, rays_o, rays_d, viewdirs, t_vals,
+                                bool(white_bkgd), noise,
                                 latents["density"], latents["color"], latents["articulation"],
                                 *params)
 
@@ -644,14 +630,15 @@ class LatentReg(torch.autograd.Function):
 
 
 def training_step(model, code_library, batch, randomized, white_bkgd, near, far, *,
-                  u_coarse=None, u_fine=None):
+                  u_coarse=None, u_fine=None, timers=None):
     """LitNeRF_AutoDecoder.training_step (model_autodecoder.py:395-477) ->
     (loss, logs{loss0, loss1, reg, psnr0, psnr1}).  ``batch`` holds rays_o / rays_d / viewdirs /
     target (B, 3) and instance_id / articulation_id (1,) as the reference's loader gives them
-    after its squeeze (model_autodecoder.py:396-399)."""
+    after its squeeze (model_autodecoder.py:396-399).  The kernels and precision are the model's
+    own (model.train_numerics)."""
     latents = code_library(batch)
     ret = model(batch, randomized, white_bkgd, near, far, latents, u_coarse=u_coarse,
-                u_fine=u_fine)
+                u_fine=u_fine, timers=timers)
     reg = LatentReg.apply(latents["density"], latents["color"], latents["articulation"])
     # loss1 + loss0 + reg and the psnrs in one launch (train.LossPair)
     loss, loss0, loss1, psnr0, psnr1 = loss_pair(ret[0][0], ret[1][0], batch["target"], reg)

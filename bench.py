@@ -10,9 +10,10 @@ synchronize on both sides, max over ranks):
   "articulated"     config C3 -- NeRF_AE_Art 320x240 frame render (N = 1 only)
   "train_step"      config C5 -- LitNeRF.training_step on 4096 rays per rank + Adam (+ the DDP
                     gradient all-reduce over RCCL on N > 1: weak scaling), f16x3 kernels
-  "train_step_bf16" the same step in C5's bf16 mode (train.PRECISION = "bf16")
+  "train_step_bf16" the same step in C5's bf16 mode (NeRF(train_precision="bf16"))
   "train_step_art"  C5 on the articulated auto-decoder (LitNeRF_AutoDecoder.training_step)
-  "train_step_art_bf16"  the same in the articulated bf16 mode (train_art.PRECISION = "bf16")
+  "train_step_art_bf16"  the same in the articulated bf16 mode
+                    (NeRF_AE_Art(train_precision="bf16"))
 each with its own ms_per_step and roofline (MFMA fraction of the fine-level MLP kernels,
 HBM byte fractions of the training kernels counting the stored activations).
 
@@ -354,8 +355,8 @@ TRAIN_PEAK = {"f16x3": 2500.0 / 3, "bf16": 2500.0}
 def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
     """C5: one LitNeRF.training_step (or LitNeRF_AutoDecoder.training_step) on 4096 rays per rank
     drawn from 8 synthetic 640x480 views, randomized sampling, loss, HIP backward, gradient
-    all-reduce (RCCL, N > 1), fused Adam with the reference schedule.  precision: the fused
-    kernels' numerics (train.PRECISION: "f16x3" fp32-class, or C5's "bf16")."""
+    all-reduce (RCCL, N > 1), fused Adam with the reference schedule.  precision: the model's
+    training numerics (train_precision: "f16x3" fp32-class, or C5's "bf16")."""
     import types
 
     from aonerf import train
@@ -373,13 +374,13 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
         from aonerf.model_autodecoder import NeRF_AE_Art
         from aonerf.synthetic import init_code_library
 
-        net = init_like_reference(NeRF_AE_Art()).to(dev)
+        net = init_like_reference(NeRF_AE_Art(train_precision=precision)).to(dev)
         lib = init_code_library(CodeLibraryArticulated(
             types.SimpleNamespace(N_max_objs=151, N_obj_code_length=128))).to(dev)
         ids = {"instance_id": torch.tensor([7], device=dev),
                "articulation_id": torch.tensor([3], device=dev)}
     else:
-        net = init_like_reference(NeRF()).to(dev)
+        net = init_like_reference(NeRF(train_precision=precision)).to(dev)
     poses = create_spheric_poses(4.0)
     focal = sapien_focal(H)
     views = [frame_rays(torch.as_tensor(poses[(5 * k) % len(poses)]), H, W, focal) for k in range(8)]
@@ -399,31 +400,24 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
     timers = {}
 
     def step(i):
-        train.TIMERS = timers if i >= args.warmup else None
+        tm = timers if i >= args.warmup else None
         idx = torch.randint(0, 8 * H * W, (nrays,), device=dev, generator=gen)
         batch = {k: v[idx] for k, v in rays_all.items()}
         batch["target"] = target_all[idx]
         opt.zero_grad()
         if art:
             batch.update(ids)
-            loss, _ = train_art.training_step(net, lib, batch, True, True, 2.0, 6.0)
+            loss, _ = train_art.training_step(net, lib, batch, True, True, 2.0, 6.0, timers=tm)
         else:
-            loss, _ = train.training_step(net, batch, True, True, 2.0, 6.0)
+            loss, _ = train.training_step(net, batch, True, True, 2.0, 6.0, timers=tm)
         loss.backward()
         sync()
         opt.step(lr=train.learning_rate(i, 200000))
 
-    old_prec = train.PRECISION
-    train.PRECISION = precision
-    if art:
-        old_art, train_art.PRECISION = train_art.PRECISION, precision
     try:
         el = timed(step, args.steps, args.warmup, world)
     finally:
-        train.TIMERS = None
-        train.PRECISION = old_prec
-        if art:
-            train_art.PRECISION = old_art
+        sync.close()
     ddp = None
     if world > 1:
         # the all-reduce is part of every timed step: the ranks draw different batches, so their
@@ -467,9 +461,9 @@ def bench_train(args, world, rank, local_rank, art=False, precision="f16x3"):
         rec["ddp"] = ddp
     if art and precision == "bf16":
         rec["roofline"]["note"] = ("the articulated bf16 mode keeps its forward in fp16x3 "
-                                   "(train_art.BF16_TRUNK = False: 3 fp16 products per MAC, peak "
-                                   "833 TF/s for that third of the FLOP); frac is against the "
-                                   "bf16 peak for the whole step")
+                                   "(TrainNumerics.art_forward 'f16_acts': 2 fp16 products per "
+                                   "MAC past the deformation MLP, which is fp16x3); frac is "
+                                   "against the bf16 peak for the whole step")
     kern = {}
     hbm_bytes = 0.0
     names = ("art_fwd_train", "art_bwd_chain", "art_dweight") if art else ("fwd_train", "bwd_chain", "dweight")

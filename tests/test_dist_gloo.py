@@ -153,8 +153,25 @@ def _ddp_bucket_worker(rank, world, port, q):
         early = two._works[0] is not None and two._works[1] is None and two.calls == 1
         two()
         same = all(torch.equal(t.grad, r) for t, r in zip(params, ref))
-        for h in two._hooks:
-            h.remove()
+        two.close()  # its hooks go with it
+        assert two._hooks == [] and two.calls == 2
+        # a sync re-created per epoch while the old one is merely dropped: the dropped object's
+        # (weakly referenced) hooks never fire, so the new one's first bucket is not disturbed
+        with GradAllReduce(params, buckets=[list(fine.parameters()),
+                                            [*coarse.parameters(), shared]]) as three:
+            backward()
+            three()
+        del three
+        import gc
+
+        gc.collect()
+        four = GradAllReduce(params, buckets=[list(fine.parameters()),
+                                              [*coarse.parameters(), shared]])
+        backward()
+        four()
+        recreated = (four.calls == 2
+                     and all(torch.equal(t.grad, r) for t, r in zip(params, ref)))
+        four.close()
         bad = GradAllReduce(params, buckets=[list(fine.parameters()), [*coarse.parameters(), shared]])
         backward()
         try:
@@ -162,8 +179,8 @@ def _ddp_bucket_worker(rank, world, port, q):
             raised = False
         except RuntimeError as e:
             raised = "already in flight" in str(e)
-        bad._works[0].wait()
-        q.put((rank, early, same, two.calls, raised))
+        bad.close()  # drains the bucket still in flight
+        q.put((rank, early, same and recreated, two.calls, raised))
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -89,13 +89,9 @@ def art_fwd_mode(request):
     (aon_mlp_art_fwd_train) or layer by layer on aon_gemm; input gradients in the fused chain
     (aon_mlp_art_bwd) or as GEMMs + aon_pos_enc_bwd.  The mixed pairs convert pos_enc(x')
     between the fused kernels' tiled copy and the GEMMs' row-major one (train_art.enc_rows /
-    _enc_tiled)."""
-    from aonerf import train_art
-
-    old = train_art.FUSED_FORWARD, train_art.FUSED_BACKWARD
-    train_art.FUSED_FORWARD, train_art.FUSED_BACKWARD = request.param
-    yield request.param
-    train_art.FUSED_FORWARD, train_art.FUSED_BACKWARD = old
+    _enc_tiled).  The model's TrainNumerics."""
+    fwd, bwd = request.param
+    return dict(fused_forward=fwd, fused_backward=bwd)
 
 
 def test_fused_art_train_forward_activations():
@@ -385,13 +381,16 @@ def test_art_c5_level_stage_isolated(level):
     assert e_bwd[wb] <= 1e-4, (wb, e_bwd[wb])
 
 
-def _make(seed=0):
+def _make(seed=0, **numerics):
+    """NeRF_AE_Art + code library with the oracle's seed weights; ``numerics``: TrainNumerics
+    fields."""
     import types
 
     from aonerf.code_library import CodeLibraryArticulated
     from aonerf.model_autodecoder import NeRF_AE_Art
+    from aonerf.numerics import TrainNumerics
 
-    net = NeRF_AE_Art().cuda()
+    net = NeRF_AE_Art(train_numerics=TrainNumerics(**numerics)).cuda()
     net.load_state_dict({k: torch.from_numpy(v) for k, v in W.art_state_dict(seed).items()})
     lib = CodeLibraryArticulated(types.SimpleNamespace(N_max_objs=151, N_obj_code_length=128)).cuda()
     lib.load_state_dict({k: torch.from_numpy(v) for k, v in W.code_library_state_dict(seed).items()})
@@ -436,7 +435,7 @@ def test_art_train_step_golden(golden, art_fwd_mode):
 
     g = golden("art_train_step.npz")
     assert W.digest(W.art_state_dict(0)) == str(g["digest"])
-    net, lib = _make(0)
+    net, lib = _make(0, **art_fwd_mode)
     loss, logs = train_art.training_step(net, lib, _batch(g), True, True, 2.0, 6.0,
                                          u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]))
     loss.backward()
@@ -480,7 +479,7 @@ def test_art_train_step_chain(golden, art_fwd_mode, loss_scale):
     from aonerf import train_art
 
     g = golden("art_train_step.npz")
-    net, lib = _make(0)
+    net, lib = _make(0, **art_fwd_mode)
     batch = _batch(g)
     latents = lib(batch)
     ret = net(batch, True, True, 2.0, 6.0, latents, u_coarse=cuda(g["u_coarse"]),
@@ -747,3 +746,38 @@ def test_art_train_step_c5_4096_rays():
 
 def L_contig(x):
     return x.detach().reshape(1, -1).contiguous()
+
+
+def test_two_art_precisions_in_one_process():
+    """Verdict r05 #5: an f16x3 and a bf16 (default fp16-activation forward) articulated model
+    train in one process, interleaved, each bit-equal to its solo run."""
+    from aonerf import train_art
+    from test_gpu_train import _step_state, c5_batch
+
+    batch, u_c, u_f = c5_batch(n=256, seed=6)
+    batch["instance_id"] = torch.tensor([7], device="cuda")
+    batch["articulation_id"] = torch.tensor([3], device="cuda")
+    solo = {}
+    for prec in ("f16x3", "bf16"):
+        net, lib = _make(0, precision=prec)
+        opt = train_art.configure_optimizers(net, lib)
+        solo[prec] = _step_state(net, opt, train_art, batch, u_c, u_f, lib)
+    (na, la_), (nb, lb_) = _make(0, precision="f16x3"), _make(0, precision="bf16")
+    oa, ob = train_art.configure_optimizers(na, la_), train_art.configure_optimizers(nb, lb_)
+    oa.zero_grad()
+    ob.zero_grad()
+    xa, _ = train_art.training_step(na, la_, batch, True, True, 2.0, 6.0, u_coarse=u_c, u_fine=u_f)
+    xb, _ = train_art.training_step(nb, lb_, batch, True, True, 2.0, 6.0, u_coarse=u_c, u_fine=u_f)
+    (xa + xb).backward()
+    got = {}
+    for prec, net, lib, loss in (("f16x3", na, la_, xa), ("bf16", nb, lb_, xb)):
+        ps = list(net.parameters()) + list(lib.parameters())
+        got[prec] = (loss.detach().cpu(), [p.grad.detach().cpu().clone() for p in ps])
+    ob.step()
+    oa.step()
+    for prec, net, lib in (("f16x3", na, la_), ("bf16", nb, lb_)):
+        loss, grads, params = solo[prec]
+        assert torch.equal(loss, got[prec][0])
+        assert all(torch.equal(x, y) for x, y in zip(grads, got[prec][1]))
+        ps = list(net.parameters()) + list(lib.parameters())
+        assert all(torch.equal(x, p.detach().cpu()) for x, p in zip(params, ps))

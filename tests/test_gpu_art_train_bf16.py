@@ -1,15 +1,16 @@
 """The articulated bf16 training mode (BASELINE config C5's "bf16" on LitNeRF_AutoDecoder;
-train_art.PRECISION = "bf16"): the backward chain and the weight-gradient GEMMs are bf16
+NeRF_AE_Art(train_precision="bf16")): the backward chain and the weight-gradient GEMMs are bf16
 throughout (aon_mlp_art_bwd_bf16, aon_gemm mma_bf16), kept activations and gradients bf16;
 compositing, the loss, their backward, the latent terms and Adam stay fp32 on fp32 master
 weights.  The forward (aon_mlp_art_fwd_train_bf16), the deformation MLP always fp16x3 (x' = delta
-+ xyz feeds pos_enc's sin(2^9 x'), model_autodecoder.py:205-212), every later layer:
-  F16_ACTS = True (default): two fp16 MFMAs per product, the weights' exact hi / lo split and the
++ xyz feeds pos_enc's sin(2^9 x'), model_autodecoder.py:205-212), every later layer
+(TrainNumerics.art_forward, a per-model setting):
+  "f16_acts" (default): two fp16 MFMAs per product, the weights' exact hi / lo split and the
     activations rounded once to fp16 -- 8x finer than the bf16 copies the backward reads;
-  all flags False: fp16x3 throughout, only the stores bf16;
-  F16_WEIGHTS: two fp16 MFMAs, the weights rounded to fp16, the activations exact;
-  BF16_TRUNK: the trunk, heads and view branch one bf16 MFMA per product (the mixed stream);
-  BF16_VIEW: the view branch only bf16.
+  "f16x3": fp16x3 throughout, only the stores bf16;
+  "f16_weights": two fp16 MFMAs, the weights rounded to fp16, the activations exact;
+  "bf16_trunk": the trunk, heads and view branch one bf16 MFMA per product (the mixed stream);
+  "bf16_view": the view branch only bf16.
 The articulated step's gradients are ill-conditioned in the forward values
 (test_gpu_art_train.test_art_train_step_c5_4096_rays): a bf16 trunk's 2^-9 forward rounding alone
 moves the deformation gradients to cosine 0.987 against the fp32 oracle, while the bf16 backward
@@ -34,38 +35,18 @@ from test_gpu_art_train import L_contig, _make, rel_err
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def art_bf16():
-    from aonerf import train_art
-
-    old = [getattr(train_art, k) for k in _FLAGS]
-    train_art.PRECISION = "bf16"
-    yield train_art
-    for k, v in zip(_FLAGS, old):
-        setattr(train_art, k, v)
-
-
-# the bf16 mode's forward numerics: fp16x3 throughout (all flags False), fp16 activations
-# (F16_ACTS) or fp16 weights (F16_WEIGHTS) past the deformation MLP, the trunk bf16
-# (BF16_TRUNK), or the view branch bf16 (BF16_VIEW)
+# the bf16 mode's forward numerics (TrainNumerics.art_forward): fp16x3 throughout, fp16
+# activations (the default) or fp16 weights past the deformation MLP, the trunk bf16, or the view
+# branch bf16
 FWD_MODES = ["f16x3_fwd", "f16x", "f16w", "bf16_trunk", "bf16_view"]
-_FLAGS = ("PRECISION", "BF16_TRUNK", "BF16_VIEW", "F16_WEIGHTS", "F16_ACTS")
+ART_FORWARD = {"f16x3_fwd": "f16x3", "f16x": "f16_acts", "f16w": "f16_weights",
+               "bf16_trunk": "bf16_trunk", "bf16_view": "bf16_view"}
 
 
-def _set_mode(train_art, mode, monkeypatch=None):
-    vals = {"BF16_TRUNK": mode == "bf16_trunk", "BF16_VIEW": mode == "bf16_view",
-            "F16_WEIGHTS": mode == "f16w", "F16_ACTS": mode == "f16x"}
-    for k, v in vals.items():
-        if monkeypatch is not None:
-            monkeypatch.setattr(train_art, k, v)
-        else:
-            setattr(train_art, k, v)
-
-
-def _level_inputs(seed=12, n=1024):
+def _level_inputs(seed=12, n=1024, **numerics):
     from test_gpu_train import c5_batch
 
-    net, lib = _make(0)
+    net, lib = _make(0, **numerics)
     batch, u_c, u_f = c5_batch(n=n, seed=seed)
     batch["instance_id"] = torch.tensor([7], device="cuda")
     batch["articulation_id"] = torch.tensor([3], device="cuda")
@@ -74,19 +55,18 @@ def _level_inputs(seed=12, n=1024):
 
 @pytest.mark.parametrize("mode", FWD_MODES)
 @pytest.mark.parametrize("level", [0, 1], ids=["coarse", "fine"])
-def test_art_bf16_forward(level, mode, monkeypatch):
+def test_art_bf16_forward(level, mode):
     """One level's training forward, f16x3 mode vs bf16 mode at the same t.  The deformation MLP
     is the fp16x3 kernel's in both, so x', pos_enc(x'), the points and the deformation layers'
     ReLU' bits are bit-identical, hd is exactly bf16(f16x3 hd) and the tiled 128-column enc_bf
-    exactly bf16(pos_enc(x')) with zero padding.  BF16_TRUNK False: everything
+    exactly bf16(pos_enc(x')) with zero padding.  The fp16x3 forward: everything
     is -- h / bot / hv exactly bf16 of the f16x3 values, raw and all ReLU' bits identical.
     True: the bf16 trunk's h / bot / hv and raw within bf16 distance of the fp64 oracle at our
-    x' (gate 2e-2 of each tensor's max).  BF16_VIEW: the trunk and bottleneck exactly as in the
+    x' (gate 2e-2 of each tensor's max).  bf16_view: the trunk and bottleneck exactly as in the
     fp16x3 forward (h / bot and their ReLU' bits), the view branch's hv and raw within bf16
     distance of the fp64 oracle."""
     from aonerf import tiles, train_art
 
-    _set_mode(train_art, mode, monkeypatch)
     trunk = mode != "f16x3_fwd"
     net, lib, batch, u_c, u_f = _level_inputs()
     latents = lib(batch)
@@ -107,7 +87,8 @@ def test_art_bf16_forward(level, mode, monkeypatch):
             masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device="cuda")
             kept = train_art._forward_level_fused(geo, P, lat, batch["rays_o"], batch["rays_d"],
                                                   batch["viewdirs"], t, raw, None, masks, bf16=bf,
-                                                  enc_bf=enc_bf if bf else None)
+                                                  enc_bf=enc_bf if bf else None,
+                                                  art_forward=ART_FORWARD[mode])
             out[bf] = (kept, raw, masks)
         torch.cuda.synchronize()
     (xyz32, hd32, enc32, h32, bot32, hv32), raw32, m32 = out[False]
@@ -164,26 +145,27 @@ def test_art_bf16_forward(level, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", FWD_MODES)
-def test_art_bf16_train_step_c5(art_bf16, mode):
+def test_art_bf16_train_step_c5(mode):
     """One C5 step of the articulated auto-decoder (4,096 rays, randomized, injected uniforms) in
     the bf16 mode: the loss against the fp32 oracle at our sample positions within 3e-3 relative,
     every MLP parameter's and latent code's gradient against the fp32 oracle (teacher-forced at
     our t) with cosine >= 0.999 and within 0.05 of its max (measured: cosine >= 0.99984, max-rel
     <= 2.1e-2 with the fp16x3 forward, 0.99919 / 0.049 with the default fp16-activation forward;
     the f16x3 mode meets 1e-3 -- or x'-attributed -- in
-    test_gpu_art_train.test_art_train_step_c5_4096_rays).  F16_WEIGHTS (not the default): cosine
-    >= 0.998, max-rel <= 0.1 (measured 0.99886 / 0.074).  BF16_TRUNK = True (the bf16 trunk
+    test_gpu_art_train.test_art_train_step_c5_4096_rays).  "f16_weights" (not the default):
+    cosine >= 0.998, max-rel <= 0.1 (measured 0.99886 / 0.074).  "bf16_trunk" (the bf16 trunk
     forward, not the default) is held to what its forward rounding allows: cosine >= 0.98,
     max-rel <= 0.3 (measured 0.987 / 0.21, the deformation gradients; the heads and view branch
-    0.9994 / 0.07).  BF16_VIEW = True (the view branch bf16, not the default either: it saves
+    0.9994 / 0.07).  "bf16_view" (the view branch bf16, not the default either: it saves
     0.23 ms of the 10.1 ms step) likewise: cosine >= 0.995, max-rel <= 0.15 (measured 0.9968 /
     0.10, again the deformation gradients -- the view branch's bf16 rounding reaches them through
     the bottleneck's gradient)."""
-    train_art = art_bf16
-    _set_mode(train_art, mode)
+    from aonerf import train_art
+
     min_cos, max_rel = {"bf16_trunk": (0.98, 0.3), "bf16_view": (0.995, 0.15),
                         "f16w": (0.998, 0.1)}.get(mode, (0.999, 0.05))
-    net, lib, batch, u_c, u_f = _level_inputs(n=4096)
+    net, lib, batch, u_c, u_f = _level_inputs(n=4096, precision="bf16",
+                                              art_forward=ART_FORWARD[mode])
     latents = lib(batch)
     ret = net(batch, True, True, 2.0, 6.0, latents, u_coarse=u_c, u_fine=u_f,
               return_intermediates=True)
@@ -225,27 +207,19 @@ def test_art_bf16_train_step_c5(art_bf16, mode):
     assert not bad, bad
 
 
-def _art_trajectory_gpu(precision, batch, steps, lr, trunk=False, view=False, f16w=False,
-                        f16x=False):
+def _art_trajectory_gpu(precision, batch, steps, lr, art_forward="f16_acts"):
     from aonerf import train_art
 
-    old = [getattr(train_art, k) for k in _FLAGS]
-    train_art.PRECISION, train_art.BF16_TRUNK, train_art.BF16_VIEW = precision, trunk, view
-    train_art.F16_WEIGHTS, train_art.F16_ACTS = f16w, f16x
-    try:
-        net, lib = _make(0)
-        opt = train_art.configure_optimizers(net, lib, lr_init=lr)
-        out = []
-        for _ in range(steps):
-            opt.zero_grad()
-            loss, _ = train_art.training_step(net, lib, batch, False, True, 2.0, 6.0)
-            loss.backward()
-            opt.step()
-            out.append(loss.item())
-        return np.array(out)
-    finally:
-        for k, v in zip(_FLAGS, old):
-            setattr(train_art, k, v)
+    net, lib = _make(0, precision=precision, art_forward=art_forward)
+    opt = train_art.configure_optimizers(net, lib, lr_init=lr)
+    out = []
+    for _ in range(steps):
+        opt.zero_grad()
+        loss, _ = train_art.training_step(net, lib, batch, False, True, 2.0, 6.0)
+        loss.backward()
+        opt.step()
+        out.append(loss.item())
+    return np.array(out)
 
 
 def _traj_batch():
@@ -316,11 +290,11 @@ def test_art_bf16_loss_trajectory():
     for seed in (1, 2, 3):
         ens[f"fp32 ulp seed {seed}"] = _oracle_trajectory(batch, steps, lr, torch.float32, seed)
     f16 = _art_trajectory_gpu("f16x3", batch, steps, lr)
-    bf = _art_trajectory_gpu("bf16", batch, steps, lr)
-    bft = _art_trajectory_gpu("bf16", batch, steps, lr, trunk=True)
-    bfv = _art_trajectory_gpu("bf16", batch, steps, lr, view=True)
-    bfw = _art_trajectory_gpu("bf16", batch, steps, lr, f16w=True)
-    bfx = _art_trajectory_gpu("bf16", batch, steps, lr, f16x=True)
+    bf = _art_trajectory_gpu("bf16", batch, steps, lr, "f16x3")
+    bft = _art_trajectory_gpu("bf16", batch, steps, lr, "bf16_trunk")
+    bfv = _art_trajectory_gpu("bf16", batch, steps, lr, "bf16_view")
+    bfw = _art_trajectory_gpu("bf16", batch, steps, lr, "f16_weights")
+    bfx = _art_trajectory_gpu("bf16", batch, steps, lr, "f16_acts")
     dist = {k: np.abs(v / ref - 1) for k, v in ens.items()}
     env = np.maximum.accumulate(np.max(np.stack(list(dist.values())), 0))
     ours = np.abs(f16 / ref - 1)
@@ -381,7 +355,7 @@ _LAYERS = (["deformations_linear.%d" % i for i in range(4)] + ["deformation_laye
 
 
 @pytest.mark.parametrize("level", [0, 1], ids=["coarse", "fine"])
-def test_art_bf16_backward_stage_isolated(level, monkeypatch):
+def test_art_bf16_backward_stage_isolated(level):
     """The bf16 backward (aon_mlp_art_bwd_bf16 + the mma_bf16 weight-gradient GEMMs) on its own:
     the fp64 oracle's autograd forced to OUR kept forward values (oracle.art_mlp_forward_kept,
     the bf16 trunk forward's bf16 activations) with OUR d raw (the compositing backward of the C5
@@ -391,7 +365,6 @@ def test_art_bf16_backward_stage_isolated(level, monkeypatch):
     from aonerf import _lib as L
     from aonerf import tiles, train_art
 
-    monkeypatch.setattr(train_art, "BF16_TRUNK", True)
     net, lib, batch, u_c, u_f = _level_inputs(n=1024)
     latents = lib(batch)
     with torch.no_grad():
@@ -408,7 +381,7 @@ def test_art_bf16_backward_stage_isolated(level, monkeypatch):
     masks = torch.empty((16, tiles.rows(R), 8), dtype=torch.int32, device="cuda")
     xyz, hd, enc, h, bot, hv, enc_bf = train_art._forward_level_fused(
         geo, P, lat_t, batch["rays_o"], batch["rays_d"], batch["viewdirs"], t, raw, None, masks,
-        bf16=True, return_enc_bf=True)
+        bf16=True, return_enc_bf=True, art_forward="bf16_trunk")
     venc = torch.empty((B, 27), device="cuda")
     L.call("aon_pos_enc", L.ptr(batch["viewdirs"]), B, 0, 4, L.ptr(venc), L.stream())
     comp = torch.empty((B, 3), device="cuda")

@@ -30,11 +30,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _net():
+def _net(train_precision="f16x3"):
     from aonerf.model import NeRF
     from aonerf.synthetic import init_like_reference
 
-    return init_like_reference(NeRF()).cuda()
+    return init_like_reference(NeRF(train_precision=train_precision)).cuda()
 
 
 def _batch(seed, n=96):
@@ -325,14 +325,11 @@ def _c5_bf16_grads(net, rank):
     from aonerf import train
 
     b, (uc, uf) = _c5_batch(rank)
-    old, train.PRECISION = train.PRECISION, "bf16"
-    try:
-        for p in net.parameters():
-            p.grad = None
-        loss, _ = train.training_step(net, b, True, True, 2.0, 6.0, u_coarse=uc, u_fine=uf)
-        loss.backward()
-    finally:
-        train.PRECISION = old
+    assert net.train_numerics.precision == "bf16"
+    for p in net.parameters():
+        p.grad = None
+    loss, _ = train.training_step(net, b, True, True, 2.0, 6.0, u_coarse=uc, u_fine=uf)
+    loss.backward()
     return [p.grad.clone() for p in net.parameters()]
 
 
@@ -344,7 +341,7 @@ def _worker_c5_bf16(rank, world, port, q):
     try:
         from aonerf.parallel import GradAllReduce
 
-        net = _net()
+        net = _net("bf16")
         _c5_bf16_grads(net, rank)
         GradAllReduce(net.parameters(), dtype=torch.bfloat16)()
         q.put((rank, [p.grad.cpu().numpy() for p in net.parameters()]))
@@ -361,7 +358,7 @@ def _worker_rccl_buckets(port, q):
     try:
         from aonerf.parallel import GradAllReduce
 
-        net = _net()
+        net = _net("bf16")
         ref = _c5_bf16_grads(net, 0)  # no collective
         fine = list(net.fine_mlp.parameters())
         coarse = list(net.coarse_mlp.parameters())
@@ -369,6 +366,7 @@ def _worker_rccl_buckets(port, q):
         got = _c5_bf16_grads(net, 0)  # the hooks issue the fine bucket inside the backward
         early = sync._works[0] is not None and sync._works[1] is None and sync.calls == 1
         sync()
+        sync.close()
         torch.cuda.synchronize()
         q.put((early, sync.calls, [g.cpu().numpy() for g in ref], [g.cpu().numpy() for g in got],
                [p.grad.cpu().numpy() for p in net.parameters()]))
@@ -403,7 +401,7 @@ def test_c5_bf16_ddp_step_two_ranks():
     exactly bf16(bf16(g0) + bf16(g1)) / 2 of the two single-rank gradients."""
     world = 2
     got = dict(_spawn(_worker_c5_bf16, world))
-    net = _net()
+    net = _net("bf16")
     g0, g1 = _c5_bf16_grads(net, 0), _c5_bf16_grads(net, 1)
     for a, b in zip(g0, g1):
         assert not torch.equal(a, b)  # different batches: the average is not trivial

@@ -739,22 +739,17 @@ def test_composite_march_ray_loop(B, S, Ns):
 
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_render_fused_march_equals_unfused(golden, precision):
-    """NeRF.forward with the fused coarse composite + resample (model.FUSED_MARCH) equals the
-    two-kernel path bit for bit, eval and randomized."""
-    from aonerf import model as M
-
+    """NeRF.forward with the fused coarse composite + resample (the model's fused_march) equals
+    the two-kernel path bit for bit, eval and randomized."""
     g = golden("forward_random.npz")
     net = make_nerf(precision)
     rays = rays_of(g)
     outs = {}
     for fused in (True, False):
-        M.FUSED_MARCH = fused
-        try:
-            outs[fused] = [net(rays, False, True, 2.0, 6.0),
-                           net(rays, True, False, 2.0, 6.0, u_coarse=cuda(g["u_coarse"]),
-                               u_fine=cuda(g["u_fine"]))]
-        finally:
-            M.FUSED_MARCH = True
+        net.fused_march = fused
+        outs[fused] = [net(rays, False, True, 2.0, 6.0),
+                       net(rays, True, False, 2.0, 6.0, u_coarse=cuda(g["u_coarse"]),
+                           u_fine=cuda(g["u_fine"]))]
     for a, b in zip(outs[True], outs[False]):
         for la, lb in zip(a, b):
             for x, y in zip(la, lb):

@@ -351,13 +351,10 @@ def test_composite_backward(S, white):
 def fwd_mode(request):
     """Training forward on the fused kernel with activation stores (aon_mlp_fwd_train) or on
     the layer-by-layer GEMMs; backward input gradients in the fused chain (aon_mlp_bwd) or as
-    GEMMs.  Every training test runs on each combination."""
-    from aonerf import train
-
-    old = train.FUSED_FORWARD, train.FUSED_BACKWARD
-    train.FUSED_FORWARD, train.FUSED_BACKWARD = request.param
-    yield request.param
-    train.FUSED_FORWARD, train.FUSED_BACKWARD = old
+    GEMMs.  Every training test runs on each combination (the model's
+    TrainNumerics)."""
+    fwd, bwd = request.param
+    return dict(fused_forward=fwd, fused_backward=bwd)
 
 
 def test_fused_train_forward_activations():
@@ -405,10 +402,12 @@ def test_fused_train_forward_activations():
         assert np.all(((a > 0) == (b > 0)) | (np.abs(b) < tol))
 
 
-def _make_trainable(seed):
+def _make_trainable(seed, **numerics):
+    """A NeRF with the oracle's seed-``seed`` weights; ``numerics``: TrainNumerics fields."""
     from aonerf.model import NeRF
+    from aonerf.numerics import TrainNumerics
 
-    net = NeRF().cuda()
+    net = NeRF(train_numerics=TrainNumerics(**numerics)).cuda()
     net.load_state_dict({k: torch.from_numpy(v) for k, v in W.nerf_state_dict(seed).items()})
     return net
 
@@ -447,7 +446,7 @@ def test_train_step_golden(golden, fwd_mode):
     from aonerf import train
 
     g = golden("train_step.npz")
-    net = _make_trainable(0)
+    net = _make_trainable(0, **fwd_mode)
     assert W.digest(W.nerf_state_dict(0)) == str(g["digest"])
     batch = {k: cuda(g[k]) for k in ("rays_o", "rays_d", "viewdirs", "target")}
     loss, logs = train.training_step(net, batch, True, True, 2.0, 6.0, u_coarse=cuda(g["u_coarse"]),
@@ -481,7 +480,7 @@ def test_train_step_chain(golden, fwd_mode, loss_scale):
     from aonerf import train
 
     g = golden("train_step.npz")
-    net = _make_trainable(0)
+    net = _make_trainable(0, **fwd_mode)
     batch = {k: cuda(g[k]) for k in ("rays_o", "rays_d", "viewdirs", "target")}
     ret = net(batch, True, True, 2.0, 6.0, u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]),
               return_weights=True, return_intermediates=True)
@@ -760,3 +759,52 @@ def test_backward_gradient_scale_invariance(fused):
     for k in (-24, 20):
         for i, (a, b) in enumerate(zip(out[k], out[0])):
             assert torch.equal(a * 2.0 ** -k, b), (k, i, float((a * 2.0 ** -k - b).abs().max()))
+
+
+def _step_state(net, opt, train_mod, batch, u_c, u_f, lib=None):
+    """One training step + Adam: (loss, grads, params after) as host copies."""
+    opt.zero_grad()
+    if lib is None:
+        loss, _ = train_mod.training_step(net, batch, True, True, 2.0, 6.0, u_coarse=u_c, u_fine=u_f)
+    else:
+        loss, _ = train_mod.training_step(net, lib, batch, True, True, 2.0, 6.0, u_coarse=u_c,
+                                          u_fine=u_f)
+    loss.backward()
+    params = list(net.parameters()) + (list(lib.parameters()) if lib is not None else [])
+    grads = [p.grad.detach().cpu().clone() for p in params]
+    opt.step()
+    return loss.detach().cpu(), grads, [p.detach().cpu().clone() for p in params]
+
+
+def test_two_precisions_in_one_process():
+    """Verdict r05 #5 (reentrant, no mutable globals): a bf16 model and an f16x3
+    model of the same weights train in ONE process, their forwards, backward and Adam steps
+    interleaved, and each is bit-equal to its solo run -- the training numerics are the model's
+    own (TrainNumerics), not a module switch."""
+    from aonerf import train
+
+    batch, u_c, u_f = c5_batch(n=512, seed=5)
+    solo = {}
+    for prec in ("f16x3", "bf16"):
+        net = _make_trainable(0, precision=prec)
+        opt = train.Adam(net.parameters())
+        solo[prec] = [_step_state(net, opt, train, batch, u_c, u_f) for _ in range(2)]
+    a, b = _make_trainable(0, precision="f16x3"), _make_trainable(0, precision="bf16")
+    oa, ob = train.Adam(a.parameters()), train.Adam(b.parameters())
+    for step in range(2):
+        oa.zero_grad()
+        ob.zero_grad()
+        la, _ = train.training_step(a, batch, True, True, 2.0, 6.0, u_coarse=u_c, u_fine=u_f)
+        lb, _ = train.training_step(b, batch, True, True, 2.0, 6.0, u_coarse=u_c, u_fine=u_f)
+        (la + lb).backward()  # one backward through both graphs: autograd interleaves them
+        ga = [p.grad.detach().cpu().clone() for p in a.parameters()]
+        gb = [p.grad.detach().cpu().clone() for p in b.parameters()]
+        ob.step()
+        oa.step()
+        for (loss, grads, params), l2, g2, net in ((solo["f16x3"][step], la, ga, a),
+                                                  (solo["bf16"][step], lb, gb, b)):
+            assert torch.equal(loss, l2.detach().cpu())
+            assert all(torch.equal(x, y) for x, y in zip(grads, g2))
+            assert all(torch.equal(x, p.detach().cpu()) for x, p in zip(params, net.parameters()))
+    # and the two precisions really differ
+    assert not torch.equal(solo["f16x3"][0][1][0], solo["bf16"][0][1][0])

@@ -1,5 +1,5 @@
 """The bf16 training mode (BASELINE config C5: "training step fwd+bwd through volume renderer,
-bf16"; train.PRECISION = "bf16"): one bf16 MFMA per product in the fused training forward
+bf16"; NeRF(train_precision="bf16")): one bf16 MFMA per product in the fused training forward
 (aon_mlp_fwd_train_bf16), the fused backward chain (aon_mlp_bwd_bf16) and the weight-gradient
 GEMMs (aon_gemm mma_bf16), activations and gradients kept as bf16; compositing, the loss, their
 backward and Adam stay fp32 on fp32 master weights.
@@ -21,12 +21,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def bf16_mode():
-    from aonerf import train
-
-    old = train.PRECISION
-    train.PRECISION = "bf16"
-    yield
-    train.PRECISION = old
+    """TrainNumerics fields of the bf16 mode (a per-model setting)."""
+    return dict(precision="bf16")
 
 
 def bf16_round(x):
@@ -78,7 +74,7 @@ def test_bf16_train_step_c5(bf16_mode):
     1e-3 here, test_gpu_train.py)."""
     from aonerf import train
 
-    net = _make_trainable(0)
+    net = _make_trainable(0, **bf16_mode)
     batch, u_c, u_f = c5_batch()
     ret = net(batch, True, True, 2.0, 6.0, u_coarse=u_c, u_fine=u_f, return_intermediates=True)
     loss = train.img2mse(ret[1][0], batch["target"]) + train.img2mse(ret[0][0], batch["target"])
@@ -119,15 +115,14 @@ def _trajectory_gpu(precision, batch, steps, lr, bucket=None):
     from aonerf import train
     from aonerf.parallel import GradAllReduce
 
-    old = train.PRECISION
-    train.PRECISION = precision
     if bucket is not None:
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = s.getsockname()[1]
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    sync = None
     try:
-        net = _make_trainable(0)
+        net = _make_trainable(0, precision=precision)
         opt = train.Adam(net.parameters(), lr=lr)
         sync = GradAllReduce(net.parameters(), dtype=bucket) if bucket is not None else None
         out = []
@@ -141,7 +136,8 @@ def _trajectory_gpu(precision, batch, steps, lr, bucket=None):
             out.append(loss.item())
         return np.array(out)
     finally:
-        train.PRECISION = old
+        if sync is not None:
+            sync.close()
         if bucket is not None:
             dist.destroy_process_group()
 

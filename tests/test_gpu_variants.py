@@ -17,8 +17,9 @@ def _ws():
 
     try:
         return L.variant("ws")
-    except ImportError as e:  # build() makes it; a missing build is a failure, not a skip
-        pytest.fail(f"variant library missing: {e}")
+    except OSError as e:  # an A/B build, not made by build(): `make -C csrc variant-ws`
+        pytest.skip(f"variant library not built (make -C articulated-object-nerf_amd/csrc "
+                    f"variant-ws): {e}")
 
 
 def _fwd(handle, name, *args):

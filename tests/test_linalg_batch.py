@@ -117,3 +117,73 @@ def test_immediate_product_reading_pending_output_flushes_first(monkeypatch):
                     ldb=128, b_kc=False, ldc=128)  # reads the pending db
         assert events == [("aon_gemm",), ("flush", 1), ("aon_gemm",)]
     assert events[-1] == ("flush", 0) or events[-1] == ("aon_gemm",)
+
+
+def _log_calls(monkeypatch):
+    events = []
+    monkeypatch.setattr(linalg, "_flush", lambda items: events.append(("flush", len(items))))
+    monkeypatch.setattr(linalg.L, "call", lambda name, *a: events.append(
+        (name, a[1]) if name == "aon_gemm_small_batch" else (name,)))
+    monkeypatch.setattr(linalg.L, "stream", lambda device=None: None)  # (no GPU here)
+    monkeypatch.setattr(linalg, "_workspace", lambda nbytes, device: None)
+    return events
+
+
+def _tiny(C, A, B, **kw):
+    # (1 x n) = (1 x k) (k x n), the latent-term shape; exact_fp32 ones are deferred
+    linalg.gemm(C, A, B, 1, C.shape[1], A.shape[1], lda=A.shape[1], a_kc=True, ldb=B.shape[1],
+                b_kc=False, ldc=C.shape[1], **kw)
+
+
+def test_small_batched_immediate_reader_flushes_first(monkeypatch):
+    """inside small_batched(), an aon_gemm that runs at once (not exact_fp32) and
+    reads a deferred tiny product's output launches after the deferred ones; an independent one
+    does not split the batch."""
+    events = _log_calls(monkeypatch)
+    lat, W = torch.zeros(1, 16), torch.zeros(16, 128)
+    fold = torch.zeros(1, 128)
+    with linalg.small_batched():
+        _tiny(fold, lat, W, exact_fp32=True)
+        _tiny(torch.zeros(1, 128), lat, W, exact_fp32=True)
+        _tiny(torch.zeros(1, 128), lat, W)  # independent, immediate
+        assert events == [("aon_gemm",)]
+        _tiny(torch.zeros(1, 8), fold[:, :16], torch.zeros(16, 8))  # reads the deferred fold
+        assert events == [("aon_gemm",), ("aon_gemm_small_batch", 2), ("aon_gemm",)]
+        _tiny(torch.zeros(1, 128), lat, W, exact_fp32=True)
+    assert events[-1] == ("aon_gemm_small_batch", 1)
+
+
+def test_small_batched_immediate_writer_of_deferred_input_flushes_first(monkeypatch):
+    events = _log_calls(monkeypatch)
+    lat, W = torch.zeros(1, 16), torch.zeros(16, 128)
+    with linalg.small_batched():
+        _tiny(torch.zeros(1, 128), lat, W, exact_fp32=True)
+        _tiny(lat, torch.zeros(1, 4), torch.zeros(4, 16))  # overwrites the deferred input
+        assert events == [("aon_gemm_small_batch", 1), ("aon_gemm",)]
+    assert events == [("aon_gemm_small_batch", 1), ("aon_gemm",)]
+
+
+def test_batched_disabled_defers_nothing(monkeypatch):
+    """batched(enabled=False) (TrainNumerics.batch_dweights False): every product at once."""
+    events = _log_calls(monkeypatch)
+    K = 8192
+    A = torch.zeros(K, 256, dtype=torch.bfloat16)
+    with linalg.batched(False):
+        _dw(torch.zeros(256, 256), A, A)
+        assert events == [("aon_gemm",)]
+    assert events == [("aon_gemm",)]
+
+
+def test_batched_without_128_tiles(monkeypatch):
+    """batched(tiles128=False): the 128-column-tile class runs at once, the 256 x 256 one is
+    deferred; the flag does not leak out of the context."""
+    events = _log_calls(monkeypatch)
+    K = 8192
+    A = torch.zeros(K, 256, dtype=torch.bfloat16)
+    A128 = torch.zeros(K, 128, dtype=torch.bfloat16)
+    with linalg.batched(True, False):
+        _dw(torch.zeros(256, 256), A, A)
+        _dw(torch.zeros(128, 256), A128, A)
+        assert events == [("aon_gemm",)]
+    assert events == [("aon_gemm",), ("flush", 1)]
+    assert linalg._batch128 is True and linalg._batch is None

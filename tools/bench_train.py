@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--max-steps", type=int, default=200000, help="schedule length (run_max_steps)")
     ap.add_argument("--precision", choices=("f16x3", "bf16"), default="f16x3",
-                    help="train.PRECISION of the vanilla step (bf16: C5's bf16 mode)")
+                    help="the model's train_precision (bf16: C5's bf16 mode)")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     args = ap.parse_args()
@@ -53,8 +53,6 @@ def main():
     world, rank, local_rank, dev = launch.init_rank(args.backend, expect_world=args.gpus)
     from aonerf import train
     from aonerf.model import NeRF
-
-    train.PRECISION = args.precision
     from aonerf.parallel import GradAllReduce
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, sapien_focal
@@ -69,13 +67,13 @@ def main():
         from aonerf.model_autodecoder import NeRF_AE_Art
         from aonerf.synthetic import init_code_library
 
-        net = init_like_reference(NeRF_AE_Art()).to(dev)
+        net = init_like_reference(NeRF_AE_Art(train_precision=args.precision)).to(dev)
         lib = init_code_library(CodeLibraryArticulated(
             types.SimpleNamespace(N_max_objs=151, N_obj_code_length=128))).to(dev)
         ids = {"instance_id": torch.tensor([7], device=dev),
                "articulation_id": torch.tensor([3], device=dev)}
     else:
-        net = init_like_reference(NeRF()).to(dev)
+        net = init_like_reference(NeRF(train_precision=args.precision)).to(dev)
     poses = create_spheric_poses(4.0)
     focal = sapien_focal(H)
     rays_all = {k: [] for k in ("rays_o", "rays_d", "viewdirs")}

@@ -1,6 +1,6 @@
 """Diagnostic (GPU): the articulated bf16 training mode's gradient error, by source.
 On C5's batch (tests/test_gpu_train.c5_batch, seed 12, 4,096 rays), for each forward numerics
-(train_art.BF16_TRUNK True: trunk / heads / view branch bf16; False: fp16x3 forward, bf16 stores):
+(art_forward "bf16_trunk": trunk / heads / view branch bf16; "f16x3": fp16x3 forward, bf16 stores):
   (i)  the whole step's gradients vs the fp32 oracle at our t (worst max-rel and cosine per
        group: deformation, trunk, heads + view, latents);
   (ii) the bf16 backward (chain + dW GEMMs) stage-isolated: the fp64 oracle's autograd forced to
@@ -58,10 +58,8 @@ def main():
     batch, u_c, u_f = c5_batch(seed=12)
     batch["instance_id"] = torch.tensor([7], device="cuda")
     batch["articulation_id"] = torch.tensor([3], device="cuda")
-    train_art.PRECISION = "bf16"
     for trunk in (True, False):
-        train_art.BF16_TRUNK = trunk
-        net, lib = _make(0)
+        net, lib = _make(0, precision="bf16", art_forward="bf16_trunk" if trunk else "f16x3")
         latents = lib(batch)
         ret = net(batch, True, True, 2.0, 6.0, latents, u_coarse=u_c, u_fine=u_f,
                   return_intermediates=True)
@@ -84,7 +82,7 @@ def main():
         want.update({f"latent {k}": v.grad for k, v in lat.items()})
         ours = {n: p.grad.cpu() for n, p in net.named_parameters()}
         ours.update({f"latent {k}": v.grad.cpu() for k, v in latents.items()})
-        print(f"BF16_TRUNK={trunk}: loss gpu {loss.item():.7f} fp32 oracle {ref_loss.item():.7f}")
+        print(f"bf16_trunk={trunk}: loss gpu {loss.item():.7f} fp32 oracle {ref_loss.item():.7f}")
         report(f"  (i) whole step vs fp32 oracle:", ours, want)
         # (ii) stage-isolated backward per level
         lat_t = tuple(L_contig(latents[k]) for k in ("density", "color", "articulation"))

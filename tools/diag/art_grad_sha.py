@@ -8,6 +8,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "articulated-object-nerf_amd"), os.path.join(ROOT, "tests")]
+if os.environ.get("AONERF_LIB"):  # an A/B build of the library (tools only)
+    from aonerf import _lib as _aon_lib  # noqa: E402
+
+    _aon_lib.use_library(os.environ["AONERF_LIB"])
 import torch  # noqa: E402
 
 
@@ -19,11 +23,10 @@ def main():
     from test_gpu_train import c5_batch
 
     from aonerf import train_art
-    train_art.PRECISION = args.precision
     batch, u_c, u_f = c5_batch(seed=12)
     batch["instance_id"] = torch.tensor([7], device="cuda")
     batch["articulation_id"] = torch.tensor([3], device="cuda")
-    net, lib = _make(0)
+    net, lib = _make(0, precision=args.precision)
     loss, _ = train_art.training_step(net, lib, batch, True, True, 2.0, 6.0, u_coarse=u_c, u_fine=u_f)
     loss.backward()
     h = hashlib.sha256()

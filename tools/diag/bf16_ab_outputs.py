@@ -14,6 +14,10 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for p in (ROOT, os.path.join(ROOT, "articulated-object-nerf_amd"), os.path.join(ROOT, "tests")):
     sys.path.insert(0, p)
+if os.environ.get("AONERF_LIB"):  # an A/B build of the library (tools only)
+    from aonerf import _lib as _aon_lib  # noqa: E402
+
+    _aon_lib.use_library(os.environ["AONERF_LIB"])
 import torch  # noqa: E402
 
 
@@ -29,8 +33,7 @@ def main():
     out = {"lib": os.environ.get("AONERF_LIB", "default")}
     batch, u_c, u_f = c5_batch(seed=12)
     # vanilla
-    train.PRECISION = "bf16"
-    net = _make_trainable(0)
+    net = _make_trainable(0, precision="bf16")
     ret = net(batch, True, True, 2.0, 6.0, u_coarse=u_c, u_fine=u_f)
     loss = train.img2mse(ret[1][0], batch["target"]) + train.img2mse(ret[0][0], batch["target"])
     loss.backward()
@@ -50,10 +53,8 @@ def main():
     # articulated
     batch["instance_id"] = torch.tensor([7], device="cuda")
     batch["articulation_id"] = torch.tensor([3], device="cuda")
-    train_art.PRECISION = "bf16"
     for trunk in (False, True):
-        train_art.BF16_TRUNK = trunk
-        net, lib = _make(0)
+        net, lib = _make(0, precision="bf16", art_forward="bf16_trunk" if trunk else "f16x3")
         latents = lib(batch)
         ret = net(batch, True, True, 2.0, 6.0, latents, u_coarse=u_c, u_fine=u_f)
         loss = train_art.img2mse(ret[1][0], batch["target"]) + train_art.img2mse(ret[0][0], batch["target"])

@@ -11,6 +11,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "articulated-object-nerf_amd"))
+if os.environ.get("AONERF_LIB"):  # an A/B build of the library (tools only)
+    from aonerf import _lib as _aon_lib  # noqa: E402
+
+    _aon_lib.use_library(os.environ["AONERF_LIB"])
 
 import torch  # noqa: E402
 

@@ -13,6 +13,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "articulated-object-nerf_amd")):
     sys.path.insert(0, p)
+if os.environ.get("AONERF_LIB"):  # an A/B build of the library (tools only)
+    from aonerf import _lib as _aon_lib  # noqa: E402
+
+    _aon_lib.use_library(os.environ["AONERF_LIB"])
 import torch  # noqa: E402
 
 

@@ -18,37 +18,26 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--art", action="store_true")
     ap.add_argument("--precision", default="bf16")
-    ap.add_argument("--trunk", action="store_true", help="articulated bf16: BF16_TRUNK = True")
-    ap.add_argument("--view", action="store_true", help="articulated bf16: BF16_VIEW = True")
-    ap.add_argument("--f16w", type=int, default=None,
-                    help="articulated bf16: F16_WEIGHTS = 0 / 1 (default: the library's setting)")
-    ap.add_argument("--f16x", type=int, default=None,
-                    help="articulated bf16: F16_ACTS = 0 / 1 (default: the library's setting)")
+    ap.add_argument("--art-forward", default="f16_acts",
+                    help="articulated bf16: TrainNumerics.art_forward (f16_acts, f16x3, "
+                         "f16_weights, bf16_view, bf16_trunk)")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--overlap", type=int, default=None,
-                    help="train.OVERLAP_DWEIGHT = 0 / 1 (default: the library's setting)")
+    ap.add_argument("--overlap", type=int, default=0, help="TrainNumerics.overlap_dweight 0 / 1")
     args = ap.parse_args()
     from test_gpu_train import _make_trainable, c5_batch
 
     from aonerf import train, train_art
     batch, _, _ = c5_batch(seed=12)
-    train.PRECISION = args.precision
-    if args.overlap is not None:
-        train.OVERLAP_DWEIGHT = bool(args.overlap)
+    numerics = dict(precision=args.precision, overlap_dweight=bool(args.overlap),
+                    art_forward=args.art_forward)
     if args.art:
         from test_gpu_art_train import _make
-        train_art.PRECISION, train_art.BF16_TRUNK = args.precision, args.trunk
-        train_art.BF16_VIEW = args.view
-        if args.f16w is not None:
-            train_art.F16_WEIGHTS = bool(args.f16w)
-        if args.f16x is not None:
-            train_art.F16_ACTS = bool(args.f16x)
         batch["instance_id"] = torch.tensor([7], device="cuda")
         batch["articulation_id"] = torch.tensor([3], device="cuda")
-        net, lib = _make(0)
+        net, lib = _make(0, **numerics)
         opt = train_art.configure_optimizers(net, lib)
     else:
-        net = _make_trainable(0)
+        net = _make_trainable(0, **numerics)
         opt = train.Adam(net.parameters())
 
     def step():
@@ -67,8 +56,8 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    print(f"{'art' if args.art else 'vanilla'} {args.precision}{' trunk' if args.trunk else ''}: "
-          f"{' overlap' if train.OVERLAP_DWEIGHT else ''}: "
+    print(f"{'art' if args.art else 'vanilla'} {args.precision} {args.art_forward if args.art else ''}"
+          f"{' overlap' if args.overlap else ''}: "
           f"{1e3 * (time.perf_counter() - t0) / args.steps:.3f} ms/step", flush=True)
 
 
