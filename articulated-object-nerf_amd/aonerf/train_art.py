@@ -209,7 +209,7 @@ def _pack_bwd(P, dev, tag="", bf16=False):
 
 def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noise=None,
                          masks=None, bf16=False, enc_bf=None, return_enc_bf=False,
-                         art_forward="f16_acts", timers=None):
+                         art_forward="f16_acts", timers=None, exact_folds=None):
     """_forward_level on the fused kernel (aon_mlp_art_fwd_train): raw (R x 4) and the kept
     activations (tiled, tiles.rows(R) rows each), the sample points (row-major) and pos_enc(x')
     (tiled, (tiles.rows(R), 64), column 63 zero); ``masks`` ((16, tiles.rows(R), 8) int32)
@@ -219,7 +219,8 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     ``enc_bf`` ((tiles.rows(R), 128) bfloat16, allocated when None) receives pos_enc(x') tiled,
     columns 63.. zero: the enc-column weight gradients' operand; ``art_forward``: its forward numerics past
     the deformation MLP, TrainNumerics.art_forward).  enc_rows() converts enc for the all-GEMM
-    backward.  ``timers``: hip events (bench.py)."""
+    backward.  ``timers``: hip events (bench.py); ``exact_folds``: the latent folds on the
+    exact-fp32 path (None: as the mode computes them -- exact in bf16, fp16x3 otherwise)."""
     B, S = t_vals.shape
     R, dev = B * S, t_vals.device
     NR = tiles.rows(R)
@@ -236,7 +237,8 @@ def _forward_level_fused(geo, P, lat, rays_o, rays_d, viewdirs, t_vals, raw, noi
     xyz = torch.empty((R, 3), device=dev)
     mixed, mixed_stream = ART_FORWARD[art_forward] if bf16 else (0, False)
     # (f16_acts, 4, and f16x3, 0, read the plain fp16x3 stream)
-    packed = _pack(geo, P, lat, S, mixed if mixed_stream else 0, exact_folds=bf16)
+    packed = _pack(geo, P, lat, S, mixed if mixed_stream else 0,
+                   exact_folds=bf16 if exact_folds is None else exact_folds)
     e0 = _train._ev(timers)
     args = (L.ptr(packed), L.ptr(rays_o), L.ptr(rays_d), L.ptr(viewdirs), L.ptr(t_vals), B, S,
             L.ptr(noise) if noise is not None else None, L.ptr(hd), L.ptr(h), L.ptr(bot),

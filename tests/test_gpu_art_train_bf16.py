@@ -56,7 +56,8 @@ def _level_inputs(seed=12, n=1024, **numerics):
 @pytest.mark.parametrize("mode", FWD_MODES)
 @pytest.mark.parametrize("level", [0, 1], ids=["coarse", "fine"])
 def test_art_bf16_forward(level, mode):
-    """One level's training forward, f16x3 mode vs bf16 mode at the same t.  The deformation MLP
+    """One level's training forward, f16x3 mode vs bf16 mode at the same t and the same
+    (fp16x3-path) latent folds -- the kernels, not the folds, under test.  The deformation MLP
     is the fp16x3 kernel's in both, so x', pos_enc(x'), the points and the deformation layers'
     ReLU' bits are bit-identical, hd is exactly bf16(f16x3 hd) and the tiled 128-column enc_bf
     exactly bf16(pos_enc(x')) with zero padding.  The fp16x3 forward: everything
@@ -88,7 +89,8 @@ def test_art_bf16_forward(level, mode):
             kept = train_art._forward_level_fused(geo, P, lat, batch["rays_o"], batch["rays_d"],
                                                   batch["viewdirs"], t, raw, None, masks, bf16=bf,
                                                   enc_bf=enc_bf if bf else None,
-                                                  art_forward=ART_FORWARD[mode])
+                                                  art_forward=ART_FORWARD[mode],
+                                                  exact_folds=False)
             out[bf] = (kept, raw, masks)
         torch.cuda.synchronize()
     (xyz32, hd32, enc32, h32, bot32, hv32), raw32, m32 = out[False]

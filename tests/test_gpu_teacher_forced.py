@@ -1,0 +1,155 @@
+"""Teacher-forced per-step training gates (verdict r05 #2), vanilla (LitNeRF.training_step,
+reference model.py:256-282, Adam :386-389) and articulated (LitNeRF_AutoDecoder.training_step,
+model_autodecoder.py:395-477, Adam over the MLPs and the code library :599-601), both training
+precisions.
+
+A free-running trajectory is chaotic (the reference parts from itself under one-ulp
+perturbations, oracle/trajectory.py), so it is printed here as a diagnostic only.  The gate is
+per step: the fp32 reference (torch autograd through the oracle + torch.optim.Adam) runs STEPS
+steps at lr 1e-3 with eval sampling and records each step's starting state (parameters, Adam
+moments, step count); for every step k the GPU model and aonerf's Adam are loaded with exactly
+that state, take ONE training step + Adam step on the GPU's own rays (the oracle gets the same
+rays, copied back), and the GPU's gradient and update are compared per tensor with the
+reference's from the same state.  The reference's self-variance is the same step re-evaluated
+in fp64 from the same state (oracle/trajectory.py).
+
+Gates, fixed before any GPU run from the CPU study tools/diag/tf_study.py (profiles/r06/tf_study/):
+  f16x3 (the parity mode, fp32-class): per tensor, relative L2 distance to the reference's
+    gradient <= max(F16X3_FACTOR x the fp64 re-evaluation's, F16X3_FLOOR), and likewise the
+    update theta' - theta_k at every step after the first.  The factor: the split keeps 22
+    significant bits against fp32's 24 (4x the rounding per product) and sums in another order.
+  bf16 (config C5's bf16 mode, 8 significant bits): per tensor, cosine to the reference's
+    gradient >= BF16_MIN_COS, and likewise the update after the first step.
+  The FIRST step's update is reported, not gated: Adam's first step from zero moments is
+  lr * g / (|g| + eps), i.e. lr * sign(g) wherever |g| >> eps, so any gradient element near zero
+  flips a whole lr -- the reference's own fp64 re-evaluation moves that update by up to 11%
+  (vanilla) / 18% (articulated) of its L2 norm (cosine 0.994 / 0.984).  Its gradient is gated.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import trajectory as T
+
+pytestmark = pytest.mark.gpu
+
+STEPS, LR = 20, 1e-3
+F16X3_FACTOR, F16X3_FLOOR = 8.0, 1e-3
+BF16_MIN_COS = 0.999
+
+
+def _gpu_batch(kind):
+    """The tests' rays as the GPU generates them (aon_frame_rays) and the batch on both sides."""
+    from aonerf.ray_utils import frame_rays
+    from aonerf.render import create_spheric_poses, sapien_focal
+
+    H, Wd = 48, 64
+    rays = frame_rays(torch.as_tensor(create_spheric_poses(4.0)[2]), H, Wd, sapien_focal(H))
+    sel = torch.arange(0, H * Wd, 12 if kind == "vanilla" else 24, device="cuda")
+    cpu = T.make_batch(kind, {k: rays[k][sel].cpu() for k in ("rays_o", "rays_d", "viewdirs")})
+    gpu = {k: (v.cuda() if torch.is_tensor(v) else torch.tensor([v], device="cuda"))
+           for k, v in cpu.items()}
+    return cpu, gpu
+
+
+_REF = {}
+
+
+def _reference(kind):
+    if kind not in _REF:
+        cpu, gpu = _gpu_batch(kind)
+        _REF[kind] = (T.reference_run(kind, cpu, STEPS, LR), gpu)
+    return _REF[kind]
+
+
+def _model(kind, precision):
+    from test_gpu_art_train import _make
+    from test_gpu_train import _make_trainable
+
+    from aonerf import train, train_art
+
+    if kind == "vanilla":
+        net = _make_trainable(0, precision=precision)
+        return net, None, train.Adam(net.parameters(), lr=LR)
+    net, lib = _make(0, precision=precision)
+    return net, lib, train_art.configure_optimizers(net, lib, lr_init=LR)
+
+
+def _named(net, lib):
+    out = dict(net.named_parameters())
+    if lib is not None:
+        out.update({"code_library." + k: v for k, v in lib.named_parameters()})
+    return out
+
+
+def _gpu_step(kind, net, lib, opt, batch, state=None):
+    """One training step + Adam on the GPU (from ``state`` when given: parameters, moments and
+    step count loaded first).  Returns (loss, grads, update) as float64 numpy per name."""
+    from aonerf import train, train_art
+
+    named = _named(net, lib)
+    index = {id(p): i for i, p in enumerate(opt.params)}
+    if state is not None:
+        with torch.no_grad():
+            for n, p in named.items():
+                p.copy_(state["theta"][n].to(p.device))
+                m, v = opt.state[index[id(p)]]
+                m.copy_(state["m"][n].to(p.device))
+                v.copy_(state["v"][n].to(p.device))
+        opt.step_count = state["step"]
+    before = {n: p.detach().double().cpu() for n, p in named.items()}
+    opt.zero_grad()
+    if kind == "vanilla":
+        loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
+    else:
+        loss, _ = train_art.training_step(net, lib, batch, False, True, 2.0, 6.0)
+    loss.backward()
+    grads = {n: p.grad.detach().double().cpu().numpy() for n, p in named.items()}
+    opt.step()
+    delta = {n: (p.detach().double().cpu() - before[n]).numpy() for n, p in named.items()}
+    return float(loss), grads, delta
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "bf16"])
+@pytest.mark.parametrize("kind", ["vanilla", "art"])
+def test_teacher_forced_steps(kind, precision):
+    rec, batch = _reference(kind)
+    net, lib, opt = _model(kind, precision)
+    bad, worst = [], {}
+    for k, r in enumerate(rec):
+        loss, grads, delta = _gpu_step(kind, net, lib, opt, batch, r["state"])
+        checks = [("grad", T.compare(grads, r["grad"]), T.compare(
+            {n: g.numpy() for n, g in r["grad64"].items()}, r["grad"]))]
+        if k > 0:
+            checks.append(("update", T.compare(delta, r["delta"]), T.compare(
+                {n: d.numpy() for n, d in r["delta64"].items()}, r["delta"])))
+        else:
+            c0 = T.compare(delta, r["delta"])
+            print(f"{kind} {precision} step 0 update (reported, not gated): worst rel "
+                  f"{max(v[0] for v in c0.values()):.2e}, min cosine "
+                  f"{min(v[1] for v in c0.values()):.5f}")
+        for what, ours, self_ in checks:
+            for n, (e, cos) in ours.items():
+                if precision == "f16x3":
+                    allow = max(F16X3_FACTOR * self_[n][0], F16X3_FLOOR)
+                    ratio = e / allow
+                    ok = e <= allow
+                else:
+                    ratio = (1 - cos) / (1 - BF16_MIN_COS)
+                    ok = cos >= BF16_MIN_COS
+                key = (what, k)
+                if ratio > worst.get(key, (0.0,))[0]:
+                    worst[key] = (ratio, n, e, cos)
+                if not ok:
+                    bad.append((k, what, n, e, cos))
+        print(f"{kind} {precision} step {k:2d}: loss gpu {loss:.6f} ref {r['loss']:.6f}  "
+              + "  ".join(f"{w} worst {worst[(w, k)][1]} rel {worst[(w, k)][2]:.2e} cos "
+                          f"{worst[(w, k)][3]:.6f} ({worst[(w, k)][0]:.2f} of gate)"
+                          for w in ("grad", "update") if (w, k) in worst))
+    # diagnostic only: the free-running trajectory (chaotic, oracle/trajectory.py)
+    net2, lib2, opt2 = _model(kind, precision)
+    free = [_gpu_step(kind, net2, lib2, opt2, batch)[0] for _ in range(len(rec))]
+    ref = np.array([r["loss"] for r in rec])
+    print(f"{kind} {precision} free-running (diagnostic): max |loss / ref - 1| "
+          f"{np.abs(np.array(free) / ref - 1).max():.2e}; final gpu {free[-1]:.6f} ref {ref[-1]:.6f}")
+    assert not bad, bad[:10]

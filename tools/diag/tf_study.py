@@ -35,9 +35,13 @@ def main():
         e = np.array([v[0] for v in c.values()])
         cs = np.array([v[1] for v in c.values()])
         worst = max(c, key=lambda n: c[n][0])
+        cg = T.compare(r["grad64"], r["grad"])
+        eg = np.array([v[0] for v in cg.values()])
         rows.append({"step": k, "loss": r["loss"], "self_rel_max": float(e.max()),
                      "self_rel_median": float(np.median(e)), "self_cos_min": float(cs.min()),
-                     "worst": worst})
+                     "worst": worst, "grad_self_rel_max": float(eg.max()),
+                     "grad_self_rel_median": float(np.median(eg)),
+                     "grad_worst": max(cg, key=lambda n: cg[n][0])})
         print(json.dumps(rows[-1]), flush=True)
     print(f"{args.kind}: {time.perf_counter() - t0:.1f} s")
     if args.out:
