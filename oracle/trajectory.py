@@ -81,7 +81,7 @@ def one_step(kind, state, batch, lr, dtype=torch.float32):
            "v": {n: opt.state[leaves[n]]["exp_avg_sq"].float().clone() for n in names},
            "step": state["step"] + 1}
     delta = {n: leaves[n].detach().double() - state["theta"][n].double() for n in names}
-    return float(loss), new, delta, grads
+    return float(loss.detach()), new, delta, grads
 
 
 def initial_state(kind, seed=0):
@@ -97,9 +97,12 @@ def reference_run(kind, batch, steps, lr, seed=0, self_variance=True):
     state = initial_state(kind, seed)
     rec = []
     for _ in range(steps):
-        loss, nxt, delta, _ = one_step(kind, state, batch, lr)
-        d64 = one_step(kind, state, batch, lr, torch.float64)[2] if self_variance else None
-        rec.append({"state": state, "loss": loss, "delta": delta, "delta64": d64})
+        loss, nxt, delta, grads = one_step(kind, state, batch, lr)
+        d64 = g64 = None
+        if self_variance:
+            _, _, d64, g64 = one_step(kind, state, batch, lr, torch.float64)
+        rec.append({"state": state, "loss": loss, "delta": delta, "delta64": d64,
+                    "grad": grads, "grad64": g64})
         state = nxt
     return rec
 

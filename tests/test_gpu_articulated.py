@@ -108,16 +108,19 @@ def test_forward_chain_and_golden(art, tag):
         assert err.max() <= ATOL
     # against the reference's own end-to-end outputs: >= 99.5% of rays within 1e-4 and every
     # outlier attributed to the reference's own conditioning (test_gpu_parity.Attribution)
-    from test_gpu_parity import Attribution, assert_e2e
+    from test_gpu_parity import Attribution, assert_e2e, self_floors
 
     att = Attribution(npy(w_c), g[f"{tag}_coarse_weights"], 128, randomized,
                       g[f"{tag}_u_fine"] if randomized else None)
+    uk = dict(randomized=True, u_coarse=g[f"{tag}_u_coarse"], u_fine=g[f"{tag}_u_fine"]) if randomized else {}
+    floors = self_floors(params, rc, [g[f"{tag}_fine_{k}"] for k in ("rgb", "acc", "depth")],
+                         latents=lat_cpu, **uk)
     for j, k, jf in ((0, "rgb", 0), (1, "acc", 1), (2, "depth", 3)):
         err = report(f"art {tag} e2e fine {k}", npy(ret[1][j]), g[f"{tag}_fine_{k}"], ATOL)
         attrib = att.rays(fine[jf].detach().numpy(), g[f"{tag}_fine_{k}"], err,
                           g[f"{tag}_env_fine_{k}"])
         att.explain(f"art {tag} e2e fine {k}", err, attrib)
-        assert_e2e(f"art {tag} e2e fine {k}", err, g[f"{tag}_env_fine_{k}"], attrib)
+        assert_e2e(f"art {tag} e2e fine {k}", err, g[f"{tag}_env_fine_{k}"], attrib, floors[k])
     mse_gpu = float(np.mean((npy(ret[1][0]) - g[f"{tag}_fine_rgb"]) ** 2))
     print(f"art {tag}: mse(gpu fine rgb, reference) = {mse_gpu:.3e}")
 
@@ -155,7 +158,7 @@ def test_full_frame_c3(art):
     link of the chain at 1e-4 against the oracle plus the direct end-to-end gate."""
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, sapien_focal
-    from test_gpu_parity import Attribution, assert_e2e
+    from test_gpu_parity import Attribution, assert_e2e, self_floors
 
     g, net, lat, lat_cpu, params = art
     H, Wd = 240, 320
@@ -195,9 +198,11 @@ def test_full_frame_c3(art):
         ref_ret, inter = O.art_nerf_forward(params, rc, False, True, 2.0, 6.0, lat_cpu,
                                             return_intermediates=True)
     att = Attribution(npy(w_c), inter[0]["weights"].detach().numpy(), 128)
+    floors = self_floors(params, rc, [ref_ret[1][j].detach().numpy() for j in range(3)],
+                         latents=lat_cpu)
     for j, k, jf in ((0, "rgb", 0), (1, "acc", 1), (2, "depth", 3)):
         want = ref_ret[1][j].detach().numpy()
         err = report(f"C3 e2e fine {k}", npy(ret[1][j][sel]), want, ATOL)
         attrib = att.rays(fine[jf].detach().numpy(), want)
         att.explain(f"C3 e2e fine {k}", err, attrib)
-        assert_e2e(f"C3 e2e fine {k}", err, None, attrib)
+        assert_e2e(f"C3 e2e fine {k}", err, None, attrib, floors[k])

@@ -33,21 +33,36 @@ import torch
 
 from oracle import nerf_oracle as O
 from oracle import weights as W
+from oracle import attribution as A
 from oracle.attribution import AMPLIFICATION, Attribution, fine_envelope, plateau_flips  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 
 E2E_ATOL = 1e-4
-E2E_MIN_FRAC = 0.995
-# depth (sum of w t, t in [2, 6]) is the quantity a moved fine sample shifts most: the reference's
-# own re-runs with an fp64 / split-K GEMM (make_golden.py env arrays) keep only 99.22% of the C1
-# frame's depths within 1e-4 of its fp32 run (32 of 4096 rays out, 2 of 480 on frame a), so the
-# depth floor sits below that self-consistency; every outlier must still be attributed
-E2E_MIN_FRAC_DEPTH = 0.985
+# The end-to-end fraction gate is the reference's self-consistency ON THE SAME RAYS (verdict r05
+# #1, oracle/attribution.py): the oracle re-run as another valid fp32 implementation of the
+# reference (its GEMMs split-K, SELF_VARIANT) against the reference's own fp32 output gives the
+# fraction of rays the reference keeps within 1e-4 of itself; ours must keep at least that
+# fraction less max(0.1 pp, 3 binomial standard errors) -- e2e_floor.  At the headline scale
+# (61,440 rays of the 640x480 bench frame, tools/diag/self_frac.py ->
+# profiles/r06/self_frac/) the reference keeps rgb 99.984% / acc 99.982% / depth 99.857%; bench.py
+# measures it on every run beside ours.  (Rounds 2-5 gated depth at a fixed 98.5% taken from the
+# C1 frame's fp64 / split-K re-runs.)
 
 
-def assert_e2e(name, err, env=None, attrib=None):
-    """Direct comparison with the reference's end-to-end output: >= 99.5% of rays within 1e-4,
+def self_floors(params, rays_cpu, ref, **kw):
+    """{quantity: floor} of our fraction within 1e-4 from the reference's self-consistency on
+    ``rays_cpu`` (ref: the reference's fp32 fine (rgb, acc, depth) there; kw: fine_outputs'
+    randomized / u_coarse / u_fine / latents ...)."""
+    sc = A.self_consistency(params, rays_cpu, ref, **kw)
+    print("  reference self-consistency (" + A.SELF_VARIANT + "): " + ", ".join(
+        f"{k} {v['frac'] * 100:.3f}% ({v['outliers']} of {v['n']} out)" for k, v in sc.items()))
+    return {k: A.e2e_floor(v["frac"], v["n"]) for k, v in sc.items()}
+
+
+def assert_e2e(name, err, env=None, attrib=None, floor=None):
+    """Direct comparison with the reference's end-to-end output: the fraction of rays within
+    1e-4 at least ``floor`` (self_floors: the reference's own self-consistency on these rays),
     and every ray outside it attributed (`attrib`: Attribution.rays; module docstring).  `env`
     (the reference's own re-association envelope) is reported for context."""
     err = np.asarray(err)
@@ -64,8 +79,9 @@ def assert_e2e(name, err, env=None, attrib=None):
     if attrib is not None:
         unexplained = np.nonzero(bad & ~attrib)[0]
         assert len(unexplained) == 0, f"{name}: rays {unexplained[:10]} off by > 1e-4, not attributed"
-    floor = E2E_MIN_FRAC_DEPTH if "depth" in name else E2E_MIN_FRAC
-    assert frac >= floor, f"{name}: only {frac * 100:.2f}% of rays within {E2E_ATOL}"
+    assert floor is not None, f"{name}: no self-consistency floor given"
+    print(f"  {name}: {frac * 100:.3f}% within 1e-4, floor {floor * 100:.3f}%")
+    assert frac >= floor, f"{name}: only {frac * 100:.3f}% of rays within {E2E_ATOL} (floor {floor * 100:.3f}%)"
 
 
 def check_chain(net, rays, params, randomized=False, white=True, u_coarse=None, u_fine=None,
@@ -416,9 +432,13 @@ def test_mlp_encoded_api(golden, nerf):
 
 
 # ----------------------------------------------------------------------------- end to end
-def check_levels(ret, g, fine_ref, randomized=False):
+def check_levels(ret, g, fine_ref, randomized=False, white=True):
     att = Attribution(npy(ret[0][3]), g["coarse_weights"], 128, randomized,
                       g["u_fine"] if randomized else None)
+    rc = {k: torch.from_numpy(g[k]) for k in ("rays_o", "rays_d", "viewdirs")}
+    uk = dict(randomized=True, u_coarse=g["u_coarse"], u_fine=g["u_fine"]) if randomized else {}
+    floors = self_floors(O.split_state_dict(W.nerf_state_dict(0)), rc,
+                         [g["fine_rgb"], g["fine_acc"], g["fine_depth"]], white_bkgd=white, **uk)
     for lv, name in enumerate(("coarse", "fine")):
         for j, k in enumerate(("rgb", "acc", "depth", "weights")):
             err = report(f"e2e {name} {k}", npy(ret[lv][j]), g[f"{name}_{k}"], E2E_ATOL)
@@ -427,7 +447,8 @@ def check_levels(ret, g, fine_ref, randomized=False):
             else:
                 attrib = att.rays(fine_ref[k], g[f"fine_{k}"], err, g[f"env_fine_{k}"])
                 att.explain(f"fine {k}", err, attrib)
-                assert_e2e(f"fine {k}", err, g[f"env_fine_{k}"], attrib)
+                assert_e2e(f"fine {k}", err, g[f"env_fine_{k}"], attrib,
+                           floors.get(k, floors["depth"]))
 
 
 def golden_coarse(g):
@@ -447,7 +468,18 @@ def test_forward_randomized_end_to_end(golden, nerf):
     ret, fine_ref = check_chain(nerf, rays_of(g), params, randomized=True, white=False,
                                 u_coarse=cuda(g["u_coarse"]), u_fine=cuda(g["u_fine"]),
                                 coarse_ref=golden_coarse(g), return_ref=True)
-    check_levels(ret, g, fine_ref, randomized=True)
+    check_levels(ret, g, fine_ref, randomized=True, white=False)
+
+
+_FLOORS = {}
+
+
+def _frame_floors(g, tag, params, rc, nc):
+    """self_floors of a golden frame (cached: both precisions gate against the same floors)."""
+    if tag not in _FLOORS:
+        _FLOORS[tag] = self_floors(params, rc, [g[f"{tag}_comp_rgb"], g[f"{tag}_acc"],
+                                                g[f"{tag}_depth"]], num_coarse_samples=nc)
+    return _FLOORS[tag]
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
@@ -469,13 +501,15 @@ def test_render_frame_chunks(golden, precision):
         rc = {k: v.cpu() for k, v in rays.items()}
         w_ref = O.render_level(params, rc, ret[0][4]["t_vals"].cpu(), 0, True)[2]
         att = Attribution(npy(ret[0][3]), w_ref.numpy(), net.num_fine_samples)
+        floors = _frame_floors(g, tag, params, rc, nc)
         out = render_rays(net, rays, chunk, True, 2.0, 6.0)
         for k in ("comp_rgb", "acc", "depth"):
             err = report(f"frame {tag} {k}", npy(out[k]), g[f"{tag}_{k}"], E2E_ATOL)
             attrib = att.rays(fine_ref["rgb" if k == "comp_rgb" else k], g[f"{tag}_{k}"], err,
                               g[f"{tag}_env_{k}"])
             att.explain(f"frame {tag} {k}", err, attrib)
-            assert_e2e(f"frame {tag} {k}", err, g[f"{tag}_env_{k}"], attrib)
+            assert_e2e(f"frame {tag} {k}", err, g[f"{tag}_env_{k}"], attrib,
+                       floors["rgb" if k == "comp_rgb" else k])
         full = render_frame(net, c2w, H, Wd, float(g[f"{tag}_focal"]))
         np.testing.assert_array_equal(npy(full[:, :3]), npy(out["comp_rgb"]))
 
@@ -577,16 +611,20 @@ def test_density_noise(golden, precision, path):
 
 
 # ----------------------------------------------------------------------------- full size
-FULL_FRAME_CHUNK = 3840  # one reference chunk (opt.py:103), the frame's central rows
+FULL_FRAME_CHUNK = 3840  # one reference chunk (opt.py:103)
+FULL_FRAME_CHUNKS = 4    # the central 15,360 rays of the frame (the object region)
 
 
 def test_full_frame_properties(nerf):
-    """640x480x(64c+128f), the bench frame: invariants at full size, then the reference on one
-    whole 3,840-ray chunk of it (the central rows, the object region; verdict r04 #1): every link
-    of the chain gated at 1e-4 on every ray, and the direct end-to-end comparison with every
+    """640x480x(64c+128f), the bench frame: invariants at full size, then the reference on the
+    central 4 x 3,840 rays of it (verdict r04 #1, r05 #1) -- on IDENTICAL rays: the oracle gets
+    the GPU's own rays (a1/a2 are bit-exact against the reference's golden rays,
+    test_ray_generation; the oracle re-run on this box's CPU may round a direction 1 ulp
+    differently through its BLAS, a different input).  Every link of the chain gated at 1e-4 on
+    every ray of one chunk; then the direct end-to-end comparison on all four: the fraction
+    within 1e-4 at least the reference's own self-consistency on these rays (self_floors), every
     outlier attributed -- plateau flip, amplification, or within the reference's own
-    implementation envelope on that ray (GEMM re-association / fp64, sin and exp correctly
-    rounded or +-1 ulp: oracle/attribution.py)."""
+    implementation envelope on that ray (oracle/attribution.py)."""
     from aonerf.ray_utils import frame_rays
     from aonerf.render import create_spheric_poses, render_frame, sapien_focal
 
@@ -604,49 +642,66 @@ def test_full_frame_properties(nerf):
     # bands rendered separately == full frame, bit for bit (per-ray independence)
     half = render_frame(nerf, c2w, H, Wd, f, p0=123 * Wd, n=7 * Wd)
     np.testing.assert_array_equal(npy(half), o[123 * Wd:130 * Wd])
-    # the reference on one whole central chunk of the same frame
-    p0 = (H * Wd) // 2 - FULL_FRAME_CHUNK // 2
-    sel = np.arange(p0, p0 + FULL_FRAME_CHUNK)
+    n = FULL_FRAME_CHUNK * FULL_FRAME_CHUNKS
+    p0 = (H * Wd) // 2 - n // 2
+    sel = np.arange(p0, p0 + n)
+    gr = frame_rays(c2w, H, Wd, f, p0=int(p0), n=n)
+    rc = {k: v.cpu() for k, v in gr.items()}
     dirs = O.get_ray_directions(H, Wd, f)
-    ro, rv, rd = O.get_rays(dirs, c2w[:3, :4], True)
-    params = O.split_state_dict(W.nerf_state_dict(0))
-    sub = {"rays_o": ro[sel], "rays_d": rd[sel], "viewdirs": rv[sel]}
-    ref_all, inter = O.nerf_forward(params, sub, False, True, 2.0, 6.0, return_intermediates=True)
-    ref = ref_all[1]
-    # every link gated at 1e-4 on the same rays, through the GPU's own rays (a1/a2 bit-exact)
-    gr = frame_rays(c2w, H, Wd, f, p0=int(p0), n=FULL_FRAME_CHUNK)
-    # a1/a2 are bit-exact against the reference's golden rays (test_ray_generation); the oracle
-    # re-run on this box's CPU may round a direction 1 ulp differently (its BLAS / vector path),
-    # which the end-to-end attribution below then sees as part of the input
-    dd = np.abs(npy(gr["rays_d"]).astype(np.float64) - rd[sel].numpy())
-    print(f"640x480 chunk rays_d: {int((dd > 0).any(-1).sum())} of {len(sel)} rays differ from "
-          f"this CPU's oracle, max {dd.max():.2e}")
+    _, _, rd_cpu = O.get_rays(dirs, c2w[:3, :4], True)
+    dd = np.abs(npy(gr["rays_d"]).astype(np.float64) - rd_cpu[sel].numpy())
+    print(f"640x480 rays_d: {int((dd > 0).any(-1).sum())} of {n} rays differ from this CPU's "
+          f"torch by <= {dd.max():.2e} (the oracle below takes the GPU's rays)")
     assert dd.max() <= 1.2e-7
-    got_sub, fine_ref = check_chain(nerf, gr, params, return_ref=True)
-    np.testing.assert_array_equal(npy(got_sub[1][0]), o[sel][:, :3])
-    att = Attribution(npy(got_sub[0][3]), inter[0]["weights"].numpy(), nerf.num_fine_samples)
+    params = O.split_state_dict(W.nerf_state_dict(0))
+    # every link at 1e-4 on the first chunk
+    c0 = {k: v[:FULL_FRAME_CHUNK] for k, v in gr.items()}
+    got_c0 = check_chain(nerf, c0, params)
+    np.testing.assert_array_equal(npy(got_c0[1][0]), o[sel[:FULL_FRAME_CHUNK]][:, :3])
+    # the reference end to end on the four chunks, its coarse weights and its self-consistency
+    ref_rgb, ref_acc, ref_depth, w_ref = [], [], [], []
+    with torch.no_grad():
+        for i in range(0, n, FULL_FRAME_CHUNK):
+            r, inter = O.nerf_forward(params, {k: v[i:i + FULL_FRAME_CHUNK] for k, v in rc.items()},
+                                      False, True, 2.0, 6.0, return_intermediates=True)
+            ref_rgb.append(r[1][0])
+            ref_acc.append(r[1][1])
+            ref_depth.append(r[1][2])
+            w_ref.append(inter[0]["weights"])
+    ref = [torch.cat(x).numpy() for x in (ref_rgb, ref_acc, ref_depth)]
+    w_ref = torch.cat(w_ref).numpy()
+    floors = self_floors(params, rc, ref)
+    with torch.no_grad():
+        mine = nerf(gr, False, True, 2.0, 6.0, return_weights=True, return_intermediates=True)
+    for j in range(3):
+        np.testing.assert_array_equal(npy(mine[1][j]), o[sel][:, (slice(0, 3), 4, 3)[j]])
+    att = Attribution(npy(mine[0][3]), w_ref, nerf.num_fine_samples)
     cols = {0: slice(0, 3), 1: 4, 2: 3}
-    errs = {j: report(f"640x480 chunk {k}", o[sel][:, cols[j]], ref[j].numpy(), E2E_ATOL)
+    errs = {j: report(f"640x480 {k}", o[sel][:, cols[j]], ref[j], E2E_ATOL)
             for j, k in ((0, "rgb"), (1, "acc"), (2, "depth"))}
-    bad = np.zeros(len(sel), bool)
+    bad = np.zeros(n, bool)
     for e in errs.values():
         bad |= (e > E2E_ATOL).reshape(len(e), -1).any(-1)
+    rows = np.nonzero(bad)[0]
     env = [None] * 3
-    if bad.any():  # the reference's own implementation envelope, on the outlier rays only
-        rows = np.nonzero(bad)[0]
-        rb = O.get_rays_fma(dirs, c2w[:3, :4])  # a2 as torch computes it in the build container
-        alt = {kk: v[sel][rows] for kk, v in zip(("rays_o", "rays_d", "viewdirs"), rb)}
-        part, worst = fine_envelope(params, {kk: v[rows] for kk, v in sub.items()}, alt_rays=alt)
-        env = [np.zeros((len(sel),) + x.shape[1:]) for x in part]
+    on_ours = [np.zeros((n, 3)), np.zeros(n), np.zeros(n)]
+    if len(rows):  # the reference at our fine samples and its envelope, on the outliers only
+        sub = {k: v[rows] for k, v in rc.items()}
+        t_f = mine[1][4]["t_vals"].cpu()[rows]
+        fr = O.render_level(params, sub, t_f, 1, True)
+        for j, jj in ((0, 0), (1, 1), (2, 3)):
+            on_ours[j][rows] = fr[jj].numpy()
+        part, worst = fine_envelope(params, sub)
+        env = [np.zeros((n,) + x.shape[1:]) for x in part]
         for full, x in zip(env, part):
             full[rows] = x
         print(f"  reference implementation envelope on the {len(rows)} outlier rays (max): " +
-              ", ".join(f"{n}/{q}: {v:.1e}" for (n, q), v in sorted(worst.items())))
+              ", ".join(f"{nm}/{q}: {v:.1e}" for (nm, q), v in sorted(worst.items())))
     for j, k in ((0, "rgb"), (2, "depth"), (1, "acc")):
         err = errs[j]
-        attrib = att.rays(fine_ref[k], ref[j].numpy(), err, env[j])
-        att.explain(f"640x480 chunk {k}", err, attrib)
-        assert_e2e(f"640x480 chunk {k}", err, env[j], attrib)
+        attrib = att.rays(on_ours[j], ref[j], err, env[j])
+        att.explain(f"640x480 {k}", err, attrib)
+        assert_e2e(f"640x480 {k}", err, env[j], attrib, floors[k])
 
 
 # ----------------------------------------------------------------------------- fused march

@@ -4,9 +4,8 @@ bf16"; NeRF(train_precision="bf16")): one bf16 MFMA per product in the fused tra
 GEMMs (aon_gemm mma_bf16), activations and gradients kept as bf16; compositing, the loss, their
 backward and Adam stay fp32 on fp32 master weights.
 
-bf16 carries 8 significant bits, so the gates are bf16-sized, and the mode is judged where a
-training mode is: by its loss trajectory against the f16x3 parity mode and the fp32 oracle
-(torch autograd + torch.optim.Adam on the reference's arithmetic), step for step.
+bf16 carries 8 significant bits, so the gates are bf16-sized; the mode is judged step by step
+against the fp32 reference, teacher-forced, in tests/test_gpu_teacher_forced.py.
 """
 import numpy as np
 import pytest
@@ -103,89 +102,6 @@ def test_bf16_train_step_c5(bf16_mode):
             worst_e, worst_c = max(worst_e, e), min(worst_c, cos)
             assert e < 0.03 and cos > 0.999, (pre + n, e, cos)
     print(f"C5 bf16 grads vs fp32 oracle: worst max-rel {worst_e:.2e}, worst cosine {worst_c:.5f}")
-
-
-def _trajectory_gpu(precision, batch, steps, lr, bucket=None):
-    """bucket: a GradAllReduce dtype -- the step then averages its gradients through a
-    world-1 gloo group's all-reduce in that dtype (the bf16 bucket rounds them to bf16)."""
-    import socket
-
-    import torch.distributed as dist
-
-    from aonerf import train
-    from aonerf.parallel import GradAllReduce
-
-    if bucket is not None:
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            port = s.getsockname()[1]
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
-    sync = None
-    try:
-        net = _make_trainable(0, precision=precision)
-        opt = train.Adam(net.parameters(), lr=lr)
-        sync = GradAllReduce(net.parameters(), dtype=bucket) if bucket is not None else None
-        out = []
-        for _ in range(steps):
-            opt.zero_grad()
-            loss, _ = train.training_step(net, batch, False, True, 2.0, 6.0)
-            loss.backward()
-            if sync is not None:
-                sync()
-            opt.step()
-            out.append(loss.item())
-        return np.array(out)
-    finally:
-        if sync is not None:
-            sync.close()
-        if bucket is not None:
-            dist.destroy_process_group()
-
-
-def test_bf16_loss_trajectory():
-    """30 Adam steps (lr 1e-3, eval sampling so every run sees the same schedule) on a 256-ray
-    batch whose target is another NeRF's render: the f16x3 trajectory tracks the fp32 oracle's
-    (torch autograd + torch.optim.Adam) within 1e-3 relative at every step; the bf16 one within
-    2% at every step (measured <= 0.6%), so it falls as far -- also with its gradients averaged
-    through the bf16 all-reduce bucket (GradAllReduce(dtype=torch.bfloat16))."""
-    from aonerf.ray_utils import frame_rays
-    from aonerf.render import create_spheric_poses, sapien_focal
-
-    H, Wd, steps, lr = 48, 64, 30, 1e-3
-    rays = frame_rays(torch.as_tensor(create_spheric_poses(4.0)[2]), H, Wd, sapien_focal(H))
-    sel = torch.arange(0, H * Wd, 12, device="cuda")
-    batch = {k: v[sel].contiguous() for k, v in rays.items()}
-    teacher = _make_trainable(3).requires_grad_(False)
-    with torch.no_grad():
-        batch["target"] = teacher(batch, False, True, 2.0, 6.0)[1][0].contiguous()
-    # the fp32 oracle trajectory
-    params = [{k: v.requires_grad_(True) for k, v in p.items()}
-              for p in O.split_state_dict(W.nerf_state_dict(0))]
-    flat = [v for p in params for v in p.values()]
-    opt = torch.optim.Adam(flat, lr=lr, betas=(0.9, 0.999))
-    rc = {k: batch[k].cpu() for k in ("rays_o", "rays_d", "viewdirs")}
-    tgt = batch["target"].cpu()
-    ref = []
-    for _ in range(steps):
-        opt.zero_grad()
-        r = O.nerf_forward(params, rc, False, True, 2.0, 6.0)
-        loss = O.img2mse(r[1][0], tgt) + O.img2mse(r[0][0], tgt)
-        loss.backward()
-        opt.step()
-        ref.append(loss.item())
-    ref = np.array(ref)
-    f16 = _trajectory_gpu("f16x3", batch, steps, lr)
-    bf = _trajectory_gpu("bf16", batch, steps, lr)
-    bfar = _trajectory_gpu("bf16", batch, steps, lr, bucket=torch.bfloat16)
-    for i in range(0, steps, 5):
-        print(f"step {i:2d}: oracle {ref[i]:.6f}  f16x3 {f16[i]:.6f}  bf16 {bf[i]:.6f}  "
-              f"bf16 + bf16 all-reduce {bfar[i]:.6f}")
-    print(f"final: oracle {ref[-1]:.6f}  f16x3 {f16[-1]:.6f}  bf16 {bf[-1]:.6f}  "
-          f"bf16 + bf16 all-reduce {bfar[-1]:.6f}")
-    np.testing.assert_allclose(bfar, ref, rtol=2e-2)
-    assert ref[-1] < 0.7 * ref[0], "the oracle run must actually train"
-    np.testing.assert_allclose(f16, ref, rtol=1e-3)
-    np.testing.assert_allclose(bf, ref, rtol=2e-2)
 
 
 @pytest.mark.parametrize("mma_bf16,dtype", [(False, torch.float32), (True, torch.float32),
