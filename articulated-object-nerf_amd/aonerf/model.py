@@ -306,13 +306,14 @@ class NeRF(nn.Module):
             if not return_intermediates:
                 out = out[:4] if return_weights else out[:3]
             ret.append(out)
-        if (not training and self.range_check and self.coarse_mlp.precision == "f16x3"
+        if (not training and self.range_check and self.coarse_mlp.precision.startswith("f16x3")
                 and not torch.cuda.is_current_stream_capturing()
                 and L.range_overflow([self.coarse_mlp._packed, self.fine_mlp._packed])):
             # an activation left the fp16x3 split's range (|x| > 8188): these outputs are
             # invalid -- render again on the exact-fp32 MFMA kernels (no range limit)
             warnings.warn("NeRF: an MLP activation exceeded the fp16x3 range; re-rendered with "
                           "precision='fp32'", RuntimeWarning)
+            prec = self.coarse_mlp.precision
             self.set_precision("fp32")
             if rng is not None:
                 torch.cuda.set_rng_state(rng, dev)
@@ -321,7 +322,7 @@ class NeRF(nn.Module):
                                     u_fine=u_fine, return_weights=return_weights,
                                     return_intermediates=return_intermediates, timers=timers)
             finally:
-                self.set_precision("f16x3")
+                self.set_precision(prec)
         return ret
 
     def _level_t(self, level, o, d, t_prev, w_prev, randomized, near, far, u_coarse, u_fine):

@@ -262,7 +262,7 @@ def _pack(P, dev, tag="", bf16=False):
     """The f16x3 (or bf16) weight stream of one level's parameters, re-packed on every call (the
     optimizer updates the parameters in place behind torch's version counters).  ``tag``: one
     buffer per level (its range-status word must survive until the optimizer step)."""
-    prec = L.PREC_BF16 if bf16 else L.PREC["f16x3"]
+    prec = L.PREC_BF16 if bf16 else L.PREC_F16X3_TRAIN
     buf = _buffer(f"fwd{'bf' if bf16 else ''}{tag}", L.lib().aon_mlp_packed_bytes(prec), dev,
                   guard=not bf16, params=[t for wb in P for t in wb])
     L.call("aon_mlp_pack", L.ctypes.byref(_params_struct(P)), prec, L.ptr(buf), L.stream(dev))

@@ -117,6 +117,59 @@ __device__ __forceinline__ float pos_enc_feature(float x0, float x1, float x2, i
   return sinf(cosine ? __fadd_rn(xb, kHalfPi) : xb);
 }
 
+// sinf for |x| < 2^17, bit for bit: OCML's __ocml_sin_f32 takes this path there on gfx9.5
+// (__ocmlpriv_trigredsmall_f32: a 3-part Cody-Waite reduction by pi/2 in fmas, then
+// __ocmlpriv_sincosred_f32's two minimax polynomials and the quadrant's sign / swap).  Called
+// directly it costs ~20 VALU; sinf itself compiles both reductions (the Payne-Hanek one for
+// |x| >= 2^17 too) and selects, ~150.  Callers guarantee the range (a wave-uniform test, falling
+// back to sinf) -- tools/sin_small_check.hip compares the two on every float below 2^17.
+__device__ __forceinline__ float sin_small(float x) {
+  const float ax = fabsf(x);
+  const float r = __builtin_rintf(__fmul_rn(ax, 0x1.45f306p-1f));  // 2/pi
+  float t = __builtin_fmaf(r, -0x1.921fb4p+0f, ax);
+  t = __builtin_fmaf(r, -0x1.4442d0p-24f, t);
+  t = __builtin_fmaf(r, -0x1.846988p-48f, t);
+  const int q = static_cast<int>(r) & 3;
+  const float t2 = __fmul_rn(t, t);
+  float ps = __builtin_fmaf(t2, -0x1.983304p-13f, 0x1.110388p-7f);
+  ps = __builtin_fmaf(t2, ps, -0x1.55553ap-3f);
+  const float sn = __builtin_fmaf(t, __fmul_rn(t2, ps), t);
+  float pc = __builtin_fmaf(t2, 0x1.aea668p-16f, -0x1.6c9e76p-10f);
+  pc = __builtin_fmaf(t2, pc, 0x1.5557eep-5f);
+  pc = __builtin_fmaf(t2, pc, -0x1.000008p-1f);
+  const float cs = __builtin_fmaf(t2, pc, 1.0f);
+  const uint32_t v = __float_as_uint((q & 1) == 0 ? sn : cs);
+  const uint32_t sgn = (q > 1 ? 0x80000000u : 0u) ^ (__float_as_uint(ax) ^ __float_as_uint(x));
+  return __uint_as_float(v ^ sgn);
+}
+constexpr float kSinSmallMax = 131072.0f;
+
+// pos_enc_feature with sin_small (fast = every |argument| of the caller's wave < 2^17): the
+// same value bit for bit
+__device__ __forceinline__ float pos_enc_feature_fast(float x0, float x1, float x2, int f,
+                                                      int min_deg, int L, bool fast) {
+  if (f < 3) return f == 0 ? x0 : (f == 1 ? x1 : x2);
+  int q = f - 3;
+  bool cosine = false;
+  if (q >= 3 * L) {
+    q -= 3 * L;
+    cosine = true;
+  }
+  if (q >= 3 * L) return 0.f;
+  const int d = q / 3, c = q - 3 * d;
+  const float xc = c == 0 ? x0 : (c == 1 ? x1 : x2);
+  const float xb = xc * __builtin_ldexpf(1.0f, min_deg + d);
+  const float arg = cosine ? __fadd_rn(xb, kHalfPi) : xb;
+  return fast ? sin_small(arg) : sinf(arg);
+}
+// wave-uniform: every pos_enc argument of this wave's points (|x| 2^(max_deg - 1) + pi/2) is
+// below sin_small's range
+__device__ __forceinline__ bool pos_enc_fast_ok(float x0, float x1, float x2, int max_deg) {
+  const float m = fmaxf(fabsf(x0), fmaxf(fabsf(x1), fabsf(x2)));
+  const bool ok = m * __builtin_ldexpf(1.0f, max_deg - 1) + 2.0f < kSinSmallMax;  // (NaN: false)
+  return __builtin_amdgcn_ballot_w64(!ok) == 0;
+}
+
 // Per-call power-of-two scale of a gradient operand from the bits of its max |x| (k_absmax):
 // |x * s| < 2^8 for the largest |x|: s = 2^(8 - e) with max = m 2^e, m in [0.5, 1).  The fp16
 // hi/lo splits of the backward chains and the weight-gradient GEMMs carry gradients at s, so

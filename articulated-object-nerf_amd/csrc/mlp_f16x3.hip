@@ -161,12 +161,22 @@ __global__ __launch_bounds__((GeomH<NCOL, BF>::kThreads), (GeomH<NCOL, BF>::kWav
       const float x0 = __fadd_rn(ro[0], __fmul_rn(tt, rd[0]));
       const float x1 = __fadd_rn(ro[1], __fmul_rn(tt, rd[1]));
       const float x2 = __fadd_rn(ro[2], __fmul_rn(tt, rd[2]));
+      const float v0 = vd[0], v1 = vd[1], v2 = vd[2];
+      auto encode = [&](auto fast) {
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < 2; ++k)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ev[k][e] = pos_enc_feature(x0, x1, x2, 32 * k + 8 * g + e, 0, 10);
+          for (int e = 0; e < 8; ++e)
+            ev[k][e] = pos_enc_feature_fast(x0, x1, x2, 32 * k + 8 * g + e, 0, 10, fast.value);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
+        for (int e = 0; e < 8; ++e)
+          vv[e] = pos_enc_feature_fast(v0, v1, v2, 8 * g + e, 0, 4, fast.value);
+      };
+      // sin_small (aon_common.hpp): the same bits as sinf when the wave's arguments allow it
+      if (pos_enc_fast_ok(x0, x1, x2, 10) && pos_enc_fast_ok(v0, v1, v2, 4))
+        encode(std::true_type{});
+      else
+        encode(std::false_type{});
     } else {
       const float* x = in0 + rr * 63;
       const float* cd = in1 + ray * 27;
