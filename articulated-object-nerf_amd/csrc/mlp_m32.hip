@@ -155,7 +155,6 @@ template <bool RELU, int NO>
 __device__ __forceinline__ void epi_pair(int q, const f16v& acc, lds_float* bias_t,
                                          Frag<NO>& out, int t) {
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
   // rows 8 (q / 2) + 4 s + 2 (q % 2) + e: bias_t already points at this lane half's 4 s
   const float b0 = bias_t[8 * (q >> 1) + 2 * (q & 1)];
   const float b1 = bias_t[8 * (q >> 1) + 2 * (q & 1) + 1];
@@ -165,19 +164,23 @@ __device__ __forceinline__ void epi_pair(int q, const f16v& acc, lds_float* bias
     v0 = fmaxf(v0, 0.0f);
     v1 = fmaxf(v1, 0.0f);
   }
-  const h2 hp = {static_cast<_Float16>(v0), static_cast<_Float16>(v1)};
-  const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
+  // the packed conversions as written instructions: left to itself hipcc rebuilt the pair a
+  // second time (two v_cvt_f16_f32 + v_perm) for the range test, or widened the fp16 halves
+  // with separate conversions instead of v_fma_mix_f32 (each asm block costs one s_nop 0)
+  uint32_t hu, lu;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hu) : "v"(v0), "v"(v1));
   out.m16 = mlp::pk_max_i16(out.m16, RELU ? hu : (hu & 0x7FFF7FFFu));
   asm("" : "+v"(out.m16));
   float d0, d1;
-  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(hu), "v"(v0));
-  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(hu), "v"(v1));
-  const h2 lp = {static_cast<_Float16>(d0), static_cast<_Float16>(d1)};
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %3, %1, -1.0, %4 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_cvt_pk_f16_f32 %5, %0, %3"
+      : "=&v"(d0), "+v"(hu), "+v"(v0), "=&v"(d1), "+v"(v1), "=&v"(lu));
   const int kk = 2 * t + (q >> 2);
   u4 wh = __builtin_bit_cast(u4, out.hi[kk]);
   u4 wl = __builtin_bit_cast(u4, out.lo[kk]);
   wh[q & 3] = hu;
-  wl[q & 3] = __builtin_bit_cast(uint32_t, lp);
+  wl[q & 3] = lu;
   out.hi[kk] = __builtin_bit_cast(h8, wh);
   out.lo[kk] = __builtin_bit_cast(h8, wl);
 }

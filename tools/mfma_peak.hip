@@ -3,12 +3,15 @@
 // held clock depends on operand toggling: MI355X_MICROARCH.md 'DVFS give-back'), 8 independent
 // accumulators per wave, every CU filled.  kind 0: v_mfma_f32_16x16x32_f16 (the f16x3 MLP's
 // instruction); kind 1: v_mfma_f32_16x16x4_f32 (the fp32 path's); kind 2: the f16x3 pattern,
-// three dependent MFMAs into one accumulator per step.  Returns TFLOP/s of the issued MFMAs.
+// three dependent MFMAs into one accumulator per step; kind 3: v_mfma_f32_32x32x16_f16 (the
+// 32x32 render MLP's, mlp_m32.hip); kind 4: its f16x3 triple.  Returns TFLOP/s of the issued
+// MFMAs.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ uint32_t mix(uint32_t x) {
   x ^= x >> 16;
@@ -20,6 +23,51 @@ __device__ __forceinline__ uint32_t mix(uint32_t x) {
 }
 
 __device__ __forceinline__ float rnd(uint32_t s) { return (mix(s) >> 8) * (1.0f / 16777216.0f) - 0.5f; }
+
+// 32x32x16: 4 independent 16-register accumulators per wave
+template <int KIND>
+__global__ __launch_bounds__(256) void k_mfma_loop32(int iters, float* out, uint64_t* stamps) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  uint64_t c0 = 0, r0 = 0;
+  if (blockIdx.x == gridDim.x / 2 && threadIdx.x == 0) {
+    c0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  f16v acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    acc[i] = f16v{};
+    acc[i][0] = rnd(t * 8 + i);
+  }
+  h8 a[2], b[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[i][e] = static_cast<_Float16>(rnd(t * 64 + 16 * i + e));
+      b[i][e] = static_cast<_Float16>(rnd(t * 64 + 32 + 16 * i + e));
+    }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc[i], 0, 0, 0);
+      if (KIND == 4) {
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], acc[i], 0, 0, 0);
+      }
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += acc[i][r];
+  out[t] = s;
+  if (blockIdx.x == gridDim.x / 2 && threadIdx.x == 0) {
+    stamps[0] = __builtin_amdgcn_s_memtime() - c0;
+    stamps[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
 
 template <int KIND>
 __global__ __launch_bounds__(256) void k_mfma_loop(int iters, float* out, uint64_t* stamps) {
@@ -88,7 +136,9 @@ extern "C" double aon_mfma_peak(int kind, int iters, int blocks, float* out, uin
   auto launch = [&]() {
     if (kind == 0) hipLaunchKernelGGL(k_mfma_loop<0>, blocks, 256, 0, 0, iters, out, stamps);
     else if (kind == 1) hipLaunchKernelGGL(k_mfma_loop<1>, blocks, 256, 0, 0, iters, out, stamps);
-    else hipLaunchKernelGGL(k_mfma_loop<2>, blocks, 256, 0, 0, iters, out, stamps);
+    else if (kind == 2) hipLaunchKernelGGL(k_mfma_loop<2>, blocks, 256, 0, 0, iters, out, stamps);
+    else if (kind == 3) hipLaunchKernelGGL(k_mfma_loop32<3>, blocks, 256, 0, 0, iters, out, stamps);
+    else hipLaunchKernelGGL(k_mfma_loop32<4>, blocks, 256, 0, 0, iters, out, stamps);
   };
   for (int w = 0; w < 3; ++w) launch();  // warm-up (and let the clock settle)
   (void)hipEventRecord(e0, 0);
@@ -104,8 +154,9 @@ extern "C" double aon_mfma_peak(int kind, int iters, int blocks, float* out, uin
   uint64_t st[2] = {0, 0};
   (void)hipMemcpy(st, stamps, sizeof(st), hipMemcpyDeviceToHost);
   *clock_ghz = st[1] ? (double)st[0] / (double)st[1] * 0.1 : 0.0;
-  const double per_mfma = kind == 1 ? 2.0 * 16 * 16 * 4 : 2.0 * 16 * 16 * 32;
-  const double mfmas = (double)blocks * 4 /* waves */ * iters * (kind == 2 ? 24 : 8) * reps;
+  const double per_mfma = kind == 1 ? 2.0 * 16 * 16 * 4 : kind >= 3 ? 2.0 * 32 * 32 * 16 : 2.0 * 16 * 16 * 32;
+  const double per_iter = kind == 2 ? 24 : kind == 3 ? 4 : kind == 4 ? 12 : 8;
+  const double mfmas = (double)blocks * 4 /* waves */ * iters * per_iter * reps;
   return mfmas * per_mfma / (ms * 1e-3) / 1e12;
 }
 

@@ -33,7 +33,8 @@ def main():
     stamps = torch.zeros(2, dtype=torch.int64, device="cuda")
     res = {"cus": cus, "blocks": blocks, "iters": args.iters}
     for name, kind, iters in (("f16_16x16x32", 0, args.iters), ("f32_16x16x4", 1, args.iters // 4),
-                              ("f16x3_triple_16x16x32", 2, args.iters // 3)):
+                              ("f16x3_triple_16x16x32", 2, args.iters // 3),
+                              ("f16_32x32x16", 3, args.iters), ("f16x3_triple_32x32x16", 4, args.iters // 3)):
         clk = ctypes.c_double(0.0)
         res[name + "_tflops"] = lib.aon_mfma_peak(kind, iters, blocks, ctypes.c_void_p(out.data_ptr()),
                                                   ctypes.c_void_p(stamps.data_ptr()), ctypes.byref(clk))
