@@ -16,9 +16,8 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libaonerf.so")
 
 c_i64, c_int, c_float, c_size, vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 
-# render precisions (aon_mlp_fwd): exact fp32 MFMA, the fp16x3 split on 16x16x32 MFMAs, and the
-# same split on 32x32x16 MFMAs (ABI 12, mlp_m32.hip)
-PREC = {"fp32": 0, "f16x3": 1, "f16x3_m32": 3}
+# render precisions (aon_mlp_fwd): exact fp32 MFMA, the fp16x3 split on 16x16x32 MFMAs
+PREC = {"fp32": 0, "f16x3": 1}
 PREC_F16X3_TRAIN = 1  # the training forwards' fp16x3 stream (aon_mlp_fwd_train)
 PREC_BF16 = 2  # the training step's bf16 mode (aon_mlp_fwd_train_bf16, aon_mlp_bwd_bf16)
 ACT_NONE, ACT_VANILLA, ACT_ARTIC = 0, 1, 2
@@ -225,7 +224,7 @@ _SIGNATURES = {
 _lib = None
 
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 def _load(path):

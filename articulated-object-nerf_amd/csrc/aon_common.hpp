@@ -77,11 +77,41 @@ __device__ __forceinline__ float nan_to_num(float x, float nan_val) {
   return x;
 }
 
+// exp as torch's vectorised CPU kernels evaluate it inside sigmoid and softplus: SLEEF
+// 3.x xexpf (the u10 variant; ATen's Vectorized<float>::exp), restated from its published
+// algorithm -- round(d/ln2) with a two-part Cody-Waite reduction, a degree-6 Horner
+// polynomial and a split 2^q scaling.  With it, 1/(1 + exp_sleef(-x)) reproduces
+// torch.sigmoid bit for bit (checked on 4M values, tests/test_transcendentals.py).
+__host__ __device__ inline float exp_sleef(float d) {  // (built with -ffp-contract=off)
+  const int q = (int)__builtin_rintf(d * 1.442695040888963407359924681f);
+  float s = __builtin_fmaf((float)q, -0.693145751953125f, d);
+  s = __builtin_fmaf((float)q, -1.428606765330187045e-06f, s);
+  float u = 0.000198527617612853646278381f;
+  u = __builtin_fmaf(u, s, 0.00139304355252534151077271f);
+  u = __builtin_fmaf(u, s, 0.00833336077630519866943359f);
+  u = __builtin_fmaf(u, s, 0.0416664853692054748535156f);
+  u = __builtin_fmaf(u, s, 0.166666671633720397949219f);
+  u = __builtin_fmaf(u, s, 0.5f);
+  u = 1.0f + __builtin_fmaf(s * s, u, s);
+  const int q1 = q >> 1, q2 = q - q1;  // 2^q as two factors so q = 128 does not overflow
+  u = (u * __builtin_bit_cast(float, (q1 + 127) << 23)) * __builtin_bit_cast(float, (q2 + 127) << 23);
+  if (d < -104.0f) u = 0.0f;
+  if (d > 100.0f) u = __builtin_inff();
+  return d != d ? d : u;
+}
+
+// exp as torch.exp evaluates it on CPU for the alpha of volumetric_rendering (MKL's
+// high-accuracy vsExp: correctly rounded in ~99% of elements): the correctly rounded fp32
+// exp, through fp64 (the double rounding is off only within 2^-29 of a midpoint)
+__host__ __device__ inline float exp_cr(float x) { return (float)::exp((double)x); }
+
 // rgb_activation / sigma_activation (reference model.py:142-143, 186-187; articulated:
-// model_autodecoder.py:265, 323), shared by the MLP epilogue and the compositor
+// model_autodecoder.py:265, 323), shared by the MLP epilogue and the compositor.
+// torch.sigmoid on CPU is 1/(1 + exp(-x)) with SLEEF's exp; F.softplus is
+// log1p(exp(x)) with SLEEF's exp and log1p (here the device log1pf).
 __device__ __forceinline__ float act_rgb(float x, int act) {
   if (act == AON_ACT_NONE) return x;
-  const float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-x)));
+  const float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, exp_sleef(-x)));
   return act == AON_ACT_ARTIC ? __fsub_rn(__fmul_rn(s, 1.002f), 0.001f) : s;
 }
 
@@ -90,7 +120,50 @@ __device__ __forceinline__ float act_sigma(float x, int act) {
   if (act == AON_ACT_VANILLA) return fmaxf(x, 0.0f);
   // softplus(x - 1) with torch's threshold 20 (model_autodecoder.py:323)
   const float z = __fsub_rn(x, 1.0f);
-  return z > 20.0f ? z : log1pf(expf(z));
+  return z > 20.0f ? z : log1pf(exp_sleef(z));
+}
+
+// sin / cos of an fp32 argument, correctly rounded: evaluated in fp64 and rounded once.  torch's
+// CPU sin / cos (the reference's pos_enc, helper.py:139, and its autograd's cos) are correctly
+// rounded in ~95% of elements; the device sinf (OCML) in ~79% -- measured on 12M arguments, and
+// this evaluation equals float(sin(double(x))) on all of them (tests/test_transcendentals.py
+// runs the same arithmetic on the host, tests/test_gpu_transcendentals.py on the device).
+// Cody-Waite reduction by pi/2 in three fmas (fdlibm's pio2_1 / pio2_2 are 33-bit: r * part is
+// exact while |r| < 2^20, i.e. |x| < kSinCrMax), then fdlibm's __kernel_sin / __kernel_cos
+// minimax polynomials on [-pi/4, pi/4] (~2^-55 relative; the single rounding to fp32 is
+// then off only within 2^-30 of a rounding midpoint).  qoff = 1 gives cos (sin(x + pi/2)).
+constexpr float kSinCrMax = 1048576.0f;
+__host__ __device__ inline float sincos_cr(float xf, int qoff) {
+  const double x = xf;
+  const double r = __builtin_rint(x * 6.36619772367581382433e-01);
+  double t = __builtin_fma(-r, 1.57079632673412561417e+00, x);
+  t = __builtin_fma(-r, 6.07710050630396597660e-11, t);
+  t = __builtin_fma(-r, 2.02226624879595063154e-21, t);
+  const int q = (static_cast<int>(r) + qoff) & 3;
+  // one Horner chain for both: sin(t) = t (1 + z (S1 + .. + z S6)), cos(t) = 1 + z (-1/2 + z (C1
+  // + .. + z C6)), z = t^2 -- the coefficients selected per lane (the two chains' registers
+  // would both stay live across the unrolled features)
+  const bool odd = q & 1;
+  const double z = t * t;
+  double p = odd ? -1.13596475577881948265e-11 : 0.0;
+  p = __builtin_fma(z, p, odd ? 2.08757232129817482790e-09 : 1.58969099521155010221e-10);
+  p = __builtin_fma(z, p, odd ? -2.75573143513906633035e-07 : -2.50507602534068634195e-08);
+  p = __builtin_fma(z, p, odd ? 2.48015872894767294178e-05 : 2.75573137070700676789e-06);
+  p = __builtin_fma(z, p, odd ? -1.38888888888741095749e-03 : -1.98412698298579493134e-04);
+  p = __builtin_fma(z, p, odd ? 4.16666666666666019037e-02 : 8.33333333332248946124e-03);
+  p = __builtin_fma(z, p, odd ? -0.5 : -1.66666666666666324348e-01);
+  p = __builtin_fma(z, p, 1.0);
+  const double v = odd ? p : t * p;
+  return static_cast<float>((q & 2) ? -v : v);
+}
+// any argument (past kSinCrMax: OCML's fp64 sin / cos, also rounded once)
+__device__ __forceinline__ float sin_cr(float x) {
+  if (__builtin_expect(fabsf(x) < kSinCrMax, 1)) return sincos_cr(x, 0);
+  return static_cast<float>(__ocml_sin_f64(static_cast<double>(x)));
+}
+__device__ __forceinline__ float cos_cr(float x) {
+  if (__builtin_expect(fabsf(x) < kSinCrMax, 1)) return sincos_cr(x, 1);
+  return static_cast<float>(__ocml_cos_f64(static_cast<double>(x)));
 }
 
 // fp32(0.5 * pi) as torch adds it to an fp32 tensor (reference helper.py:139)
@@ -114,38 +187,11 @@ __device__ __forceinline__ float pos_enc_feature(float x0, float x1, float x2, i
   const int d = q / 3, c = q - 3 * d;
   const float xc = c == 0 ? x0 : (c == 1 ? x1 : x2);
   const float xb = xc * __builtin_ldexpf(1.0f, min_deg + d);  // exact power-of-two scaling
-  return sinf(cosine ? __fadd_rn(xb, kHalfPi) : xb);
+  return sin_cr(cosine ? __fadd_rn(xb, kHalfPi) : xb);
 }
 
-// sinf for |x| < 2^17, bit for bit: OCML's __ocml_sin_f32 takes this path there on gfx9.5
-// (__ocmlpriv_trigredsmall_f32: a 3-part Cody-Waite reduction by pi/2 in fmas, then
-// __ocmlpriv_sincosred_f32's two minimax polynomials and the quadrant's sign / swap).  Called
-// directly it costs ~20 VALU; sinf itself compiles both reductions (the Payne-Hanek one for
-// |x| >= 2^17 too) and selects, ~150.  Callers guarantee the range (a wave-uniform test, falling
-// back to sinf) -- tools/sin_small_check.hip compares the two on every float below 2^17.
-__device__ __forceinline__ float sin_small(float x) {
-  const float ax = fabsf(x);
-  const float r = __builtin_rintf(__fmul_rn(ax, 0x1.45f306p-1f));  // 2/pi
-  float t = __builtin_fmaf(r, -0x1.921fb4p+0f, ax);
-  t = __builtin_fmaf(r, -0x1.4442d0p-24f, t);
-  t = __builtin_fmaf(r, -0x1.846988p-48f, t);
-  const int q = static_cast<int>(r) & 3;
-  const float t2 = __fmul_rn(t, t);
-  float ps = __builtin_fmaf(t2, -0x1.983304p-13f, 0x1.110388p-7f);
-  ps = __builtin_fmaf(t2, ps, -0x1.55553ap-3f);
-  const float sn = __builtin_fmaf(t, __fmul_rn(t2, ps), t);
-  float pc = __builtin_fmaf(t2, 0x1.aea668p-16f, -0x1.6c9e76p-10f);
-  pc = __builtin_fmaf(t2, pc, 0x1.5557eep-5f);
-  pc = __builtin_fmaf(t2, pc, -0x1.000008p-1f);
-  const float cs = __builtin_fmaf(t2, pc, 1.0f);
-  const uint32_t v = __float_as_uint((q & 1) == 0 ? sn : cs);
-  const uint32_t sgn = (q > 1 ? 0x80000000u : 0u) ^ (__float_as_uint(ax) ^ __float_as_uint(x));
-  return __uint_as_float(v ^ sgn);
-}
-constexpr float kSinSmallMax = 131072.0f;
-
-// pos_enc_feature with sin_small (fast = every |argument| of the caller's wave < 2^17): the
-// same value bit for bit
+// pos_enc_feature with the range test hoisted (fast = every |argument| of the caller's wave
+// below kSinCrMax: no per-value branch): the same value bit for bit
 __device__ __forceinline__ float pos_enc_feature_fast(float x0, float x1, float x2, int f,
                                                       int min_deg, int L, bool fast) {
   if (f < 3) return f == 0 ? x0 : (f == 1 ? x1 : x2);
@@ -160,13 +206,13 @@ __device__ __forceinline__ float pos_enc_feature_fast(float x0, float x1, float 
   const float xc = c == 0 ? x0 : (c == 1 ? x1 : x2);
   const float xb = xc * __builtin_ldexpf(1.0f, min_deg + d);
   const float arg = cosine ? __fadd_rn(xb, kHalfPi) : xb;
-  return fast ? sin_small(arg) : sinf(arg);
+  return fast ? sincos_cr(arg, 0) : sin_cr(arg);
 }
 // wave-uniform: every pos_enc argument of this wave's points (|x| 2^(max_deg - 1) + pi/2) is
-// below sin_small's range
+// below kSinCrMax
 __device__ __forceinline__ bool pos_enc_fast_ok(float x0, float x1, float x2, int max_deg) {
   const float m = fmaxf(fabsf(x0), fmaxf(fabsf(x1), fabsf(x2)));
-  const bool ok = m * __builtin_ldexpf(1.0f, max_deg - 1) + 2.0f < kSinSmallMax;  // (NaN: false)
+  const bool ok = m * __builtin_ldexpf(1.0f, max_deg - 1) + 2.0f < kSinCrMax;  // (NaN: false)
   return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 

@@ -26,8 +26,8 @@ __global__ void k_pos_enc_bwd(const float* __restrict__ x, int64_t ldx,
     for (int d = 0; d < L; ++d) {
       const float s = __builtin_ldexpf(1.0f, min_deg + d);
       const float xb = __fmul_rn(xc, s);  // exact (power of two)
-      const float g_xb = __fadd_rn(__fmul_rn(gr[3 + 3 * d + c], cosf(xb)),
-                                   __fmul_rn(gr[3 + 3 * L + 3 * d + c], cosf(__fadd_rn(xb, kHalfPi))));
+      const float g_xb = __fadd_rn(__fmul_rn(gr[3 + 3 * d + c], cos_cr(xb)),
+                                   __fmul_rn(gr[3 + 3 * L + 3 * d + c], cos_cr(__fadd_rn(xb, kHalfPi))));
       acc = __fadd_rn(acc, __fmul_rn(g_xb, s));
     }
     float v = __fadd_rn(gr[c], acc);

@@ -62,7 +62,7 @@ __device__ __forceinline__ void composite_ray(const float (&tt)[NB], const f4 (&
     if (valid) {
       const float dist = (i + 1 < S) ? __fsub_rn(tn, ti) : 1e10f;
       const float sgm = act_sigma(raw[b].w, act);
-      alpha = __fsub_rn(1.0f, expf(__fmul_rn(-sgm, __fmul_rn(dist, dnorm))));
+      alpha = __fsub_rn(1.0f, exp_cr(__fmul_rn(-sgm, __fmul_rn(dist, dnorm))));
       if (i + 1 < S) f = (double)__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f);
     }
     const double incl = wave_incl_prod(f);

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(64 * kWaves, AON_MARCH_ROWS_OCC) void k_march_rows(
     for (int m = 0; m < 5; ++m) {
       const float dist = m < 4 ? __fsub_rn(tn[m], tt[m]) : 1e10f;
       const float sgm = act_sigma(rw[m].w, act);
-      alpha[m] = __fsub_rn(1.0f, expf(__fmul_rn(-sgm, __fmul_rn(dist, dnorm))));
+      alpha[m] = __fsub_rn(1.0f, exp_cr(__fmul_rn(-sgm, __fmul_rn(dist, dnorm))));
       if (m < 4) f[m] = (double)__fadd_rn(__fsub_rn(1.0f, alpha[m]), 1e-10f);
     }
     // ---- transmittance: wave_incl_prod's association over samples 0..63 (block m = row m of

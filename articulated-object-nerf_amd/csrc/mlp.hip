@@ -257,7 +257,6 @@ extern "C" size_t aon_mlp_packed_bytes(int precision) {
   // (bf16: bf16 weights in the hi blocks)
   if (precision == AON_PREC_FP32 || precision == AON_PREC_F16X3 || precision == AON_PREC_BF16)
     return kPackedBytesF32;
-  if (precision == AON_PREC_F16X3_M32) return packed_bytes_m32();
   return 0;
 }
 
@@ -283,24 +282,10 @@ extern "C" int aon_mlp_pack(const aon_mlp_params* prm, int precision, void* pack
                             aon_stream_t stream) {
   AON_REQUIRE(prm && packed, "null pointer");
   AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3 ||
-                  precision == AON_PREC_BF16 || precision == AON_PREC_F16X3_M32,
+                  precision == AON_PREC_BF16,
               "unsupported precision");
   AON_REQUIRE(aligned16(packed), "packed buffer must be 16-byte aligned");
   if (check_mlp_params(prm, __func__)) return -1;
-  if (precision == AON_PREC_F16X3_M32) {
-    const float* w[kNumLayers];
-    const float* b[kNumLayers];
-    for (int i = 0; i < 8; ++i) {
-      w[i] = prm->pts_w[i];
-      b[i] = prm->pts_b[i];
-    }
-    w[LDEN] = prm->density_w;    b[LDEN] = prm->density_b;
-    w[LBOT] = prm->bottleneck_w; b[LBOT] = prm->bottleneck_b;
-    w[LVIEW] = prm->views_w;     b[LVIEW] = prm->views_b;
-    w[LRGB] = prm->rgb_w;        b[LRGB] = prm->rgb_b;
-    for (int i = 0; i < kNumLayers; ++i) AON_REQUIRE(w[i] && b[i], "null layer parameter");
-    return pack_m32(w, b, packed, (hipStream_t)stream);
-  }
   PackArgs a;
   for (int i = 0; i < 8; ++i) {
     a.w[i] = prm->pts_w[i];
@@ -330,8 +315,7 @@ static int mlp_launch(int mode, const void* packed, int precision, const float* 
                       const float* a1, const float* a2, const float* a3, int64_t B, int S,
                       int act, float* raw, aon_stream_t stream) {
   AON_REQUIRE(packed && raw && a0 && a1, "null pointer");
-  AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3 ||
-                  precision == AON_PREC_F16X3_M32,
+  AON_REQUIRE(precision == AON_PREC_FP32 || precision == AON_PREC_F16X3,
               "unsupported precision (AON_PREC_BF16 is the training forward's: aon_mlp_fwd_train_bf16)");
   AON_REQUIRE(B >= 0 && S >= 1, "bad shape");
   AON_REQUIRE(act >= AON_ACT_NONE && act <= AON_ACT_ARTIC, "bad activation");
@@ -343,8 +327,6 @@ static int mlp_launch(int mode, const void* packed, int precision, const float* 
   if (precision == AON_PREC_F16X3 && mode == 0)
     return launch_ws_f16x3(packed, a0, a1, a2, a3, B, S, act, raw, (hipStream_t)stream);
 #endif
-  if (precision == AON_PREC_F16X3_M32)
-    return launch_m32(mode, packed, a0, a1, a2, a3, B, S, act, raw, (hipStream_t)stream);
   if (precision == AON_PREC_F16X3)
     return launch_f16x3(mode, AON_F16X3_NCOL, packed, a0, a1, a2, a3, B, S, act, raw,
                         (hipStream_t)stream);

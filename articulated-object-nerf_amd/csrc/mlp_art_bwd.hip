@@ -81,7 +81,7 @@ struct EncBwd {
       const float sc = __builtin_ldexpf(1.0f, d);
       const float xc = comp == 0 ? x0 : (comp == 1 ? x1 : x2);
       const float xb = __fmul_rn(xc, sc);  // exact
-      a = __fmul_rn(__fmul_rn(tot, cosf(cosine ? __fadd_rn(xb, kHalfPi) : xb)), sc);
+      a = __fmul_rn(__fmul_rn(tot, cos_cr(cosine ? __fadd_rn(xb, kHalfPi) : xb)), sc);
     } else {
       comp = 3;  // padding row
     }
@@ -135,7 +135,7 @@ struct EncBwdReg {
       const float sc = __builtin_ldexpf(1.0f, d);
       const float xc = comp == 0 ? x[c][0] : (comp == 1 ? x[c][1] : x[c][2]);
       const float xb = __fmul_rn(xc, sc);  // exact
-      a = __fmul_rn(__fmul_rn(tot, cosf(cosine ? __fadd_rn(xb, kHalfPi) : xb)), sc);
+      a = __fmul_rn(__fmul_rn(tot, cos_cr(cosine ? __fadd_rn(xb, kHalfPi) : xb)), sc);
     } else {
       comp = 3;  // padding row
     }

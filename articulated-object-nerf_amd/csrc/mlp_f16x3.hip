@@ -167,12 +167,17 @@ __global__ __launch_bounds__((GeomH<NCOL, BF>::kThreads), (GeomH<NCOL, BF>::kWav
         for (int k = 0; k < 2; ++k)
 #pragma unroll
           for (int e = 0; e < 8; ++e)
+          {
             ev[k][e] = pos_enc_feature_fast(x0, x1, x2, 32 * k + 8 * g + e, 0, 10, fast.value);
+            __builtin_amdgcn_sched_barrier(0);  // one feature's fp64 temporaries live at a time
+          }
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
+        for (int e = 0; e < 8; ++e) {
           vv[e] = pos_enc_feature_fast(v0, v1, v2, 8 * g + e, 0, 4, fast.value);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       };
-      // sin_small (aon_common.hpp): the same bits as sinf when the wave's arguments allow it
+      // every argument of the wave below kSinCrMax (aon_common.hpp): no per-value range branch
       if (pos_enc_fast_ok(x0, x1, x2, 10) && pos_enc_fast_ok(v0, v1, v2, 4))
         encode(std::true_type{});
       else

@@ -361,12 +361,6 @@ int launch_f16x3(int mode, int ncol, const void* packed, const float* a0, const 
 #ifndef AON_DATAFLOW_WS_BUILD
 #define AON_DATAFLOW_WS_BUILD 0
 #endif
-// the fp16x3 render forward on v_mfma_f32_32x32x16_f16 (mlp_m32.hip, AON_PREC_F16X3_M32): its
-// own stream layout; w / b: the 12 layers' torch parameters in kLayers order
-size_t packed_bytes_m32();
-int pack_m32(const float* const* w, const float* const* b, void* packed, hipStream_t stream);
-int launch_m32(int mode, const void* packed, const float* a0, const float* a1, const float* a2,
-               const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream);
 int launch_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,
                     const float* a3, int64_t B, int S, int act, float* raw, hipStream_t stream);
 int launch_art_ws_f16x3(const void* packed, const float* a0, const float* a1, const float* a2,

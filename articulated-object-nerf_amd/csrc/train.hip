@@ -19,7 +19,7 @@ __device__ __forceinline__ void wave_sync_t() {
 // model_autodecoder.py:321-323)
 __device__ __forceinline__ float dact_rgb(float x, int act) {
   if (act == AON_ACT_NONE) return 1.0f;
-  const float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-x)));
+  const float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, exp_sleef(-x)));
   const float d = __fmul_rn(s, __fsub_rn(1.0f, s));
   return act == AON_ACT_ARTIC ? __fmul_rn(d, 1.002f) : d;
 }
@@ -27,8 +27,12 @@ __device__ __forceinline__ float dact_rgb(float x, int act) {
 __device__ __forceinline__ float dact_sigma(float x, int act) {
   if (act == AON_ACT_NONE) return 1.0f;
   if (act == AON_ACT_VANILLA) return x > 0.0f ? 1.0f : 0.0f;
-  const float z = __fsub_rn(x, 1.0f);  // softplus(z)' = sigmoid(z), threshold 20
-  return z > 20.0f ? 1.0f : __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-z)));
+  // softplus(z)' with threshold 20, as torch's CPU softplus_backward forms it: e/(e + 1)
+  // with e = exp(z) (SLEEF)
+  const float z = __fsub_rn(x, 1.0f);
+  if (z > 20.0f) return 1.0f;
+  const float e = exp_sleef(z);
+  return __fdiv_rn(e, __fadd_rn(e, 1.0f));
 }
 
 // Backward of volumetric_rendering for one ray per wave.  With f_j = 1 - alpha_j + 1e-10,
@@ -73,7 +77,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void k_composite_bwd(
         const float D = __fmul_rn(dist, dnorm);
         const float sraw = sig[r * sig_stride];
         const float sgm = act_sigma(sraw, act);
-        const float e = expf(__fmul_rn(-sgm, D));
+        const float e = exp_cr(__fmul_rn(-sgm, D));
         const float a = __fsub_rn(1.0f, e);
         alpha[b] = a;
         if (i + 1 < S) {

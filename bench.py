@@ -52,10 +52,9 @@ NC, NF = 64, 128
 MAC_PER_SAMPLE = 593_408            # NeRFMLP multiply-accumulates per sample
 # Dense MFMA peak of the issued instruction, in ALGORITHMIC (fp32-class) FLOP/s: fp32 MFMA
 # 157.3 TF; fp16 MFMA 2500 TF, of which f16x3 spends 3 products per fp32-class MAC -> 833.3.
-PEAK_TFLOPS = {"fp32": 157.3, "f16x3": 2500.0 / 3, "f16x3_m32": 2500.0 / 3}
-ISSUED_PEAK = {"fp32": ("v_mfma_f32_16x16x4_f32", 157.3, 1), "f16x3": ("v_mfma_f32_16x16x32_f16", 2500.0, 3),
-               "f16x3_m32": ("v_mfma_f32_32x32x16_f16", 2500.0, 3)}
-KERNEL = {"fp32": "k_mlp_fwd_f32", "f16x3": "k_mlp_fwd_f16x3", "f16x3_m32": "k_mlp_fwd_m32"}
+PEAK_TFLOPS = {"fp32": 157.3, "f16x3": 2500.0 / 3}
+ISSUED_PEAK = {"fp32": ("v_mfma_f32_16x16x4_f32", 157.3, 1), "f16x3": ("v_mfma_f32_16x16x32_f16", 2500.0, 3)}
+KERNEL = {"fp32": "k_mlp_fwd_f32", "f16x3": "k_mlp_fwd_f16x3"}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -189,8 +188,7 @@ def main():
     ppath = os.path.join(ROOT, "profiles", "mfma_peak.json")
     if achieved and os.path.exists(ppath):
         mp = json.load(open(ppath))
-        key = {"fp32": "f32_16x16x4_tflops", "f16x3": "f16_16x16x32_tflops",
-               "f16x3_m32": "f16_32x32x16_tflops"}[args.precision]
+        key = {"fp32": "f32_16x16x4_tflops", "f16x3": "f16_16x16x32_tflops"}[args.precision]
         if mp.get(key):
             iss = out["roofline"]["issued"]
             iss["measured_dtype_peak_tflops"] = mp[key]

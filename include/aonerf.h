@@ -24,7 +24,9 @@ extern "C" {
 
 typedef void* aon_stream_t; /* hipStream_t */
 
-#define AON_ABI_VERSION 12
+#define AON_ABI_VERSION 13 /* 13: pos_enc's sin and the alpha exp correctly rounded, sigmoid as
+                            * torch's CPU kernel forms it; the 32x32x16 precision of ABI 12
+                            * (value 3) withdrawn: measured slower */
 
 /* Precision of the MLP GEMMs (see DESIGN.md "MLP precision modes"). */
 #define AON_PREC_FP32 0  /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32) */
@@ -33,10 +35,6 @@ typedef void* aon_stream_t; /* hipStream_t */
 #define AON_PREC_BF16 2  /* bf16 operands, 1 product per weight (v_mfma_f32_16x16x32_bf16), fp32
                          * accumulate: the training step's bf16 mode (BASELINE config C5) --
                          * aon_mlp_fwd_train_bf16 / aon_mlp_bwd_bf16 / aon_gemm with bf16 operands */
-#define AON_PREC_F16X3_M32 3 /* ABI 12: the AON_PREC_F16X3 numerics on v_mfma_f32_32x32x16_f16, 32
-                              * samples per wave -- the render forwards (aon_mlp_fwd,
-                              * aon_mlp_fwd_encoded) only; its own packed layout
-                              * (aon_mlp_packed_bytes(3), aon_mlp_pack(.., 3, ..)) */
 
 /* Output activation applied by the compositor (reference model.py:186-187,
  * model_autodecoder.py:321-323). */

@@ -35,10 +35,9 @@ def test_header_symbols_exported(L):
 
 def test_abi_version_and_sizes(L):
     lib = L.lib()
-    assert lib.aon_abi_version() == L.ABI_VERSION == 12
-    assert lib.aon_mlp_packed_bytes(0) == 2368 * 1024 + 2464 * 4 + 16  # + the status block
-    # ABI 12: the 32x32x16 render stream (32-row output tiles: 2,496 bias floats)
-    assert lib.aon_mlp_packed_bytes(3) == 2368 * 1024 + 2496 * 4 + 16
+    assert lib.aon_abi_version() == L.ABI_VERSION == 13
+    # precision 3 (ABI 12's 32x32x16 render stream) is withdrawn: no packed size
+    assert lib.aon_mlp_packed_bytes(3) == 0
     assert lib.aon_mlp_packed_bytes(99) == 0
 
 

@@ -125,7 +125,7 @@ def npy(t):
     return t.detach().float().cpu().numpy()
 
 
-PRECISIONS = ["fp32", "f16x3", "f16x3_m32"]
+PRECISIONS = ["fp32", "f16x3"]
 
 
 def make_nerf(precision, **kw):

@@ -4,7 +4,7 @@
 // accumulators per wave, every CU filled.  kind 0: v_mfma_f32_16x16x32_f16 (the f16x3 MLP's
 // instruction); kind 1: v_mfma_f32_16x16x4_f32 (the fp32 path's); kind 2: the f16x3 pattern,
 // three dependent MFMAs into one accumulator per step; kind 3: v_mfma_f32_32x32x16_f16 (the
-// 32x32 render MLP's, mlp_m32.hip); kind 4: its f16x3 triple.  Returns TFLOP/s of the issued
+// withdrawn 32x32 render MLP's, git e46498b); kind 4: its f16x3 triple.  Returns TFLOP/s of the issued
 // MFMAs.
 #include <hip/hip_runtime.h>
 #include <cstdint>
