@@ -102,8 +102,32 @@ __host__ __device__ inline float exp_sleef(float d) {  // (built with -ffp-contr
 
 // exp as torch.exp evaluates it on CPU for the alpha of volumetric_rendering (MKL's
 // high-accuracy vsExp: correctly rounded in ~99% of elements): the correctly rounded fp32
-// exp, through fp64 (the double rounding is off only within 2^-29 of a midpoint)
-__host__ __device__ inline float exp_cr(float x) { return (float)::exp((double)x); }
+// exp, evaluated in fp64 and rounded once.  Every alpha argument is -sigma * delta <= 0: k =
+// round(x / ln2) and r = x - k ln2 (fdlibm's two-part ln2, fmas; |r| <= 0.347), then the degree-12
+// Taylor polynomial (remainder < 2^-52) and 2^k by v_ldexp_f64 -- fewer live fp64 temporaries
+// than the general fp64 exp (the fine compositor runs at 80 VGPRs).  Arguments below -120 (fp32
+// result 0) are clamped; NaN propagates; x > 0 is outside the domain the callers use (correct
+// to x = 88, where fp32 overflows anyway only through the polynomial's accuracy at |r| <= 0.347).
+__host__ __device__ inline float exp_cr(float xf) {
+  const double x = xf < -120.0f ? -120.0 : (double)xf;
+  const double k = __builtin_rint(x * 1.44269504088896338700e+00);
+  double r = __builtin_fma(-k, 6.93147180369123816490e-01, x);
+  r = __builtin_fma(-k, 1.90821492927058770002e-10, r);
+  double p = 1.0 / 479001600.0;
+  p = __builtin_fma(r, p, 1.0 / 39916800.0);
+  p = __builtin_fma(r, p, 1.0 / 3628800.0);
+  p = __builtin_fma(r, p, 1.0 / 362880.0);
+  p = __builtin_fma(r, p, 1.0 / 40320.0);
+  p = __builtin_fma(r, p, 1.0 / 5040.0);
+  p = __builtin_fma(r, p, 1.0 / 720.0);
+  p = __builtin_fma(r, p, 1.0 / 120.0);
+  p = __builtin_fma(r, p, 1.0 / 24.0);
+  p = __builtin_fma(r, p, 1.0 / 6.0);
+  p = __builtin_fma(r, p, 0.5);
+  p = __builtin_fma(r, p, 1.0);
+  p = __builtin_fma(r, p, 1.0);
+  return (float)__builtin_ldexp(p, (int)k);
+}
 
 // rgb_activation / sigma_activation (reference model.py:142-143, 186-187; articulated:
 // model_autodecoder.py:265, 323), shared by the MLP epilogue and the compositor.

@@ -134,16 +134,22 @@ def main():
     comp_ms, comp_rows = avg_ms("comp1")
     march_ms, march_rows = avg_ms("march0")
     extra = {}
+
+    def run(name, fn, *a, **k):  # progress on stderr (the JSON line stays alone on stdout)
+        if rank == 0:
+            print(f"[bench] {name}", file=sys.stderr, flush=True)
+        extra[name] = fn(*a, **k)
+
     if not args.no_extra:  # every rank takes part (the C5 step all-reduces over RCCL)
         if world == 1:
             if args.precision != "fp32":
-                extra["render_fp32"] = bench_render_fp32(args, c2w, focal)
-            extra["articulated"] = bench_articulated(args)
-        extra["train_step"] = bench_train(args, world, rank, local_rank)
-        extra["train_step_bf16"] = bench_train(args, world, rank, local_rank, precision="bf16")
-        extra["train_step_art"] = bench_train(args, world, rank, local_rank, art=True)
-        extra["train_step_art_bf16"] = bench_train(args, world, rank, local_rank, art=True,
-                                                   precision="bf16")
+                run("render_fp32", bench_render_fp32, args, c2w, focal)
+            run("articulated", bench_articulated, args)
+        run("train_step", bench_train, args, world, rank, local_rank)
+        run("train_step_bf16", bench_train, args, world, rank, local_rank, precision="bf16")
+        run("train_step_art", bench_train, args, world, rank, local_rank, art=True)
+        run("train_step_art_bf16", bench_train, args, world, rank, local_rank, art=True,
+            precision="bf16")
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -519,6 +525,10 @@ def cpu_baseline(net, frame, c2w, focal, nchunks):
     rc = {k: v.cpu() for k, v in rays.items()}
     dirs = O.get_ray_directions(H, W, focal)
     _, _, rd_host = O.get_rays(dirs, c2w[:3, :4], True)
+    def progress(what):  # (stderr: the JSON line stays alone on stdout)
+        return lambda i, m: print(f"[bench] cpu_baseline {what}: {i} / {m} rays", file=sys.stderr,
+                                  flush=True)
+
     t0 = time.perf_counter()
     outs, w_ref = [], []
     with torch.no_grad():
@@ -527,12 +537,13 @@ def cpu_baseline(net, frame, c2w, focal, nchunks):
             ret, inter = O.nerf_forward(params, sub, False, True, 2.0, 6.0, return_intermediates=True)
             outs.append(ret[1])
             w_ref.append(inter[0]["weights"])
+            progress("oracle")(i + 3840, n)
     dt = time.perf_counter() - t0
     ref = [torch.cat([o[j] for o in outs]).numpy() for j in range(3)]  # rgb, acc, depth
     w_ref = torch.cat(w_ref).numpy()
     # the reference's self-consistency on the same rays (another valid fp32 implementation)
     t1 = time.perf_counter()
-    selfc = A.self_consistency(params, rc, ref)
+    selfc = A.self_consistency(params, rc, ref, progress=progress(A.SELF_VARIANT + " re-run"))
     dt_self = time.perf_counter() - t1
     f = frame[p0:p0 + n].cpu().numpy()
     gpu = [f[:, :3], f[:, 4], f[:, 3]]

@@ -265,11 +265,12 @@ class Attribution:
 
 # ----------------------------------------------------------------------------- self-consistency
 def fine_outputs(params, rays, chunk=3840, white_bkgd=True, near=2.0, far=6.0, randomized=False,
-                 u_coarse=None, u_fine=None, latents=None, **kw):
+                 u_coarse=None, u_fine=None, latents=None, progress=None, **kw):
     """The oracle's fine (rgb, acc, depth) on ``rays``, chunk by chunk as the reference's
     render_rays does (model.py:295-348), as float64 numpy arrays: vanilla NeRF.forward
     (nerf_forward), or NeRF_AE_Art.forward (art_nerf_forward) when ``latents`` are given.
-    randomized: with the injected uniforms ``u_coarse`` / ``u_fine`` (per-ray rows)."""
+    randomized: with the injected uniforms ``u_coarse`` / ``u_fine`` (per-ray rows).
+    progress(i, n): called after each chunk (long CPU runs report as they go)."""
     n = rays["rays_o"].shape[0]
     outs = []
     with torch.no_grad():
@@ -286,6 +287,8 @@ def fine_outputs(params, rays, chunk=3840, white_bkgd=True, near=2.0, far=6.0, r
                 r = O.art_nerf_forward(params, sub, randomized, white_bkgd, near, far, latents,
                                        **uk, **kw)
             outs.append(r[1])
+            if progress is not None:
+                progress(min(i + chunk, n), n)
     return [torch.cat([o[j] for o in outs]).detach().numpy().astype(np.float64) for j in range(3)]
 
 
