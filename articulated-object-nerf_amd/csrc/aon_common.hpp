@@ -108,7 +108,13 @@ __host__ __device__ inline float exp_sleef(float d) {  // (built with -ffp-contr
 // than the general fp64 exp (the fine compositor runs at 80 VGPRs).  Arguments below -120 (fp32
 // result 0) are clamped; NaN propagates; x > 0 is outside the domain the callers use (correct
 // to x = 88, where fp32 overflows anyway only through the polynomial's accuracy at |r| <= 0.347).
+#ifndef AON_ALPHA_EXP_DEVICE
+#define AON_ALPHA_EXP_DEVICE 0  // 1: timing-only A/B build -- the device's own expf (not the torch value)
+#endif
 __host__ __device__ inline float exp_cr(float xf) {
+#if AON_ALPHA_EXP_DEVICE
+  return expf(xf);
+#endif
   const double x = xf < -120.0f ? -120.0 : (double)xf;
   const double k = __builtin_rint(x * 1.44269504088896338700e+00);
   double r = __builtin_fma(-k, 6.93147180369123816490e-01, x);

@@ -15,6 +15,7 @@
 // sample's other three lane groups with ds_bpermute, added to xyz in fp32 and encoded in
 // registers, so nothing leaves the chip between the deformation and the raw outputs.
 #include "mlp_f16x3_core.hpp"
+#include <type_traits>
 #include "param_check.hpp"
 
 namespace aon {
@@ -89,8 +90,16 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
       const float tt = in3[rr];
 #pragma unroll
       for (int q = 0; q < 3; ++q) px[c][q] = __fadd_rn(ro[q], __fmul_rn(tt, rd[q]));
+      // (the range test hoisted out of the sines: one wave-uniform branch, aon_common.hpp)
+      auto venc_fn = [&](auto fast) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) vv[e] = pos_enc_feature(vd[0], vd[1], vd[2], 8 * g + e, 0, 4);
+        for (int e = 0; e < 8; ++e)
+          vv[e] = pos_enc_feature_fast(vd[0], vd[1], vd[2], 8 * g + e, 0, 4, fast.value);
+      };
+      if (pos_enc_fast_ok(vd[0], vd[1], vd[2], 4))
+        venc_fn(std::true_type{});
+      else
+        venc_fn(std::false_type{});
     } else {
       const float* x = in0 + rr * 3;
       const float* cd = in1 + ray * 27;
@@ -148,14 +157,22 @@ __global__ __launch_bounds__(GeomH<NCOL>::kThreads, NCOL == 1 ? 2 : 1) void k_ml
 #pragma unroll
     for (int q = 0; q < 3; ++q) q3[q] = __fadd_rn(__shfl(dlt[c][q], j, 64), px[c][q]);
     float fv[2][8], ev[2][8];
+    auto enc_fn = [&](auto fast) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+      for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = pos_enc_feature(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10);
-        fv[k][e] = f;
-        ev[k][e] = f * act_scale<BFM>();
-      }
+        for (int e = 0; e < 8; ++e) {
+          const float f =
+              pos_enc_feature_fast(q3[0], q3[1], q3[2], 32 * k + 8 * g + e, 0, 10, fast.value);
+          fv[k][e] = f;
+          ev[k][e] = f * act_scale<BFM>();
+          __builtin_amdgcn_sched_barrier(0);  // one feature's fp64 temporaries live at a time
+        }
+    };
+    if (pos_enc_fast_ok(q3[0], q3[1], q3[2], 10))
+      enc_fn(std::true_type{});
+    else
+      enc_fn(std::false_type{});
     if (STORE && keep_row(rows[c], N)) {
       store_enc_f32<PREC == 0 ? 64 : 16>(ts.enc, rows[c], g, fv);
       if (PREC != 0) store_enc_bf(ts.enc_bf, rows[c], g, fv);

@@ -76,15 +76,33 @@ def _net(sd, precision="f16x3"):
     return net.requires_grad_(False)
 
 
-def _coarse_vs_oracle(net, g, params):
+def _coarse_vs_oracle(net, g, params, kernel_math=False):
+    """max |GPU - oracle| over the coarse rgb / acc / weights.  kernel_math: the oracle with the
+    kernels' correctly rounded sin / exp (attribution.kernel_transcendentals) -- at |h| ~ 1e5 the
+    scaled first layer amplifies a one-ulp pos_enc sine difference between the kernels' correctly
+    rounded value and torch's MKL sine past 1e-4 (r06g: 1.4e-4 against the plain oracle), which
+    is not what the fallback test is about (the fallback's fp32 arithmetic); the plain-oracle
+    distance is printed beside it."""
+    from oracle import attribution as A
+
     rays = {k: torch.from_numpy(g[k]).cuda() for k in ("rays_o", "rays_d", "viewdirs")}
     with warnings.catch_warnings(record=True) as w:
         warnings.simplefilter("always")
         ret = net(rays, False, True, 2.0, 6.0, return_weights=True, return_intermediates=True)
     rc = {k: v.cpu() for k, v in rays.items()}
-    ref = O.render_level(params, rc, ret[0][4]["t_vals"].cpu(), 0, True)
-    err = max(float((ret[0][0].cpu() - ref[0]).abs().max()), float((ret[0][1].cpu() - ref[1]).abs().max()),
-              float((ret[0][3].cpu() - ref[2]).abs().max()))
+    t = ret[0][4]["t_vals"].cpu()
+
+    def dist(ref):
+        return max(float((ret[0][0].cpu() - ref[0]).abs().max()),
+                   float((ret[0][1].cpu() - ref[1]).abs().max()),
+                   float((ret[0][3].cpu() - ref[2]).abs().max()))
+
+    err = dist(O.render_level(params, rc, t, 0, True))
+    if kernel_math:
+        with A.kernel_transcendentals():
+            err_k = dist(O.render_level(params, rc, t, 0, True))
+        print(f"  vs the plain oracle {err:.2e}; vs the oracle with the kernels' sin / exp {err_k:.2e}")
+        err = err_k
     return err, [str(x.message) for x in w], net
 
 
@@ -126,15 +144,16 @@ def test_outside_range_detected_and_rendered_in_fp32(golden, target, status):
         L.call("aon_mlp_read_status", L.ptr(net.coarse_mlp._packed), packed.numel() * 4,
                ctypes.byref(st), L.stream(packed.device))
         assert st.value == 0
-    # the render path: warns, re-renders on the fp32 kernels, matches the oracle
-    err, warns, net = _coarse_vs_oracle(net, g, params)
+    # the render path: warns, re-renders on the fp32 kernels, matches the oracle (with the
+    # kernels' transcendentals: see _coarse_vs_oracle)
+    err, warns, net = _coarse_vs_oracle(net, g, params, kernel_math=True)
     print(f"fallback render at |h| ~ {m:.0f}: max |gpu - oracle| {err:.2e}; warnings {warns}")
     assert any("fp16x3 range" in w for w in warns)
     assert net.coarse_mlp.precision == "f16x3"  # restored after the fallback
     assert err <= 1e-4
     # the fp32 path itself never reports
     n32 = _net(sd, "fp32")
-    e32, w32, _ = _coarse_vs_oracle(n32, g, params)
+    e32, w32, _ = _coarse_vs_oracle(n32, g, params, kernel_math=True)
     assert not w32 and e32 <= 1e-4
 
 
