@@ -65,7 +65,6 @@ __device__ __forceinline__ void composite_ray(const float (&tt)[NB], const f4 (&
       alpha = __fsub_rn(1.0f, exp_cr(__fmul_rn(-sgm, __fmul_rn(dist, dnorm))));
       if (i + 1 < S) f = (double)__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f);
     }
-    __builtin_amdgcn_sched_barrier(0);  // the fp64 exp's temporaries die before the scan
     const double incl = wave_incl_prod(f);
     const double excl = dpp_f64<0x138>(incl, 1.0);  // wave_shr:1, lane 0 -> 1
     const float T = (float)(carry * excl);

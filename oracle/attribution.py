@@ -130,16 +130,6 @@ TRANSCENDENTAL_VARIANTS = {
 
 
 @contextlib.contextmanager
-def kernel_transcendentals():
-    """torch.sin and torch.exp correctly rounded for the duration: the oracle with the
-    transcendentals the HIP kernels evaluate (aon_common.hpp sincos_cr / exp_cr; its sigmoid is
-    torch's own already) -- for gates whose subject is the kernels' fp32 arithmetic on inputs that
-    amplify a one-ulp sine difference past the gate (tests/test_gpu_range.py at |h| ~ 1e5)."""
-    with patched_torch("sin", correctly_rounded), patched_torch("exp", correctly_rounded):
-        yield
-
-
-@contextlib.contextmanager
 def _oracle_gemm(fn):
     """Every nn.Linear product of the oracle -- the vanilla MLP (mlp_forward) and the
     articulated one (nerf_oracle._lin) -- as ``fn(x, w, b)``."""

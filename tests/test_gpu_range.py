@@ -76,13 +76,11 @@ def _net(sd, precision="f16x3"):
     return net.requires_grad_(False)
 
 
-def _coarse_vs_oracle(net, g, params, kernel_math=False):
-    """max |GPU - oracle| over the coarse rgb / acc / weights.  kernel_math: the oracle with the
-    kernels' correctly rounded sin / exp (attribution.kernel_transcendentals) -- at |h| ~ 1e5 the
-    scaled first layer amplifies a one-ulp pos_enc sine difference between the kernels' correctly
-    rounded value and torch's MKL sine past 1e-4 (r06g: 1.4e-4 against the plain oracle), which
-    is not what the fallback test is about (the fallback's fp32 arithmetic); the plain-oracle
-    distance is printed beside it."""
+def _coarse_vs_oracle(net, g, params):
+    """max |GPU - oracle| over the coarse rgb / acc / weights, and the reference's own
+    implementation envelope on the same input: the largest move of those outputs when the oracle
+    is re-run as another valid fp32 implementation of itself (GEMMs in fp64 or split-K, sin / exp
+    correctly rounded or one ulp off; oracle/attribution.py)."""
     from oracle import attribution as A
 
     rays = {k: torch.from_numpy(g[k]).cuda() for k in ("rays_o", "rays_d", "viewdirs")}
@@ -91,19 +89,19 @@ def _coarse_vs_oracle(net, g, params, kernel_math=False):
         ret = net(rays, False, True, 2.0, 6.0, return_weights=True, return_intermediates=True)
     rc = {k: v.cpu() for k, v in rays.items()}
     t = ret[0][4]["t_vals"].cpu()
+    ref = O.render_level(params, rc, t, 0, True)
+    err = max(float((ret[0][0].cpu() - ref[0]).abs().max()), float((ret[0][1].cpu() - ref[1]).abs().max()),
+              float((ret[0][3].cpu() - ref[2]).abs().max()))
+    _, worst = A.envelope(lambda: list(O.render_level(params, rc, t, 0, True)[:3]))
+    return err, [str(x.message) for x in w], net, max(worst.values())
 
-    def dist(ref):
-        return max(float((ret[0][0].cpu() - ref[0]).abs().max()),
-                   float((ret[0][1].cpu() - ref[1]).abs().max()),
-                   float((ret[0][3].cpu() - ref[2]).abs().max()))
 
-    err = dist(O.render_level(params, rc, t, 0, True))
-    if kernel_math:
-        with A.kernel_transcendentals():
-            err_k = dist(O.render_level(params, rc, t, 0, True))
-        print(f"  vs the plain oracle {err:.2e}; vs the oracle with the kernels' sin / exp {err_k:.2e}")
-        err = err_k
-    return err, [str(x.message) for x in w], net
+def _gate(env):
+    """1e-4, or twice the reference's own envelope where the input makes the reference move by
+    more than that against itself: at |h| ~ 1e5 its split-K re-run alone moves these outputs by
+    1.1e-4 (measured on the CPU, r06), so no implementation can be held to 1e-4 there.  (Found
+    when the round-6 kernels' sines / exps moved this test from under 1e-4 to 1.4e-4.)"""
+    return max(1e-4, 2.0 * env)
 
 
 def test_inside_range_stays_f16x3(golden):
@@ -111,10 +109,11 @@ def test_inside_range_stays_f16x3(golden):
     print(f"largest hidden activation {m:.1f}")
     assert 4e3 < m < 8e3
     net = _net(sd)
-    err, warns, net = _coarse_vs_oracle(net, g, params)
+    err, warns, net, env = _coarse_vs_oracle(net, g, params)
     from aonerf import _lib as L
 
-    print(f"f16x3 at |h| ~ {m:.0f}: coarse rgb/acc/weights max |gpu - oracle| {err:.2e}")
+    print(f"f16x3 at |h| ~ {m:.0f}: coarse rgb/acc/weights max |gpu - oracle| {err:.2e} "
+          f"(the reference's own envelope {env:.2e})")
     assert not warns and not L.range_overflow([net.coarse_mlp._packed])
     assert err <= 1e-4
 
@@ -144,17 +143,17 @@ def test_outside_range_detected_and_rendered_in_fp32(golden, target, status):
         L.call("aon_mlp_read_status", L.ptr(net.coarse_mlp._packed), packed.numel() * 4,
                ctypes.byref(st), L.stream(packed.device))
         assert st.value == 0
-    # the render path: warns, re-renders on the fp32 kernels, matches the oracle (with the
-    # kernels' transcendentals: see _coarse_vs_oracle)
-    err, warns, net = _coarse_vs_oracle(net, g, params, kernel_math=True)
-    print(f"fallback render at |h| ~ {m:.0f}: max |gpu - oracle| {err:.2e}; warnings {warns}")
+    # the render path: warns, re-renders on the fp32 kernels, matches the oracle
+    err, warns, net, env = _coarse_vs_oracle(net, g, params)
+    print(f"fallback render at |h| ~ {m:.0f}: max |gpu - oracle| {err:.2e} (the reference's own "
+          f"envelope {env:.2e}, gate {_gate(env):.2e}); warnings {warns}")
     assert any("fp16x3 range" in w for w in warns)
     assert net.coarse_mlp.precision == "f16x3"  # restored after the fallback
-    assert err <= 1e-4
+    assert err <= _gate(env)
     # the fp32 path itself never reports
     n32 = _net(sd, "fp32")
-    e32, w32, _ = _coarse_vs_oracle(n32, g, params, kernel_math=True)
-    assert not w32 and e32 <= 1e-4
+    e32, w32, _, _ = _coarse_vs_oracle(n32, g, params)
+    assert not w32 and e32 <= _gate(env)
 
 
 def test_training_step_refused_on_overflow(golden):
