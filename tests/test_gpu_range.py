@@ -77,10 +77,9 @@ def _net(sd, precision="f16x3"):
 
 
 def _coarse_vs_oracle(net, g, params):
-    """max |GPU - oracle| over the coarse rgb / acc / weights, and the reference's own
-    implementation envelope on the same input: the largest move of those outputs when the oracle
-    is re-run as another valid fp32 implementation of itself (GEMMs in fp64 or split-K, sin / exp
-    correctly rounded or one ulp off; oracle/attribution.py)."""
+    """max |GPU - oracle| over the coarse rgb / acc / weights, and the same distance for the
+    GPU and for the oracle's own fp32 result measured from a more accurate evaluation of the
+    reference (its GEMMs in fp64, sin / exp correctly rounded: oracle/attribution.py variants)."""
     from oracle import attribution as A
 
     rays = {k: torch.from_numpy(g[k]).cuda() for k in ("rays_o", "rays_d", "viewdirs")}
@@ -89,19 +88,26 @@ def _coarse_vs_oracle(net, g, params):
         ret = net(rays, False, True, 2.0, 6.0, return_weights=True, return_intermediates=True)
     rc = {k: v.cpu() for k, v in rays.items()}
     t = ret[0][4]["t_vals"].cpu()
-    ref = O.render_level(params, rc, t, 0, True)
-    err = max(float((ret[0][0].cpu() - ref[0]).abs().max()), float((ret[0][1].cpu() - ref[1]).abs().max()),
-              float((ret[0][3].cpu() - ref[2]).abs().max()))
-    _, worst = A.envelope(lambda: list(O.render_level(params, rc, t, 0, True)[:3]))
-    return err, [str(x.message) for x in w], net, max(worst.values())
+    gpu = [ret[0][0].cpu(), ret[0][1].cpu(), ret[0][3].cpu()]
+
+    def dist(a, b):
+        return max(float((x - y).abs().max()) for x, y in zip(a, b))
+
+    ref = O.render_level(params, rc, t, 0, True)[:3]
+    v = A.oracle_variants()
+    with v["fp64_gemm"](), v["sin_cr"](), v["exp_cr"]():
+        acc = O.render_level(params, rc, t, 0, True)[:3]
+    return dist(gpu, ref), [str(x.message) for x in w], net, (dist(gpu, acc), dist(ref, acc))
 
 
-def _gate(env):
-    """1e-4, or twice the reference's own envelope where the input makes the reference move by
-    more than that against itself: at |h| ~ 1e5 its split-K re-run alone moves these outputs by
-    1.1e-4 (measured on the CPU, r06), so no implementation can be held to 1e-4 there.  (Found
-    when the round-6 kernels' sines / exps moved this test from under 1e-4 to 1.4e-4.)"""
-    return max(1e-4, 2.0 * env)
+def _ok(err, acc):
+    """Within 1e-4 of the fp32 reference, or -- where the input is conditioned so badly that the
+    reference's own fp32 result sits farther than that from a more accurate evaluation of
+    itself -- no farther from that evaluation than 2x the reference is.  (At |h| ~ 1e5 the
+    reference's split-K re-run alone moves these outputs by 6e-5 - 1.1e-4 by machine; round 6's
+    kernels measured 1.4e-4 from the fp32 reference there: r06g-i.)"""
+    ours, theirs = acc
+    return err <= 1e-4 or ours <= max(1e-4, 2.0 * theirs)
 
 
 def test_inside_range_stays_f16x3(golden):
@@ -109,11 +115,11 @@ def test_inside_range_stays_f16x3(golden):
     print(f"largest hidden activation {m:.1f}")
     assert 4e3 < m < 8e3
     net = _net(sd)
-    err, warns, net, env = _coarse_vs_oracle(net, g, params)
+    err, warns, net, acc = _coarse_vs_oracle(net, g, params)
     from aonerf import _lib as L
 
     print(f"f16x3 at |h| ~ {m:.0f}: coarse rgb/acc/weights max |gpu - oracle| {err:.2e} "
-          f"(the reference's own envelope {env:.2e})")
+          f"(from the accurate evaluation: gpu {acc[0]:.2e}, reference fp32 {acc[1]:.2e})")
     assert not warns and not L.range_overflow([net.coarse_mlp._packed])
     assert err <= 1e-4
 
@@ -144,16 +150,16 @@ def test_outside_range_detected_and_rendered_in_fp32(golden, target, status):
                ctypes.byref(st), L.stream(packed.device))
         assert st.value == 0
     # the render path: warns, re-renders on the fp32 kernels, matches the oracle
-    err, warns, net, env = _coarse_vs_oracle(net, g, params)
-    print(f"fallback render at |h| ~ {m:.0f}: max |gpu - oracle| {err:.2e} (the reference's own "
-          f"envelope {env:.2e}, gate {_gate(env):.2e}); warnings {warns}")
+    err, warns, net, acc = _coarse_vs_oracle(net, g, params)
+    print(f"fallback render at |h| ~ {m:.0f}: max |gpu - oracle| {err:.2e}; from the accurate "
+          f"evaluation: gpu {acc[0]:.2e}, reference fp32 {acc[1]:.2e}; warnings {warns}")
     assert any("fp16x3 range" in w for w in warns)
     assert net.coarse_mlp.precision == "f16x3"  # restored after the fallback
-    assert err <= _gate(env)
+    assert _ok(err, acc)
     # the fp32 path itself never reports
     n32 = _net(sd, "fp32")
-    e32, w32, _, _ = _coarse_vs_oracle(n32, g, params)
-    assert not w32 and e32 <= _gate(env)
+    e32, w32, _, acc32 = _coarse_vs_oracle(n32, g, params)
+    assert not w32 and _ok(e32, acc32)
 
 
 def test_training_step_refused_on_overflow(golden):
