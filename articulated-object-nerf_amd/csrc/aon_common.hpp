@@ -196,6 +196,9 @@ __device__ __forceinline__ float cos_cr(float x) {
   return static_cast<float>(__ocml_cos_f64(static_cast<double>(x)));
 }
 
+#ifndef AON_POS_ENC_NOSIN
+#define AON_POS_ENC_NOSIN 0
+#endif
 // fp32(0.5 * pi) as torch adds it to an fp32 tensor (reference helper.py:139)
 constexpr float kHalfPi = 1.57079637050628662109375f;
 
@@ -236,7 +239,12 @@ __device__ __forceinline__ float pos_enc_feature_fast(float x0, float x1, float 
   const float xc = c == 0 ? x0 : (c == 1 ? x1 : x2);
   const float xb = xc * __builtin_ldexpf(1.0f, min_deg + d);
   const float arg = cosine ? __fadd_rn(xb, kHalfPi) : xb;
+#if AON_POS_ENC_NOSIN  // timing-only A/B build: no sine at all (wrong values; bounds its cost)
+  (void)fast;
+  return arg;
+#else
   return fast ? sincos_cr(arg, 0) : sin_cr(arg);
+#endif
 }
 // wave-uniform: every pos_enc argument of this wave's points (|x| 2^(max_deg - 1) + pi/2) is
 // below kSinCrMax
