@@ -625,8 +625,7 @@ def test_art_train_step_c5_4096_rays():
         tgt = target.cpu()
         ref_e2e = (O.img2mse(e2e[1][0], tgt) + O.img2mse(e2e[0][0], tgt)).item()
     ref, ref_loss, xps = {}, None, {}
-    for mode, dtype in (("fp32", torch.float32), ("fp64", torch.float64), ("forced", torch.float64),
-                        ("forced32", torch.float32)):
+    for mode, dtype in (("fp32", torch.float32), ("fp64", torch.float64), ("forced", torch.float64)):
         rays = {k: batch[k].cpu().to(dtype) for k in ("rays_o", "rays_d", "viewdirs")}
         params = [{k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
                   for p in O.split_state_dict(W.art_state_dict(0))]
@@ -720,7 +719,6 @@ def test_art_train_step_c5_4096_rays():
     for name, want in ref["fp32"].items():
         ea = rel_err(ours[name], ref["masked"][name])
         lottery = rel_err(ours[name], ref["forced"][name])
-        lottery32 = rel_err(ref["forced32"][name], ref["forced"][name])
         env = rel_err(want, ref["fp64"][name])
         r = next(v for pre, v in ratio.items() if name.startswith(pre))
         e = rel_err(ours[name], want)
@@ -733,8 +731,8 @@ def test_art_train_step_c5_4096_rays():
         if e > allow:
             (attributed if ok_a and r <= 1.5 else unexplained).append(name)
         if e > 1e-4 or ea > 1e-5 or not ok_a:
-            print(f"  {name:45s} (A) mask-forced {ea:.2e}, unforced {lottery:.2e} (fp32 oracle "
-                  f"{lottery32:.2e})  (B) ours {e:.2e}  oracle fp32-vs-fp64 {env:.2e}"
+            print(f"  {name:45s} (A) mask-forced {ea:.2e}, unforced {lottery:.2e}  (B) ours {e:.2e}"
+                  f"  oracle fp32-vs-fp64 {env:.2e}"
                   f"{'  ATTRIBUTED' if name in attributed else ''}")
     print(f"C5 art grads (4096 rays): (A) x'- and mask-forced worst error / 1e-4 {worst_a:.2f}; (B) "
           f"free-running worst error / allowance {worst_b:.2f}, {len(attributed)} tensor(s) "
