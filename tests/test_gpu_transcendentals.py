@@ -84,6 +84,8 @@ def test_pos_enc_sin_correctly_rounded():
     from aonerf import helper as H
     g = torch.Generator().manual_seed(3)
     x = (torch.rand((1 << 18, 3), generator=g) * 12.0 - 6.0)
+    # the last 4,096 points far out: arguments x 2^9 past kSinCrMax (2^20) take the fp64 OCML sine
+    x[-4096:] *= 1000.0
     got = H.pos_enc(x.cuda(), 0, 10).cpu().numpy()
     xb = (x[:, None, :] * torch.tensor([2.0 ** i for i in range(10)])[:, None]).reshape(-1, 30)
     args = torch.cat([xb, xb + 0.5 * np.pi], -1).numpy()
